@@ -1,0 +1,164 @@
+#!/usr/bin/env python3
+"""Benchmark: Gauss-Newton iterations/s of the device-resident bundle-adjustment loop.
+
+Workload (BASELINE.json configs[3] = the north-star target scene): synthetic single-camera
+fish-eye, 1000 images x 50,000 tie points (500,000 image points, 10 per tie point), inner
+constraints, free network, all EOP + IOP + 5 radial + 2 decentering terms, fp64.  A step is one
+full Gauss-Newton iteration (BuildAwG linearisation + normal equations + Schur reduction +
+bordered Cholesky solve + back-substitution + de-scaling + xhat update + sumabs), inputs resident
+in HBM.  With --gpus N (torchrun, one process per GPU) the observations are sharded by tie point
+and the reduced system is all-reduced over RCCL (strong scaling of the same scene).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3|4|5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 matrix (AMD public spec; survey section 8(d))
+
+
+def scene_folder(config, rank, world):
+    from fba_amd import synth
+    folder = os.path.join(os.environ.get("FBA_BENCH_DIR", "/tmp/fba_bench"), f"c{config}")
+    marker = os.path.join(folder, ".done")
+    if rank == 0 and not os.path.exists(marker):
+        synth.make_config(config, folder)
+        open(marker, "w").close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    return folder
+
+
+def phase_roofline(ds, ms_phase, n_steps):
+    """Per-phase algorithmic work ('Measurement') -> roofline numbers."""
+    n_pts, nI, nT = ds.n_pts, ds.numImg, ds.numtie
+    nk = ds.settings["Num_Radial_Distortions"]
+    cw = 5 + nk
+    u_c = 6 * nI + cw * ds.numCam
+    n_pad = (u_c + 63) // 64 * 64
+    t = {k: v / n_steps for k, v in ms_phase.items()}
+    chol_flops = n_pad ** 3 / 3.0 + 8.0 * n_pad ** 2
+    lin_bytes = (176 * n_pts + 336 * nT + 744 * nI)
+    return t, chol_flops, lin_bytes
+
+
+def cpu_baseline(folder, seconds):
+    """The oracle (test infrastructure) timed on the host: a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    try:
+        import fba_cpu  # C restatement (oracle/fba_cpu.c), block-sparse, OpenMP
+    except Exception as e:  # noqa: BLE001
+        return {"value": None, "unit": "iter/s", "cores": 0, "kind": "port", "sample": f"unavailable: {e}"}
+    return fba_cpu.time_iterations(folder, seconds)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, default=4)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--verbose", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    import torch
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    import fba_import
+    fba = fba_import.load()
+
+    folder = scene_folder(args.config, rank, world)
+    ds = fba.load_folder(folder)
+    stream = torch.cuda.current_stream(dev).cuda_stream if world > 1 else None
+    ctx = fba.capi.Context(ds.pack(), fba.capi.make_settings(ds.settings), device=local, rank=rank, world=world,
+                           stream=stream, verbose=args.verbose)
+    if world > 1:
+        from fba_amd.parallel import ShardedStep
+        step = ShardedStep(ctx, device=dev)
+    else:
+        step = ctx.step
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    ctx.set_timing(True)
+    phases = np.zeros(8)
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    dsum = []
+    for _ in range(args.steps):
+        dsum.append(step())
+        phases += ctx.timings()
+    torch.cuda.synchronize(dev)
+    barrier()
+    dt = time.perf_counter() - t0
+    ctx.set_timing(False)
+    if world > 1:
+        import torch.distributed as dist
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    names = ["linearize", "point", "accumulate", "border", "cholesky", "backward", "update", "total"]
+    ms = {n: float(v) for n, v in zip(names, phases)}
+    t, chol_flops, lin_bytes = phase_roofline(ds, ms, args.steps)
+    dominant = max(names[:-1], key=lambda k: t[k])
+    if dominant in ("cholesky",):
+        roof = {"bound": "mfma", "kernel": "cholesky (k_potrf_diag+k_trsm_panel+k_syrk_update)",
+                "achieved": chol_flops / (t["cholesky"] * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s"}
+    else:
+        roof = {"bound": "hbm", "kernel": dominant, "achieved": lin_bytes / (t[dominant] * 1e-3) / 1e9,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    roof["frac"] = roof["achieved"] / roof["peak"]
+    roof["traffic"] = None
+    value = args.steps / dt
+    out = {
+        "metric": "Gauss-Newton iter/sec (BuildAwG+solve) and image-point obs/sec",
+        "value": value, "unit": "iter/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"synthetic fish-eye config {args.config}: {ds.numImg} images x {ds.numtie} tie "
+                               f"points, {ds.n_pts} image points, inner constraints, nK=5",
+                   "n_pts": ds.n_pts, "n_img": ds.numImg, "n_tie": ds.numtie, "u": int(ctx.u),
+                   "parallelism": f"obs-shard{world}"},
+        "obs_per_s": ds.n_pts * value,
+        "phase_ms": {k: t[k] for k in names},
+        "deltasum_last": dsum[-1] if dsum else None,
+        "roofline": roof,
+    }
+    ctx.close()
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(folder, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

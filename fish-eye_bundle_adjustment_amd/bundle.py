@@ -1,0 +1,167 @@
+"""Reference-named host API over libfba.so.
+
+The reference's hot path is a set of MATLAB functions plus an inline loop; these wrappers keep
+their names, argument meaning and error behaviour (first output = error flag, 0 ok / 1 fail) so a
+caller can switch function by function:
+
+    [error, xhat, xhatnames] = Buildxhat(data, ...)            functions/Buildxhat.m:2
+    [error, A, misclosure, G, dist_scaling] = BuildAwG(data, xhat)   functions/BuildAwG.m:14
+    RSD = BuildRSD(v, data, xhat)                               functions/BuildRSD.m:1
+    main_error = main(folder, plot)                             main.m:10
+
+Every numeric result comes from the HIP path (libfba.so); nothing here computes a Jacobian, a
+normal matrix or a solve.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import capi
+from .io import Dataset, IngestError, load_folder, xhat_names
+
+
+def _ctx(data: Dataset, device=0, **kw):
+    ctx = getattr(data, "_fba_ctx", None)
+    if ctx is None or kw:
+        ctx = capi.Context(data.pack(), capi.make_settings(data.settings), device=device, **kw)
+        if not kw:
+            data._fba_ctx = ctx
+    return ctx
+
+
+def Buildxhat(data: Dataset):
+    """Buildxhat.m:2 -> (error, xhat, xhatnames)."""
+    try:
+        ctx = _ctx(data)
+        return 0, ctx.buildxhat(), xhat_names(data)
+    except capi.FBAError as e:
+        print(f"Error Buildxhat(): {e}")
+        return 1, None, None
+
+
+def BuildAwG(data: Dataset, xhat):
+    """BuildAwG.m:14 -> (error, A, misclosure, G, dist_scaling); A dense n x u (debug/parity form).
+
+    G is the scalar 0 when inner constraints are off (BuildAwG.m:38); dist_scaling columns 1-2
+    carry the reference's 1-based xhat indices of the first radial / decentering unknown."""
+    try:
+        ctx = _ctx(data)
+        A, w, G, ds = ctx.build_awg(np.asarray(xhat, dtype=np.float64))
+        return 0, A, w, (G if G is not None else 0), ds
+    except capi.FBAError as e:
+        print(f"BuildAwG: {e}")
+        return 1, None, None, None, None
+
+
+def BuildRSD(v, data: Dataset, xhat):
+    """BuildRSD.m:1-43: rows [targetID, imageID, x, y, r, vx, vy, vr, vt].
+
+    Radial/tangential split of given residuals with xp, yp taken from xhat when estimated.  (Inside
+    the GPU loop the same rows are produced by the device residual kernel; this host form serves
+    callers that hold a v of their own.)"""
+    s = data.settings
+    u_img = sum(int(s[k]) for k in ("Estimate_Xc", "Estimate_Yc", "Estimate_Zc", "Estimate_w", "Estimate_p",
+                                      "Estimate_k"))
+    u_cam = int(s["Estimate_c"]) + int(s["Estimate_xp"]) + int(s["Estimate_yp"]) + \
+        int(s["Estimate_radial"]) * int(s["Num_Radial_Distortions"]) + int(s["Estimate_decent"]) * 2
+    v = np.asarray(v, dtype=np.float64)
+    base = u_img * data.numImg + data.cam * u_cam
+    cnt = 0
+    iop = np.array([c[6][:2] for c in data.INT[: data.numCam]])
+    if s["Estimate_xp"]:
+        xp = np.asarray(xhat)[base]
+        cnt = 1
+    else:
+        xp = iop[data.cam, 0]
+    yp = np.asarray(xhat)[base + cnt] if s["Estimate_yp"] else iop[data.cam, 1]
+    vx, vy = v[0::2], v[1::2]
+    xb = data.xy[:, 0] - xp
+    yb = data.xy[:, 1] - yp
+    theta = np.arctan2(yb, xb)
+    phi = np.arctan2(vy, vx)
+    vd = np.sqrt(vx ** 2 + vy ** 2)
+    num = np.stack([np.sqrt(xb ** 2 + yb ** 2), vx, vy, vd * np.cos(theta - phi), vd * np.sin(theta - phi)], 1)
+    return [[data.pho_target[i], data.pho_image[i], data.xy[i, 0], data.xy[i, 1], *num[i]] for i in range(len(num))]
+
+
+@dataclass
+class Adjustment:
+    xhat: np.ndarray
+    xhatnames: list
+    iterations: int
+    deltasum: np.ndarray
+    v: np.ndarray
+    rsd: np.ndarray          # (n_pts, 5): r vx vy vr vt
+    rms: tuple               # RMSx, RMSy, RMS
+    sigma02: float
+    seconds: float
+
+
+def adjust(data: Dataset, device=0, verbose=False) -> Adjustment:
+    """main.m:386-602 on one GPU: Buildxhat, the Gauss-Newton loop, residuals and sigma0^2."""
+    t0 = time.perf_counter()
+    ctx = capi.Context(data.pack(), capi.make_settings(data.settings), device=device, verbose=verbose)
+    try:
+        it, hist = ctx.adjust()
+        t1 = time.perf_counter()
+        xhat = ctx.get_xhat()
+        v, rsd, st = ctx.residuals()
+    finally:
+        ctx.close()
+    return Adjustment(xhat=xhat, xhatnames=xhat_names(data), iterations=it, deltasum=hist, v=v, rsd=rsd,
+                      rms=(st[0], st[1], st[2]), sigma02=st[3], seconds=t1 - t0)
+
+
+def write_outputs(data: Dataset, res: Adjustment, folder):
+    """Minimal .out summary (main.m:646-682 fields) and the .rsd table (main.m:957, BuildRSD.m:6)."""
+    s = data.settings
+    name = os.path.splitext(s["Output_Filename"])[0]
+    out = os.path.join(folder, s["Output_Filename"])
+    ic = int(s["Inner_Constraints"])
+    with open(out, "w") as fh:
+        fh.write("Fish-eye model Bundle Adjustment (MI355X HIP path)\n\n")
+        fh.write(f"Time Taken:\t\t{res.seconds:.6f} seconds\nIterations:\t\t{res.iterations}\n"
+                 f"Model Used:\t\t{s['type']}\n\nSettings used:\n")
+        for k, v in s.items():
+            fh.write(f"{k}\t\t{v}\n")
+        fh.write("\nObservations/Unknowns Summary\n\n")
+        rows = [("Number of Photos", data.numImg), ("Number of Cameras", data.numCam),
+                ("Number of tie/control points", data.numGCP),
+                ("Number of tie/control points to be estimated", data.numtie), ("Total Unknowns", len(res.xhat)),
+                ("Number of image points", data.n_pts), ("Total number of observations", data.n),
+                ("Number of Inner Constraints", 7 * ic),
+                ("Total Number of Observations", data.n + 7 * ic),
+                ("Total Degrees of Freedom", data.n + 7 * ic - len(res.xhat)),
+                ("A-Posteriori", f"{res.sigma02:.10g}"), ("RMSx", f"{res.rms[0]:.10g}"),
+                ("RMSy", f"{res.rms[1]:.10g}"), ("RMS", f"{res.rms[2]:.10g}")]
+        for k, v in rows:
+            fh.write(f"{k}\t{v}\n")
+        fh.write("\nEstimated unknowns\n")
+        for nm, x in zip(res.xhatnames, res.xhat):
+            fh.write(f"{nm}\t{x:.10g}\n")
+    with open(os.path.join(folder, name + ".rsd"), "w") as fh:
+        for i in range(data.n_pts):
+            r = res.rsd[i]
+            fh.write(f"{data.pho_target[i]}\t{data.pho_image[i]}\t{data.xy[i, 0]:.10g}\t{data.xy[i, 1]:.10g}\t"
+                     f"{r[0]:.10g}\t{r[1]:.10g}\t{r[2]:.10g}\t{r[3]:.10g}\t{r[4]:.10g}\n")
+    return out
+
+
+def main(folder: str = "", plot: bool = False, device=0) -> int:
+    """main.m:10 contract: returns main_error (0 ok, 1 failure).  Plots (main.m:502-584) are not
+    produced; `plot` is accepted for signature compatibility."""
+    project_dir = os.getcwd()
+    folder = folder or project_dir
+    try:
+        data = load_folder(folder, project_dir=None if folder == project_dir else project_dir)
+        res = adjust(data, device=device)
+        write_outputs(data, res, folder)
+    except (IngestError, capi.FBAError) as e:
+        print(f"Error: {e}")
+        return 1
+    return 0

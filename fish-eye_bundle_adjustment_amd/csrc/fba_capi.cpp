@@ -1,0 +1,682 @@
+// fba_capi.cpp -- the extern "C" boundary of libfba.so (include/fba.h).
+//
+// Host side of the device-resident Gauss-Newton loop: validates the packed problem, builds the
+// observation orderings (tie observations grouped by point, CSR lists per image, co-visible image
+// pairs), allocates device memory once, and drives the kernels of fba_kernels.hip / fba_chol.hip.
+// The loop semantics are the reference's main.m:407-494; the unknown layout is Buildxhat.m:6-134.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <tuple>
+
+#include "fba_internal.h"
+
+namespace fba {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+template <typename T>
+static int dalloc(T** p, size_t n) {
+    if (n == 0) n = 1;
+    FBA_HIP(hipMalloc((void**)p, n * sizeof(T)));
+    return FBA_OK;
+}
+template <typename T>
+static int upload(T** p, const std::vector<T>& v) {
+    int rc = dalloc(p, v.size());
+    if (rc) return rc;
+    if (!v.empty()) FBA_HIP(hipMemcpy(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return FBA_OK;
+}
+
+static int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
+
+static int check_settings(const fba_settings* s) {
+    if (!s) { set_error("settings is NULL"); return FBA_ERR_ARG; }
+    if (s->type < 0 || s->type > 4) { set_error("BuildAwG, invalid type in data.settings.type"); return FBA_ERR_TYPE; }
+    if (s->num_radial < 1) {
+        // BuildAwG.m:18-20 clamps a local copy to 1 but Buildxhat.m:13 does not: with 0 the reference
+        // indexes an empty K (radial not estimated) or misaligns columns (estimated).
+        set_error("Num_Radial_Distortions must be >= 1");
+        return FBA_ERR_UNSUPPORTED;
+    }
+    if (s->num_radial > FBA_NK_MAX) { set_error("Num_Radial_Distortions > FBA_NK_MAX"); return FBA_ERR_UNSUPPORTED; }
+    if (!(s->meas_std_x > 0) || !(s->meas_std_y > 0)) { set_error("Meas_std must be > 0"); return FBA_ERR_ARG; }
+    if (s->inner_constraints &&
+        !(s->est_Xc && s->est_Yc && s->est_Zc && s->est_omega && s->est_phi && s->est_kappa)) {
+        // BuildAwG.m:525 writes 6 rows per image: the reference assumes all EOPs are estimated
+        set_error("Inner_Constraints requires all six EOPs to be estimated (BuildAwG.m:525)");
+        return FBA_ERR_UNSUPPORTED;
+    }
+    return FBA_OK;
+}
+
+static void compute_layout(const fba_problem* p, const fba_settings* s, Layout& L) {
+    L.n_img = p->n_img;
+    L.n_cam = p->n_cam;
+    L.n_tie = p->n_tie;
+    L.nk = s->num_radial;
+    L.cw = 5 + L.nk;
+    L.u_c = 6 * (int64_t)L.n_img + (int64_t)L.cw * L.n_cam;
+    L.u_full = L.u_c + 3 * (int64_t)L.n_tie;
+    L.n_pad = round_up(std::max<int64_t>(L.u_c, 1), NB);
+    L.ld = L.n_pad;
+    L.nrhs = s->inner_constraints ? 8 : 1;
+    L.u_img = s->est_Xc + s->est_Yc + s->est_Zc + s->est_omega + s->est_phi + s->est_kappa;
+    L.u_cam = s->est_c + s->est_xp + s->est_yp + s->est_radial * s->num_radial + s->est_decent * 2;
+    L.u_ref = (int64_t)L.u_img * L.n_img + (int64_t)L.u_cam * L.n_cam + 3 * (int64_t)L.n_tie;
+}
+
+static void full_to_ref_map(const fba_settings* s, const Layout& L, std::vector<int64_t>& map) {
+    map.assign(L.u_full, -1);
+    const int ee[6] = {s->est_Xc, s->est_Yc, s->est_Zc, s->est_omega, s->est_phi, s->est_kappa};
+    for (int e = 0; e < L.n_img; ++e) {
+        int cnt = 0;
+        for (int a = 0; a < 6; ++a)
+            if (ee[a]) map[6 * (int64_t)e + a] = (int64_t)e * L.u_img + cnt++;
+    }
+    std::vector<int> ce(L.cw, 0);
+    ce[0] = s->est_xp;
+    ce[1] = s->est_yp;
+    ce[2] = s->est_c;
+    for (int j = 0; j < L.nk; ++j) ce[3 + j] = s->est_radial;
+    ce[3 + L.nk] = ce[4 + L.nk] = s->est_decent;
+    for (int k = 0; k < L.n_cam; ++k) {
+        int cnt = 0;
+        for (int c = 0; c < L.cw; ++c)
+            if (ce[c]) map[6 * (int64_t)L.n_img + (int64_t)k * L.cw + c] = (int64_t)L.u_img * L.n_img + (int64_t)k * L.u_cam + cnt++;
+    }
+    const int64_t tb = (int64_t)L.u_img * L.n_img + (int64_t)L.u_cam * L.n_cam;
+    for (int64_t t = 0; t < 3 * (int64_t)L.n_tie; ++t) map[L.u_c + t] = tb + t;
+}
+
+static int check_problem(const fba_problem* p, const fba_settings* s) {
+    if (!p) { set_error("problem is NULL"); return FBA_ERR_ARG; }
+    if (p->n_pts < 0 || p->n_img < 0 || p->n_cam < 0 || p->n_tie < 0) { set_error("negative size"); return FBA_ERR_ARG; }
+    if (p->n_pts > 0 && (!p->xy || !p->img || !p->cam || !p->tie || !p->xyz_fixed)) {
+        set_error("NULL observation array");
+        return FBA_ERR_ARG;
+    }
+    if ((p->n_img > 0 && !p->eop0) || (p->n_cam > 0 && (!p->iop0 || !p->cam_info)) || (p->n_tie > 0 && !p->tie0)) {
+        set_error("NULL parameter array");
+        return FBA_ERR_ARG;
+    }
+    for (int k = 0; k < p->n_cam; ++k) {
+        const double yd = p->cam_info[5 * k];
+        if (yd != 1.0 && yd != -1.0) { set_error("y_dir should be +-1 only (main.m:334-337)"); return FBA_ERR_ARG; }
+    }
+    std::vector<int32_t> img_cam(p->n_img, -1), tie_cam(p->n_tie, -1);
+    for (int64_t i = 0; i < p->n_pts; ++i) {
+        const int e = p->img[i], k = p->cam[i], t = p->tie[i];
+        if (e < 0 || e >= p->n_img) { set_error("image index out of range (EXT must list the images of .pho in order)"); return FBA_ERR_ARG; }
+        if (k < 0 || k >= p->n_cam) { set_error("camera index out of range"); return FBA_ERR_ARG; }
+        if (t < -1 || t >= p->n_tie) { set_error("tie index out of range"); return FBA_ERR_ARG; }
+        if (img_cam[e] < 0) img_cam[e] = k;
+        else if (img_cam[e] != k) { set_error("observations of one image with different cameras"); return FBA_ERR_ARG; }
+        if (t >= 0) {
+            if (tie_cam[t] < 0) tie_cam[t] = k;
+            else if (tie_cam[t] != k) {
+                set_error("tie point observed by more than one camera: not implemented in this build");
+                return FBA_ERR_UNSUPPORTED;
+            }
+        }
+    }
+    (void)s;
+    return FBA_OK;
+}
+
+// contiguous tie ranges balanced by observation count; control observations by contiguous ranges
+static void partition(const fba_problem* p, int world, std::vector<int32_t>& tie_owner, std::vector<int32_t>& ctl_owner) {
+    tie_owner.assign(p->n_tie, 0);
+    ctl_owner.assign(p->n_pts, -1);
+    std::vector<int64_t> cnt(p->n_tie, 0);
+    int64_t n_ctl = 0;
+    for (int64_t i = 0; i < p->n_pts; ++i) {
+        if (p->tie[i] >= 0) cnt[p->tie[i]]++;
+        else n_ctl++;
+    }
+    const int64_t n_tie_obs = p->n_pts - n_ctl;
+    int64_t acc = 0;
+    for (int t = 0; t < p->n_tie; ++t) {
+        // owner = floor(world * (obs before the middle of this point) / total)
+        const int64_t mid2 = 2 * acc + cnt[t];
+        int r = n_tie_obs > 0 ? (int)((mid2 * world) / (2 * n_tie_obs)) : 0;
+        tie_owner[t] = std::min(std::max(r, 0), world - 1);
+        acc += cnt[t];
+    }
+    int64_t q = 0;
+    for (int64_t i = 0; i < p->n_pts; ++i) {
+        if (p->tie[i] >= 0) continue;
+        ctl_owner[i] = n_ctl > 0 ? (int32_t)std::min<int64_t>((q * world) / n_ctl, world - 1) : 0;
+        ++q;
+    }
+}
+
+static void destroy(Ctx* c) {
+    if (!c) return;
+    void* ptrs[] = {c->d_xy, c->d_img, c->d_cam, c->d_pt, c->d_ctl, c->d_lp_tie, c->d_lp_start, c->d_lp_cam,
+                    c->d_img_start, c->d_img_obs, c->d_cam_lp, c->d_cam_ctl, c->d_pair_e, c->d_pair_start,
+                    c->d_pair_ij, c->d_xfull, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
+                    c->d_pt_tab, c->d_slab, c->d_S, c->d_X, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
+                    c->d_active, c->d_counted, c->d_obs_pho};
+    for (void* q : ptrs)
+        if (q) (void)hipFree(q);
+    if (c->h_pinned) (void)hipHostFree(c->h_pinned);
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+static int create(const fba_problem* p, const fba_settings* s, const fba_options* o, Ctx** out) {
+    int rc = check_settings(s);
+    if (rc) return rc;
+    rc = check_problem(p, s);
+    if (rc) return rc;
+    fba_options opt{};
+    opt.world = 1;
+    if (o) opt = *o;
+    if (opt.world < 1 || opt.rank < 0 || opt.rank >= opt.world) { set_error("bad rank/world"); return FBA_ERR_ARG; }
+
+    Ctx* c = new Ctx();
+    c->prob = *p;
+    c->set = *s;
+    c->opt = opt;
+    c->n_pts = p->n_pts;
+    Layout& L = c->L;
+    compute_layout(p, s, L);
+    full_to_ref_map(s, L, c->full_to_ref);
+
+    FBA_HIP(hipSetDevice(opt.device));
+    c->device = opt.device;
+    if (opt.stream) {
+        c->stream = (hipStream_t)opt.stream;
+    } else {
+        FBA_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->own_stream = true;
+    }
+
+    // initial full-space parameters
+    c->xfull0.assign(L.u_full, 0.0);
+    for (int64_t i = 0; i < 6 * (int64_t)L.n_img; ++i) c->xfull0[i] = p->eop0[i];
+    for (int64_t i = 0; i < (int64_t)L.cw * L.n_cam; ++i) c->xfull0[6 * (int64_t)L.n_img + i] = p->iop0[i];
+    for (int64_t i = 0; i < 3 * (int64_t)L.n_tie; ++i) c->xfull0[L.u_c + i] = p->tie0[i];
+
+    // shard
+    std::vector<int32_t> ctl_owner;
+    partition(p, opt.world, c->tie_owner, ctl_owner);
+
+    // local tie points sorted by (camera, tie index); their observations in PHO order
+    std::vector<std::vector<int64_t>> tie_obs(L.n_tie);
+    std::vector<int32_t> tie_cam(L.n_tie, 0);
+    for (int64_t i = 0; i < p->n_pts; ++i)
+        if (p->tie[i] >= 0) {
+            tie_obs[p->tie[i]].push_back(i);
+            tie_cam[p->tie[i]] = p->cam[i];
+        }
+    std::vector<int32_t> lps;
+    for (int t = 0; t < L.n_tie; ++t)
+        if (c->tie_owner[t] == opt.rank && !tie_obs[t].empty()) lps.push_back(t);
+    std::stable_sort(lps.begin(), lps.end(), [&](int32_t a, int32_t b) { return tie_cam[a] < tie_cam[b]; });
+    c->n_lp = (int64_t)lps.size();
+
+    std::vector<double> xy;
+    std::vector<int32_t> img, cam, pt, lp_start, lp_cam, cam_lp(L.n_cam + 1, 0), cam_ctl(L.n_cam + 1, 0);
+    std::vector<double> ctl;
+    std::vector<int64_t>& pho = c->obs_pho;
+    lp_start.push_back(0);
+    for (int64_t lp = 0; lp < c->n_lp; ++lp) {
+        const int t = lps[lp];
+        for (int64_t i : tie_obs[t]) {
+            pho.push_back(i);
+            xy.push_back(p->xy[2 * i]);
+            xy.push_back(p->xy[2 * i + 1]);
+            img.push_back(p->img[i]);
+            cam.push_back(p->cam[i]);
+            pt.push_back((int32_t)lp);
+        }
+        lp_start.push_back((int32_t)pho.size());
+        lp_cam.push_back(tie_cam[t]);
+        cam_lp[tie_cam[t] + 1]++;
+    }
+    c->n_obs_tie = (int64_t)pho.size();
+    // control observations of this rank, sorted by camera (stable in PHO order)
+    std::vector<int64_t> ctls;
+    for (int64_t i = 0; i < p->n_pts; ++i)
+        if (p->tie[i] < 0 && ctl_owner[i] == opt.rank) ctls.push_back(i);
+    std::stable_sort(ctls.begin(), ctls.end(), [&](int64_t a, int64_t b) { return p->cam[a] < p->cam[b]; });
+    for (size_t q = 0; q < ctls.size(); ++q) {
+        const int64_t i = ctls[q];
+        pho.push_back(i);
+        xy.push_back(p->xy[2 * i]);
+        xy.push_back(p->xy[2 * i + 1]);
+        img.push_back(p->img[i]);
+        cam.push_back(p->cam[i]);
+        pt.push_back(-1 - (int32_t)q);
+        for (int m = 0; m < 3; ++m) ctl.push_back(p->xyz_fixed[3 * i + m]);
+        cam_ctl[p->cam[i] + 1]++;
+    }
+    for (int k = 0; k < L.n_cam; ++k) {
+        cam_lp[k + 1] += cam_lp[k];
+        cam_ctl[k + 1] += cam_ctl[k];
+    }
+    c->n_obs = (int64_t)pho.size();
+    if (c->n_obs >= (int64_t)1 << 31) { set_error("too many observations per rank"); destroy(c); return FBA_ERR_UNSUPPORTED; }
+    c->n_obs_pad = round_up(std::max<int64_t>(c->n_obs, 1), 64);
+    c->n_lp_pad = round_up(std::max<int64_t>(c->n_lp, 1), 64);
+
+    // per image CSR of local observations (PHO order within an image)
+    std::vector<int32_t> img_start(L.n_img + 1, 0), img_obs(c->n_obs);
+    {
+        std::vector<int64_t> ord(c->n_obs);
+        std::iota(ord.begin(), ord.end(), 0);
+        std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
+            return img[a] != img[b] ? img[a] < img[b] : pho[a] < pho[b];
+        });
+        for (int64_t q = 0; q < c->n_obs; ++q) {
+            img_obs[q] = (int32_t)ord[q];
+            img_start[img[ord[q]] + 1]++;
+        }
+        for (int e = 0; e < L.n_img; ++e) img_start[e + 1] += img_start[e];
+    }
+
+    // co-visible image pairs: for every local point, every pair of its observations in distinct images
+    std::vector<std::tuple<int32_t, int32_t, int32_t, int32_t>> terms;  // (e1, e2, i, j), e1 > e2
+    for (int64_t lp = 0; lp < c->n_lp; ++lp) {
+        const int a0 = lp_start[lp], a1 = lp_start[lp + 1];
+        for (int i = a0; i < a1; ++i)
+            for (int j = a0; j < a1; ++j) {
+                if (img[i] == img[j]) {
+                    if (i != j) {
+                        set_error("a tie point is measured twice in one image: not implemented in this build");
+                        destroy(c);
+                        return FBA_ERR_UNSUPPORTED;
+                    }
+                    continue;
+                }
+                if (img[i] > img[j]) terms.emplace_back(img[i], img[j], i, j);
+            }
+    }
+    std::sort(terms.begin(), terms.end());
+    std::vector<int32_t> pair_e, pair_start, pair_ij;
+    for (size_t q = 0; q < terms.size(); ++q) {
+        const auto& tq = terms[q];
+        if (q == 0 || std::get<0>(tq) != std::get<0>(terms[q - 1]) || std::get<1>(tq) != std::get<1>(terms[q - 1])) {
+            pair_e.push_back(std::get<0>(tq));
+            pair_e.push_back(std::get<1>(tq));
+            pair_start.push_back((int32_t)q);
+        }
+        pair_ij.push_back(std::get<2>(tq));
+        pair_ij.push_back(std::get<3>(tq));
+    }
+    pair_start.push_back((int32_t)terms.size());
+    c->n_pairs = (int64_t)pair_e.size() / 2;
+    c->n_pair_terms = (int64_t)terms.size();
+    terms.clear();
+    terms.shrink_to_fit();
+
+    // which full-space entries are estimated / owned / counted
+    std::vector<uint8_t> active(L.n_pad, 0), counted(L.u_full, 0);
+    c->full_owned.assign(L.u_full, 0);
+    for (int64_t i = 0; i < L.u_c; ++i) {
+        active[i] = c->full_to_ref[i] >= 0 ? 1 : 0;
+        counted[i] = (opt.rank == 0 && active[i]) ? 1 : 0;
+        c->full_owned[i] = opt.rank == 0 ? 1 : 0;
+    }
+    for (int t = 0; t < L.n_tie; ++t)
+        for (int m = 0; m < 3; ++m) {
+            const int64_t i = L.u_c + 3 * (int64_t)t + m;
+            counted[i] = c->tie_owner[t] == opt.rank ? 1 : 0;
+            c->full_owned[i] = counted[i];
+        }
+
+    // device allocations
+    std::vector<int32_t> lp_tie(lps.begin(), lps.end());
+    std::vector<double> caminfo(p->cam_info, p->cam_info + 5 * (size_t)L.n_cam);
+    if ((rc = upload(&c->d_xy, xy)) || (rc = upload(&c->d_img, img)) || (rc = upload(&c->d_cam, cam)) ||
+        (rc = upload(&c->d_pt, pt)) || (rc = upload(&c->d_ctl, ctl)) || (rc = upload(&c->d_lp_tie, lp_tie)) ||
+        (rc = upload(&c->d_lp_start, lp_start)) || (rc = upload(&c->d_lp_cam, lp_cam)) ||
+        (rc = upload(&c->d_img_start, img_start)) || (rc = upload(&c->d_img_obs, img_obs)) ||
+        (rc = upload(&c->d_cam_lp, cam_lp)) || (rc = upload(&c->d_cam_ctl, cam_ctl)) ||
+        (rc = upload(&c->d_pair_e, pair_e)) || (rc = upload(&c->d_pair_start, pair_start)) ||
+        (rc = upload(&c->d_pair_ij, pair_ij)) || (rc = upload(&c->d_xfull, c->xfull0)) ||
+        (rc = upload(&c->d_caminfo, caminfo)) || (rc = upload(&c->d_active, active)) ||
+        (rc = upload(&c->d_counted, counted)) || (rc = upload(&c->d_obs_pho, pho))) {
+        destroy(c);
+        return rc;
+    }
+    const int nj = 9 + L.cw;
+    c->ncomp = 2 * nj + 2;
+    c->cam_tab_stride = CAM_TAB_HDR + 2 * L.nk;
+    c->pt_comp = 12 + 6 * L.cw;
+    const int npk = L.cw * (L.cw + 1) / 2 + L.cw;
+    c->n_part = (int)std::max<int64_t>((L.u_full + 255) / 256, (c->n_obs + 255) / 256 * 3) + 8;
+    if ((rc = dalloc(&c->d_delta, L.u_full)) || (rc = dalloc(&c->d_img_tab, (size_t)L.n_img * IMG_TAB)) ||
+        (rc = dalloc(&c->d_cam_tab, (size_t)L.n_cam * c->cam_tab_stride)) ||
+        (rc = dalloc(&c->d_G, (size_t)std::max(L.n_img, 1) * 42)) ||
+        (rc = dalloc(&c->d_J, (size_t)c->ncomp * c->n_obs_pad)) || (rc = dalloc(&c->d_WT, (size_t)36 * c->n_obs_pad)) ||
+        (rc = dalloc(&c->d_pt_tab, (size_t)c->pt_comp * c->n_lp_pad)) ||
+        (rc = dalloc(&c->d_slab, (size_t)std::max(L.n_cam, 1) * NSLAB * npk)) ||
+        (rc = dalloc(&c->d_S, (size_t)(L.n_pad + NB) * L.ld)) || (rc = dalloc(&c->d_X, (size_t)L.n_pad)) ||
+        (rc = dalloc(&c->d_scal, 16)) || (rc = dalloc(&c->d_part, (size_t)c->n_part)) ||
+        (rc = dalloc(&c->d_res, (size_t)7 * std::max<int64_t>(c->n_obs, 1)))) {
+        destroy(c);
+        return rc;
+    }
+    FBA_HIP(hipMemset(c->d_delta, 0, sizeof(double) * L.u_full));
+    FBA_HIP(hipMemset(c->d_scal, 0, sizeof(double) * 16));
+    FBA_HIP(hipHostMalloc((void**)&c->h_pinned, sizeof(double) * 64));
+    for (auto& e : c->ev) FBA_HIP(hipEventCreate(&e));
+    if (opt.verbose)
+        fprintf(stderr, "[fba] rank %d/%d: n_obs %ld (tie %ld), points %ld, pairs %ld (%ld terms), u_c %ld, n_pad %ld\n",
+                opt.rank, opt.world, (long)c->n_obs, (long)c->n_obs_tie, (long)c->n_lp, (long)c->n_pairs,
+                (long)c->n_pair_terms, (long)L.u_c, (long)L.n_pad);
+    *out = c;
+    return FBA_OK;
+}
+
+static int set_xhat_ref(Ctx* c, const double* xhat) {
+    std::vector<double> xf = c->xfull0;
+    for (int64_t i = 0; i < c->L.u_full; ++i)
+        if (c->full_to_ref[i] >= 0) xf[i] = xhat[c->full_to_ref[i]];
+    FBA_HIP(hipMemcpyAsync(c->d_xfull, xf.data(), sizeof(double) * xf.size(), hipMemcpyHostToDevice, c->stream));
+    FBA_HIP(hipStreamSynchronize(c->stream));
+    c->have_lin = false;
+    c->have_delta = false;
+    return FBA_OK;
+}
+
+static inline void mark(Ctx* c, int i) {
+    if (c->timing) (void)hipEventRecord(c->ev[i], c->stream);
+}
+
+static int accumulate(Ctx* c) {
+    int rc;
+    mark(c, 0);
+    if ((rc = launch_params(*c)) || (rc = launch_linearize(*c))) return rc;
+    mark(c, 1);
+    if ((rc = launch_point(*c))) return rc;
+    mark(c, 2);
+    if ((rc = launch_accumulate(*c))) return rc;
+    mark(c, 3);
+    c->have_lin = true;
+    return FBA_OK;
+}
+
+static int solve_update(Ctx* c, double* dsum) {
+    int rc;
+    const Layout& L = c->L;
+    if (!c->have_lin) { set_error("fba_solve_update before fba_accumulate"); return FBA_ERR_ARG; }
+    if ((rc = launch_border(*c))) return rc;
+    mark(c, 4);
+    if ((rc = launch_cholesky(*c))) return rc;
+    mark(c, 5);
+    FBA_HIP(hipMemsetAsync(c->d_delta + L.u_c, 0, sizeof(double) * (L.u_full - L.u_c), c->stream));
+    if ((rc = launch_backward(*c))) return rc;
+    mark(c, 6);
+    if ((rc = launch_backsub_update(*c))) return rc;
+    mark(c, 7);
+    FBA_HIP(hipMemcpyAsync(c->h_pinned, c->d_scal, sizeof(double) * 4, hipMemcpyDeviceToHost, c->stream));
+    FBA_HIP(hipStreamSynchronize(c->stream));
+    if (c->timing) {
+        float ms;
+        for (int i = 0; i < 7; ++i) {
+            (void)hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]);
+            c->last_ms[i] = ms;
+        }
+        (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[7]);
+        c->last_ms[7] = ms;
+    }
+    c->have_delta = true;
+    c->iterations++;
+    const double info = c->h_pinned[1];
+    *dsum = c->h_pinned[2];
+    if (info != 0.0) {
+        char buf[160];
+        snprintf(buf, sizeof buf, "reduced normal matrix not positive definite (pivot %ld): singular / unconstrained network",
+                 (long)info);
+        set_error(buf);
+        return FBA_ERR_NOT_SPD;
+    }
+    if (!std::isfinite(*dsum)) { set_error("non-finite correction vector"); return FBA_ERR_NONFINITE; }
+    return FBA_OK;
+}
+
+}  // namespace fba
+
+using namespace fba;
+
+extern "C" {
+
+const char* fba_last_error(void) { return g_err.c_str(); }
+int fba_abi_version(void) { return FBA_ABI_VERSION; }
+
+int fba_count_unknowns(const fba_problem* p, const fba_settings* s, int64_t* u_out) {
+    if (!p || !s || !u_out) { set_error("NULL argument"); return FBA_ERR_ARG; }
+    Layout L;
+    fba_settings s2 = *s;
+    if (s2.num_radial < 1) s2.num_radial = 1;
+    compute_layout(p, &s2, L);
+    *u_out = (int64_t)(s->est_Xc + s->est_Yc + s->est_Zc + s->est_omega + s->est_phi + s->est_kappa) * p->n_img +
+             (int64_t)(s->est_c + s->est_xp + s->est_yp + s->est_radial * s->num_radial + s->est_decent * 2) * p->n_cam +
+             3 * (int64_t)p->n_tie;
+    return FBA_OK;
+}
+
+int fba_partition(const fba_problem* p, int32_t world, int32_t* tie_owner, int32_t* ctl_owner) {
+    if (!p || world < 1) { set_error("bad argument"); return FBA_ERR_ARG; }
+    std::vector<int32_t> t, q;
+    partition(p, world, t, q);
+    if (tie_owner) std::copy(t.begin(), t.end(), tie_owner);
+    if (ctl_owner) std::copy(q.begin(), q.end(), ctl_owner);
+    return FBA_OK;
+}
+
+int fba_create(const fba_problem* p, const fba_settings* s, const fba_options* o, fba_ctx** out) {
+    if (!out) { set_error("out is NULL"); return FBA_ERR_ARG; }
+    *out = nullptr;
+    Ctx* c = nullptr;
+    int rc = create(p, s, o, &c);
+    if (rc) return rc;
+    *out = reinterpret_cast<fba_ctx*>(c);
+    return FBA_OK;
+}
+
+void fba_destroy(fba_ctx* ctx) { destroy(reinterpret_cast<Ctx*>(ctx)); }
+
+int fba_buildxhat(fba_ctx* ctx, double* xhat, int64_t* u_out) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }
+    if (u_out) *u_out = c->L.u_ref;
+    if (xhat)
+        for (int64_t i = 0; i < c->L.u_full; ++i)
+            if (c->full_to_ref[i] >= 0) xhat[c->full_to_ref[i]] = c->xfull0[i];
+    return FBA_OK;
+}
+
+int fba_set_xhat(fba_ctx* ctx, const double* xhat) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c || !xhat) { set_error("NULL argument"); return FBA_ERR_ARG; }
+    return set_xhat_ref(c, xhat);
+}
+
+int fba_get_xhat(fba_ctx* ctx, double* xhat, int32_t owned_only) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c || !xhat) { set_error("NULL argument"); return FBA_ERR_ARG; }
+    std::vector<double> xf(c->L.u_full);
+    FBA_HIP(hipMemcpyAsync(xf.data(), c->d_xfull, sizeof(double) * xf.size(), hipMemcpyDeviceToHost, c->stream));
+    FBA_HIP(hipStreamSynchronize(c->stream));
+    for (int64_t i = 0; i < c->L.u_full; ++i)
+        if (c->full_to_ref[i] >= 0) xhat[c->full_to_ref[i]] = (owned_only && !c->full_owned[i]) ? 0.0 : xf[i];
+    return FBA_OK;
+}
+
+int fba_build_awg(fba_ctx* ctx, const double* xhat, double* A, double* w, double* G, double* dist_scaling) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }
+    int rc;
+    if (xhat && (rc = set_xhat_ref(c, xhat))) return rc;
+    if ((rc = launch_params(*c)) || (rc = launch_linearize(*c))) return rc;
+    const Layout& L = c->L;
+    const int64_t n = 2 * c->n_pts, u = L.u_ref;
+    double *dA = nullptr, *dW = nullptr;
+    int64_t* dmap = nullptr;
+    if ((rc = dalloc(&dA, (size_t)n * u)) || (rc = dalloc(&dW, (size_t)n)) || (rc = upload(&dmap, c->full_to_ref)))
+        return rc;
+    FBA_HIP(hipMemsetAsync(dA, 0, sizeof(double) * n * u, c->stream));
+    FBA_HIP(hipMemsetAsync(dW, 0, sizeof(double) * n, c->stream));
+    if ((rc = launch_dense_awg(*c, dA, dW, dmap, n, u))) return rc;
+    if (A) FBA_HIP(hipMemcpyAsync(A, dA, sizeof(double) * n * u, hipMemcpyDeviceToHost, c->stream));
+    if (w) FBA_HIP(hipMemcpyAsync(w, dW, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    std::vector<double> g((size_t)std::max(L.n_img, 1) * 42), ct((size_t)L.n_cam * c->cam_tab_stride);
+    FBA_HIP(hipMemcpyAsync(g.data(), c->d_G, sizeof(double) * g.size(), hipMemcpyDeviceToHost, c->stream));
+    FBA_HIP(hipMemcpyAsync(ct.data(), c->d_cam_tab, sizeof(double) * ct.size(), hipMemcpyDeviceToHost, c->stream));
+    FBA_HIP(hipStreamSynchronize(c->stream));
+    (void)hipFree(dA);
+    (void)hipFree(dW);
+    (void)hipFree(dmap);
+    if (G && c->set.inner_constraints) {
+        std::fill(G, G + u * 7, 0.0);
+        for (int e = 0; e < L.n_img; ++e)
+            for (int a = 0; a < 6; ++a) {
+                const int64_t r = c->full_to_ref[6 * (int64_t)e + a];
+                for (int m = 0; m < 7; ++m) G[r + m * u] = g[(size_t)e * 42 + a * 7 + m];
+            }
+    }
+    if (dist_scaling) {
+        const int nc = L.n_cam, ncol = 2 + L.nk;
+        std::fill(dist_scaling, dist_scaling + (size_t)nc * ncol, 0.0);
+        for (int k = 0; k < nc; ++k) {
+            // the reference stores 1-based xhat indices (BuildAwG.m:138, :150)
+            const int64_t base = 6 * (int64_t)L.n_img + (int64_t)k * L.cw;
+            if (c->set.est_radial) dist_scaling[k + 0 * nc] = (double)(c->full_to_ref[base + 3] + 1);
+            if (c->set.est_decent) dist_scaling[k + 1 * nc] = (double)(c->full_to_ref[base + 3 + L.nk] + 1);
+            for (int j = 0; j < L.nk; ++j)
+                dist_scaling[k + (2 + j) * nc] = ct[(size_t)k * c->cam_tab_stride + CAM_TAB_HDR + L.nk + j];
+        }
+    }
+    c->have_lin = false;
+    return FBA_OK;
+}
+
+int fba_accumulate(fba_ctx* ctx) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }
+    return accumulate(c);
+}
+
+int fba_reduce_buffer(fba_ctx* ctx, void** dev_ptr, int64_t* n_doubles) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c || !dev_ptr || !n_doubles) { set_error("NULL argument"); return FBA_ERR_ARG; }
+    *dev_ptr = c->d_S;
+    *n_doubles = (c->L.n_pad + 1) * c->L.ld;  // lower normal matrix + RHS row 0
+    return FBA_OK;
+}
+
+int fba_solve_update(fba_ctx* ctx, double* deltasum_part) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }
+    double d = 0.0;
+    int rc = solve_update(c, &d);
+    if (deltasum_part) *deltasum_part = d;
+    return rc;
+}
+
+int fba_step(fba_ctx* ctx, double* deltasum) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }
+    if (c->opt.world != 1) { set_error("fba_step is single-GPU; use fba_accumulate/fba_solve_update"); return FBA_ERR_ARG; }
+    int rc = accumulate(c);
+    if (rc) return rc;
+    double d = 0.0;
+    rc = solve_update(c, &d);
+    if (deltasum) *deltasum = d;
+    return rc;
+}
+
+int fba_adjust(fba_ctx* ctx, int32_t* iterations, double* deltasum_hist) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }
+    double deltasum = 100.0;  // main.m:407
+    int count = 0;
+    while (deltasum > c->set.threshold) {  // main.m:412
+        ++count;
+        int rc = fba_step(ctx, &deltasum);
+        if (deltasum_hist) deltasum_hist[count - 1] = deltasum;
+        if (iterations) *iterations = count;
+        if (rc) return rc;
+        if (count >= c->set.iteration_cap) break;  // main.m:490-493
+    }
+    if (iterations) *iterations = count;
+    return FBA_OK;
+}
+
+int fba_residuals(fba_ctx* ctx, double* v, double* rsd, double* stats) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }
+    if (!c->have_lin || !c->have_delta) { set_error("fba_residuals needs at least one iteration"); return FBA_ERR_ARG; }
+    int rc = launch_residuals(*c);
+    if (rc) return rc;
+    const int64_t n = c->n_obs;
+    const int nblk = (int)((n + 255) / 256);
+    std::vector<double> res(7 * (size_t)n), part(3 * (size_t)nblk);
+    if (n > 0) {
+        FBA_HIP(hipMemcpyAsync(res.data(), c->d_res, sizeof(double) * res.size(), hipMemcpyDeviceToHost, c->stream));
+        FBA_HIP(hipMemcpyAsync(part.data(), c->d_part, sizeof(double) * part.size(), hipMemcpyDeviceToHost, c->stream));
+    }
+    FBA_HIP(hipStreamSynchronize(c->stream));
+    if (v) std::fill(v, v + 2 * c->n_pts, 0.0);
+    if (rsd) std::fill(rsd, rsd + 5 * c->n_pts, 0.0);
+    for (int64_t o = 0; o < n; ++o) {
+        const int64_t i = c->obs_pho[o];
+        if (v) { v[2 * i] = res[2 * o]; v[2 * i + 1] = res[2 * o + 1]; }
+        if (rsd)
+            for (int m = 0; m < 5; ++m) rsd[5 * i + m] = res[2 * n + 5 * o + m];
+    }
+    double sx = 0, sy = 0, sp = 0;
+    for (int b = 0; b < nblk; ++b) { sx += part[3 * b]; sy += part[3 * b + 1]; sp += part[3 * b + 2]; }
+    if (stats) {
+        const double nu = (double)(2 * c->n_pts - c->L.u_ref);
+        if (c->opt.world == 1) {
+            const double rx = std::sqrt(sx / (double)c->n_pts), ry = std::sqrt(sy / (double)c->n_pts);
+            stats[0] = rx; stats[1] = ry; stats[2] = std::sqrt(rx * rx + ry * ry);
+            stats[3] = sp / nu;  // main.m:601: v'Pv / (n - u)
+        } else {
+            stats[0] = sx; stats[1] = sy; stats[2] = 0; stats[3] = 0;
+        }
+        stats[4] = sp;
+        stats[5] = nu;
+    }
+    return FBA_OK;
+}
+
+int fba_finish_stats(const fba_problem* p, const fba_settings* s, const double* sums, double vtpv, double* stats) {
+    if (!p || !s || !sums || !stats) { set_error("NULL argument"); return FBA_ERR_ARG; }
+    int64_t u = 0;
+    fba_count_unknowns(p, s, &u);
+    const double n = (double)p->n_pts;
+    const double rx = std::sqrt(sums[0] / n), ry = std::sqrt(sums[1] / n);
+    const double nu = (double)(2 * p->n_pts - u);
+    stats[0] = rx; stats[1] = ry; stats[2] = std::sqrt(rx * rx + ry * ry);
+    stats[3] = vtpv / nu; stats[4] = vtpv; stats[5] = nu;
+    return FBA_OK;
+}
+
+int fba_last_timings(fba_ctx* ctx, double* ms) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c || !ms) { set_error("NULL argument"); return FBA_ERR_ARG; }
+    for (int i = 0; i < 8; ++i) ms[i] = c->last_ms[i];
+    return FBA_OK;
+}
+
+int fba_set_timing(fba_ctx* ctx, int32_t enabled) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }
+    c->timing = enabled != 0;
+    return FBA_OK;
+}
+
+}  // extern "C"

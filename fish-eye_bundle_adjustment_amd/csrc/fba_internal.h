@@ -1,0 +1,137 @@
+// fba_internal.h -- device layout and context of libfba.so (not part of the ABI).
+//
+// Unknowns live on the device in a FULL parameter space: every image carries all 6 EOPs
+// (Xc Yc Zc omega phi kappa) and every camera all CW = 5 + nK IOPs (xp yp c K1..KnK P1 P2),
+// followed by 3 coordinates per tie point.  Parameters the .cfg does not estimate get zero
+// Jacobian columns, a unit diagonal in the reduced system and a zero correction, so the kernels
+// need no per-flag variants; the reference's compressed xhat (Buildxhat.m:6-134) is produced only
+// at the ABI boundary through the index maps below.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/fba.h"
+
+namespace fba {
+
+constexpr int NB = 64;        // Cholesky block size (rows/cols of one panel block)
+constexpr int NSLAB = 64;     // slabs per camera in the two-stage camera-block reduction
+
+// per-image device table (k_params): eop[6], M[9], dM/domega[9], dM/dphi[9], dM/dkappa[9], pad
+constexpr int IMG_TAB = 48;
+// per-camera device table: xp yp c ydir P1 P2 rmax2 pad, K[nK], scale[nK] (rmax^(2j))
+constexpr int CAM_TAB_HDR = 8;
+
+struct Layout {
+    int n_img = 0, n_cam = 0, n_tie = 0, nk = 1, cw = 6;
+    int64_t u_c = 0;      // 6*n_img + cw*n_cam (camera-side full unknowns)
+    int64_t u_full = 0;   // u_c + 3*n_tie
+    int64_t n_pad = 0;    // u_c rounded up to NB
+    int64_t ld = 0;       // leading dimension of the normal matrix (row-major)
+    int nrhs = 1;         // 1 (+7 with inner constraints)
+    int64_t u_ref = 0;    // the reference's u
+    int u_img = 0, u_cam = 0;
+};
+
+struct Ctx {
+    fba_problem prob{};   // shallow copy (pointers valid only during fba_create)
+    fba_settings set{};
+    fba_options opt{};
+    Layout L;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int device = 0;
+
+    // host copies of the problem (kept for residual output, xhat mapping)
+    int64_t n_pts = 0;
+    std::vector<int64_t> full_to_ref;   // [u_full] -> reference xhat index or -1
+    std::vector<double> xfull0;         // initial full-space parameters
+    std::vector<int32_t> tie_owner;     // [n_tie]
+    std::vector<uint8_t> full_owned;    // [u_full] entries this rank owns (for owned_only output)
+
+    // local (this rank) observation order
+    int64_t n_obs = 0;       // local image points
+    int64_t n_obs_tie = 0;   // of which tie observations (first), then control
+    int64_t n_obs_pad = 0;
+    int64_t n_lp = 0;        // local tie points
+    std::vector<int64_t> obs_pho;  // local obs -> PHO row
+
+    // ---- device buffers ----
+    double* d_xy = nullptr;      // [2*n_obs] x,y interleaved
+    int32_t* d_img = nullptr;    // [n_obs]
+    int32_t* d_cam = nullptr;    // [n_obs]
+    int32_t* d_pt = nullptr;     // [n_obs] local point (>=0) or -1-ctl
+    double* d_ctl = nullptr;     // [3*n_ctl] fixed XYZ of control observations
+    int32_t* d_lp_tie = nullptr; // [n_lp] global tie index of local point
+    int32_t* d_lp_start = nullptr;   // [n_lp+1] obs range of each local point
+    int32_t* d_lp_cam = nullptr;     // [n_lp] camera of each local point
+    int32_t* d_img_start = nullptr;  // [n_img+1] CSR of local obs per image
+    int32_t* d_img_obs = nullptr;
+    int32_t* d_cam_lp = nullptr;     // [n_cam+1] local point range per camera (points sorted by camera)
+    int32_t* d_cam_ctl = nullptr;    // [n_cam+1] control obs range per camera (within control section)
+    int64_t n_pairs = 0, n_pair_terms = 0;
+    int32_t* d_pair_e = nullptr;     // [2*n_pairs] (e1,e2) with e1 > e2
+    int32_t* d_pair_start = nullptr; // [n_pairs+1]
+    int32_t* d_pair_ij = nullptr;    // [2*n_pair_terms] (obs in e1, obs in e2)
+
+    double* d_xfull = nullptr;   // [u_full]
+    double* d_delta = nullptr;   // [u_full] last de-scaled correction
+    double* d_img_tab = nullptr; // [n_img*IMG_TAB]
+    double* d_cam_tab = nullptr; // [n_cam*cam_tab_stride]
+    int cam_tab_stride = 0;
+    double* d_G = nullptr;       // [n_img*42] inner-constraint blocks (6x7 per image, row-major)
+    double* d_J = nullptr;       // [ncomp*n_obs_pad] per-obs Jacobian rows + misclosure
+    int ncomp = 0;
+    double* d_WT = nullptr;      // [36*n_obs_pad] per-obs W (18) and T = W V^-1 (18)
+    double* d_pt_tab = nullptr;  // [pt_comp*n_lp_pad] Vinv(6) vb(3) b(3) Wc(3cw) Tc(3cw)
+    int pt_comp = 0;
+    int64_t n_lp_pad = 0;
+    double* d_slab = nullptr;    // camera reduction slabs
+    double* d_S = nullptr;       // [(n_pad+NB)*ld] normal matrix (lower) + RHS rows
+    double* d_X = nullptr;       // [nrhs*n_pad] solution of the bordered solve (row per rhs)
+    double* d_scal = nullptr;    // scalars: [0] alpha^2, [1] info, [2..] partial sums
+    double* d_part = nullptr;    // block partial sums
+    int n_part = 0;
+    double* d_res = nullptr;     // [7*n_obs] v (2) + rsd (5)
+    double* d_caminfo = nullptr; // [5*n_cam]
+    uint8_t* d_active = nullptr; // [n_pad] 1 = estimated camera-side parameter
+    uint8_t* d_counted = nullptr;// [u_full] 1 = counted in this rank's sumabs share
+    int64_t* d_obs_pho = nullptr;// [n_obs] PHO row of each local observation
+    double* h_pinned = nullptr;  // pinned host scratch
+
+    // state
+    bool have_lin = false;       // d_J holds a linearisation
+    bool have_delta = false;
+    int iterations = 0;
+    bool timing = false;
+    hipEvent_t ev[9] = {};
+    double last_ms[8] = {0};
+};
+
+// error helpers
+void set_error(const std::string& msg);
+#define FBA_HIP(call)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (call);                                                        \
+        if (e_ != hipSuccess) {                                                        \
+            fba::set_error(std::string("HIP error ") + hipGetErrorString(e_) + " at " + \
+                           __FILE__ + ":" + std::to_string(__LINE__) + " (" #call ")"); \
+            return FBA_ERR_HIP;                                                        \
+        }                                                                              \
+    } while (0)
+
+// kernel launchers (fba_kernels.hip / fba_chol.hip)
+int launch_params(Ctx& c);
+int launch_linearize(Ctx& c);
+int launch_point(Ctx& c);
+int launch_accumulate(Ctx& c);   // zero S, image, pair, camera blocks, unit diagonal for unused
+int launch_border(Ctx& c);       // alpha, G G^T border, RHS rows
+int launch_cholesky(Ctx& c);     // factor + forward solve of RHS rows
+int launch_backward(Ctx& c);     // border combine + backward solve -> delta_c
+int launch_backsub_update(Ctx& c);
+int launch_residuals(Ctx& c);    // v per obs, partial sums
+int launch_dense_awg(Ctx& c, double* dA, double* dG, const int64_t* d_map, int64_t n_rows, int64_t u_ref);
+
+}  // namespace fba

@@ -1,0 +1,174 @@
+/*
+ * fba.h -- C-ABI of libfba.so, the MI355X-native Gauss-Newton bundle-adjustment inner loop.
+ *
+ * Drop-in boundary for the reference's MATLAB hot path (wynandtredoux/Fish-Eye_Bundle_Adjustment):
+ *
+ *   fba_buildxhat     replaces  [error, xhat, xhatnames] = Buildxhat(data, EXT, INT, TIE, CNT)
+ *                               functions/Buildxhat.m:2 (called at main.m:388)
+ *   fba_build_awg     replaces  [error, A, misclosure, G, dist_scaling] = BuildAwG(data, xhat)
+ *                               functions/BuildAwG.m:14 (called at main.m:416); dense debug form
+ *   fba_accumulate +
+ *   fba_solve_update  replace   one pass of the inline loop body main.m:413-488
+ *                               (BuildAwG -> u = A'Pw, N = A'PA -> bordered solve -> de-scale ->
+ *                               xhat += delta -> deltasum = sumabs(delta)), split at the point where a
+ *                               multi-GPU caller all-reduces the normal equations
+ *   fba_step          = fba_accumulate + fba_solve_update (single GPU)
+ *   fba_adjust        replaces  the whole loop main.m:407-494 (while deltasum > threshold, cap)
+ *   fba_residuals     replaces  v = A*delta + w (main.m:569), RSD = BuildRSD(v, data, xhat)
+ *                               (functions/BuildRSD.m:1, main.m:571), RMSx/RMSy/RMS (main.m:594-598),
+ *                               sigma02 = v'Pv/(n-u) (main.m:601)
+ *
+ * Conventions (mirroring the reference's): every function returns 0 on success and a nonzero
+ * FBA_ERR_* code where the reference would set error = 1 (BuildAwG.m:16, Buildxhat.m:3); the message
+ * is available from fba_last_error().  No exceptions cross the ABI.  All arrays are caller-owned
+ * host buffers; indices are 0-based (the reference's are 1-based); reals are IEEE fp64.
+ * A context owns its device memory and is bound to one GPU; it is not re-entrant.
+ */
+#ifndef FBA_H_
+#define FBA_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FBA_ABI_VERSION 1
+
+/* projection models, BuildAwG.m:184-213 (the reference's `typeint`) */
+enum {
+    FBA_TYPE_FISHEYE = 0,       /* equidistant:  -c*U/R*atan(R/W)           */
+    FBA_TYPE_PINHOLE = 1,       /* collinearity: -c*U/W                     */
+    FBA_TYPE_EQUISOLID = 2,     /* -2c*U/R*sin(atan(R/W)/2)                 */
+    FBA_TYPE_ORTHOGRAPHIC = 3,  /* -c*U/R*sin(atan(R/W))                    */
+    FBA_TYPE_STEREOGRAPHIC = 4  /* -2c*U/R*tan(atan(R/W)/2)                 */
+};
+
+/* error codes */
+enum {
+    FBA_OK = 0,
+    FBA_ERR_ARG = 1,         /* invalid argument / inconsistent problem                  */
+    FBA_ERR_TYPE = 2,        /* invalid Type (BuildAwG.m:209-213)                        */
+    FBA_ERR_HIP = 3,         /* HIP runtime failure                                      */
+    FBA_ERR_NOT_SPD = 4,     /* reduced normal matrix not positive definite              */
+    FBA_ERR_UNSUPPORTED = 5, /* input outside what this build implements (message says) */
+    FBA_ERR_NONFINITE = 6    /* non-finite correction (divergence guard)                 */
+};
+
+#define FBA_NK_MAX 8 /* maximum Num_Radial_Distortions */
+
+/* The .cfg flags that parameterise the hot path (main.m:150-171, findSetting.m). */
+typedef struct fba_settings {
+    int32_t est_Xc, est_Yc, est_Zc, est_omega, est_phi, est_kappa; /* Estimate_Xc..Estimate_Kappa */
+    int32_t est_xp, est_yp, est_c;                                  /* Estimate_xp/_yp/_c          */
+    int32_t est_radial;                                             /* Estimate_Radial_Distortions */
+    int32_t est_decent;                                             /* Estimate_Decentering_...    */
+    int32_t num_radial;        /* Num_Radial_Distortions (clamped >= 1, BuildAwG.m:18-20)   */
+    int32_t type;              /* FBA_TYPE_*                                                */
+    int32_t inner_constraints; /* Inner_Constraints                                         */
+    int32_t iteration_cap;     /* Iteration_Cap                                             */
+    int32_t reserved;
+    double threshold;          /* Threshold_Value                                           */
+    double meas_std_x;         /* Meas_std                                                  */
+    double meas_std_y;         /* Meas_std_y (= Meas_std when absent, main.m:397-402)       */
+} fba_settings;
+
+/*
+ * Packed problem (structure-of-arrays).  This is the reference's `data` struct (main.m:280-383)
+ * after its joins: one entry per PHO row, in PHO order.
+ */
+typedef struct fba_problem {
+    int64_t n_pts;            /* image points = PHO rows (n = 2*n_pts observations)         */
+    int32_t n_img;            /* numImg: images = EXT rows 0..n_img-1 (Buildxhat.m:22)      */
+    int32_t n_cam;            /* numCam: cameras = INT pairs 0..n_cam-1 (Buildxhat.m:65)    */
+    int32_t n_tie;            /* numtie: estimated object points (TIE order)                */
+    int32_t reserved;
+    const double* xy;         /* [2*n_pts]  x0 y0 x1 y1 ... (pixels)                        */
+    const int32_t* img;       /* [n_pts]    ext_index (EXT row)                              */
+    const int32_t* cam;       /* [n_pts]    cam_num (INT pair), must equal EXT's camera     */
+    const int32_t* tie;       /* [n_pts]    tieIndex, or -1 for a fixed (control) point      */
+    const double* xyz_fixed;  /* [3*n_pts]  CNT coordinates (used where tie < 0)            */
+    const double* eop0;       /* [6*n_img]  EXT Xc Yc Zc omega phi kappa (radians)          */
+    const double* iop0;       /* [n_cam*(5+num_radial)] INT xp yp c K1..Knk P1 P2           */
+    const double* cam_info;   /* [5*n_cam]  y_dir xmin ymin xmax ymax                        */
+    const double* tie0;       /* [3*n_tie]  CNT coordinates of the TIE list                  */
+} fba_problem;
+
+typedef struct fba_options {
+    int32_t device;      /* HIP device ordinal                                              */
+    int32_t rank;        /* this process's rank (observation shard), 0 for single GPU      */
+    int32_t world;       /* number of ranks, 1 for single GPU                               */
+    int32_t verbose;
+    void* stream;        /* hipStream_t to run on, or NULL for a context-owned stream       */
+} fba_options;
+
+typedef struct fba_ctx fba_ctx;
+
+/* Thread-local message of the last failure. */
+const char* fba_last_error(void);
+int fba_abi_version(void);
+
+/* Number of unknowns u of the reference's xhat (Buildxhat.m:6-15); host only. */
+int fba_count_unknowns(const fba_problem* p, const fba_settings* s, int64_t* u_out);
+
+/* Deterministic observation shard: owner rank of every tie point (contiguous ranges balanced by
+ * observation count) and of every control observation; host only, no GPU needed. */
+int fba_partition(const fba_problem* p, int32_t world, int32_t* tie_owner /*[n_tie]*/,
+                  int32_t* ctl_owner /*[n_pts], -1 for tie observations*/);
+
+int fba_create(const fba_problem* p, const fba_settings* s, const fba_options* o, fba_ctx** out);
+void fba_destroy(fba_ctx* ctx);
+
+/* Buildxhat.m: initial xhat in the reference's layout.  xhat may be NULL to query u only. */
+int fba_buildxhat(fba_ctx* ctx, double* xhat /*[u]*/, int64_t* u_out);
+
+/* Set / get the device-resident xhat (reference layout).  With owned_only != 0 the entries this
+ * rank does not own are returned as 0 (tie points of other ranks; camera entries on rank > 0), so
+ * that a sum over ranks reassembles the full vector. */
+int fba_set_xhat(fba_ctx* ctx, const double* xhat);
+int fba_get_xhat(fba_ctx* ctx, double* xhat, int32_t owned_only);
+
+/* BuildAwG.m (dense debug/parity form): A is n x u column-major (n = 2*n_pts, PHO row order),
+ * w is n, G is u x 7 column-major (only when inner constraints are on; may be NULL),
+ * dist_scaling is n_cam x (2+num_radial) column-major with 0-based xhat indices in columns 0-1.
+ * Any output pointer may be NULL. */
+int fba_build_awg(fba_ctx* ctx, const double* xhat, double* A, double* w, double* G,
+                  double* dist_scaling);
+
+/* One Gauss-Newton iteration, split for multi-GPU callers:
+ *   fba_accumulate      linearise this rank's observations at the device xhat and accumulate the
+ *                       (point-reduced) normal equations into the reduce buffer;
+ *   fba_reduce_buffer   device pointer + length (doubles) of that buffer: ranks sum it elementwise
+ *                       (e.g. an RCCL all-reduce) between the two calls;
+ *   fba_solve_update    bordered solve, point back-substitution, de-scaling, xhat update.
+ *                       *deltasum_part receives this rank's share of sumabs(delta) (sum over ranks
+ *                       = the reference's deltasum).
+ * fba_step does both halves on one GPU and returns the full deltasum. */
+int fba_accumulate(fba_ctx* ctx);
+int fba_reduce_buffer(fba_ctx* ctx, void** dev_ptr, int64_t* n_doubles);
+int fba_solve_update(fba_ctx* ctx, double* deltasum_part);
+int fba_step(fba_ctx* ctx, double* deltasum);
+
+/* main.m:407-494: iterate while deltasum > threshold, at most iteration_cap times.
+ * deltasum_hist (may be NULL) receives one entry per iteration (capacity iteration_cap). */
+int fba_adjust(fba_ctx* ctx, int32_t* iterations, double* deltasum_hist);
+
+/* main.m:567-602 + BuildRSD.m: from the last iteration's linearisation and de-scaled delta.
+ * v [2*n_pts] (PHO order), rsd [5*n_pts] row-major per point: r, vx, vy, vr, vt,
+ * stats [6]: RMSx, RMSy, RMS, sigma02, vTPv, n-u.  Pointers may be NULL.  With world > 1 each rank
+ * fills only its observations (others 0) and stats hold this rank's partial sums
+ * (sum vx^2, sum vy^2, 0, 0, vTPv, n-u); fba_finish_stats turns reduced sums into RMS / sigma02. */
+int fba_residuals(fba_ctx* ctx, double* v, double* rsd, double* stats);
+int fba_finish_stats(const fba_problem* p, const fba_settings* s, const double* sums /*[2]: sum vx^2, sum vy^2*/,
+                     double vtpv, double* stats /*[6]*/);
+
+/* Per-phase device timings of the last fba_step / fba_accumulate+fba_solve_update, in ms:
+ * [0] params+linearize, [1] point-side, [2] image/pair/camera accumulation, [3] border,
+ * [4] Cholesky+forward, [5] backward+border solve, [6] back-substitution+update, [7] total. */
+int fba_last_timings(fba_ctx* ctx, double* ms /*[8]*/);
+int fba_set_timing(fba_ctx* ctx, int32_t enabled);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FBA_H_ */

@@ -1,0 +1,727 @@
+"""CPU oracle: a NumPy restatement of the reference's Gauss-Newton bundle adjustment.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in the product (``fish-eye_bundle_adjustment_amd/``) may
+import, call or link this module; only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` use it, and only as the checker / reported baseline.
+
+What it restates (reference = wynandtredoux/Fish-Eye_Bundle_Adjustment, MATLAB, read as text):
+
+* ingest: ``functions/ReadFiles.m:49`` (whitespace/tab tokens, ``#`` comments),
+  ``functions/findSetting.m:7-55`` (quoted -> string, else str2double, NaN / 0-1 checks),
+  ``main.m:112-177`` (mandatory keys and defaults), ``main.m:196-264`` (deg->rad, missing
+  distortions -> 0, Estimate_AllGCP -> sorted unique PHO ids), ``main.m:277-384`` (per image point
+  joins into EXT / INT / CNT / TIE, numImg / numCam / n).
+* ``functions/Buildxhat.m:2-135``: unknown layout.
+* ``functions/BuildAwG.m:14-528``: forward model (5 projection types), Jacobian A (EOP, IOP,
+  scaled distortion, tie columns), misclosure w, inner-constraint G, dist_scaling.  The
+  reference's Jacobian is machine-generated symbolic text; this restatement uses the chain rule
+  of the same forward model.  ``tests/golden/jac_golden.json`` (numbers produced by evaluating the
+  reference's own expression text in 40-digit mpmath, ``tests/golden/make_jac_golden.py``) pins it.
+* ``main.m:396-494``: weights, normal equations, bordered explicit inverse, distortion de-scaling,
+  update, ``functions/sumabs.m`` convergence test, iteration cap.
+* ``main.m:567-602`` + ``functions/BuildRSD.m:1-43``: v = A*delta + w (last linearisation, the
+  de-scaled delta), RSD rows, RMSx / RMSy / RMS, sigma0^2 = v'Pv/(n-u).
+
+Indices are 0-based here; the reference's are 1-based.
+"""
+from __future__ import annotations
+
+import math
+import os
+import re
+from dataclasses import dataclass, field
+
+import numpy as np
+
+TYPES = ("fisheye", "pinhole", "equisolid", "orthographic", "stereographic")
+
+
+class OracleError(RuntimeError):
+    pass
+
+
+# ----------------------------------------------------------------------------------------------
+# ingest (ReadFiles.m:49, findSetting.m, main.m:60-384)
+# ----------------------------------------------------------------------------------------------
+def read_table(path):
+    """ReadFiles.m:49 -- readmatrix(..., Delimiter {' ','\\t'} joined, leading ignored, '#')."""
+    rows = []
+    with open(path, "r") as fh:
+        for line in fh:
+            line = line.split("#", 1)[0]
+            toks = line.split()
+            if toks:
+                rows.append(toks)
+    return rows
+
+
+def find_file(folder, ext):
+    """ReadFiles.m:9-47: exactly one *.ext file expected in the folder."""
+    hits = sorted(f for f in os.listdir(folder) if f.endswith(ext))
+    if len(hits) != 1:
+        raise OracleError(f"expected exactly one {ext} file in {folder}, found {len(hits)}")
+    return os.path.join(folder, hits[0])
+
+
+def _str2double(s):
+    try:
+        return float(s)
+    except ValueError:
+        return float("nan")
+
+
+def find_setting(cfg, key, check01=False):
+    """findSetting.m:7-55.  Returns (value, ok)."""
+    for row in cfg:
+        if row[0] == key:
+            sval = row[1] if len(row) > 1 else ""
+            if len(sval) >= 1 and sval[0] == "'" and sval[-1] == "'":
+                value = sval[1:-1]
+            else:
+                value = _str2double(sval)
+            if isinstance(value, float) and math.isnan(value):
+                return value, False
+            if check01 and value not in (0.0, 1.0):
+                return value, False
+            return value, True
+    return -1, False
+
+
+@dataclass
+class Data:
+    settings: dict
+    # per image point (PHO row order), 0-based indices
+    x: np.ndarray
+    y: np.ndarray
+    target: list
+    image: list
+    ext_index: np.ndarray
+    cam_num: np.ndarray
+    tie_index: np.ndarray  # -1 if not a tie point
+    eop_fixed: np.ndarray  # (n_pts, 6) Xc Yc Zc w p k (radians)
+    iop_fixed: np.ndarray  # (n_pts, 3 + nK + 2) xp yp c K.. P1 P2
+    bounds: np.ndarray  # (n_pts, 5) y_dir xmin ymin xmax ymax
+    xyz_fixed: np.ndarray  # (n_pts, 3) from CNT
+    numImg: int
+    numCam: int
+    n: int
+    numGCP: int
+    numtie: int
+    EXT: list = field(default_factory=list)  # [id, cam, Xc, Yc, Zc, w, p, k]
+    INT: list = field(default_factory=list)  # per camera: (id, ydir, xmin, ymin, xmax, ymax, [xp yp c K.. P..])
+    TIE: list = field(default_factory=list)
+    CNT: list = field(default_factory=list)
+
+
+def load_folder(folder):
+    """main.m:60-384 restated (non-batch mode with the .cfg taken from the folder)."""
+    cfg = read_table(find_file(folder, ".cfg"))
+    pho = read_table(find_file(folder, ".pho"))
+    ext = read_table(find_file(folder, ".ext"))
+    cnt = read_table(find_file(folder, ".cnt"))
+    intr = read_table(find_file(folder, ".int"))
+
+    s = {}
+    v, ok = find_setting(cfg, "Output_Filename")  # main.m:116-120
+    s["Output_Filename"] = v if ok else os.path.basename(os.path.abspath(folder)) + ".out"
+    v, ok = find_setting(cfg, "Meas_std")  # main.m:123-130
+    if ok:
+        s["Meas_std"] = v
+        vy, oky = find_setting(cfg, "Meas_std_y")
+        s["Meas_std_y"] = vy if oky else v
+    else:  # the reference then fails in rmfield (main.m:399); sigma = 1 is the documented intent
+        s["Meas_std"] = 1.0
+        s["Meas_std_y"] = 1.0
+    v, ok = find_setting(cfg, "Type")  # main.m:133-137
+    s["type"] = v if ok else "fisheye"
+    v, ok = find_setting(cfg, "Check_Points", True)
+    s["Check_Points"] = v if ok else 0
+    mandatory = [  # main.m:150-171
+        ("Iteration_Cap", "Iteration_Cap", False),
+        ("threshold", "Threshold_Value", False),
+        ("Inner_Constraints", "Inner_Constraints", True),
+        ("Estimate_Xc", "Estimate_Xc", True),
+        ("Estimate_Yc", "Estimate_Yc", True),
+        ("Estimate_Zc", "Estimate_Zc", True),
+        ("Estimate_w", "Estimate_Omega", True),
+        ("Estimate_p", "Estimate_Phi", True),
+        ("Estimate_k", "Estimate_Kappa", True),
+        ("Estimate_c", "Estimate_c", True),
+        ("Estimate_xp", "Estimate_xp", True),
+        ("Estimate_yp", "Estimate_yp", True),
+        ("Estimate_radial", "Estimate_Radial_Distortions", True),
+        ("Num_Radial_Distortions", "Num_Radial_Distortions", False),
+        ("Estimate_decent", "Estimate_Decentering_Distortions", True),
+        ("Estimate_tie", "Estimate_tie", True),
+        ("Estimate_AllGCP", "Estimate_AllGCP", True),
+    ]
+    for name, key, c01 in mandatory:
+        v, ok = find_setting(cfg, key, c01)
+        if not ok:
+            raise OracleError(f"Error getting settings ({key})")
+        s[name] = int(v) if c01 else v
+    s["Iteration_Cap"] = int(s["Iteration_Cap"])
+    nK = int(s["Num_Radial_Distortions"])
+    s["Num_Radial_Distortions"] = nK
+
+    TIE = []
+    if s["Estimate_tie"] == 1 and s["Estimate_AllGCP"] == 0:  # main.m:180-188
+        TIE = [r[0] for r in read_table(find_file(folder, ".tie"))]
+
+    # main.m:196-257 string -> double, degrees -> radians
+    EXT = []
+    for r in ext:
+        EXT.append([r[0], r[1], _str2double(r[2]), _str2double(r[3]), _str2double(r[4]),
+                    _str2double(r[5]) * math.pi / 180, _str2double(r[6]) * math.pi / 180,
+                    _str2double(r[7]) * math.pi / 180])
+    CNT = [[r[0], _str2double(r[1]), _str2double(r[2]), _str2double(r[3])] for r in cnt]
+    INT = []
+    for i in range(0, len(intr), 2):
+        r1, r2 = intr[i], intr[i + 1]
+        vals = [_str2double(r2[j]) for j in range(3)]
+        for j in range(3, 5 + nK):  # missing distortions -> 0 (main.m:244-254)
+            vals.append(_str2double(r2[j]) if j < len(r2) else 0.0)
+        INT.append((r1[0], _str2double(r1[1]), _str2double(r1[2]), _str2double(r1[3]),
+                    _str2double(r1[4]), _str2double(r1[5]), vals))
+    if s["Estimate_AllGCP"] == 1:  # main.m:261-264: unique() sorts
+        TIE = sorted(set(r[0] for r in pho))
+        s["Estimate_tie"] = 1
+
+    # main.m:280-378 per image point joins
+    ext_pos = {}
+    for j, r in enumerate(EXT):
+        ext_pos.setdefault(r[0], j)
+    int_pos = {}
+    for j, r in enumerate(INT):
+        int_pos.setdefault(r[0], j)
+    cnt_pos = {}
+    for j, r in enumerate(CNT):
+        cnt_pos.setdefault(r[0], j)
+    tie_pos = {}
+    for j, t in enumerate(TIE):
+        tie_pos.setdefault(t, j)
+
+    npts = len(pho)
+    x = np.empty(npts)
+    y = np.empty(npts)
+    ext_index = np.empty(npts, np.int64)
+    cam_num = np.empty(npts, np.int64)
+    tie_index = np.empty(npts, np.int64)
+    eop = np.empty((npts, 6))
+    iop = np.empty((npts, 5 + nK))
+    bounds = np.empty((npts, 5))
+    xyz = np.empty((npts, 3))
+    cams = []
+    cnt_used = set()
+    for i, r in enumerate(pho):
+        x[i] = _str2double(r[2])
+        y[i] = _str2double(r[3])
+        if r[1] not in ext_pos:
+            raise OracleError(f"Could not find image {r[1]} from .pho in .ext")
+        e = ext_pos[r[1]]
+        ext_index[i] = e
+        cam = EXT[e][1]
+        cams.append(cam)
+        eop[i] = EXT[e][2:8]
+        if cam not in int_pos:
+            raise OracleError(f"Could not find camera {cam} from .ext in .int")
+        c = int_pos[cam]
+        cam_num[i] = c
+        iop[i] = INT[c][6]
+        if INT[c][1] not in (1.0, -1.0):
+            raise OracleError("y_dir should be +-1 only")
+        bounds[i] = [INT[c][1], INT[c][2], INT[c][3], INT[c][4], INT[c][5]]
+        if r[0] not in cnt_pos:
+            raise OracleError(f"Could not find target {r[0]} from .pho in .cnt")
+        k = cnt_pos[r[0]]
+        cnt_used.add(k)
+        xyz[i] = CNT[k][1:4]
+        tie_index[i] = tie_pos.get(r[0], -1)
+    data = Data(
+        settings=s, x=x, y=y, target=[r[0] for r in pho], image=[r[1] for r in pho],
+        ext_index=ext_index, cam_num=cam_num, tie_index=tie_index, eop_fixed=eop,
+        iop_fixed=iop, bounds=bounds, xyz_fixed=xyz,
+        numImg=len(set(r[1] for r in pho)), numCam=len(set(cams)), n=2 * npts,
+        numGCP=len(cnt_used), numtie=len(TIE), EXT=EXT, INT=INT, TIE=TIE, CNT=CNT)
+    return data
+
+
+# ----------------------------------------------------------------------------------------------
+# Buildxhat.m
+# ----------------------------------------------------------------------------------------------
+def counts(s):
+    """BuildAwG.m:24-25 (u_perimage, u_percam)."""
+    u_img = s["Estimate_Xc"] + s["Estimate_Yc"] + s["Estimate_Zc"] + s["Estimate_w"] + \
+        s["Estimate_p"] + s["Estimate_k"]
+    u_cam = s["Estimate_c"] + s["Estimate_xp"] + s["Estimate_yp"] + \
+        s["Estimate_radial"] * s["Num_Radial_Distortions"] + s["Estimate_decent"] * 2
+    return int(u_img), int(u_cam)
+
+
+def buildxhat(data):
+    """Buildxhat.m:2-135: [per EXT row Xc Yc Zc w p k] ++ [per camera xp yp c K.. P..] ++ [tie XYZ]."""
+    s = data.settings
+    nK = s["Num_Radial_Distortions"]
+    xhat, names = [], []
+    eflags = ["Estimate_Xc", "Estimate_Yc", "Estimate_Zc", "Estimate_w", "Estimate_p", "Estimate_k"]
+    enames = ["Xc", "Yc", "Zc", "w", "p", "k"]
+    for i in range(data.numImg):
+        r = data.EXT[i]
+        for j in range(6):
+            if s[eflags[j]]:
+                xhat.append(r[2 + j])
+                names.append(f"{enames[j]}_{r[0]}_{r[1]}")
+    for i in range(data.numCam):
+        cid, vals = data.INT[i][0], data.INT[i][6]
+        for j, (flag, nm) in enumerate([("Estimate_xp", "xp"), ("Estimate_yp", "yp"), ("Estimate_c", "c")]):
+            if s[flag]:
+                xhat.append(vals[j])
+                names.append(f"{nm}_{cid}")
+        if s["Estimate_radial"]:
+            for j in range(nK):
+                xhat.append(vals[3 + j])
+                names.append(f"k{j + 1}_{cid}")
+        if s["Estimate_decent"]:
+            for j in range(2):
+                xhat.append(vals[3 + nK + j])
+                names.append(f"p{j + 1}_{cid}")
+    cnt_pos = {}
+    for j, r in enumerate(data.CNT):
+        cnt_pos.setdefault(r[0], j)
+    for t in data.TIE:
+        if t not in cnt_pos:
+            raise OracleError(f"Error Buildxhat(): can't find {t} from .tie in .cnt")
+        r = data.CNT[cnt_pos[t]]
+        xhat.extend(r[1:4])
+        names.extend([f"X_{t}", f"Y_{t}", f"Z_{t}"])
+    return np.array(xhat, dtype=np.float64), names
+
+
+# ----------------------------------------------------------------------------------------------
+# forward model + chain-rule Jacobian (BuildAwG.m:160-503)
+# ----------------------------------------------------------------------------------------------
+def rotation(w, p, k):
+    """M(w,p,k) and its partials, rows as in BuildAwG.m:163-165 (U,V,W = M @ (X-Xc))."""
+    cw, sw, cp, sp, ck, sk = np.cos(w), np.sin(w), np.cos(p), np.sin(p), np.cos(k), np.sin(k)
+    z = np.zeros_like(w)
+    M = np.stack([
+        np.stack([ck * cp, cw * sk + ck * sp * sw, sk * sw - ck * cw * sp], -1),
+        np.stack([-cp * sk, ck * cw - sk * sp * sw, ck * sw + cw * sk * sp], -1),
+        np.stack([sp, -cp * sw, cp * cw], -1)], -2)
+    Mw = np.stack([
+        np.stack([z, -sw * sk + ck * sp * cw, sk * cw + ck * sw * sp], -1),
+        np.stack([z, -ck * sw - sk * sp * cw, ck * cw - sw * sk * sp], -1),
+        np.stack([z, -cp * cw, -cp * sw], -1)], -2)
+    Mp = np.stack([
+        np.stack([-ck * sp, ck * cp * sw, -ck * cw * cp], -1),
+        np.stack([sp * sk, -sk * cp * sw, cw * sk * cp], -1),
+        np.stack([cp, sp * sw, -sp * cw], -1)], -2)
+    Mk = np.stack([
+        np.stack([-sk * cp, cw * ck - sk * sp * sw, ck * sw + sk * cw * sp], -1),
+        np.stack([-cp * ck, -sk * cw - ck * sp * sw, -sk * sw + cw * ck * sp], -1),
+        np.stack([z, z, z], -1)], -2)
+    return M, Mw, Mp, Mk
+
+
+def radial_factor(typeint, R, W):
+    """s(R,W) with f_proj = -c*(U,ydir*V)*s, and its partials (BuildAwG.m:184-208)."""
+    if typeint == 1:  # pinhole: -c U / W
+        s = 1.0 / W
+        return s, np.zeros_like(R), -1.0 / (W * W)
+    t = np.arctan(R / W)
+    q = R * R + W * W
+    t_R = W / q
+    t_W = -R / q
+    if typeint == 0:  # equidistant: atan(R/W)/R
+        g, g_t = t, np.ones_like(t)
+    elif typeint == 2:  # equisolid: 2 sin(t/2)/R
+        g, g_t = 2.0 * np.sin(0.5 * t), np.cos(0.5 * t)
+    elif typeint == 3:  # orthographic: sin(t)/R
+        g, g_t = np.sin(t), np.cos(t)
+    elif typeint == 4:  # stereographic: 2 tan(t/2)/R
+        g, g_t = 2.0 * np.tan(0.5 * t), 1.0 / np.cos(0.5 * t) ** 2
+    else:
+        raise OracleError("BuildAwG, invalid type in data.settings.type")
+    s = g / R
+    s_R = g_t * t_R / R - g / (R * R)
+    s_W = g_t * t_W / R
+    return s, s_R, s_W
+
+
+def point_model(typeint, eop, xyz, xp, yp, c, K, P, ydir, x, y):
+    """Per image point: (fx, fy) and partials.  All arrays over points.
+
+    Returns f (n,2), J_eop (n,2,6) [Xc Yc Zc w p k], J_xyz (n,2,3), J_c (n,2),
+    J_xp (n,2), J_yp (n,2), and the distortion helpers (xbar, ybar, r).
+    BuildAwG.m:163-212 (model), :216-352 (EOP), :373-414 (IOP), :454-495 (tie).
+    """
+    M, Mw, Mp, Mk = rotation(eop[:, 3], eop[:, 4], eop[:, 5])
+    d = xyz - eop[:, :3]
+    UVW = np.einsum("nij,nj->ni", M, d)
+    U, V, W = UVW[:, 0], UVW[:, 1], UVW[:, 2]
+    R = np.sqrt(U * U + V * V)
+    s, s_R, s_W = radial_factor(typeint, R, W)
+    xbar = x - xp
+    ybar = y - yp
+    r = np.sqrt(xbar * xbar + ybar * ybar)
+    nK = K.shape[1]
+    dr = np.zeros_like(r)
+    for j in range(nK):
+        dr = dr + K[:, j] * r ** (2 * (j + 1))
+    decx = P[:, 0] * (ybar ** 2 + 3 * xbar ** 2) + 2 * P[:, 1] * xbar * ybar
+    decy = P[:, 1] * (xbar ** 2 + 3 * ybar ** 2) + 2 * P[:, 0] * xbar * ybar
+    fx = -c * U * s + xp + dr * xbar + decx
+    fy = -c * ydir * V * s + yp + dr * ybar + decy
+
+    # d(U,V,W)/dq for q in [Xc Yc Zc w p k] -> (n,3,6)
+    dUVW = np.empty((len(x), 3, 6))
+    dUVW[:, :, 0:3] = -M
+    dUVW[:, :, 3] = np.einsum("nij,nj->ni", Mw, d)
+    dUVW[:, :, 4] = np.einsum("nij,nj->ni", Mp, d)
+    dUVW[:, :, 5] = np.einsum("nij,nj->ni", Mk, d)
+
+    def chain(dq):  # dq: (n,3,m) -> d(fx,fy) (n,2,m)
+        dU, dV, dW = dq[:, 0], dq[:, 1], dq[:, 2]
+        dR = (U[:, None] * dU + V[:, None] * dV) / R[:, None]
+        ds = s_R[:, None] * dR + s_W[:, None] * dW
+        gx = -c[:, None] * (dU * s[:, None] + U[:, None] * ds)
+        gy = -(c * ydir)[:, None] * (dV * s[:, None] + V[:, None] * ds)
+        return np.stack([gx, gy], 1)
+
+    J_eop = chain(dUVW)
+    J_xyz = chain(M)  # d(UVW)/d(XYZ) = M
+    J_c = np.stack([-U * s, -ydir * V * s], 1)
+    # xp / yp (BuildAwG.m:373-398)
+    dxp_rad = np.zeros_like(r)
+    dyp_rad = np.zeros_like(r)
+    dxp_rad2 = np.zeros_like(r)
+    dyp_rad2 = np.zeros_like(r)
+    for j in range(1, nK + 1):
+        Kj = K[:, j - 1]
+        r2jm2 = r ** ((j - 1) * 2)
+        dxp_rad = dxp_rad - Kj * r ** (2 * j) - 2 * j * Kj * xbar ** 2 * r2jm2
+        dyp_rad = dyp_rad - 2 * j * Kj * xbar * ybar * r2jm2
+        dxp_rad2 = dxp_rad2 - 2 * j * Kj * xbar * ybar * r2jm2
+        dyp_rad2 = dyp_rad2 - Kj * r ** (2 * j) - 2 * j * Kj * ybar ** 2 * r2jm2
+    J_xp = np.stack([1 + dxp_rad - 6 * P[:, 0] * xbar - 2 * P[:, 1] * ybar,
+                     0 + dyp_rad - 2 * P[:, 0] * ybar - 2 * P[:, 1] * xbar], 1)
+    J_yp = np.stack([0 + dxp_rad2 - 2 * P[:, 1] * xbar - 2 * P[:, 0] * ybar,
+                     1 + dyp_rad2 - 6 * P[:, 1] * ybar - 2 * P[:, 0] * xbar], 1)
+    return dict(f=np.stack([fx, fy], 1), J_eop=J_eop, J_xyz=J_xyz, J_c=J_c, J_xp=J_xp,
+                J_yp=J_yp, xbar=xbar, ybar=ybar, r=r, U=U, V=V, W=W)
+
+
+def gather_params(data, xhat):
+    """BuildAwG.m:50-158: fetch each parameter from xhat if estimated, else the fixed value."""
+    s = data.settings
+    nK = max(s["Num_Radial_Distortions"], 1)  # BuildAwG.m:18-20
+    u_img, u_cam = counts(s)
+    npts = len(data.x)
+    eop = data.eop_fixed.copy()
+    base = data.ext_index * u_img
+    cnt = 0
+    for j, flag in enumerate(["Estimate_Xc", "Estimate_Yc", "Estimate_Zc", "Estimate_w", "Estimate_p",
+                              "Estimate_k"]):
+        if s[flag]:
+            eop[:, j] = xhat[base + cnt]
+            cnt += 1
+    xyz = data.xyz_fixed.copy()
+    tie = data.tie_index >= 0
+    toff = u_img * data.numImg + u_cam * data.numCam + 3 * data.tie_index
+    for j in range(3):
+        xyz[tie, j] = xhat[toff[tie] + j]
+    ibase = u_img * data.numImg + data.cam_num * u_cam
+    iop = data.iop_fixed
+    cnt = 0
+    vals = {}
+    for nm, flag, col in [("xp", "Estimate_xp", 0), ("yp", "Estimate_yp", 1), ("c", "Estimate_c", 2)]:
+        if s[flag]:
+            vals[nm] = xhat[ibase + cnt]
+            cnt += 1
+        else:
+            vals[nm] = iop[:, col].copy()
+    rad_off = None
+    if s["Estimate_radial"]:
+        rad_off = ibase + cnt
+        K = np.stack([xhat[rad_off + j] for j in range(nK)], 1)
+        cnt += nK
+    else:
+        K = iop[:, 3:3 + nK].copy()
+    dec_off = None
+    if s["Estimate_decent"]:
+        dec_off = ibase + cnt
+        P = np.stack([xhat[dec_off], xhat[dec_off + 1]], 1)
+    else:
+        P = iop[:, 3 + s["Num_Radial_Distortions"]:5 + s["Num_Radial_Distortions"]].copy()
+    if P.shape[1] < 2:
+        P = np.zeros((npts, 2))
+    return eop, xyz, vals["xp"], vals["yp"], vals["c"], K, P, rad_off, dec_off
+
+
+def build_awg(data, xhat):
+    """BuildAwG.m:14-528 restated.  Returns (A, w, G or None, dist_scaling)."""
+    s = data.settings
+    if s["type"] not in TYPES:
+        raise OracleError("BuildAwG, invalid type in data.settings.type")
+    typeint = TYPES.index(s["type"])
+    nK = max(s["Num_Radial_Distortions"], 1)
+    u = len(xhat)
+    u_img, u_cam = counts(s)
+    npts = len(data.x)
+    eop, xyz, xp, yp, c, K, P, rad_off, dec_off = gather_params(data, xhat)
+    ydir = data.bounds[:, 0]
+    m = point_model(typeint, eop, xyz, xp, yp, c, K, P, ydir, data.x, data.y)
+    A = np.zeros((2 * npts, u))
+    rows = np.arange(npts)
+    # EOP block (BuildAwG.m:216-365)
+    cnt = 0
+    for j, flag in enumerate(["Estimate_Xc", "Estimate_Yc", "Estimate_Zc", "Estimate_w", "Estimate_p",
+                              "Estimate_k"]):
+        if s[flag]:
+            col = data.ext_index * u_img + cnt
+            A[2 * rows, col] = m["J_eop"][:, 0, j]
+            A[2 * rows + 1, col] = m["J_eop"][:, 1, j]
+            cnt += 1
+    # IOP + distortions (BuildAwG.m:369-451)
+    ibase = u_img * data.numImg + data.cam_num * u_cam
+    cnt = 0
+    for key, flag in [("J_xp", "Estimate_xp"), ("J_yp", "Estimate_yp"), ("J_c", "Estimate_c")]:
+        if s[flag]:
+            A[2 * rows, ibase + cnt] = m[key][:, 0]
+            A[2 * rows + 1, ibase + cnt] = m[key][:, 1]
+            cnt += 1
+    b = data.bounds
+    rmax = np.sqrt(((b[:, 3] - b[:, 1]) * 0.5) ** 2 + ((b[:, 4] - b[:, 2]) * 0.5) ** 2)
+    dist_scaling = np.zeros((data.numCam, 2 + nK))
+    for j in range(1, nK + 1):
+        dist_scaling[data.cam_num, 1 + j] = rmax ** (2 * j)
+    # columns 0-1 hold 1-based xhat indices, as the reference (BuildAwG.m:138, :150)
+    if rad_off is not None:
+        dist_scaling[data.cam_num, 0] = rad_off + 1
+    if dec_off is not None:
+        dist_scaling[data.cam_num, 1] = dec_off + 1
+    xbar, ybar, r = m["xbar"], m["ybar"], m["r"]
+    if s["Estimate_radial"]:
+        for j in range(1, nK + 1):
+            sc = dist_scaling[data.cam_num, 1 + j]
+            A[2 * rows, ibase + cnt] = r ** (2 * j) * xbar / sc
+            A[2 * rows + 1, ibase + cnt] = r ** (2 * j) * ybar / sc
+            cnt += 1
+    if s["Estimate_decent"]:
+        sc = dist_scaling[data.cam_num, 2]
+        A[2 * rows, ibase + cnt] = (ybar ** 2 + 3 * xbar ** 2) / sc
+        A[2 * rows, ibase + cnt + 1] = (2 * xbar * ybar) / sc
+        A[2 * rows + 1, ibase + cnt] = (2 * xbar * ybar) / sc
+        A[2 * rows + 1, ibase + cnt + 1] = (xbar ** 2 + 3 * ybar ** 2) / sc
+    # tie points (BuildAwG.m:454-503)
+    tie = data.tie_index >= 0
+    toff = u_img * data.numImg + u_cam * data.numCam + 3 * data.tie_index
+    tr = rows[tie]
+    for j in range(3):
+        A[2 * tr, toff[tie] + j] = m["J_xyz"][tie, 0, j]
+        A[2 * tr + 1, toff[tie] + j] = m["J_xyz"][tie, 1, j]
+    # misclosure (BuildAwG.m:505-512)
+    w = np.empty(2 * npts)
+    w[0::2] = m["f"][:, 0] - data.x
+    w[1::2] = m["f"][:, 1] - data.y
+    # inner constraints (BuildAwG.m:514-527)
+    G = None
+    if s["Inner_Constraints"]:
+        G = np.zeros((u, 7))
+        seen = set()
+        for i in range(npts):
+            e = int(data.ext_index[i])
+            if e in seen:
+                continue
+            seen.add(e)
+            G[e * u_img:e * u_img + 6, :] = gblock(*eop[i, :5])
+    return A, w, G, dist_scaling
+
+
+def gblock(Xc, Yc, Zc, w, p):
+    """BuildAwG.m:516-523: 6x7 inner-constraint block of one image."""
+    return np.array([
+        [1, 0, 0, 0, -Zc, Yc, Xc],
+        [0, 1, 0, Zc, 0, -Xc, Yc],
+        [0, 0, 1, -Yc, Xc, 0, Zc],
+        [0, 0, 0, -1, -math.sin(w) * math.tan(p), math.cos(w) * math.tan(p), 0],
+        [0, 0, 0, 0, -math.cos(w), -math.sin(w), 0],
+        [0, 0, 0, 0, math.sin(w) / math.cos(p), -math.cos(w) / math.cos(p), 0],
+    ], dtype=np.float64)
+
+
+# ----------------------------------------------------------------------------------------------
+# main.m:396-494 -- the Gauss-Newton loop (dense, explicit bordered inverse)
+# ----------------------------------------------------------------------------------------------
+def weights(data):
+    """main.m:396-405: P = diag(1/sx^2, 1/sy^2, ...) (priori = 1), as a vector."""
+    s = data.settings
+    P = np.empty(data.n)
+    P[0::2] = 1.0 / (s["Meas_std"] ** 2)
+    P[1::2] = 1.0 / (s["Meas_std_y"] ** 2)
+    return P
+
+
+def descale(data, delta, dist_scaling):
+    """main.m:460-482: de-scale the radial and decentering corrections."""
+    s = data.settings
+    delta = delta.copy()
+    for i in range(dist_scaling.shape[0]):
+        if s["Estimate_radial"]:
+            ri = int(dist_scaling[i, 0]) - 1
+            for j in range(s["Num_Radial_Distortions"]):
+                delta[ri + j] /= dist_scaling[i, 2 + j]
+        if s["Estimate_decent"]:
+            di = int(dist_scaling[i, 1]) - 1
+            delta[di] /= dist_scaling[i, 2]
+            delta[di + 1] /= dist_scaling[i, 2]
+    return delta
+
+
+def solve_dense(data, A, w, G, P):
+    """main.m:424-444 (explicit (bordered) inverse)."""
+    u_vec = A.T @ (P * w)
+    N = A.T @ (P[:, None] * A)
+    if data.settings["Inner_Constraints"]:
+        d = G.shape[1]
+        NG = np.block([[N, G], [G.T, np.zeros((d, d))]])
+        Cx = np.linalg.inv(NG)
+        delta = -(Cx @ np.concatenate([u_vec, np.zeros(d)]))[: len(u_vec)]
+        Cx = Cx[: len(u_vec), : len(u_vec)]
+    else:
+        Cx = np.linalg.inv(N)
+        delta = -Cx @ u_vec
+    return delta, Cx
+
+
+@dataclass
+class Result:
+    xhat: np.ndarray
+    names: list
+    iterations: int
+    deltasum: list
+    xhat_hist: list
+    A: np.ndarray
+    w: np.ndarray
+    G: object
+    dist_scaling: np.ndarray
+    delta: np.ndarray
+    v: np.ndarray
+    rsd: np.ndarray
+    rms: tuple
+    sigma02: float
+    w0: np.ndarray = None
+
+
+def adjust(data, solver=None, max_iter=None):
+    """main.m:386-602 restated.  `solver(data, A, w, G, P) -> delta` may replace the explicit
+    inverse (the block-sparse Schur restatement below) for scenes too large for dense N."""
+    s = data.settings
+    xhat, names = buildxhat(data)
+    P = weights(data)
+    deltasum = 100.0
+    count = 0
+    hist = [xhat.copy()]
+    dsum = []
+    cap = s["Iteration_Cap"] if max_iter is None else min(s["Iteration_Cap"], max_iter)
+    w0 = None
+    while deltasum > s["threshold"]:
+        count += 1
+        A, w, G, dist_scaling = build_awg(data, xhat)
+        if w0 is None:
+            w0 = w.copy()
+        if solver is None:
+            delta, _ = solve_dense(data, A, w, G, P)
+        else:
+            delta = solver(data, A, w, G, P)
+        delta = descale(data, delta, dist_scaling)
+        xhat = xhat + delta
+        hist.append(xhat.copy())
+        deltasum = float(np.sum(np.abs(delta)))  # sumabs.m:12-14
+        dsum.append(deltasum)
+        if count >= cap:
+            break
+    v = A @ delta + w  # main.m:569 (last A, w; de-scaled delta)
+    rsd = build_rsd(data, v, xhat)
+    rmsx = math.sqrt(np.mean(v[0::2] ** 2))
+    rmsy = math.sqrt(np.mean(v[1::2] ** 2))
+    sigma02 = float(v @ (P * v)) / (A.shape[0] - A.shape[1])  # main.m:601
+    return Result(xhat=xhat, names=names, iterations=count, deltasum=dsum, xhat_hist=hist, A=A, w=w,
+                  G=G, dist_scaling=dist_scaling, delta=delta, v=v, rsd=rsd,
+                  rms=(rmsx, rmsy, math.sqrt(rmsx ** 2 + rmsy ** 2)), sigma02=sigma02, w0=w0)
+
+
+def build_rsd(data, v, xhat):
+    """BuildRSD.m:1-43: per point [r, vx, vy, vr, vt] (ids / x / y are carried by the caller)."""
+    s = data.settings
+    u_img, u_cam = counts(s)
+    ibase = u_img * data.numImg + data.cam_num * u_cam
+    cnt = 0
+    if s["Estimate_xp"]:
+        xp = xhat[ibase]
+        cnt = 1
+    else:
+        xp = data.iop_fixed[:, 0]
+    if s["Estimate_yp"]:
+        yp = xhat[ibase + cnt]
+    else:
+        yp = data.iop_fixed[:, 1]
+    vx, vy = v[0::2], v[1::2]
+    xbar = data.x - xp
+    ybar = data.y - yp
+    theta = np.arctan2(ybar, xbar)
+    phi = np.arctan2(vy, vx)
+    vd = np.sqrt(vx ** 2 + vy ** 2)
+    return np.stack([np.sqrt(xbar ** 2 + ybar ** 2), vx, vy, vd * np.cos(theta - phi),
+                     vd * np.sin(theta - phi)], 1)
+
+
+# ----------------------------------------------------------------------------------------------
+# Block-sparse restatement of the same normal-equation solve (for scenes where dense N is
+# infeasible).  Mathematically identical to solve_dense: tie points are eliminated by the
+# Schur complement, and the inner-constraint border is solved on the reduced system.
+# ----------------------------------------------------------------------------------------------
+def solve_schur(data, A, w, G, P):
+    s = data.settings
+    u_img, u_cam = counts(s)
+    uc = u_img * data.numImg + u_cam * data.numCam
+    nT = data.numtie
+    Ac = A[:, :uc]
+    Ap = A[:, uc:]
+    if hasattr(Ac, "toarray"):
+        Ac = Ac.toarray()
+    PA = P[:, None] * Ac
+    Ncc = Ac.T @ PA
+    uc_vec = Ac.T @ (P * w)
+    if nT == 0:
+        S, r = Ncc, uc_vec
+        V_inv = None
+    else:
+        Ap = np.asarray(Ap)
+        # per tie point 3x3 V and the camera-point coupling, row-sparse assembly
+        V = np.zeros((nT, 3, 3))
+        bp = np.zeros(nT)
+        Ncp = Ac.T @ (P[:, None] * Ap)  # uc x 3nT (dense here: test-size scenes only)
+        Npp = Ap.T @ (P[:, None] * Ap)
+        up = Ap.T @ (P * w)
+        for t in range(nT):
+            V[t] = Npp[3 * t:3 * t + 3, 3 * t:3 * t + 3]
+        Vi = np.linalg.inv(V)
+        Vinv = np.zeros((3 * nT, 3 * nT))
+        for t in range(nT):
+            Vinv[3 * t:3 * t + 3, 3 * t:3 * t + 3] = Vi[t]
+        S = Ncc - Ncp @ Vinv @ Ncp.T
+        r = uc_vec - Ncp @ (Vinv @ up)
+        V_inv = (Vinv, Ncp, up)
+    if s["Inner_Constraints"]:
+        Gc = G[:uc]
+        d = Gc.shape[1]
+        KKT = np.block([[S, Gc], [Gc.T, np.zeros((d, d))]])
+        dc = np.linalg.solve(KKT, np.concatenate([-r, np.zeros(d)]))[:uc]
+    else:
+        dc = np.linalg.solve(S, -r)
+    if V_inv is None:
+        return dc
+    Vinv, Ncp, up = V_inv
+    dp = -Vinv @ (up + Ncp.T @ dc)
+    return np.concatenate([dc, dp])

@@ -1,0 +1,23 @@
+#!/bin/bash
+# GPU-box check: each GPU step under its own time limit; stop at the first abort / fault / timeout
+# (exit codes other than 0 = ok and 1 = test/assert failure).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+run() {
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
+  if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit "$rc"; fi
+}
+for step in "$@"; do
+  case "$step" in
+    tests) run tests 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py --steps 5 --warmup 1 --verbose ;;
+    benchq) run bench 600 python bench.py --steps 5 --warmup 1 --no-cpu --verbose ;;
+    prof) cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+          run prof 600 rocprofv3 --kernel-trace --stats -d "$PWD/gpurun_out/prof" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
+  esac
+done

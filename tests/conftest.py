@@ -1,0 +1,114 @@
+import os
+import shutil
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+CAM0 = os.path.join(GOLDEN, "cam0")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
+
+
+@pytest.fixture(scope="session")
+def fba():
+    import fba_import
+    return fba_import.load()
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import fba_oracle
+    return fba_oracle
+
+
+def variant_folder(tmp_root, name, cfg_edits, src=CAM0):
+    """Copy cam0 with edited .cfg keys (value strings as in the .cfg)."""
+    dst = os.path.join(tmp_root, name)
+    os.makedirs(dst, exist_ok=True)
+    for f in os.listdir(src):
+        if not f.endswith(".cfg"):
+            shutil.copy(os.path.join(src, f), dst)
+    lines = open(os.path.join(src, "config.cfg")).read().splitlines()
+    out, seen = [], set()
+    for ln in lines:
+        toks = ln.split("#", 1)[0].split()
+        if toks and toks[0] in cfg_edits:
+            out.append(f"{toks[0]}\t{cfg_edits[toks[0]]}")
+            seen.add(toks[0])
+        else:
+            out.append(ln)
+    for k, v in cfg_edits.items():
+        if k not in seen:
+            out.append(f"{k}\t{v}")
+    with open(os.path.join(dst, "config.cfg"), "w") as fh:
+        fh.write("\n".join(out) + "\n")
+    return dst
+
+
+STAGE1 = {"Inner_Constraints": "0", "Estimate_xp": "0", "Estimate_yp": "0", "Estimate_c": "0",
+          "Estimate_Radial_Distortions": "0", "Estimate_Decentering_Distortions": "0", "Estimate_tie": "0"}
+
+CAM0_VARIANTS = {
+    "stage3_pinhole": {},
+    "stage3_fisheye": {"Type": "'fisheye'"},
+    "stage1_pinhole": STAGE1,
+    "stage3_equisolid": {"Type": "'equisolid'"},
+    "stage3_orthographic": {"Type": "'orthographic'"},
+    "stage3_stereographic": {"Type": "'stereographic'"},
+    "stage3_noic_pinhole": {"Inner_Constraints": "0"},
+    "stage3_sigy_pinhole": {"Meas_std_y": "0.4"},
+}
+
+
+@pytest.fixture(scope="session")
+def cam0_folders(tmp_path_factory):
+    root = str(tmp_path_factory.mktemp("cam0v"))
+    return {k: variant_folder(root, k, v) for k, v in CAM0_VARIANTS.items()}
+
+
+def param_groups(names):
+    """Group unknown names (Buildxhat.m naming) for normwise-per-group relative errors."""
+    groups = {}
+    for i, nm in enumerate(names):
+        key = nm.split("_", 1)[0]
+        if key in ("Xc", "Yc", "Zc"):
+            key = "XYZc"
+        elif key in ("w", "p", "k"):
+            key = "wpk"
+        elif key in ("X", "Y", "Z"):
+            key = "XYZ"
+        groups.setdefault(key, []).append(i)
+    return {k: np.array(v) for k, v in groups.items()}
+
+
+def distortion_scale(names, dist_scaling):
+    """Multiply K_j by rmax^(2j) and P by rmax^2 (the reference's own scaling, BuildAwG.m:422-443)."""
+    sc = np.ones(len(names))
+    for i, nm in enumerate(names):
+        head = nm.split("_", 1)[0]
+        if head[0] == "k" and head[1:].isdigit():
+            sc[i] = dist_scaling[0, 1 + int(head[1:])]
+        elif head[0] == "p" and head[1:].isdigit():
+            sc[i] = dist_scaling[0, 2]
+    return sc
+
+
+def group_rel_err(a, b, names, dist_scaling=None):
+    """max over parameter groups of max|a-b| / max|b| (distortion terms in the scaled units)."""
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    if dist_scaling is not None:
+        sc = distortion_scale(names, dist_scaling)
+        a, b = a * sc, b * sc
+    worst = {}
+    for g, idx in param_groups(names).items():
+        den = max(np.max(np.abs(b[idx])), 1e-300)
+        worst[g] = float(np.max(np.abs(a[idx] - b[idx])) / den)
+    return worst

@@ -1,0 +1,111 @@
+"""CPU: pin the oracle (oracle/fba_oracle.py) before trusting it.
+
+* The Jacobian and forward model against tests/golden/jac_golden.json: numbers obtained by
+  evaluating the reference's OWN generated expression text (functions/BuildAwG.m:163-207,
+  :223-348, :401-414, :457-495) at 40 digits (tests/golden/make_jac_golden.py), all 5 types.
+* The cam0 runs against the committed fixtures (tests/golden/cam0_*.npz, written by
+  tests/golden/make_cam0_golden.py) -- a regression pin of the restatement itself.
+* The block-sparse (Schur) restatement against the explicit bordered inverse of main.m:432.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import CAM0, CAM0_VARIANTS, GOLDEN, group_rel_err
+
+EOP_NAMES = {"A14": (0, 0), "A15": (0, 1), "A16": (0, 2), "A11": (0, 3), "A12": (0, 4), "A13": (0, 5),
+             "A24": (1, 0), "A25": (1, 1), "A26": (1, 2), "A21": (1, 3), "A22": (1, 4), "A23": (1, 5)}
+TIE_NAMES = {"dx_dX": (0, 0), "dx_dY": (0, 1), "dx_dZ": (0, 2), "dy_dX": (1, 0), "dy_dY": (1, 1), "dy_dZ": (1, 2)}
+
+
+@pytest.fixture(scope="module")
+def jac():
+    with open(os.path.join(GOLDEN, "jac_golden.json")) as fh:
+        return json.load(fh)
+
+
+@pytest.mark.parametrize("t", range(5))
+def test_jacobian_matches_reference_expressions(oracle, jac, t):
+    typ = jac["types"][t]
+    pts = jac["points"]
+    n = len(pts)
+    eop = np.array([[p["Xc"], p["Yc"], p["Zc"], p["w"], p["p"], p["k"]] for p in pts])
+    xyz = np.array([[p["X"], p["Y"], p["Z"]] for p in pts])
+    c = np.array([p["c"] for p in pts])
+    yd = np.array([p["y_dir"] for p in pts])
+    xp = np.array([p["xp"] for p in pts])
+    yp = np.array([p["yp"] for p in pts])
+    # x = xp, y = yp and K = P = 0: the distortion terms vanish as in the golden (delta_r = 0)
+    m = oracle.point_model(t, eop, xyz, xp, yp, c, np.zeros((n, 1)), np.zeros((n, 2)), yd, xp, yp)
+    tol = 1e-12
+    for i, row in enumerate(jac["values"][typ]):
+        for nm, (a, b) in EOP_NAMES.items():
+            assert m["J_eop"][i, a, b] == pytest.approx(row[nm], rel=tol, abs=1e-300), (typ, i, nm)
+        for nm, (a, b) in TIE_NAMES.items():
+            assert m["J_xyz"][i, a, b] == pytest.approx(row[nm], rel=tol), (typ, i, nm)
+        assert m["J_c"][i, 0] == pytest.approx(row["Ax_c"], rel=tol)
+        assert m["J_c"][i, 1] == pytest.approx(row["Ay_c"], rel=tol)
+        assert m["f"][i, 0] == pytest.approx(row["fx"], rel=tol)
+        assert m["f"][i, 1] == pytest.approx(row["fy"], rel=tol)
+
+
+def test_jacobian_distortion_terms_by_finite_differences(oracle):
+    """BuildAwG.m:373-445 hand-written xp/yp/K/P partials: compare with central differences."""
+    rng = np.random.default_rng(3)
+    n = 16
+    eop = np.column_stack([rng.uniform(-10, 10, (n, 3)), rng.uniform(-0.3, 0.3, (n, 3))])
+    xyz = eop[:, :3] + np.column_stack([rng.uniform(-500, 500, (n, 2)), -rng.uniform(800, 2000, n)])
+    K = np.tile([-3e-9, 1e-15, 2e-21, 0.0, 0.0], (n, 1))
+    P = np.tile([1e-7, -5e-8], (n, 1))
+    c = np.full(n, 650.0)
+    yd = -np.ones(n)
+    x = rng.uniform(100, 1900, n)
+    y = rng.uniform(100, 1900, n)
+    xp, yp = np.full(n, 1024.3), np.full(n, 1023.7)
+    m = oracle.point_model(0, eop, xyz, xp, yp, c, K, P, yd, x, y)
+    h = 1e-4
+    for which, key in (("xp", "J_xp"), ("yp", "J_yp")):
+        d = np.zeros(n) + h
+        args_p = (xp + d, yp) if which == "xp" else (xp, yp + d)
+        args_m = (xp - d, yp) if which == "xp" else (xp, yp - d)
+        fp = oracle.point_model(0, eop, xyz, *args_p, c, K, P, yd, x, y)["f"]
+        fm = oracle.point_model(0, eop, xyz, *args_m, c, K, P, yd, x, y)["f"]
+        np.testing.assert_allclose(m[key], (fp - fm) / (2 * h), rtol=1e-7, atol=1e-8)
+
+
+def test_cam0_ingest(oracle):
+    d = oracle.load_folder(CAM0)
+    assert (d.numImg, d.numCam, d.n, d.numtie, d.numGCP) == (42, 1, 2058, 106, 109)
+    assert oracle.counts(d.settings) == (6, 10)
+    x, names = oracle.buildxhat(d)
+    assert len(x) == 580 and names[0].startswith("Xc_101") and names[252] == "xp_0"
+    assert d.settings["type"] == "pinhole" and d.settings["Meas_std_y"] == 0.3
+
+
+@pytest.mark.parametrize("variant", sorted(CAM0_VARIANTS))
+def test_cam0_oracle_regression(oracle, cam0_folders, variant):
+    path = os.path.join(GOLDEN, f"cam0_{variant}.npz")
+    g = np.load(path, allow_pickle=False)
+    d = oracle.load_folder(cam0_folders[variant])
+    r = oracle.adjust(d)
+    assert r.iterations == int(g["iterations"])
+    names = [str(s) for s in g["names"]]
+    err = group_rel_err(r.xhat, g["xhat"], names, g["dist_scaling"])
+    assert max(err.values()) < 1e-10, err
+    assert r.sigma02 == pytest.approx(float(g["sigma02"]), rel=1e-10)
+    np.testing.assert_allclose(r.deltasum, g["deltasum"], rtol=1e-6)
+
+
+def test_schur_restatement_equals_bordered_inverse(oracle, fba, tmp_path):
+    from fba_amd import synth
+    sc = synth.generate(10, 120, seed=11)
+    folder = synth.write_folder(sc, str(tmp_path / "s"))
+    d = oracle.load_folder(folder)
+    r1 = oracle.adjust(d, max_iter=3)
+    r2 = oracle.adjust(d, solver=oracle.solve_schur, max_iter=3)
+    _, _, _, ds = oracle.build_awg(d, r1.xhat)
+    err = group_rel_err(r2.xhat, r1.xhat, r1.names, ds)
+    assert max(err.values()) < 1e-9, err
+    assert r2.sigma02 == pytest.approx(r1.sigma02, rel=1e-9)
