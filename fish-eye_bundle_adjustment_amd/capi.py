@@ -21,7 +21,7 @@ NK_MAX = 8
 EXPORTS = (
     "fba_last_error", "fba_abi_version", "fba_count_unknowns", "fba_partition", "fba_create",
     "fba_destroy", "fba_buildxhat", "fba_set_xhat", "fba_get_xhat", "fba_build_awg",
-    "fba_accumulate", "fba_reduce_buffer", "fba_solve_update", "fba_step", "fba_adjust",
+    "fba_accumulate", "fba_reduce_buffer", "fba_synchronize", "fba_solve_update", "fba_step", "fba_adjust",
     "fba_residuals", "fba_finish_stats", "fba_last_timings", "fba_set_timing",
 )
 
@@ -70,6 +70,7 @@ def _load():
         "fba_build_awg": ([P, P, P, P, P, P], C.c_int),
         "fba_accumulate": ([P], C.c_int),
         "fba_reduce_buffer": ([P, P, P], C.c_int),
+        "fba_synchronize": ([P], C.c_int),
         "fba_solve_update": ([P, P], C.c_int),
         "fba_step": ([P, P], C.c_int),
         "fba_adjust": ([P, P, P], C.c_int),
@@ -198,6 +199,9 @@ class Context:
         p, n = C.c_void_p(), C.c_int64()
         check(lib.fba_reduce_buffer(self.h, C.byref(p), C.byref(n)))
         return p.value, n.value
+
+    def synchronize(self):
+        check(lib.fba_synchronize(self.h))
 
     def solve_update(self):
         d = C.c_double()

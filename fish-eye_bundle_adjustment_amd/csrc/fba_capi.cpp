@@ -576,6 +576,13 @@ int fba_reduce_buffer(fba_ctx* ctx, void** dev_ptr, int64_t* n_doubles) {
     return FBA_OK;
 }
 
+int fba_synchronize(fba_ctx* ctx) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }
+    FBA_HIP(hipStreamSynchronize(c->stream));
+    return FBA_OK;
+}
+
 int fba_solve_update(fba_ctx* ctx, double* deltasum_part) {
     Ctx* c = reinterpret_cast<Ctx*>(ctx);
     if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }

@@ -2,16 +2,17 @@
 //
 // The reference inverts the bordered normal matrix explicitly, Cx = [N G; G' 0]^-1
 // (main.m:428-440).  Here the tie points have already been eliminated (Schur complement), the
-// border is folded in as M = S + a^2 G G' (SPD whenever the bordered matrix is nonsingular), and
+// border is folded in as M = S + G W G' (SPD whenever the bordered matrix is nonsingular; W = one
+// equilibrating weight per constraint column, fba_kernels.hip k_border_weights), and
 //   M = L L'        right-looking blocked Cholesky, NB = 64:
 //                     k_potrf_diag   64x64 diagonal block in LDS (one workgroup)
 //                     k_trsm_panel   rows below the diagonal block, one thread per row
 //                     k_syrk_update  trailing update C -= L_i L_j' on v_mfma_f64_16x16x4_f64
-//   forward solve    the right-hand sides [r | aG] are stored as extra ROWS below M, so the
+//   forward solve    the right-hand sides [r | G W^1/2] are stored as extra ROWS below M, so the
 //                    factorisation's panel solves compute Y' = (L^-1 B)' as a by-product
-//   border combine   H = Z'Z, h = Z'y, k = -H^-1 h, y <- y + Z k      (Z, y = forward-solved aG, r)
+//   border combine   H = Z'Z, h = Z'y, k = -H^-1 h, y <- y + Z k      (Z, y = forward-solved G W^1/2, r)
 //   backward solve   L' x = y, one launch per block row (k_trsv_bwd)
-// so delta_c = -x = -M^-1 (r + aG k) satisfies [S aG; aG' 0][delta; k] = [-r; 0] exactly as the
+// so delta_c = -x = -M^-1 (r + G W^1/2 k) satisfies [S G; G' 0][delta; W^1/2 k] = [-r; 0] as the
 // reference's bordered system does.
 #include "fba_internal.h"
 

@@ -91,7 +91,7 @@ struct Ctx {
     double* d_slab = nullptr;    // camera reduction slabs
     double* d_S = nullptr;       // [(n_pad+NB)*ld] normal matrix (lower) + RHS rows
     double* d_X = nullptr;       // [nrhs*n_pad] solution of the bordered solve (row per rhs)
-    double* d_scal = nullptr;    // scalars: [0] alpha^2, [1] info, [2..] partial sums
+    double* d_scal = nullptr;    // scalars: [1] Cholesky failure flag, [2] sumabs, [8..14] border weights
     double* d_part = nullptr;    // block partial sums
     int n_part = 0;
     double* d_res = nullptr;     // [7*n_obs] v (2) + rsd (5)

@@ -12,7 +12,7 @@
 //   k_image         one workgroup per image: reduced diagonal block, image-camera block, RHS rows
 //   k_pairs         one wave per co-visible image pair: off-diagonal reduced blocks
 //   k_cam_*         two-stage deterministic reduction of the camera block
-//   k_border        inner-constraint bordering M = S + a^2 G G' (reference: NG = [N G; G' 0],
+//   k_border        inner-constraint bordering M = S + G W G' (reference: NG = [N G; G' 0],
 //                   main.m:428-432), unit diagonal for fixed parameters, RHS rows
 //   k_backsub       tie-point corrections from the camera-side solution
 //   k_update        de-scaling of distortion corrections (main.m:460-482), xhat += delta
@@ -484,31 +484,33 @@ __global__ void k_cam_stage2(const double* __restrict__ slab, double* __restrict
 }
 
 // ------------------------------------------------------------------------------------------------
-// border: alpha^2 = trace(S_eop)/trace(G G^T); S += alpha^2 G G^T (lower, EOP rows);
-// unit diagonal for fixed/padding rows; RHS rows 1..7 = alpha G
+// border: M = S + G W G^T with one weight per constraint column, w_m = 1 / sum_i G_im^2 / S_ii
+// (EOP rows).  The constraints G^T delta = 0 are invariant to the column weights; this choice
+// equilibrates the added curvature against S row by row, so the Cholesky of M keeps S's precision
+// (a single trace-based weight put 1e7 x S_ii on the translation rows of cam0 and lost 7 digits).
+// scal layout: [1] Cholesky failure flag, [2] sumabs, [8..14] w_m
 // ------------------------------------------------------------------------------------------------
-__global__ void k_alpha(const double* __restrict__ S, const double* __restrict__ G, double* __restrict__ scal,
-                        int64_t ld, int n_img, int ic) {
-    __shared__ double sa[256], sb[256];
-    double a = 0.0, b = 0.0;
+__global__ void k_border_weights(const double* __restrict__ S, const double* __restrict__ G,
+                                 double* __restrict__ scal, int64_t ld, int n_img, int ic) {
+    __shared__ double red[7][256];
+    double a[7] = {0, 0, 0, 0, 0, 0, 0};
     if (ic) {
         for (int64_t i = threadIdx.x; i < 6 * (int64_t)n_img; i += blockDim.x) {
-            a += S[i * ld + i];
+            const double sii = S[i * ld + i];
+            if (!(sii > 0.0)) continue;
             const double* g = G + (i / 6) * 42 + (i % 6) * 7;
-            for (int m = 0; m < 7; ++m) b += g[m] * g[m];
+            for (int m = 0; m < 7; ++m) a[m] += g[m] * g[m] / sii;
         }
     }
-    sa[threadIdx.x] = a; sb[threadIdx.x] = b;
+    for (int m = 0; m < 7; ++m) red[m][threadIdx.x] = a[m];
     __syncthreads();
     for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w) { sa[threadIdx.x] += sa[threadIdx.x + w]; sb[threadIdx.x] += sb[threadIdx.x + w]; }
+        if (threadIdx.x < w)
+            for (int m = 0; m < 7; ++m) red[m][threadIdx.x] += red[m][threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
-        double al = (sb[0] > 0.0 && sa[0] > 0.0) ? sa[0] / sb[0] : 1.0;
-        scal[0] = al;
-        scal[1] = 0.0;  // info (Cholesky failure flag)
-    }
+    if (threadIdx.x < 7) scal[8 + threadIdx.x] = red[threadIdx.x][0] > 0.0 ? 1.0 / red[threadIdx.x][0] : 1.0;
+    if (threadIdx.x == 0) scal[1] = 0.0;  // Cholesky failure flag
 }
 
 __global__ void k_border(double* __restrict__ S, const double* __restrict__ G, const double* __restrict__ scal,
@@ -519,17 +521,16 @@ __global__ void k_border(double* __restrict__ S, const double* __restrict__ G, c
     if (blockIdx.x > blockIdx.y) return;
     const int64_t n = 6 * (int64_t)n_img;
     if (!ic || i >= n) return;
-    const double al = scal[0];
     const double* gi = G + (i / 6) * 42 + (i % 6) * 7;
     double g[7];
-    for (int m = 0; m < 7; ++m) g[m] = gi[m];
+    for (int m = 0; m < 7; ++m) g[m] = gi[m] * scal[8 + m];
     for (int jj = threadIdx.x; jj < 64; jj += blockDim.x) {
         const int64_t j = jb + jj;
         if (j > i || j >= n) continue;
         const double* gj = G + (j / 6) * 42 + (j % 6) * 7;
         double acc = 0.0;
         for (int m = 0; m < 7; ++m) acc += g[m] * gj[m];
-        S[i * ld + j] += al * acc;
+        S[i * ld + j] += acc;
     }
 }
 
@@ -544,9 +545,9 @@ __global__ void k_finish_rhs(double* __restrict__ S, const double* __restrict__ 
         S[n_pad * ld + i] = 0.0;
     }
     if (ic) {
-        const double al = sqrt(scal[0]);
         for (int m = 0; m < 7; ++m)
-            S[(n_pad + 1 + m) * ld + i] = (i < 6 * (int64_t)n_img) ? al * G[(i / 6) * 42 + (i % 6) * 7 + m] : 0.0;
+            S[(n_pad + 1 + m) * ld + i] =
+                (i < 6 * (int64_t)n_img) ? sqrt(scal[8 + m]) * G[(i / 6) * 42 + (i % 6) * 7 + m] : 0.0;
     }
 }
 
@@ -824,7 +825,7 @@ int launch_accumulate(Ctx& c) {
 int launch_border(Ctx& c) {
     const Layout& L = c.L;
     const int ic = c.set.inner_constraints;
-    k_alpha<<<1, 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, L.ld, L.n_img, ic);
+    k_border_weights<<<1, 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, L.ld, L.n_img, ic);
     FBA_HIP(hipGetLastError());
     if (ic) {
         const int nb = (int)((6 * (int64_t)L.n_img + 63) / 64);

@@ -130,7 +130,9 @@ int fba_get_xhat(fba_ctx* ctx, double* xhat, int32_t owned_only);
 
 /* BuildAwG.m (dense debug/parity form): A is n x u column-major (n = 2*n_pts, PHO row order),
  * w is n, G is u x 7 column-major (only when inner constraints are on; may be NULL),
- * dist_scaling is n_cam x (2+num_radial) column-major with 0-based xhat indices in columns 0-1.
+ * dist_scaling is n_cam x (2+num_radial) column-major; columns 0-1 hold the reference's 1-based xhat
+ * index of the first radial / decentering unknown (0 when not estimated, BuildAwG.m:138, :150),
+ * columns 2.. rmax^(2j) (BuildAwG.m:424-426).
  * Any output pointer may be NULL. */
 int fba_build_awg(fba_ctx* ctx, const double* xhat, double* A, double* w, double* G,
                   double* dist_scaling);
@@ -146,6 +148,9 @@ int fba_build_awg(fba_ctx* ctx, const double* xhat, double* A, double* w, double
  * fba_step does both halves on one GPU and returns the full deltasum. */
 int fba_accumulate(fba_ctx* ctx);
 int fba_reduce_buffer(fba_ctx* ctx, void** dev_ptr, int64_t* n_doubles);
+/* Block until every operation queued on the context's stream has completed (needed before a
+ * caller touches the reduce buffer from another stream or the host). */
+int fba_synchronize(fba_ctx* ctx);
 int fba_solve_update(fba_ctx* ctx, double* deltasum_part);
 int fba_step(fba_ctx* ctx, double* deltasum);
 

@@ -112,3 +112,47 @@ def group_rel_err(a, b, names, dist_scaling=None):
         den = max(np.max(np.abs(b[idx])), 1e-300)
         worst[g] = float(np.max(np.abs(a[idx] - b[idx])) / den)
     return worst
+
+
+def solver_spread(oracle, od, ro, perturb=1e-14):
+    """How far exact restatements of the reference land from each other, per parameter group and for
+    sigma0^2 and the first deltasum.  Three variants of the oracle run:
+      * LU of the bordered system instead of its explicit inverse (main.m:432);
+      * the loop started from an xhat perturbed by `perturb` relative (the inner-constraint datum is
+        re-derived from every iterate, BuildAwG.m:516-523, so the limit depends on the path);
+      * the misclosure w perturbed by one ulp of f (any implementation of the forward model --
+        the reference's generated expressions included -- rounds f differently).
+    On the path-sensitive cam0 variants (inner constraints + control points + a non-pinhole model)
+    the high-order distortion terms move by up to ~1e-4; no implementation can be closer."""
+    def solve_lu(data, A, w, G, P):
+        u = A.T @ (P * w)
+        N = A.T @ (P[:, None] * A)
+        if G is None:
+            return np.linalg.solve(N, -u)
+        NG = np.block([[N, G], [G.T, np.zeros((7, 7))]])
+        return np.linalg.solve(NG, np.concatenate([-u, np.zeros(7)]))[: len(u)]
+    runs = [oracle.adjust(od, solver=solve_lu)]
+    x0, names = oracle.buildxhat(od)
+    rng = np.random.default_rng(0)
+    orig_x, orig_awg = oracle.buildxhat, oracle.build_awg
+    try:
+        oracle.buildxhat = lambda d: (x0 * (1 + perturb * rng.standard_normal(len(x0))), names)
+        runs.append(oracle.adjust(od))
+        oracle.buildxhat = orig_x
+
+        def awg_ulp(d, x):
+            A, w, G, ds = orig_awg(d, x)
+            f = w + np.column_stack([d.x, d.y]).reshape(-1)
+            return A, w + np.spacing(np.abs(f)) * rng.choice([-1.0, 1.0], size=len(w)), G, ds
+        oracle.build_awg = awg_ulp
+        runs.append(oracle.adjust(od))
+    finally:
+        oracle.buildxhat, oracle.build_awg = orig_x, orig_awg
+    out = {}
+    for r in runs:
+        e = group_rel_err(r.xhat, ro.xhat, ro.names, ro.dist_scaling)
+        e["sigma02"] = abs(r.sigma02 - ro.sigma02) / ro.sigma02
+        e["deltasum0"] = abs(r.deltasum[0] - ro.deltasum[0]) / ro.deltasum[0]
+        for k, v in e.items():
+            out[k] = max(out.get(k, 0.0), v)
+    return out

@@ -109,3 +109,33 @@ def test_schur_restatement_equals_bordered_inverse(oracle, fba, tmp_path):
     err = group_rel_err(r2.xhat, r1.xhat, r1.names, ds)
     assert max(err.values()) < 1e-9, err
     assert r2.sigma02 == pytest.approx(r1.sigma02, rel=1e-9)
+
+
+def test_pinhole_cam0_is_well_conditioned(oracle, cam0_folders):
+    """The shipped configuration: two exact solvers of the restatement (explicit bordered inverse,
+    main.m:432, and LU of the same system) agree far below the 1e-9 bar on every group, so the GPU
+    parity test holds it to 1e-9 everywhere (tests/test_gpu_parity.py)."""
+    from conftest import solver_spread
+    od = oracle.load_folder(cam0_folders["stage3_pinhole"])
+    ro = oracle.adjust(od)
+    sp = solver_spread(oracle, od, ro)
+    assert max(v for k, v in sp.items() if k not in ("sigma02", "deltasum0")) < 5e-11, sp
+
+
+def test_fisheye_cam0_is_path_sensitive(oracle, cam0_folders):
+    """cam0 under a fish-eye model (pinhole-calibrated start, inner constraints + 3 control points):
+    the high-order distortion terms of the converged solution move by >1e-7 relative when the start
+    is perturbed by 1e-13 -- no implementation can match the reference there at 1e-9."""
+    od = oracle.load_folder(cam0_folders["stage3_fisheye"])
+    r1 = oracle.adjust(od)
+    x0, names = oracle.buildxhat(od)
+    rng = np.random.default_rng(0)
+    orig = oracle.buildxhat
+    try:
+        oracle.buildxhat = lambda d: (x0 * (1 + 1e-13 * rng.standard_normal(len(x0))), names)
+        r2 = oracle.adjust(od)
+    finally:
+        oracle.buildxhat = orig
+    err = group_rel_err(r2.xhat, r1.xhat, r1.names, r1.dist_scaling)
+    assert max(err.values()) > 1e-8
+    assert err["XYZ"] < 1e-8 and err["XYZc"] < 1e-8
