@@ -4,14 +4,20 @@
 // (main.m:428-440).  Here the tie points have already been eliminated (Schur complement), the
 // border is folded in as M = S + G W G' (SPD whenever the bordered matrix is nonsingular; W = one
 // equilibrating weight per constraint column, fba_kernels.hip k_border_weights), and
-//   M = L L'        right-looking blocked Cholesky, NB = 64:
-//                     k_potrf_diag   64x64 diagonal block in LDS (one workgroup)
-//                     k_trsm_panel   rows below the diagonal block, one thread per row
-//                     k_syrk_update  trailing update C -= L_i L_j' on v_mfma_f64_16x16x4_f64
-//   forward solve    the right-hand sides [r | G W^1/2] are stored as extra ROWS below M, so the
-//                    factorisation's panel solves compute Y' = (L^-1 B)' as a by-product
-//   border combine   H = Z'Z, h = Z'y, k = -H^-1 h, y <- y + Z k      (Z, y = forward-solved G W^1/2, r)
-//   backward solve   L' x = y, one launch per block row (k_trsv_bwd)
+//
+//   M = L L'        right-looking blocked Cholesky, NB = 128, every step three launches:
+//     k_potrf128    the 128x128 diagonal block, LDS-resident in one workgroup: 8 sub-panels of 16
+//                   (16x16 factor in registers with v_readlane broadcasts, its 16x16 inverse, then
+//                   the in-block panel solve and trailing update on v_mfma_f64_16x16x4_f64); writes
+//                   L_kk and the eight 16x16 inverses D_s = L_ss^-1 used by the solves below
+//     k_trsm128     the panel below, X = A L_kk^-T by blocked substitution
+//                   X_s = (A_s - sum_{t<s} X_t L_st^T) D_s^T: all MFMA, 16 rows per wave
+//     k_syrk128     trailing update C -= X_i X_j^T, 128x128 tiles (4 waves x 64x64), K = 128
+//                   staged through LDS in 32-deep slices, v_mfma_f64_16x16x4_f64
+//   forward solve   the right-hand sides [r | G W^1/2] are stored as extra ROWS below M (one extra
+//                   block row), so the panel solves compute Y' = (L^-1 B)' as a by-product
+//   border combine  H = Z'Z, h = Z'y, k = -H^-1 h, y <- y + Z k      (Z, y = forward-solved G W^1/2, r)
+//   backward solve  L' x = y, one launch per block row (k_trsv_bwd128, blocked with the D_s)
 // so delta_c = -x = -M^-1 (r + G W^1/2 k) satisfies [S G; G' 0][delta; W^1/2 k] = [-r; 0] as the
 // reference's bordered system does.
 #include "fba_internal.h"
@@ -20,150 +26,288 @@ namespace fba {
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
+constexpr int CB = 128;   // outer block
+constexpr int IB = 16;    // inner block (MFMA tile)
+constexpr int LDA = 130;  // LDS row stride in doubles for 128-wide tiles: bank = (4r + 2k) mod 64
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ dbl4 mfma(double a, double b, dbl4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_potrf_diag(double* __restrict__ S, int64_t ld, int64_t k0,
-                                                    double* __restrict__ scal) {
-    __shared__ double A[64][65];
-    const int tid = threadIdx.x;
-    for (int idx = tid; idx < 64 * 64; idx += 256) {
-        const int r = idx >> 6, c = idx & 63;
-        A[r][c] = S[(k0 + r) * ld + k0 + c];
+// k_potrf128: factor the 128x128 diagonal block at (k0, k0); 256 threads
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_t ld, int64_t k0,
+                                                  double* __restrict__ dinv, double* __restrict__ scal) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* A = smem;                  // [128][LDA]
+    double* Dl = smem + CB * LDA;      // [16][17] current inverse D_s
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    for (int idx = tid; idx < CB * CB / 2; idx += 256) {
+        const int r = idx >> 6, c = (idx & 63) * 2;
+        const double2 v = *reinterpret_cast<const double2*>(S + (k0 + r) * ld + k0 + c);
+        A[r * LDA + c] = v.x;
+        A[r * LDA + c + 1] = v.y;
     }
     __syncthreads();
-    for (int j = 0; j < 64; ++j) {
-        if (tid == 0) {
-            double d = A[j][j];
-            if (!(d > 0.0)) {
-                if (scal[1] == 0.0) scal[1] = (double)(k0 + j + 1);
-                d = 1.0;
-            }
-            A[j][j] = sqrt(d);
-        }
-        __syncthreads();
-        if (tid > j && tid < 64) A[tid][j] /= A[j][j];
-        __syncthreads();
-        for (int idx = tid; idx < 64 * 64; idx += 256) {
-            const int i = idx >> 6, l = idx & 63;
-            if (l > j && i >= l) A[i][l] -= A[i][j] * A[l][j];
-        }
-        __syncthreads();
-    }
-    for (int idx = tid; idx < 64 * 64; idx += 256) {
-        const int r = idx >> 6, c = idx & 63;
-        if (c <= r) S[(k0 + r) * ld + k0 + c] = A[r][c];
-    }
-}
-
-// rows [row0, row0 + 64*gridDim.x): A_ik <- A_ik L_kk^-T  (one thread per row)
-__global__ __launch_bounds__(64) void k_trsm_panel(double* __restrict__ S, int64_t ld, int64_t k0, int64_t row0) {
-    __shared__ double Lk[64][65];
-    __shared__ double inv[64];
-    const int tid = threadIdx.x;
-    for (int c = 0; c < 64; ++c) Lk[tid][c] = S[(k0 + tid) * ld + k0 + c];
-    __syncthreads();
-    inv[tid] = 1.0 / Lk[tid][tid];
-    __syncthreads();
-    const int64_t row = row0 + (int64_t)blockIdx.x * 64 + tid;
-    double* a = S + row * ld + k0;
-    double x[64];
-#pragma unroll
-    for (int j = 0; j < 64; ++j) x[j] = a[j];
-#pragma unroll
-    for (int j = 0; j < 64; ++j) {
-        double s = x[j];
-#pragma unroll
-        for (int m = 0; m < j; ++m) s -= x[m] * Lk[j][m];
-        x[j] = s * inv[j];
-    }
-#pragma unroll
-    for (int j = 0; j < 64; ++j) a[j] = x[j];
-}
-
-// trailing update of block (i, j), j <= i, both below panel kb; i == nb is the RHS block row.
-// 256 threads = 4 waves, each wave a 32x32 quadrant = 2x2 tiles of 16x16 (v_mfma_f64_16x16x4_f64).
-__global__ __launch_bounds__(256) void k_syrk_update(double* __restrict__ S, int64_t ld, int64_t kb, int64_t nb) {
-    const int64_t bi = kb + 1 + blockIdx.y;
-    const int64_t bj = kb + 1 + blockIdx.x;
-    if (bi < nb && bj > bi) return;
-    __shared__ double As[64][66];
-    __shared__ double Bs[64][66];
-    const int tid = threadIdx.x;
-    const int64_t k0 = kb * 64;
-    {
-        const int r = tid >> 2, q = (tid & 3) * 16;
-        const double* ga = S + (bi * 64 + r) * ld + k0 + q;
-        const double* gb = S + (bj * 64 + r) * ld + k0 + q;
-#pragma unroll
-        for (int c = 0; c < 16; c += 2) {
-            const double2 va = *reinterpret_cast<const double2*>(ga + c);
-            const double2 vb = *reinterpret_cast<const double2*>(gb + c);
-            As[r][q + c] = va.x; As[r][q + c + 1] = va.y;
-            Bs[r][q + c] = vb.x; Bs[r][q + c + 1] = vb.y;
-        }
-    }
-    __syncthreads();
-    const int wave = tid >> 6, lane = tid & 63;
-    const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
     const int lr = lane & 15, lk = lane >> 4;
-    dbl4 acc[2][2];
+    for (int s = 0; s < CB / IB; ++s) {
+        const int c0 = s * IB;
+        if (wave == 0) {
+            // (a) 16x16 factor: lane i (< 16) holds row c0+i of the sub-block in registers
+            double a[IB];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+            for (int c = 0; c < IB; ++c) a[c] = (lane < IB) ? A[(c0 + lane) * LDA + c0 + c] : 0.0;
+            bool bad = false;
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+            for (int j = 0; j < IB; ++j) {
+                double d = readlane_d(a[j], j);
+                if (!(d > 0.0)) { bad = true; d = 1.0; }
+                const double sd = sqrt(d), inv = 1.0 / sd;
+                a[j] = (lane == j) ? sd : (lane > j ? a[j] * inv : a[j]);
 #pragma unroll
-    for (int kk = 0; kk < 64; kk += 4) {
-        double av[2], bv[2];
+                for (int l = j + 1; l < IB; ++l) a[l] -= a[j] * readlane_d(a[j], l);
+            }
+            if (bad && lane == 0 && scal[1] == 0.0) scal[1] = (double)(k0 + c0 + 1);
+            if (lane < IB) {
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            av[t] = As[wr + t * 16 + lr][kk + lk];
-            bv[t] = Bs[wc + t * 16 + lr][kk + lk];
+                for (int c = 0; c < IB; ++c)
+                    if (c <= lane) A[(c0 + lane) * LDA + c0 + c] = a[c];
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the block's L is in LDS
+            __builtin_amdgcn_wave_barrier();
+            // (b) D_s = L_ss^-1: lane c (< 16) computes column c by forward substitution
+            double x[IB];
+#pragma unroll
+            for (int i = 0; i < IB; ++i) {
+                double acc = (i == lane) ? 1.0 : 0.0;
+#pragma unroll
+                for (int m = 0; m < i; ++m) acc -= A[(c0 + i) * LDA + c0 + m] * x[m];
+                x[i] = acc / A[(c0 + i) * LDA + c0 + i];
+            }
+            if (lane < IB) {
+#pragma unroll
+                for (int i = 0; i < IB; ++i) {
+                    const double v = (i >= lane) ? x[i] : 0.0;
+                    Dl[i * 17 + lane] = v;
+                    dinv[((k0 / CB) * (CB / IB) + s) * (IB * IB) + i * IB + lane] = v;
+                }
+            }
+        }
+        __syncthreads();
+        // (c) in-block panel solve: rows below the sub-block, X = A_s D_s^T  (16-row tiles)
+        for (int t = s + 1 + wave; t < CB / IB; t += 4) {
+            const int r0 = t * IB;
+            dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int kk = 0; kk < IB; kk += 4) {
+                const double av = A[(r0 + lr) * LDA + c0 + kk + lk];
+                const double bv = Dl[lr * 17 + kk + lk];  // B[k][n] = D[n][k]
+                acc = mfma(av, bv, acc);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) A[(r0 + lk + 4 * r) * LDA + c0 + lr] = acc[r];
+        }
+        __syncthreads();
+        // (d) in-block trailing update of the lower tiles (ti >= tj > s), K = 16
+        const int m = CB / IB - 1 - s;
+        const int ntile = m * (m + 1) / 2;
+        for (int q = wave; q < ntile; q += 4) {
+            int ti = 0, rem = q;
+            while (rem > ti) { rem -= ti + 1; ++ti; }
+            const int tj = rem;
+            const int R = (s + 1 + ti) * IB, C = (s + 1 + tj) * IB;
+            dbl4 acc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] = A[(R + lk + 4 * r) * LDA + C + lr];
+#pragma unroll
+            for (int kk = 0; kk < IB; kk += 4) {
+                const double av = -A[(R + lr) * LDA + c0 + kk + lk];
+                const double bv = A[(C + lr) * LDA + c0 + kk + lk];
+                acc = mfma(av, bv, acc);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) A[(R + lk + 4 * r) * LDA + C + lr] = acc[r];
+        }
+        __syncthreads();
+    }
+    for (int idx = tid; idx < CB * CB; idx += 256) {
+        const int r = idx >> 7, c = idx & 127;
+        if (c <= r) S[(k0 + r) * ld + k0 + c] = A[r * LDA + c];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_trsm128: rows [row0, row0 + 64*gridDim.x) of the panel at columns [k0, k0+128):
+//   X = A L^-T by blocked substitution, X_s = (A_s - sum_{t<s} X_t L_st^T) D_s^T.
+// 256 threads = 4 waves x 16 rows; each wave works on its own rows (no barriers).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t ld, int64_t k0, int64_t row0,
+                                                 const double* __restrict__ dinv) {
+    __shared__ __attribute__((aligned(16))) double X[4][IB][LDA];
+    __shared__ __attribute__((aligned(16))) double T[4][IB][17];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int lr = lane & 15, lk = lane >> 4;
+    const int64_t rbase = row0 + (int64_t)blockIdx.x * 64 + wave * IB;
+    double* Xw = &X[wave][0][0];
+    double* Tw = &T[wave][0][0];
+    // load the wave's 16 x 128 panel rows
+    for (int idx = lane; idx < IB * CB / 2; idx += 64) {
+        const int r = idx >> 6, c = (idx & 63) * 2;
+        const double2 v = *reinterpret_cast<const double2*>(S + (rbase + r) * ld + k0 + c);
+        Xw[r * LDA + c] = v.x;
+        Xw[r * LDA + c + 1] = v.y;
+    }
+    const double* L = S + k0 * ld + k0;
+    const double* Dk = dinv + (k0 / CB) * (CB / IB) * (IB * IB);
+    for (int s = 0; s < CB / IB; ++s) {
+        const int c0 = s * IB;
+        // Z = A_s - sum_{t<s} X_t L_st^T : output 16x16, K = 16 s
+        dbl4 acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = Xw[(lk + 4 * r) * LDA + c0 + lr];
+        for (int kk = 0; kk < c0; kk += 4) {
+            const double av = -Xw[lr * LDA + kk + lk];
+            const double bv = L[(c0 + lr) * ld + kk + lk];  // B[k][n] = L[c0+n][k]
+            acc = mfma(av, bv, acc);
+        }
+        // Z (D layout) -> LDS, then X_s = Z D_s^T
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Tw[(lk + 4 * r) * 17 + lr] = acc[r];
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+        dbl4 out = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < IB; kk += 4) {
+            const double av = Tw[lr * 17 + kk + lk];
+            const double bv = Dk[s * IB * IB + lr * IB + kk + lk];  // B[k][n] = D[n][k]
+            out = mfma(av, bv, out);
         }
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-                acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
+        for (int r = 0; r < 4; ++r) Xw[(lk + 4 * r) * LDA + c0 + lr] = out[r];
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
     }
-    // D layout (f64 16x16x4): lane holds D[row = (lane>>4) + 4*r][col = lane & 15]
+    for (int idx = lane; idx < IB * CB / 2; idx += 64) {
+        const int r = idx >> 6, c = (idx & 63) * 2;
+        double2 v;
+        v.x = Xw[r * LDA + c];
+        v.y = Xw[r * LDA + c + 1];
+        *reinterpret_cast<double2*>(S + (rbase + r) * ld + k0 + c) = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_syrk128: trailing update C(bi,bj) -= X_bi X_bj^T, 128x128 tiles, K = 128 in 32-deep LDS slices.
+// Tiles are enumerated by the host: j in [jlo, jhi) block columns, i >= j block rows (i == nb is the
+// RHS block row).  4 waves, each a 64x64 quadrant = 4x4 MFMA tiles.
+// ------------------------------------------------------------------------------------------------
+constexpr int KS = 32;
+constexpr int LDK = 34;   // LDS stride of a 32-deep slice: bank = (4r + 2k) mod 64, conflict-free
+
+__global__ __launch_bounds__(256) void k_syrk128(double* __restrict__ S, int64_t ld, int64_t kb, int64_t nb,
+                                                 int64_t jlo, int64_t jhi) {
+    // decode blockIdx.x -> (bi, bj), bj in [jlo, jhi), bi in [bj, nb] (nb = RHS block row)
+    int64_t q = blockIdx.x, bj = jlo, bi = 0;
+    for (;;) {
+        const int64_t cnt = nb - bj + 1;
+        if (q < cnt) { bi = bj + q; break; }
+        q -= cnt;
+        ++bj;
+    }
+    (void)jhi;
+    __shared__ __attribute__((aligned(16))) double As[CB][LDK];
+    __shared__ __attribute__((aligned(16))) double Bs[CB][LDK];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int lr = lane & 15, lk = lane >> 4;
+    const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
+    const int64_t k0 = kb * CB;
+    dbl4 acc[4][4];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < 4; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+    const double* ga = S + (bi * CB) * ld + k0;
+    const double* gb = S + (bj * CB) * ld + k0;
+    for (int ks = 0; ks < CB; ks += KS) {
+        // 128 rows x 32 cols per operand: 256 threads x 8 doubles (4 x double2)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int idx = tid + p * 256;         // 512 (row, quad) pairs
+            const int r = idx >> 2, c = (idx & 3) * 8;
+            const double* pa = ga + r * ld + ks + c;
+            const double* pb = gb + r * ld + ks + c;
+#pragma unroll
+            for (int h = 0; h < 8; h += 2) {
+                const double2 va = *reinterpret_cast<const double2*>(pa + h);
+                const double2 vb = *reinterpret_cast<const double2*>(pb + h);
+                As[r][c + h] = va.x; As[r][c + h + 1] = va.y;
+                Bs[r][c + h] = vb.x; Bs[r][c + h + 1] = vb.y;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < KS; kk += 4) {
+            double av[4], bv[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                av[t] = As[wr + t * 16 + lr][kk + lk];
+                bv[t] = Bs[wc + t * 16 + lr][kk + lk];
+            }
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) acc[a][b] = mfma(av[a], bv[b], acc[a][b]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int64_t row = bi * 64 + wr + a * 16 + lk + 4 * r;
-                const int64_t col = bj * 64 + wc + b * 16 + lr;
+                const int64_t row = bi * CB + wr + a * 16 + lk + 4 * r;
+                const int64_t col = bj * CB + wc + b * 16 + lr;
                 S[row * ld + col] -= acc[a][b][r];
             }
 }
 
 // ------------------------------------------------------------------------------------------------
 // border combine (inner constraints): RHS rows n_pad + 0 (y) and n_pad + 1..7 (Z), length n
+// ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, int64_t ld, int64_t n_pad) {
-    __shared__ double red[256];
+    __shared__ double red[8][256];
     __shared__ double H[7][8];
     __shared__ double kk[7];
     const int tid = threadIdx.x;
     const double* y = S + n_pad * ld;
     for (int a = 0; a < 7; ++a) {
         const double* za = S + (n_pad + 1 + a) * ld;
-        for (int b = 0; b < 8; ++b) {
-            if (b > 0 && b - 1 < a) continue;  // symmetric: H[a][b-1] = H[b-1][a]
-            const double* zb = (b == 0) ? y : S + (n_pad + b) * ld;
-            double acc = 0.0;
-            for (int64_t i = tid; i < n_pad; i += 256) acc += za[i] * zb[i];
-            red[tid] = acc;
-            __syncthreads();
-            for (int w = 128; w > 0; w >>= 1) {
-                if (tid < w) red[tid] += red[tid + w];
-                __syncthreads();
-            }
-            if (tid == 0) {
-                H[a][b] = red[0];
-                if (b > 0) H[b - 1][a + 1] = red[0];
-            }
+        double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int64_t i = tid; i < n_pad; i += 256) {
+            const double z = za[i];
+            acc[0] += z * y[i];
+            for (int b = a; b < 7; ++b) acc[1 + b] += z * S[(n_pad + 1 + b) * ld + i];
+        }
+        for (int b = 0; b < 8; ++b) red[b][tid] = acc[b];
+        __syncthreads();
+        for (int w = 128; w > 0; w >>= 1) {
+            if (tid < w)
+                for (int b = 0; b < 8; ++b) red[b][tid] += red[b][tid + w];
             __syncthreads();
         }
+        if (tid == 0) {
+            H[a][0] = red[0][0];
+            for (int b = a; b < 7; ++b) { H[a][1 + b] = red[1 + b][0]; H[b][1 + a] = red[1 + b][0]; }
+        }
+        __syncthreads();
     }
     if (tid == 0) {
         // solve H[:,1..7] k = -H[:,0]  (SPD 7x7; Gaussian elimination with partial pivoting)
@@ -202,34 +346,52 @@ __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, 
     }
 }
 
-// backward solve step: x_kb = L_kbkb^-T y_kb (every block redundantly), then block jb < kb updates
-// y_jb -= L_{kb,jb}^T x_kb; block jb == kb stores x_kb.  One wave per block.
-__global__ __launch_bounds__(64) void k_trsv_bwd(double* __restrict__ S, int64_t ld, int64_t n_pad, int64_t kb,
-                                                 double* __restrict__ X) {
-    __shared__ double Lk[64][65];
-    __shared__ double xs[64];
-    const int lane = threadIdx.x;
-    const int64_t k0 = kb * 64;
-    for (int r = 0; r < 64; ++r) Lk[r][lane] = S[(k0 + r) * ld + k0 + lane];
+// ------------------------------------------------------------------------------------------------
+// backward solve step kb: every workgroup solves L_kk^T x = y_kb (blocked with the D_s, 128 threads),
+// then workgroup jb < kb updates y_jb -= L_{kb,jb}^T x; workgroup kb stores x.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(128) void k_trsv_bwd128(double* __restrict__ S, int64_t ld, int64_t n_pad, int64_t kb,
+                                                     const double* __restrict__ dinv, double* __restrict__ X) {
+    __shared__ double xs[CB];
+    __shared__ double part[8][IB];
+    const int tid = threadIdx.x;
+    const int64_t k0 = kb * CB;
     double* y = S + n_pad * ld;
-    double yl = y[k0 + lane];
+    xs[tid] = y[k0 + tid];
     __syncthreads();
-    for (int i = 63; i >= 0; --i) {
-        if (lane == i) xs[i] = yl / Lk[i][i];
+    const double* L = S + k0 * ld + k0;
+    const double* Dk = dinv + kb * (CB / IB) * (IB * IB);
+    for (int s = CB / IB - 1; s >= 0; --s) {
+        const int c0 = s * IB;
+        // z_c = y_{c0+c} - sum_{r >= c0+16} L[r][c0+c] x_r : 8 threads per column, strided rows
+        const int c = tid & 15, g = tid >> 4;
+        double acc = 0.0;
+        for (int r = c0 + IB + g; r < CB; r += 8) acc += L[r * ld + c0 + c] * xs[r];
+        part[g][c] = acc;
         __syncthreads();
-        if (lane < i) yl -= Lk[i][lane] * xs[i];
+        if (tid < IB) {
+            double z = xs[c0 + tid];
+            for (int h = 0; h < 8; ++h) z -= part[h][tid];
+            part[0][tid] = z;  // reuse after the reads above (same thread wrote part[*][tid] reads only)
+        }
+        __syncthreads();
+        if (tid < IB) {
+            // x_c = sum_m D[m][c] z_m   (D_s^T z)
+            double v = 0.0;
+            for (int m = 0; m < IB; ++m) v += Dk[s * IB * IB + m * IB + tid] * part[0][m];
+            xs[c0 + tid] = v;
+        }
+        __syncthreads();
     }
-    __syncthreads();
     const int64_t jb = blockIdx.x;
     if (jb == kb) {
-        X[k0 + lane] = xs[lane];
+        X[k0 + tid] = xs[tid];
         return;
     }
-    // y_jb[c] -= sum_r L[k0 + r][jb*64 + c] * x[r]
     double acc = 0.0;
-    const double* Lr = S + k0 * ld + jb * 64 + lane;
-    for (int r = 0; r < 64; ++r) acc += Lr[r * ld] * xs[r];
-    y[jb * 64 + lane] -= acc;
+    const double* Lr = S + k0 * ld + jb * CB + tid;
+    for (int r = 0; r < CB; ++r) acc += Lr[r * ld] * xs[r];
+    y[jb * CB + tid] -= acc;
 }
 
 __global__ void k_neg_copy(const double* __restrict__ X, double* __restrict__ delta, int64_t u_c) {
@@ -239,24 +401,35 @@ __global__ void k_neg_copy(const double* __restrict__ X, double* __restrict__ de
 
 // ------------------------------------------------------------------------------------------------
 int launch_cholesky(Ctx& c) {
-    const int64_t ld = c.L.ld, nb = c.L.n_pad / NB;
+    const int64_t ld = c.L.ld, nb = c.L.n_pad / CB;
+    const size_t lds_potrf = sizeof(double) * (CB * LDA + IB * 17);
     for (int64_t kb = 0; kb < nb; ++kb) {
-        k_potrf_diag<<<1, 256, 0, c.stream>>>(c.d_S, ld, kb * NB, c.d_scal);
-        k_trsm_panel<<<(unsigned)(nb - kb), 64, 0, c.stream>>>(c.d_S, ld, kb * NB, (kb + 1) * NB);
-        const int64_t m = nb - kb - 1;
-        if (m > 0) k_syrk_update<<<dim3((unsigned)m, (unsigned)(m + 1)), 256, 0, c.stream>>>(c.d_S, ld, kb, nb);
+        k_potrf128<<<1, 256, lds_potrf, c.stream>>>(c.d_S, ld, kb * CB, c.d_dinv, c.d_scal);
+        // panel rows below the diagonal block, RHS block row included: (nb - kb) * 128 rows
+        k_trsm128<<<(unsigned)((nb - kb) * 2), 256, 0, c.stream>>>(c.d_S, ld, kb * CB, (kb + 1) * CB, c.d_dinv);
+        const int64_t m = nb - kb - 1;  // trailing block columns
+        if (m > 0) {
+            const int64_t tiles = m * (m + 1) / 2 + m;  // lower tiles + RHS block row
+            k_syrk128<<<(unsigned)tiles, 256, 0, c.stream>>>(c.d_S, ld, kb, nb, kb + 1, nb);
+        }
     }
     FBA_HIP(hipGetLastError());
     return FBA_OK;
 }
 
 int launch_backward(Ctx& c) {
-    const int64_t ld = c.L.ld, nb = c.L.n_pad / NB;
+    const int64_t ld = c.L.ld, nb = c.L.n_pad / CB;
     if (c.set.inner_constraints) k_border_combine<<<1, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad);
     for (int64_t kb = nb - 1; kb >= 0; --kb)
-        k_trsv_bwd<<<(unsigned)(kb + 1), 64, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, kb, c.d_X);
+        k_trsv_bwd128<<<(unsigned)(kb + 1), 128, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, kb, c.d_dinv, c.d_X);
     k_neg_copy<<<(unsigned)((c.L.u_c + 255) / 256), 256, 0, c.stream>>>(c.d_X, c.d_delta, c.L.u_c);
     FBA_HIP(hipGetLastError());
+    return FBA_OK;
+}
+
+int chol_setup(Ctx& c) {
+    const size_t lds_potrf = sizeof(double) * (CB * LDA + IB * 17);
+    FBA_HIP(hipFuncSetAttribute((const void*)k_potrf128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_potrf));
     return FBA_OK;
 }
 

@@ -16,7 +16,7 @@
 
 namespace fba {
 
-constexpr int NB = 64;        // Cholesky block size (rows/cols of one panel block)
+constexpr int NB = 128;       // Cholesky block size (rows/cols of one panel block, fba_chol.hip)
 constexpr int NSLAB = 64;     // slabs per camera in the two-stage camera-block reduction
 
 // per-image device table (k_params): eop[6], M[9], dM/domega[9], dM/dphi[9], dM/dkappa[9], pad
@@ -90,7 +90,8 @@ struct Ctx {
     int64_t n_lp_pad = 0;
     double* d_slab = nullptr;    // camera reduction slabs
     double* d_S = nullptr;       // [(n_pad+NB)*ld] normal matrix (lower) + RHS rows
-    double* d_X = nullptr;       // [nrhs*n_pad] solution of the bordered solve (row per rhs)
+    double* d_X = nullptr;       // [n_pad] solution of the bordered solve
+    double* d_dinv = nullptr;    // [(n_pad/NB)*8*256] inverses of the 16x16 diagonal blocks of L
     double* d_scal = nullptr;    // scalars: [1] Cholesky failure flag, [2] sumabs, [8..14] border weights
     double* d_part = nullptr;    // block partial sums
     int n_part = 0;
@@ -128,6 +129,7 @@ int launch_linearize(Ctx& c);
 int launch_point(Ctx& c);
 int launch_accumulate(Ctx& c);   // zero S, image, pair, camera blocks, unit diagonal for unused
 int launch_border(Ctx& c);       // alpha, G G^T border, RHS rows
+int chol_setup(Ctx& c);          // one-time kernel attributes
 int launch_cholesky(Ctx& c);     // factor + forward solve of RHS rows
 int launch_backward(Ctx& c);     // border combine + backward solve -> delta_c
 int launch_backsub_update(Ctx& c);

@@ -18,6 +18,6 @@ for step in "$@"; do
     bench) run bench 600 python bench.py --steps 5 --warmup 1 --verbose ;;
     benchq) run bench 600 python bench.py --steps 5 --warmup 1 --no-cpu --verbose ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-          run prof 600 rocprofv3 --kernel-trace --stats -d "$PWD/gpurun_out/prof" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
+          run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
   esac
 done
