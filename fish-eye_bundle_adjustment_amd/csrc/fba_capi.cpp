@@ -157,7 +157,7 @@ static void partition(const fba_problem* p, int world, std::vector<int32_t>& tie
 
 static void destroy(Ctx* c) {
     if (!c) return;
-    void* ptrs[] = {c->d_xy, c->d_img, c->d_cam, c->d_pt, c->d_ctl, c->d_lp_tie, c->d_lp_start, c->d_lp_cam,
+    void* ptrs[] = {c->d_chunk_obs, c->d_chunk_pt, c->d_xy, c->d_img, c->d_cam, c->d_pt, c->d_ctl, c->d_lp_tie, c->d_lp_start, c->d_lp_cam,
                     c->d_img_start, c->d_img_obs, c->d_cam_lp, c->d_cam_ctl, c->d_pair_e, c->d_pair_start,
                     c->d_pair_ij, c->d_xfull, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
                     c->d_pt_tab, c->d_slab, c->d_S, c->d_X, c->d_dinv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
@@ -268,6 +268,29 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     c->n_obs_pad = round_up(std::max<int64_t>(c->n_obs, 1), 64);
     c->n_lp_pad = round_up(std::max<int64_t>(c->n_lp, 1), 64);
 
+    // k_lin_point chunks: consecutive whole tie points with <= 256 observations, then control ones
+    std::vector<int32_t> chunk_obs{0}, chunk_pt{0};
+    for (int64_t lp = 0; lp < c->n_lp; ++lp) {
+        if (lp_start[lp + 1] - lp_start[lp] > 256) {
+            set_error("a tie point with more than 256 observations: not implemented in this build");
+            destroy(c);
+            return FBA_ERR_UNSUPPORTED;
+        }
+        if (lp_start[lp + 1] - chunk_obs.back() > 256) {
+            chunk_obs.push_back(lp_start[lp]);
+            chunk_pt.push_back((int32_t)lp);
+        }
+    }
+    if (c->n_lp > 0) {
+        chunk_obs.push_back(lp_start[c->n_lp]);
+        chunk_pt.push_back((int32_t)c->n_lp);
+    }
+    for (int64_t o = c->n_obs_tie; o < c->n_obs; o += 256) {
+        chunk_obs.push_back((int32_t)std::min<int64_t>(o + 256, c->n_obs));
+        chunk_pt.push_back((int32_t)c->n_lp);
+    }
+    c->n_chunks = (int64_t)chunk_obs.size() - 1;
+
     // per image CSR of local observations (PHO order within an image)
     std::vector<int32_t> img_start(L.n_img + 1, 0), img_obs(c->n_obs);
     {
@@ -344,7 +367,8 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         (rc = upload(&c->d_pair_e, pair_e)) || (rc = upload(&c->d_pair_start, pair_start)) ||
         (rc = upload(&c->d_pair_ij, pair_ij)) || (rc = upload(&c->d_xfull, c->xfull0)) ||
         (rc = upload(&c->d_caminfo, caminfo)) || (rc = upload(&c->d_active, active)) ||
-        (rc = upload(&c->d_counted, counted)) || (rc = upload(&c->d_obs_pho, pho))) {
+        (rc = upload(&c->d_counted, counted)) || (rc = upload(&c->d_obs_pho, pho)) ||
+        (rc = upload(&c->d_chunk_obs, chunk_obs)) || (rc = upload(&c->d_chunk_pt, chunk_pt))) {
         destroy(c);
         return rc;
     }

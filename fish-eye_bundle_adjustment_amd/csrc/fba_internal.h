@@ -17,7 +17,7 @@
 namespace fba {
 
 constexpr int NB = 128;       // Cholesky block size (rows/cols of one panel block, fba_chol.hip)
-constexpr int NSLAB = 64;     // slabs per camera in the two-stage camera-block reduction
+constexpr int NSLAB = 512;    // slabs per camera in the two-stage camera-block reduction
 
 // per-image device table (k_params): eop[6], M[9], dM/domega[9], dM/dphi[9], dM/dkappa[9], pad
 constexpr int IMG_TAB = 48;
@@ -71,6 +71,9 @@ struct Ctx {
     int32_t* d_img_obs = nullptr;
     int32_t* d_cam_lp = nullptr;     // [n_cam+1] local point range per camera (points sorted by camera)
     int32_t* d_cam_ctl = nullptr;    // [n_cam+1] control obs range per camera (within control section)
+    int64_t n_chunks = 0;            // k_lin_point workgroups: whole tie points, <= 256 observations
+    int32_t* d_chunk_obs = nullptr;  // [n_chunks+1] observation range of each chunk
+    int32_t* d_chunk_pt = nullptr;   // [n_chunks+1] local point range of each chunk
     int64_t n_pairs = 0, n_pair_terms = 0;
     int32_t* d_pair_e = nullptr;     // [2*n_pairs] (e1,e2) with e1 > e2
     int32_t* d_pair_start = nullptr; // [n_pairs+1]
@@ -82,10 +85,10 @@ struct Ctx {
     double* d_cam_tab = nullptr; // [n_cam*cam_tab_stride]
     int cam_tab_stride = 0;
     double* d_G = nullptr;       // [n_img*42] inner-constraint blocks (6x7 per image, row-major)
-    double* d_J = nullptr;       // [ncomp*n_obs_pad] per-obs Jacobian rows + misclosure
+    double* d_J = nullptr;       // [n_obs_pad][ncomp] per-obs Jacobian rows + misclosure (obs-major)
     int ncomp = 0;
-    double* d_WT = nullptr;      // [36*n_obs_pad] per-obs W (18) and T = W V^-1 (18)
-    double* d_pt_tab = nullptr;  // [pt_comp*n_lp_pad] Vinv(6) vb(3) b(3) Wc(3cw) Tc(3cw)
+    double* d_WT = nullptr;      // [n_obs_pad][36] per-obs W (18) and T = W V^-1 (18)
+    double* d_pt_tab = nullptr;  // [n_lp_pad][pt_comp] Vinv(6) vb(3) b(3) Wc(3cw) Tc(3cw)
     int pt_comp = 0;
     int64_t n_lp_pad = 0;
     double* d_slab = nullptr;    // camera reduction slabs

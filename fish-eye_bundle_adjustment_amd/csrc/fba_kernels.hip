@@ -4,11 +4,11 @@
 //   k_params        per image: EOPs + rotation M and dM/d(omega,phi,kappa) (BuildAwG.m:163-165),
 //                   inner-constraint block G (BuildAwG.m:516-523); per camera: IOPs, rmax^(2j)
 //                   scales (BuildAwG.m:422-426)
-//   k_linearize     one thread per image point: misclosure w (BuildAwG.m:505-512) and the 2 Jacobian
+//   k_lin_point     one thread per image point: misclosure w (BuildAwG.m:505-512) and the 2 Jacobian
 //                   rows over [6 EOP | xp yp c K1..Knk P1 P2 | X Y Z] (BuildAwG.m:216-503) by the
-//                   chain rule of the forward model (BuildAwG.m:163-213)
-//   k_point         one thread per tie point: V = Jp'PJp, Vinv, the coupling blocks W = Je'PJp and
-//                   T = W Vinv per observation (Schur elimination of the tie points)
+//                   chain rule of the forward model (BuildAwG.m:163-213); then, per chunk of whole
+//                   tie points in LDS, V = Jp'PJp, Vinv and the couplings W = Je'PJp, T = W Vinv
+//                   (Schur elimination of the tie points)
 //   k_image         one workgroup per image: reduced diagonal block, image-camera block, RHS rows
 //   k_pairs         one wave per co-visible image pair: off-diagonal reduced blocks
 //   k_cam_*         two-stage deterministic reduction of the camera block
@@ -23,7 +23,6 @@
 
 namespace fba {
 
-__device__ __forceinline__ int64_t jc_index(int r, int col, int nj) { return (int64_t)(r * nj + col); }
 
 // ------------------------------------------------------------------------------------------------
 // k_params: per-image and per-camera tables
@@ -92,32 +91,28 @@ __global__ void k_params(const double* __restrict__ xfull, const double* __restr
     }
 }
 
+
 // ------------------------------------------------------------------------------------------------
-// k_linearize: one thread per image point
+// Device layouts (observation-major so a thread / wave touches contiguous bytes):
+//   J   [o][JS], JS = 2*NJ + 2: Jacobian row x (NJ columns: 6 EOP | CW camera | 3 XYZ), row y, w
+//   WT  [o][36]: W[a][m] = (Je' P Jp)[a][m] at 3a+m, T = W Vinv at 18+3a+m
+//   PT  [p][PS], PS = 12 + 6*CW: Vinv (00 01 02 11 12 22), vb = Vinv b, b, Wc[c][m], Tc = Wc Vinv
 // ------------------------------------------------------------------------------------------------
 template <int NK>
-__global__ __launch_bounds__(256) void k_linearize(
-    const double* __restrict__ xy, const int32_t* __restrict__ img, const int32_t* __restrict__ cam,
-    const int32_t* __restrict__ pt, const int32_t* __restrict__ lp_tie, const double* __restrict__ ctl,
-    const double* __restrict__ xfull, const double* __restrict__ img_tab, const double* __restrict__ cam_tab,
-    double* __restrict__ J, int64_t n_obs, int64_t stride, int64_t u_c, int type, int cam_stride,
-    unsigned eop_mask, unsigned cam_mask) {
-    constexpr int CW = 5 + NK;
-    constexpr int NJ = 9 + CW;
-    int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (o >= n_obs) return;
-    const double x = xy[2 * o], y = xy[2 * o + 1];
-    const int e = img[o], k = cam[o], p = pt[o];
-    const double* it = img_tab + (int64_t)e * IMG_TAB;
-    const double* ct = cam_tab + (int64_t)k * cam_stride;
-    double X, Y, Z;
-    if (p >= 0) {
-        const double* q = xfull + u_c + 3 * (int64_t)lp_tie[p];
-        X = q[0]; Y = q[1]; Z = q[2];
-    } else {
-        const double* q = ctl + 3 * (int64_t)(-1 - p);
-        X = q[0]; Y = q[1]; Z = q[2];
-    }
+struct Lay {
+    static constexpr int CW = 5 + NK;
+    static constexpr int NJ = 9 + CW;
+    static constexpr int JS = 2 * NJ + 2;
+    static constexpr int PS = 12 + 6 * CW;
+};
+
+// Forward model and Jacobian of one image point (BuildAwG.m:163-503 by the chain rule).
+template <int NK>
+__device__ __forceinline__ void obs_model(double x, double y, const double* __restrict__ it,
+                                          const double* __restrict__ ct, double X, double Y, double Z, bool tie,
+                                          int type, unsigned eop_mask, unsigned cam_mask,
+                                          double (&jr)[2][Lay<NK>::NJ], double& w0, double& w1) {
+    constexpr int CW = Lay<NK>::CW;
     const double d0 = X - it[0], d1 = Y - it[1], d2 = Z - it[2];
     const double* M = it + 6;
     const double U = M[0] * d0 + M[1] * d1 + M[2] * d2;
@@ -161,13 +156,9 @@ __global__ __launch_bounds__(256) void k_linearize(
     }
     const double decx = P1 * (yb * yb + 3.0 * xb * xb) + 2.0 * P2 * xb * yb;
     const double decy = P2 * (xb * xb + 3.0 * yb * yb) + 2.0 * P1 * xb * yb;
-    const double cs = c * s;
     const double cys = c * ydir;
-    const double fx = -cs * U + xp + dr * xb + decx;
+    const double fx = -c * s * U + xp + dr * xb + decx;
     const double fy = -cys * V * s + yp + dr * yb + decy;
-
-    auto put = [&](int r, int col, double v) { J[jc_index(r, col, NJ) * stride + o] = v; };
-    // chain rule through (U,V,W) -> (fx,fy)
     auto chain = [&](double dU, double dV, double dW, double& gx, double& gy) {
         const double dR = (U * dU + V * dV) / R;
         const double ds = (type == FBA_TYPE_PINHOLE) ? sW * dW : sR * dR + sW * dW;
@@ -175,293 +166,392 @@ __global__ __launch_bounds__(256) void k_linearize(
         gy = -cys * (dV * s + V * ds);
     };
     double gx, gy;
-    // EOP columns Xc Yc Zc: d(UVW)/dXc = -M[:,0] ...
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
+    for (int q = 0; q < 3; ++q) {  // Xc Yc Zc: d(UVW)/dXc = -M[:,q]; tie XYZ = -(that)
         chain(-M[q], -M[3 + q], -M[6 + q], gx, gy);
         const double en = (eop_mask >> q) & 1u ? 1.0 : 0.0;
-        put(0, q, gx * en);
-        put(1, q, gy * en);
-        if (p >= 0) { put(0, 6 + CW + q, -gx); put(1, 6 + CW + q, -gy); }  // d/dX = -d/dXc
-        else { put(0, 6 + CW + q, 0.0); put(1, 6 + CW + q, 0.0); }
+        jr[0][q] = gx * en;
+        jr[1][q] = gy * en;
+        jr[0][6 + CW + q] = tie ? -gx : 0.0;
+        jr[1][6 + CW + q] = tie ? -gy : 0.0;
     }
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
+    for (int a = 0; a < 3; ++a) {  // omega phi kappa
         const double* Md = it + 15 + 9 * a;
         const double dU = Md[0] * d0 + Md[1] * d1 + Md[2] * d2;
         const double dV = Md[3] * d0 + Md[4] * d1 + Md[5] * d2;
         const double dW = Md[6] * d0 + Md[7] * d1 + Md[8] * d2;
         chain(dU, dV, dW, gx, gy);
         const double en = (eop_mask >> (3 + a)) & 1u ? 1.0 : 0.0;
-        put(0, 3 + a, gx * en);
-        put(1, 3 + a, gy * en);
+        jr[0][3 + a] = gx * en;
+        jr[1][3 + a] = gy * en;
     }
-    // camera columns: xp yp c K1..KNK P1 P2 (BuildAwG.m:373-445)
     auto cen = [&](int col) { return (cam_mask >> col) & 1u ? 1.0 : 0.0; };
-    {
-        double ax = 1.0 - dr - dxr - 6.0 * P1 * xb - 2.0 * P2 * yb;  // d fx / d xp
-        double ay = -dxy - 2.0 * P1 * yb - 2.0 * P2 * xb;            // d fy / d xp
-        put(0, 6, ax * cen(0)); put(1, 6, ay * cen(0));
-        double bx = -dxy - 2.0 * P2 * xb - 2.0 * P1 * yb;            // d fx / d yp
-        double by = 1.0 - dr - dyr - 6.0 * P2 * yb - 2.0 * P1 * xb;  // d fy / d yp
-        put(0, 7, bx * cen(1)); put(1, 7, by * cen(1));
-        put(0, 8, -U * s * cen(2)); put(1, 8, -ydir * V * s * cen(2));  // d/dc
-    }
+    // camera columns xp yp c K1..KNK P1 P2 (BuildAwG.m:373-445)
+    jr[0][6] = (1.0 - dr - dxr - 6.0 * P1 * xb - 2.0 * P2 * yb) * cen(0);
+    jr[1][6] = (-dxy - 2.0 * P1 * yb - 2.0 * P2 * xb) * cen(0);
+    jr[0][7] = (-dxy - 2.0 * P2 * xb - 2.0 * P1 * yb) * cen(1);
+    jr[1][7] = (1.0 - dr - dyr - 6.0 * P2 * yb - 2.0 * P1 * xb) * cen(1);
+    jr[0][8] = -U * s * cen(2);
+    jr[1][8] = -ydir * V * s * cen(2);
 #pragma unroll
     for (int j = 1; j <= NK; ++j) {
         const double en = cen(2 + j);
-        put(0, 8 + j, r2j[j] * xb / sc[j - 1] * en);
-        put(1, 8 + j, r2j[j] * yb / sc[j - 1] * en);
+        jr[0][8 + j] = r2j[j] * xb / sc[j - 1] * en;
+        jr[1][8 + j] = r2j[j] * yb / sc[j - 1] * en;
     }
-    {
-        const double en1 = cen(3 + NK), en2 = cen(4 + NK);
-        const double s1 = sc[0];
-        put(0, 9 + NK, (yb * yb + 3.0 * xb * xb) / s1 * en1);
-        put(1, 9 + NK, 2.0 * xb * yb / s1 * en1);
-        put(0, 10 + NK, 2.0 * xb * yb / s1 * en2);
-        put(1, 10 + NK, (xb * xb + 3.0 * yb * yb) / s1 * en2);
-    }
-    J[(int64_t)(2 * NJ) * stride + o] = fx - x;
-    J[(int64_t)(2 * NJ + 1) * stride + o] = fy - y;
+    const double s1 = sc[0], en1 = cen(3 + NK), en2 = cen(4 + NK);
+    jr[0][9 + NK] = (yb * yb + 3.0 * xb * xb) / s1 * en1;
+    jr[1][9 + NK] = 2.0 * xb * yb / s1 * en1;
+    jr[0][10 + NK] = 2.0 * xb * yb / s1 * en2;
+    jr[1][10 + NK] = (xb * xb + 3.0 * yb * yb) / s1 * en2;
+    w0 = fx - x;
+    w1 = fy - y;
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_point: one thread per local tie point (Schur elimination of the 3 point unknowns)
-// pt_tab components: [0..5] Vinv (00 01 02 11 12 22), [6..8] vb = Vinv b, [9..11] b,
-//                    [12 .. 12+3CW) Wc[c][m], [12+3CW .. 12+6CW) Tc[c][m] = (Wc Vinv)[c][m]
-// WT per obs: [0..17] W[a][m] = (Je' P Jp)[a][m], [18..35] T = W Vinv
+// k_lin_point: one workgroup per chunk of whole tie points (<= 256 observations), one thread per
+// image point.  (1) linearise and store J; (2) one thread per point reduces its observations
+// (staged in LDS): V = Jp'PJp, b = Jp'Pw, Wc = Jc'PJp, Vinv, vb, Tc; (3) one thread per observation
+// forms W = Je'PJp and T = W Vinv.  Chunks of control observations run step (1) only.
 // ------------------------------------------------------------------------------------------------
 template <int NK>
-__global__ __launch_bounds__(64) void k_point(const double* __restrict__ J, const int32_t* __restrict__ lp_start,
-                                              double* __restrict__ pt_tab, double* __restrict__ WT, int64_t n_lp,
-                                              int64_t stride, int64_t pstride, double px, double py) {
-    constexpr int CW = 5 + NK;
-    constexpr int NJ = 9 + CW;
-    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n_lp) return;
-    const int o0 = lp_start[p], o1 = lp_start[p + 1];
-    double V00 = 0, V01 = 0, V02 = 0, V11 = 0, V12 = 0, V22 = 0, b0 = 0, b1 = 0, b2 = 0;
-    double Wc[CW][3];
-#pragma unroll
-    for (int c = 0; c < CW; ++c) Wc[c][0] = Wc[c][1] = Wc[c][2] = 0.0;
-    for (int o = o0; o < o1; ++o) {
-        double jp[2][3], w[2];
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-#pragma unroll
-            for (int m = 0; m < 3; ++m) jp[r][m] = J[jc_index(r, 6 + CW + m, NJ) * stride + o];
-            w[r] = J[(int64_t)(2 * NJ + r) * stride + o];
+__global__ __launch_bounds__(256) void k_lin_point(
+    const double* __restrict__ xy, const int32_t* __restrict__ img, const int32_t* __restrict__ cam,
+    const int32_t* __restrict__ pt, const int32_t* __restrict__ lp_tie, const double* __restrict__ ctl,
+    const double* __restrict__ xfull, const double* __restrict__ img_tab, const double* __restrict__ cam_tab,
+    const int32_t* __restrict__ chunk_obs, const int32_t* __restrict__ chunk_pt, const int32_t* __restrict__ lp_start,
+    double* __restrict__ J, double* __restrict__ WT, double* __restrict__ PT, int64_t u_c, int type, int cam_stride,
+    unsigned eop_mask, unsigned cam_mask, double px, double py) {
+    using LY = Lay<NK>;
+    constexpr int CW = LY::CW, NJ = LY::NJ, JS = LY::JS, PS = LY::PS;
+    constexpr int SH = 8 + 2 * CW;  // Jp (2x3), w (2), Jc (2xCW)
+    __shared__ double sh[256][SH + 1];
+    __shared__ double vinv[256][6];
+    const int t = threadIdx.x;
+    const int c = blockIdx.x;
+    const int o0 = chunk_obs[c], o1 = chunk_obs[c + 1];
+    const int p0 = chunk_pt[c], p1 = chunk_pt[c + 1];
+    const int o = o0 + t;
+    const bool active = o < o1;
+    double jr[2][NJ];
+    double w0 = 0.0, w1 = 0.0;
+    int p = -1;
+    if (active) {
+        const double x = xy[2 * (int64_t)o], y = xy[2 * (int64_t)o + 1];
+        const int e = img[o], k = cam[o];
+        p = pt[o];
+        double X, Y, Z;
+        if (p >= 0) {
+            const double* q = xfull + u_c + 3 * (int64_t)lp_tie[p];
+            X = q[0]; Y = q[1]; Z = q[2];
+        } else {
+            const double* q = ctl + 3 * (int64_t)(-1 - p);
+            X = q[0]; Y = q[1]; Z = q[2];
         }
-        const double pr[2] = {px, py};
+        obs_model<NK>(x, y, img_tab + (int64_t)e * IMG_TAB, cam_tab + (int64_t)k * cam_stride, X, Y, Z, p >= 0, type,
+                      eop_mask, cam_mask, jr, w0, w1);
+        double* Jo = J + (int64_t)o * JS;
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const double a0 = pr[r] * jp[r][0], a1 = pr[r] * jp[r][1], a2 = pr[r] * jp[r][2];
-            V00 += a0 * jp[r][0]; V01 += a0 * jp[r][1]; V02 += a0 * jp[r][2];
-            V11 += a1 * jp[r][1]; V12 += a1 * jp[r][2]; V22 += a2 * jp[r][2];
-            b0 += a0 * w[r]; b1 += a1 * w[r]; b2 += a2 * w[r];
+        for (int q = 0; q < NJ; q += 1) { Jo[q] = jr[0][q]; Jo[NJ + q] = jr[1][q]; }
+        Jo[2 * NJ] = w0;
+        Jo[2 * NJ + 1] = w1;
+        if (p >= 0) {
 #pragma unroll
-            for (int c = 0; c < CW; ++c) {
-                const double jc = J[jc_index(r, 6 + c, NJ) * stride + o];
-                Wc[c][0] += jc * a0; Wc[c][1] += jc * a1; Wc[c][2] += jc * a2;
+            for (int m = 0; m < 3; ++m) { sh[t][m] = jr[0][6 + CW + m]; sh[t][3 + m] = jr[1][6 + CW + m]; }
+            sh[t][6] = w0;
+            sh[t][7] = w1;
+#pragma unroll
+            for (int q = 0; q < CW; ++q) { sh[t][8 + q] = jr[0][6 + q]; sh[t][8 + CW + q] = jr[1][6 + q]; }
+        }
+    }
+    if (p1 == p0) return;  // control chunk (uniform across the workgroup)
+    __syncthreads();
+    if (t < p1 - p0) {
+        const int lp = p0 + t;
+        const int a0 = lp_start[lp] - o0, a1 = lp_start[lp + 1] - o0;
+        double V00 = 0, V01 = 0, V02 = 0, V11 = 0, V12 = 0, V22 = 0, b0 = 0, b1 = 0, b2 = 0;
+        double Wc[CW][3];
+#pragma unroll
+        for (int q = 0; q < CW; ++q) Wc[q][0] = Wc[q][1] = Wc[q][2] = 0.0;
+        for (int i = a0; i < a1; ++i) {
+            const double* r = sh[i];
+#pragma unroll
+            for (int row = 0; row < 2; ++row) {
+                const double pr = row ? py : px;
+                const double j0 = r[3 * row], j1 = r[3 * row + 1], j2 = r[3 * row + 2], wv = r[6 + row];
+                const double q0 = pr * j0, q1 = pr * j1, q2 = pr * j2;
+                V00 += q0 * j0; V01 += q0 * j1; V02 += q0 * j2;
+                V11 += q1 * j1; V12 += q1 * j2; V22 += q2 * j2;
+                b0 += q0 * wv; b1 += q1 * wv; b2 += q2 * wv;
+#pragma unroll
+                for (int q = 0; q < CW; ++q) {
+                    const double jc = r[8 + row * CW + q];
+                    Wc[q][0] += jc * q0; Wc[q][1] += jc * q1; Wc[q][2] += jc * q2;
+                }
             }
         }
+        // symmetric 3x3 inverse (adjugate)
+        const double c00 = V11 * V22 - V12 * V12, c01 = V02 * V12 - V01 * V22, c02 = V01 * V12 - V02 * V11;
+        const double id = 1.0 / (V00 * c00 + V01 * c01 + V02 * c02);
+        const double I00 = c00 * id, I01 = c01 * id, I02 = c02 * id;
+        const double I11 = (V00 * V22 - V02 * V02) * id, I12 = (V01 * V02 - V00 * V12) * id,
+                     I22 = (V00 * V11 - V01 * V01) * id;
+        double* P = PT + (int64_t)lp * PS;
+        P[0] = I00; P[1] = I01; P[2] = I02; P[3] = I11; P[4] = I12; P[5] = I22;
+        P[6] = I00 * b0 + I01 * b1 + I02 * b2;
+        P[7] = I01 * b0 + I11 * b1 + I12 * b2;
+        P[8] = I02 * b0 + I12 * b1 + I22 * b2;
+        P[9] = b0; P[10] = b1; P[11] = b2;
+#pragma unroll
+        for (int q = 0; q < CW; ++q) {
+            P[12 + 3 * q] = Wc[q][0];
+            P[13 + 3 * q] = Wc[q][1];
+            P[14 + 3 * q] = Wc[q][2];
+            P[12 + 3 * CW + 3 * q] = Wc[q][0] * I00 + Wc[q][1] * I01 + Wc[q][2] * I02;
+            P[13 + 3 * CW + 3 * q] = Wc[q][0] * I01 + Wc[q][1] * I11 + Wc[q][2] * I12;
+            P[14 + 3 * CW + 3 * q] = Wc[q][0] * I02 + Wc[q][1] * I12 + Wc[q][2] * I22;
+        }
+        vinv[t][0] = I00; vinv[t][1] = I01; vinv[t][2] = I02;
+        vinv[t][3] = I11; vinv[t][4] = I12; vinv[t][5] = I22;
     }
-    // symmetric 3x3 inverse (adjugate)
-    const double c00 = V11 * V22 - V12 * V12, c01 = V02 * V12 - V01 * V22, c02 = V01 * V12 - V02 * V11;
-    const double det = V00 * c00 + V01 * c01 + V02 * c02;
-    const double id = 1.0 / det;
-    const double I00 = c00 * id, I01 = c01 * id, I02 = c02 * id;
-    const double I11 = (V00 * V22 - V02 * V02) * id, I12 = (V01 * V02 - V00 * V12) * id,
-                 I22 = (V00 * V11 - V01 * V01) * id;
-    const double vb0 = I00 * b0 + I01 * b1 + I02 * b2;
-    const double vb1 = I01 * b0 + I11 * b1 + I12 * b2;
-    const double vb2 = I02 * b0 + I12 * b1 + I22 * b2;
-    double* t = pt_tab + p;
-    t[0 * pstride] = I00; t[1 * pstride] = I01; t[2 * pstride] = I02;
-    t[3 * pstride] = I11; t[4 * pstride] = I12; t[5 * pstride] = I22;
-    t[6 * pstride] = vb0; t[7 * pstride] = vb1; t[8 * pstride] = vb2;
-    t[9 * pstride] = b0; t[10 * pstride] = b1; t[11 * pstride] = b2;
-#pragma unroll
-    for (int c = 0; c < CW; ++c) {
-        t[(12 + 3 * c + 0) * pstride] = Wc[c][0];
-        t[(12 + 3 * c + 1) * pstride] = Wc[c][1];
-        t[(12 + 3 * c + 2) * pstride] = Wc[c][2];
-        t[(12 + 3 * CW + 3 * c + 0) * pstride] = Wc[c][0] * I00 + Wc[c][1] * I01 + Wc[c][2] * I02;
-        t[(12 + 3 * CW + 3 * c + 1) * pstride] = Wc[c][0] * I01 + Wc[c][1] * I11 + Wc[c][2] * I12;
-        t[(12 + 3 * CW + 3 * c + 2) * pstride] = Wc[c][0] * I02 + Wc[c][1] * I12 + Wc[c][2] * I22;
-    }
-    for (int o = o0; o < o1; ++o) {
-        double jp[2][3];
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int m = 0; m < 3; ++m) jp[r][m] = J[jc_index(r, 6 + CW + m, NJ) * stride + o];
+    __syncthreads();
+    if (active && p >= 0) {
+        const double* vi = vinv[p - p0];
+        const double I00 = vi[0], I01 = vi[1], I02 = vi[2], I11 = vi[3], I12 = vi[4], I22 = vi[5];
+        double* Wo = WT + (int64_t)o * 36;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
-            const double je0 = px * J[jc_index(0, a, NJ) * stride + o];
-            const double je1 = py * J[jc_index(1, a, NJ) * stride + o];
-            const double w0 = je0 * jp[0][0] + je1 * jp[1][0];
-            const double w1 = je0 * jp[0][1] + je1 * jp[1][1];
-            const double w2 = je0 * jp[0][2] + je1 * jp[1][2];
-            WT[(int64_t)(3 * a + 0) * stride + o] = w0;
-            WT[(int64_t)(3 * a + 1) * stride + o] = w1;
-            WT[(int64_t)(3 * a + 2) * stride + o] = w2;
-            WT[(int64_t)(18 + 3 * a + 0) * stride + o] = w0 * I00 + w1 * I01 + w2 * I02;
-            WT[(int64_t)(18 + 3 * a + 1) * stride + o] = w0 * I01 + w1 * I11 + w2 * I12;
-            WT[(int64_t)(18 + 3 * a + 2) * stride + o] = w0 * I02 + w1 * I12 + w2 * I22;
+            const double e0 = px * jr[0][a], e1 = py * jr[1][a];
+            const double v0 = e0 * jr[0][6 + CW + 0] + e1 * jr[1][6 + CW + 0];
+            const double v1 = e0 * jr[0][6 + CW + 1] + e1 * jr[1][6 + CW + 1];
+            const double v2 = e0 * jr[0][6 + CW + 2] + e1 * jr[1][6 + CW + 2];
+            Wo[3 * a] = v0; Wo[3 * a + 1] = v1; Wo[3 * a + 2] = v2;
+            Wo[18 + 3 * a] = v0 * I00 + v1 * I01 + v2 * I02;
+            Wo[19 + 3 * a] = v0 * I01 + v1 * I11 + v2 * I12;
+            Wo[20 + 3 * a] = v0 * I02 + v1 * I12 + v2 * I22;
         }
     }
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_image: one workgroup per image; thread q owns one output entry:
+// k_image: one workgroup per image; 32 observations at a time staged in LDS (J row, W/T, the
+// point's vb and Wc); thread q owns one output entry:
 //   q < 21            reduced diagonal block U_e (lower, a >= b)
 //   21 <= q < 27      reduced RHS r_e
 //   27 <= q < 27+6CW  image-camera block (camera row c, image column a)
+// Two thread groups split the staged observations; their sums are added in a fixed order.
 // ------------------------------------------------------------------------------------------------
 __constant__ int c_tri_a[21] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 4, 5, 5, 5, 5, 5, 5};
 __constant__ int c_tri_b[21] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4, 0, 1, 2, 3, 4, 5};
 
 template <int NK>
-__global__ __launch_bounds__(128) void k_image(const double* __restrict__ J, const double* __restrict__ WT,
-                                               const double* __restrict__ pt_tab, const int32_t* __restrict__ pt,
+__global__ __launch_bounds__(256) void k_image(const double* __restrict__ J, const double* __restrict__ WT,
+                                               const double* __restrict__ PT, const int32_t* __restrict__ pt,
                                                const int32_t* __restrict__ cam, const int32_t* __restrict__ img_start,
                                                const int32_t* __restrict__ img_obs, double* __restrict__ S, int64_t ld,
-                                               int64_t n_pad, int n_img, int64_t stride, int64_t pstride,
-                                               double px, double py) {
-    constexpr int CW = 5 + NK;
-    constexpr int NJ = 9 + CW;
+                                               int64_t n_pad, int n_img, double px, double py) {
+    using LY = Lay<NK>;
+    constexpr int CW = LY::CW, NJ = LY::NJ, JS = LY::JS, PS = LY::PS;
+    constexpr int F = JS + 36 + 3 + 3 * CW;  // J row | W,T | vb | Wc
+    constexpr int CH = 32;
+    constexpr int NOUT = 27 + 6 * CW;
+    __shared__ double st[CH][F + 1];
+    __shared__ double part[128];
+    __shared__ int so[CH];
     const int e = blockIdx.x;
-    const int q = threadIdx.x;
+    const int tid = threadIdx.x;
+    const int g = tid >> 7, q = tid & 127;
     const int i0 = img_start[e], i1 = img_start[e + 1];
     if (i0 == i1) return;
-    if (q >= 27 + 6 * CW) return;
-    int kind, a, b;
+    int kind = 0, a = 0, b = 0;
     if (q < 21) { kind = 0; a = c_tri_a[q]; b = c_tri_b[q]; }
-    else if (q < 27) { kind = 1; a = q - 21; b = 0; }
-    else { kind = 2; a = (q - 27) % 6; b = (q - 27) / 6; }  // b = camera column
+    else if (q < 27) { kind = 1; a = q - 21; }
+    else if (q < NOUT) { kind = 2; a = (q - 27) % 6; b = (q - 27) / 6; }
     double acc = 0.0;
-    for (int i = i0; i < i1; ++i) {
-        const int o = img_obs[i];
-        const int p = pt[o];
-        const double ea0 = J[jc_index(0, a, NJ) * stride + o];
-        const double ea1 = J[jc_index(1, a, NJ) * stride + o];
-        double s0, s1;
-        if (kind == 0) { s0 = J[jc_index(0, b, NJ) * stride + o]; s1 = J[jc_index(1, b, NJ) * stride + o]; }
-        else if (kind == 1) { s0 = J[(int64_t)(2 * NJ) * stride + o]; s1 = J[(int64_t)(2 * NJ + 1) * stride + o]; }
-        else { s0 = J[jc_index(0, 6 + b, NJ) * stride + o]; s1 = J[jc_index(1, 6 + b, NJ) * stride + o]; }
-        acc += px * ea0 * s0 + py * ea1 * s1;
-        if (p >= 0) {
-            if (kind == 0) {
-                const double* T = WT + (int64_t)(18 + 3 * a) * stride + o;
-                const double* Wb = WT + (int64_t)(3 * b) * stride + o;
-                acc -= T[0] * Wb[0] + T[stride] * Wb[stride] + T[2 * stride] * Wb[2 * stride];
-            } else if (kind == 1) {
-                const double* Wa = WT + (int64_t)(3 * a) * stride + o;
-                const double* vb = pt_tab + 6 * pstride + p;
-                acc -= Wa[0] * vb[0] + Wa[stride] * vb[pstride] + Wa[2 * stride] * vb[2 * pstride];
-            } else {
-                const double* T = WT + (int64_t)(18 + 3 * a) * stride + o;
-                const double* Wc = pt_tab + (int64_t)(12 + 3 * b) * pstride + p;
-                acc -= T[0] * Wc[0] + T[stride] * Wc[pstride] + T[2 * stride] * Wc[2 * pstride];
+    for (int base = i0; base < i1; base += CH) {
+        const int n = min(CH, i1 - base);
+        if (tid < n) so[tid] = img_obs[base + tid];
+        __syncthreads();
+        for (int idx = tid; idx < n * F; idx += 256) {
+            const int k = idx / F, f = idx - k * F;
+            const int o = so[k];
+            double v;
+            if (f < JS) v = J[(int64_t)o * JS + f];
+            else if (f < JS + 36) v = WT[(int64_t)o * 36 + (f - JS)];
+            else {
+                const int p = pt[o];
+                const int ff = f - JS - 36;  // 0..2 vb, 3.. Wc
+                v = (p < 0) ? 0.0 : PT[(int64_t)p * PS + (ff < 3 ? 6 + ff : 12 + ff - 3)];
+            }
+            st[k][f] = v;
+        }
+        __syncthreads();
+        if (q < NOUT) {
+            for (int k = g; k < n; k += 2) {
+                const double* r = st[k];
+                const double ea0 = r[a], ea1 = r[NJ + a];
+                const bool tie = pt[so[k]] >= 0;
+                if (kind == 0) {
+                    acc += px * ea0 * r[b] + py * ea1 * r[NJ + b];
+                    if (tie) {
+                        const double* T = r + JS + 18 + 3 * a;
+                        const double* W = r + JS + 3 * b;
+                        acc -= T[0] * W[0] + T[1] * W[1] + T[2] * W[2];
+                    }
+                } else if (kind == 1) {
+                    acc += px * ea0 * r[2 * NJ] + py * ea1 * r[2 * NJ + 1];
+                    if (tie) {
+                        const double* W = r + JS + 3 * a;
+                        const double* vb = r + JS + 36;
+                        acc -= W[0] * vb[0] + W[1] * vb[1] + W[2] * vb[2];
+                    }
+                } else {
+                    acc += px * ea0 * r[6 + b] + py * ea1 * r[NJ + 6 + b];
+                    if (tie) {
+                        const double* T = r + JS + 18 + 3 * a;
+                        const double* Wc = r + JS + 39 + 3 * b;
+                        acc -= T[0] * Wc[0] + T[1] * Wc[1] + T[2] * Wc[2];
+                    }
+                }
             }
         }
+        __syncthreads();
     }
-    if (kind == 0) {
-        S[(int64_t)(6 * e + a) * ld + 6 * e + b] = acc;
-    } else if (kind == 1) {
-        S[n_pad * ld + 6 * e + a] = acc;
-    } else {
-        const int k = cam[img_obs[i0]];
-        S[(int64_t)(6 * (int64_t)n_img + (int64_t)k * CW + b) * ld + 6 * e + a] = acc;
+    if (g == 1) part[q] = acc;
+    __syncthreads();
+    if (g == 0 && q < NOUT) {
+        acc += part[q];
+        if (kind == 0) {
+            S[(int64_t)(6 * e + a) * ld + 6 * e + b] = acc;
+        } else if (kind == 1) {
+            S[n_pad * ld + 6 * e + a] = acc;
+        } else {
+            const int k = cam[img_obs[i0]];
+            S[(int64_t)(6 * (int64_t)n_img + (int64_t)k * CW + b) * ld + 6 * e + a] = acc;
+        }
     }
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_pairs: off-diagonal image-image blocks S(e1,e2) = -sum W_i Vinv W_j^T over shared tie points
+// k_pairs: off-diagonal image-image blocks S(e1,e2) = -sum W_i Vinv W_j^T over shared tie points;
+// one wave per co-visible pair, lanes 0..35 own the 6x6 entries, 4 terms in flight.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_pairs(const double* __restrict__ WT, const int32_t* __restrict__ pair_e,
                                               const int32_t* __restrict__ pair_start, const int32_t* __restrict__ pair_ij,
-                                              double* __restrict__ S, int64_t ld, int64_t stride) {
+                                              double* __restrict__ S, int64_t ld) {
     const int64_t pr = blockIdx.x;
     const int q = threadIdx.x;
     if (q >= 36) return;
     const int a = q / 6, b = q % 6;
     const int e1 = pair_e[2 * pr], e2 = pair_e[2 * pr + 1];
     const int t0 = pair_start[pr], t1 = pair_start[pr + 1];
-    double acc = 0.0;
-    for (int t = t0; t < t1; ++t) {
-        const int i = pair_ij[2 * t], j = pair_ij[2 * t + 1];
-        const double* T = WT + (int64_t)(18 + 3 * a) * stride + i;
-        const double* W = WT + (int64_t)(3 * b) * stride + j;
-        acc -= T[0] * W[0] + T[stride] * W[stride] + T[2 * stride] * W[2 * stride];
+    double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
+    int t = t0;
+    for (; t + 4 <= t1; t += 4) {
+        const int2 ij0 = *reinterpret_cast<const int2*>(pair_ij + 2 * t);
+        const int2 ij1 = *reinterpret_cast<const int2*>(pair_ij + 2 * t + 2);
+        const int2 ij2 = *reinterpret_cast<const int2*>(pair_ij + 2 * t + 4);
+        const int2 ij3 = *reinterpret_cast<const int2*>(pair_ij + 2 * t + 6);
+        const double* T0 = WT + (int64_t)ij0.x * 36 + 18 + 3 * a; const double* W0 = WT + (int64_t)ij0.y * 36 + 3 * b;
+        const double* T1 = WT + (int64_t)ij1.x * 36 + 18 + 3 * a; const double* W1 = WT + (int64_t)ij1.y * 36 + 3 * b;
+        const double* T2 = WT + (int64_t)ij2.x * 36 + 18 + 3 * a; const double* W2 = WT + (int64_t)ij2.y * 36 + 3 * b;
+        const double* T3 = WT + (int64_t)ij3.x * 36 + 18 + 3 * a; const double* W3 = WT + (int64_t)ij3.y * 36 + 3 * b;
+        acc0 -= T0[0] * W0[0] + T0[1] * W0[1] + T0[2] * W0[2];
+        acc1 -= T1[0] * W1[0] + T1[1] * W1[1] + T1[2] * W1[2];
+        acc2 -= T2[0] * W2[0] + T2[1] * W2[1] + T2[2] * W2[2];
+        acc3 -= T3[0] * W3[0] + T3[1] * W3[1] + T3[2] * W3[2];
     }
-    S[(int64_t)(6 * e1 + a) * ld + 6 * e2 + b] = acc;
+    for (; t < t1; ++t) {
+        const int i = pair_ij[2 * t], j = pair_ij[2 * t + 1];
+        const double* T = WT + (int64_t)i * 36 + 18 + 3 * a;
+        const double* W = WT + (int64_t)j * 36 + 3 * b;
+        acc0 -= T[0] * W[0] + T[1] * W[1] + T[2] * W[2];
+    }
+    S[(int64_t)(6 * e1 + a) * ld + 6 * e2 + b] = (acc0 + acc1) + (acc2 + acc3);
 }
 
 // ------------------------------------------------------------------------------------------------
-// camera block: stage 1 (NSLAB x n_cam workgroups) -> slabs, stage 2 -> S
+// camera block: stage 1 (NSLAB x n_cam workgroups) -> slabs, stage 2 -> S.  Each slab covers a
+// contiguous range of the camera's tie points (their observations are contiguous) and of its
+// control observations; observations and point rows are staged through LDS 32 at a time.
 // entry q < CW(CW+1)/2: lower (c1 >= c2);  q >= that: RHS entry c
 // ------------------------------------------------------------------------------------------------
 template <int NK>
-__global__ __launch_bounds__(128) void k_cam_stage1(const double* __restrict__ J, const double* __restrict__ pt_tab,
+__global__ __launch_bounds__(128) void k_cam_stage1(const double* __restrict__ J, const double* __restrict__ PT,
                                                     const int32_t* __restrict__ lp_start,
                                                     const int32_t* __restrict__ cam_lp, const int32_t* __restrict__ cam_ctl,
-                                                    double* __restrict__ slab, int64_t n_obs_tie, int64_t stride,
-                                                    int64_t pstride, double px, double py) {
-    constexpr int CW = 5 + NK;
-    constexpr int NJ = 9 + CW;
+                                                    double* __restrict__ slab, int64_t n_obs_tie, double px, double py) {
+    using LY = Lay<NK>;
+    constexpr int CW = LY::CW, NJ = LY::NJ, JS = LY::JS, PS = LY::PS;
     constexpr int NPK = CW * (CW + 1) / 2;
+    constexpr int CH = 32;
+    constexpr int FP = 3 + 6 * CW;  // vb, Wc, Tc of a point
+    __shared__ double so[CH][2 * CW + 3];
+    __shared__ double sp[CH][FP + 1];
     const int s = blockIdx.x, k = blockIdx.y, q = threadIdx.x;
-    if (q >= NPK + CW) return;
-    int c1, c2 = -1;
+    int c1 = 0, c2 = -1;
     if (q < NPK) {
-        c1 = 0;
         int rem = q;
         while (rem > c1) { rem -= c1 + 1; ++c1; }
         c2 = rem;
     } else {
         c1 = q - NPK;
     }
+    const bool act = q < NPK + CW;
     double acc = 0.0;
-    // tie points of camera k, slab s
     const int64_t p0 = cam_lp[k], p1 = cam_lp[k + 1];
     const int64_t np = p1 - p0;
     const int64_t a0 = p0 + np * s / NSLAB, a1 = p0 + np * (s + 1) / NSLAB;
-    for (int64_t p = a0; p < a1; ++p) {
-        const int o0 = lp_start[p], o1 = lp_start[p + 1];
-        for (int o = o0; o < o1; ++o) {
-            const double j10 = J[jc_index(0, 6 + c1, NJ) * stride + o];
-            const double j11 = J[jc_index(1, 6 + c1, NJ) * stride + o];
-            double s0, s1;
-            if (c2 >= 0) { s0 = J[jc_index(0, 6 + c2, NJ) * stride + o]; s1 = J[jc_index(1, 6 + c2, NJ) * stride + o]; }
-            else { s0 = J[(int64_t)(2 * NJ) * stride + o]; s1 = J[(int64_t)(2 * NJ + 1) * stride + o]; }
-            acc += px * j10 * s0 + py * j11 * s1;
-        }
-        if (c2 >= 0) {
-            const double* T = pt_tab + (int64_t)(12 + 3 * CW + 3 * c1) * pstride + p;
-            const double* W = pt_tab + (int64_t)(12 + 3 * c2) * pstride + p;
-            acc -= T[0] * W[0] + T[pstride] * W[pstride] + T[2 * pstride] * W[2 * pstride];
-        } else {
-            const double* W = pt_tab + (int64_t)(12 + 3 * c1) * pstride + p;
-            const double* vb = pt_tab + 6 * pstride + p;
-            acc -= W[0] * vb[0] + W[pstride] * vb[pstride] + W[2 * pstride] * vb[2 * pstride];
-        }
-    }
-    // control observations of camera k, slab s
     const int64_t q0 = cam_ctl[k], q1 = cam_ctl[k + 1];
     const int64_t nq = q1 - q0;
     const int64_t b0 = q0 + nq * s / NSLAB, b1 = q0 + nq * (s + 1) / NSLAB;
-    for (int64_t oo = b0; oo < b1; ++oo) {
-        const int64_t o = n_obs_tie + oo;
-        const double j10 = J[jc_index(0, 6 + c1, NJ) * stride + o];
-        const double j11 = J[jc_index(1, 6 + c1, NJ) * stride + o];
-        double s0, s1;
-        if (c2 >= 0) { s0 = J[jc_index(0, 6 + c2, NJ) * stride + o]; s1 = J[jc_index(1, 6 + c2, NJ) * stride + o]; }
-        else { s0 = J[(int64_t)(2 * NJ) * stride + o]; s1 = J[(int64_t)(2 * NJ + 1) * stride + o]; }
-        acc += px * j10 * s0 + py * j11 * s1;
+    // direct terms over the observations: tie observations of points [a0,a1), then control ones
+    const int64_t oa0 = (a0 < a1) ? lp_start[a0] : 0, oa1 = (a0 < a1) ? lp_start[a1] : 0;
+    for (int pass = 0; pass < 2; ++pass) {
+        const int64_t lo = pass == 0 ? oa0 : n_obs_tie + b0;
+        const int64_t hi = pass == 0 ? oa1 : n_obs_tie + b1;
+        for (int64_t base = lo; base < hi; base += CH) {
+            const int n = (int)min((int64_t)CH, hi - base);
+            for (int idx = q; idx < n * (2 * CW + 2); idx += 128) {
+                const int kk = idx / (2 * CW + 2), f = idx - kk * (2 * CW + 2);
+                const double* r = J + (base + kk) * JS;
+                so[kk][f] = (f < CW) ? r[6 + f] : (f < 2 * CW ? r[NJ + 6 + f - CW] : r[2 * NJ + f - 2 * CW]);
+            }
+            __syncthreads();
+            if (act)
+                for (int kk = 0; kk < n; ++kk) {
+                    const double* r = so[kk];
+                    const double s0 = (c2 >= 0) ? r[c2] : r[2 * CW];
+                    const double s1 = (c2 >= 0) ? r[CW + c2] : r[2 * CW + 1];
+                    acc += px * r[c1] * s0 + py * r[CW + c1] * s1;
+                }
+            __syncthreads();
+        }
     }
-    slab[((int64_t)k * NSLAB + s) * (NPK + CW) + q] = acc;
+    // Schur terms of the points [a0, a1)
+    for (int64_t base = a0; base < a1; base += CH) {
+        const int n = (int)min((int64_t)CH, a1 - base);
+        for (int idx = q; idx < n * FP; idx += 128) {
+            const int kk = idx / FP, f = idx - kk * FP;
+            sp[kk][f] = PT[(base + kk) * PS + 6 + (f < 3 ? f : f + 3)];
+        }
+        __syncthreads();
+        if (act)
+            for (int kk = 0; kk < n; ++kk) {
+                const double* r = sp[kk];  // vb 0..2, Wc 3.., Tc 3+3CW..
+                if (c2 >= 0) {
+                    const double* T = r + 3 + 3 * CW + 3 * c1;
+                    const double* W = r + 3 + 3 * c2;
+                    acc -= T[0] * W[0] + T[1] * W[1] + T[2] * W[2];
+                } else {
+                    const double* W = r + 3 + 3 * c1;
+                    acc -= W[0] * r[0] + W[1] * r[1] + W[2] * r[2];
+                }
+            }
+        __syncthreads();
+    }
+    if (act) slab[((int64_t)k * NSLAB + s) * (NPK + CW) + q] = acc;
 }
 
 template <int NK>
@@ -551,36 +641,39 @@ __global__ void k_finish_rhs(double* __restrict__ S, const double* __restrict__ 
     }
 }
 
+
 // ------------------------------------------------------------------------------------------------
 // back-substitution of tie points: dp = -(vb + sum_o T_o^T d_e(o) + Tc^T d_cam)
 // ------------------------------------------------------------------------------------------------
 template <int NK>
-__global__ void k_backsub(const double* __restrict__ WT, const double* __restrict__ pt_tab,
+__global__ void k_backsub(const double* __restrict__ WT, const double* __restrict__ PT,
                           const int32_t* __restrict__ lp_start, const int32_t* __restrict__ lp_tie,
                           const int32_t* __restrict__ lp_cam, const int32_t* __restrict__ img,
-                          double* __restrict__ delta, int64_t n_lp, int64_t stride, int64_t pstride, int64_t u_c,
-                          int n_img) {
-    constexpr int CW = 5 + NK;
+                          double* __restrict__ delta, int64_t n_lp, int64_t u_c, int n_img) {
+    using LY = Lay<NK>;
+    constexpr int CW = LY::CW, PS = LY::PS;
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n_lp) return;
-    double d0 = pt_tab[6 * pstride + p], d1 = pt_tab[7 * pstride + p], d2 = pt_tab[8 * pstride + p];
+    const double* P = PT + p * PS;
+    double d0 = P[6], d1 = P[7], d2 = P[8];
     for (int o = lp_start[p]; o < lp_start[p + 1]; ++o) {
         const double* de = delta + 6 * (int64_t)img[o];
+        const double* T = WT + (int64_t)o * 36 + 18;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
-            const double* T = WT + (int64_t)(18 + 3 * a) * stride + o;
-            d0 += T[0] * de[a]; d1 += T[stride] * de[a]; d2 += T[2 * stride] * de[a];
+            d0 += T[3 * a] * de[a]; d1 += T[3 * a + 1] * de[a]; d2 += T[3 * a + 2] * de[a];
         }
     }
     const double* dk = delta + 6 * (int64_t)n_img + (int64_t)lp_cam[p] * CW;
+    const double* Tc = P + 12 + 3 * CW;
 #pragma unroll
     for (int c = 0; c < CW; ++c) {
-        const double* T = pt_tab + (int64_t)(12 + 3 * CW + 3 * c) * pstride + p;
-        d0 += T[0] * dk[c]; d1 += T[pstride] * dk[c]; d2 += T[2 * pstride] * dk[c];
+        d0 += Tc[3 * c] * dk[c]; d1 += Tc[3 * c + 1] * dk[c]; d2 += Tc[3 * c + 2] * dk[c];
     }
     double* out = delta + u_c + 3 * (int64_t)lp_tie[p];
     out[0] = -d0; out[1] = -d1; out[2] = -d2;
 }
+
 
 // ------------------------------------------------------------------------------------------------
 // update: de-scale (main.m:460-482), xhat += delta, partial sumabs (fixed-order block sums)
@@ -631,6 +724,7 @@ __global__ void k_sum_parts(const double* __restrict__ part, int n, double* __re
     if (threadIdx.x == 0) *out = red[0];
 }
 
+
 // ------------------------------------------------------------------------------------------------
 // residuals: v = J delta + w (main.m:569; delta = de-scaled last correction, as the reference),
 // RSD (BuildRSD.m:29-40) with xp,yp of the updated parameters; block partials of vx^2, vy^2, v'Pv
@@ -641,10 +735,10 @@ __global__ __launch_bounds__(256) void k_residuals(const double* __restrict__ J,
                                                    const int32_t* __restrict__ pt, const int32_t* __restrict__ lp_tie,
                                                    const double* __restrict__ delta, const double* __restrict__ xfull,
                                                    double* __restrict__ v, double* __restrict__ rsd,
-                                                   double* __restrict__ part, int64_t n_obs, int64_t stride,
-                                                   int64_t u_c, int n_img, double px, double py) {
-    constexpr int CW = 5 + NK;
-    constexpr int NJ = 9 + CW;
+                                                   double* __restrict__ part, int64_t n_obs, int64_t u_c, int n_img,
+                                                   double px, double py) {
+    using LY = Lay<NK>;
+    constexpr int CW = LY::CW, NJ = LY::NJ, JS = LY::JS;
     __shared__ double red[3][256];
     const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double sx = 0.0, sy = 0.0, sp = 0.0;
@@ -652,18 +746,20 @@ __global__ __launch_bounds__(256) void k_residuals(const double* __restrict__ J,
         const int e = img[o], k = cam[o], p = pt[o];
         const double* de = delta + 6 * (int64_t)e;
         const double* dk = delta + 6 * (int64_t)n_img + (int64_t)k * CW;
+        const double* Jo = J + o * JS;
         double vv[2];
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
-            double acc = J[(int64_t)(2 * NJ + r) * stride + o];
+            const double* jr = Jo + r * NJ;
+            double acc = Jo[2 * NJ + r];
 #pragma unroll
-            for (int a = 0; a < 6; ++a) acc += J[jc_index(r, a, NJ) * stride + o] * de[a];
+            for (int a = 0; a < 6; ++a) acc += jr[a] * de[a];
 #pragma unroll
-            for (int c = 0; c < CW; ++c) acc += J[jc_index(r, 6 + c, NJ) * stride + o] * dk[c];
+            for (int c = 0; c < CW; ++c) acc += jr[6 + c] * dk[c];
             if (p >= 0) {
                 const double* dp = delta + u_c + 3 * (int64_t)lp_tie[p];
 #pragma unroll
-                for (int m = 0; m < 3; ++m) acc += J[jc_index(r, 6 + CW + m, NJ) * stride + o] * dp[m];
+                for (int m = 0; m < 3; ++m) acc += jr[6 + CW + m] * dp[m];
             }
             vv[r] = acc;
         }
@@ -702,28 +798,30 @@ __global__ void k_dense_awg(const double* __restrict__ J, const int32_t* __restr
                             const int32_t* __restrict__ cam, const int32_t* __restrict__ pt,
                             const int32_t* __restrict__ lp_tie, const int64_t* __restrict__ obs_pho,
                             const int64_t* __restrict__ map, double* __restrict__ A, double* __restrict__ w,
-                            int64_t n_obs, int64_t stride, int64_t n_rows, int64_t u_c, int n_img) {
-    constexpr int CW = 5 + NK;
-    constexpr int NJ = 9 + CW;
+                            int64_t n_obs, int64_t n_rows, int64_t u_c, int n_img) {
+    using LY = Lay<NK>;
+    constexpr int CW = LY::CW, NJ = LY::NJ, JS = LY::JS;
     const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (o >= n_obs) return;
     const int e = img[o], k = cam[o], p = pt[o];
     const int64_t row0 = 2 * obs_pho[o];
+    const double* Jo = J + o * JS;
     for (int r = 0; r < 2; ++r) {
         const int64_t row = row0 + r;
-        w[row] = J[(int64_t)(2 * NJ + r) * stride + o];
+        const double* jr = Jo + r * NJ;
+        w[row] = Jo[2 * NJ + r];
         for (int a = 0; a < 6; ++a) {
             const int64_t col = map[6 * (int64_t)e + a];
-            if (col >= 0) A[col * n_rows + row] = J[jc_index(r, a, NJ) * stride + o];
+            if (col >= 0) A[col * n_rows + row] = jr[a];
         }
         for (int c = 0; c < CW; ++c) {
             const int64_t col = map[6 * (int64_t)n_img + (int64_t)k * CW + c];
-            if (col >= 0) A[col * n_rows + row] = J[jc_index(r, 6 + c, NJ) * stride + o];
+            if (col >= 0) A[col * n_rows + row] = jr[6 + c];
         }
         if (p >= 0) {
             for (int m = 0; m < 3; ++m) {
                 const int64_t col = map[u_c + 3 * (int64_t)lp_tie[p] + m];
-                if (col >= 0) A[col * n_rows + row] = J[jc_index(r, 6 + CW + m, NJ) * stride + o];
+                if (col >= 0) A[col * n_rows + row] = jr[6 + CW + m];
             }
         }
     }
@@ -759,7 +857,6 @@ static inline unsigned cam_mask(const fba_settings& s, int nk) {
 static inline double px_of(const Ctx& c) { return 1.0 / (c.set.meas_std_x * c.set.meas_std_x); }
 static inline double py_of(const Ctx& c) { return 1.0 / (c.set.meas_std_y * c.set.meas_std_y); }
 
-
 int launch_params(Ctx& c) {
     const int n = c.L.n_img + c.L.n_cam;
     k_params<<<(n + 63) / 64, 64, 0, c.stream>>>(c.d_xfull, c.d_caminfo, c.d_img_tab, c.d_cam_tab, c.d_G,
@@ -769,14 +866,15 @@ int launch_params(Ctx& c) {
     return FBA_OK;
 }
 
+// linearisation fused with the tie-point reduction (the dense debug path uses the same kernel)
 int launch_linearize(Ctx& c) {
-    if (c.n_obs == 0) return FBA_OK;
+    if (c.n_chunks == 0) return FBA_OK;
     const unsigned em = eop_mask(c.set), cm = cam_mask(c.set, c.L.nk);
-    const int blocks = (int)((c.n_obs + 255) / 256);
 #define LIN(NKV)                                                                                               \
-    k_linearize<NKV><<<blocks, 256, 0, c.stream>>>(c.d_xy, c.d_img, c.d_cam, c.d_pt, c.d_lp_tie, c.d_ctl,      \
-                                                   c.d_xfull, c.d_img_tab, c.d_cam_tab, c.d_J, c.n_obs,        \
-                                                   c.n_obs_pad, c.L.u_c, c.set.type, c.cam_tab_stride, em, cm)
+    k_lin_point<NKV><<<(unsigned)c.n_chunks, 256, 0, c.stream>>>(                                              \
+        c.d_xy, c.d_img, c.d_cam, c.d_pt, c.d_lp_tie, c.d_ctl, c.d_xfull, c.d_img_tab, c.d_cam_tab,             \
+        c.d_chunk_obs, c.d_chunk_pt, c.d_lp_start, c.d_J, c.d_WT, c.d_pt_tab, c.L.u_c, c.set.type,              \
+        c.cam_tab_stride, em, cm, px_of(c), py_of(c))
     FBA_NK_DISPATCH(c.L.nk, LIN);
 #undef LIN
     FBA_HIP(hipGetLastError());
@@ -784,14 +882,7 @@ int launch_linearize(Ctx& c) {
 }
 
 int launch_point(Ctx& c) {
-    if (c.n_lp == 0) return FBA_OK;
-    const int blocks = (int)((c.n_lp + 63) / 64);
-#define PT(NKV)                                                                                            \
-    k_point<NKV><<<blocks, 64, 0, c.stream>>>(c.d_J, c.d_lp_start, c.d_pt_tab, c.d_WT, c.n_lp, c.n_obs_pad, \
-                                              c.n_lp_pad, px_of(c), py_of(c))
-    FBA_NK_DISPATCH(c.L.nk, PT);
-#undef PT
-    FBA_HIP(hipGetLastError());
+    (void)c;  // fused into k_lin_point
     return FBA_OK;
 }
 
@@ -800,21 +891,19 @@ int launch_accumulate(Ctx& c) {
     FBA_HIP(hipMemsetAsync(c.d_S, 0, sizeof(double) * (size_t)(L.n_pad + NB) * L.ld, c.stream));
     const double px = px_of(c), py = py_of(c);
 #define IMG(NKV)                                                                                          \
-    k_image<NKV><<<L.n_img, 128, 0, c.stream>>>(c.d_J, c.d_WT, c.d_pt_tab, c.d_pt, c.d_cam, c.d_img_start, \
-                                                c.d_img_obs, c.d_S, L.ld, L.n_pad, L.n_img, c.n_obs_pad,   \
-                                                c.n_lp_pad, px, py)
+    k_image<NKV><<<L.n_img, 256, 0, c.stream>>>(c.d_J, c.d_WT, c.d_pt_tab, c.d_pt, c.d_cam, c.d_img_start, \
+                                                c.d_img_obs, c.d_S, L.ld, L.n_pad, L.n_img, px, py)
     FBA_NK_DISPATCH(L.nk, IMG);
 #undef IMG
     FBA_HIP(hipGetLastError());
     if (c.n_pairs > 0) {
-        k_pairs<<<(unsigned)c.n_pairs, 64, 0, c.stream>>>(c.d_WT, c.d_pair_e, c.d_pair_start, c.d_pair_ij, c.d_S,
-                                                           L.ld, c.n_obs_pad);
+        k_pairs<<<(unsigned)c.n_pairs, 64, 0, c.stream>>>(c.d_WT, c.d_pair_e, c.d_pair_start, c.d_pair_ij, c.d_S, L.ld);
         FBA_HIP(hipGetLastError());
     }
     dim3 g1(NSLAB, L.n_cam);
 #define CAM(NKV)                                                                                               \
     k_cam_stage1<NKV><<<g1, 128, 0, c.stream>>>(c.d_J, c.d_pt_tab, c.d_lp_start, c.d_cam_lp, c.d_cam_ctl,     \
-                                                c.d_slab, c.n_obs_tie, c.n_obs_pad, c.n_lp_pad, px, py);      \
+                                                c.d_slab, c.n_obs_tie, px, py);                               \
     k_cam_stage2<NKV><<<L.n_cam, 128, 0, c.stream>>>(c.d_slab, c.d_S, L.ld, L.n_pad, L.n_img)
     FBA_NK_DISPATCH(L.nk, CAM);
 #undef CAM
@@ -844,8 +933,7 @@ int launch_backsub_update(Ctx& c) {
         const int blocks = (int)((c.n_lp + 255) / 256);
 #define BS(NKV)                                                                                               \
     k_backsub<NKV><<<blocks, 256, 0, c.stream>>>(c.d_WT, c.d_pt_tab, c.d_lp_start, c.d_lp_tie, c.d_lp_cam,    \
-                                                 c.d_img, c.d_delta, c.n_lp, c.n_obs_pad, c.n_lp_pad, L.u_c, \
-                                                 L.n_img)
+                                                 c.d_img, c.d_delta, c.n_lp, L.u_c, L.n_img)
         FBA_NK_DISPATCH(L.nk, BS);
 #undef BS
         FBA_HIP(hipGetLastError());
@@ -866,8 +954,7 @@ int launch_residuals(Ctx& c) {
 #define RS(NKV)                                                                                                \
     k_residuals<NKV><<<blocks, 256, 0, c.stream>>>(c.d_J, c.d_xy, c.d_img, c.d_cam, c.d_pt, c.d_lp_tie,        \
                                                    c.d_delta, c.d_xfull, c.d_res, c.d_res + 2 * c.n_obs,       \
-                                                   c.d_part, c.n_obs, c.n_obs_pad, L.u_c, L.n_img, px_of(c),   \
-                                                   py_of(c))
+                                                   c.d_part, c.n_obs, L.u_c, L.n_img, px_of(c), py_of(c))
     FBA_NK_DISPATCH(L.nk, RS);
 #undef RS
     FBA_HIP(hipGetLastError());
@@ -880,8 +967,8 @@ int launch_dense_awg(Ctx& c, double* dA, double* dW, const int64_t* d_map, int64
     const int blocks = (int)((c.n_obs + 255) / 256);
 #define DA(NKV)                                                                                               \
     k_dense_awg<NKV><<<blocks, 256, 0, c.stream>>>(c.d_J, c.d_img, c.d_cam, c.d_pt, c.d_lp_tie,               \
-                                                   c.d_obs_pho, d_map, dA, dW, c.n_obs, c.n_obs_pad,      \
-                                                   n_rows, c.L.u_c, c.L.n_img)
+                                                   c.d_obs_pho, d_map, dA, dW, c.n_obs, n_rows, c.L.u_c,      \
+                                                   c.L.n_img)
     FBA_NK_DISPATCH(c.L.nk, DA);
 #undef DA
     FBA_HIP(hipGetLastError());
