@@ -167,6 +167,11 @@ static void destroy(Ctx* c) {
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto e : c->ev_trsm)
+        if (e) (void)hipEventDestroy(e);
+    for (auto e : c->ev_rest)
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

@@ -5,7 +5,7 @@
 // border is folded in as M = S + G W G' (SPD whenever the bordered matrix is nonsingular; W = one
 // equilibrating weight per constraint column, fba_kernels.hip k_border_weights), and
 //
-//   M = L L'        right-looking blocked Cholesky, NB = 128, every step three launches:
+//   M = L L'        right-looking blocked Cholesky, NB = 128, depth-1 lookahead on two streams:
 //     k_potrf128    the 128x128 diagonal block, LDS-resident in one workgroup: 8 sub-panels of 16
 //                   (16x16 factor in registers with v_readlane broadcasts, its 16x16 inverse, then
 //                   the in-block panel solve and trailing update on v_mfma_f64_16x16x4_f64); writes
@@ -36,6 +36,14 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     return __hiloint2double(hi, lo);
 }
 
+// 1/sqrt(d) from v_rsq_f64 refined by two Newton steps (full double precision), no IEEE divide
+__device__ __forceinline__ double rsqrt_d(double d) {
+    double r = __builtin_amdgcn_rsq(d);
+    r = r * (1.5 - 0.5 * d * r * r);
+    r = r * (1.5 - 0.5 * d * r * r);
+    return r;
+}
+
 __device__ __forceinline__ dbl4 mfma(double a, double b, dbl4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
@@ -48,6 +56,7 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* A = smem;                  // [128][LDA]
     double* Dl = smem + CB * LDA;      // [16][17] current inverse D_s
+    double* rd = Dl + IB * 17;         // [16] reciprocal diagonal of the current L_ss
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     for (int idx = tid; idx < CB * CB / 2; idx += 256) {
         const int r = idx >> 6, c = (idx & 63) * 2;
@@ -69,7 +78,8 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
             for (int j = 0; j < IB; ++j) {
                 double d = readlane_d(a[j], j);
                 if (!(d > 0.0)) { bad = true; d = 1.0; }
-                const double sd = sqrt(d), inv = 1.0 / sd;
+                const double inv = rsqrt_d(d), sd = d * inv;
+                if (lane == 0) rd[j] = inv;
                 a[j] = (lane == j) ? sd : (lane > j ? a[j] * inv : a[j]);
 #pragma unroll
                 for (int l = j + 1; l < IB; ++l) a[l] -= a[j] * readlane_d(a[j], l);
@@ -89,7 +99,7 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
                 double acc = (i == lane) ? 1.0 : 0.0;
 #pragma unroll
                 for (int m = 0; m < i; ++m) acc -= A[(c0 + i) * LDA + c0 + m] * x[m];
-                x[i] = acc / A[(c0 + i) * LDA + c0 + i];
+                x[i] = acc * rd[i];
             }
             if (lane < IB) {
 #pragma unroll
@@ -204,16 +214,17 @@ __global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_syrk128: trailing update C(bi,bj) -= X_bi X_bj^T, 128x128 tiles, K = 128 in 32-deep LDS slices.
-// Tiles are enumerated by the host: j in [jlo, jhi) block columns, i >= j block rows (i == nb is the
-// RHS block row).  4 waves, each a 64x64 quadrant = 4x4 MFMA tiles.
+// k_syrk128: trailing update C(bi,bj) -= X_bi X_bj^T, 128x128 tiles, K = 128 in 32-deep slices.
+// Tiles: block columns bj in [jlo, jlo + ncol), block rows bi in [bj, nb] (bi == nb: RHS block row).
+// 4 waves, each a 64x64 quadrant = 4x4 MFMA tiles.  The accumulators start from C (its loads overlap
+// the first slice), each next slice is prefetched into registers while the MFMAs of the current one
+// run, and the epilogue is a plain store.
 // ------------------------------------------------------------------------------------------------
 constexpr int KS = 32;
 constexpr int LDK = 34;   // LDS stride of a 32-deep slice: bank = (4r + 2k) mod 64, conflict-free
 
 __global__ __launch_bounds__(256) void k_syrk128(double* __restrict__ S, int64_t ld, int64_t kb, int64_t nb,
-                                                 int64_t jlo, int64_t jhi) {
-    // decode blockIdx.x -> (bi, bj), bj in [jlo, jhi), bi in [bj, nb] (nb = RHS block row)
+                                                 int64_t jlo) {
     int64_t q = blockIdx.x, bj = jlo, bi = 0;
     for (;;) {
         const int64_t cnt = nb - bj + 1;
@@ -221,43 +232,51 @@ __global__ __launch_bounds__(256) void k_syrk128(double* __restrict__ S, int64_t
         q -= cnt;
         ++bj;
     }
-    (void)jhi;
     __shared__ __attribute__((aligned(16))) double As[CB][LDK];
     __shared__ __attribute__((aligned(16))) double Bs[CB][LDK];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int lr = lane & 15, lk = lane >> 4;
     const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
     const int64_t k0 = kb * CB;
+    double* Cp = S + (bi * CB + wr + lk) * ld + bj * CB + wc + lr;
     dbl4 acc[4][4];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
-    const double* ga = S + (bi * CB) * ld + k0;
-    const double* gb = S + (bj * CB) * ld + k0;
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[a][b][r] = Cp[(a * 16 + 4 * r) * ld + b * 16];
+    // staging: thread -> (row rr, 16 columns at cc) of the 128 x 32 slice, for A and B
+    const int rr = tid >> 1, cc = (tid & 1) * 16;
+    const double* ga = S + (bi * CB + rr) * ld + k0 + cc;
+    const double* gb = S + (bj * CB + rr) * ld + k0 + cc;
+    double2 pa[8], pb[8];
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        pa[h] = *reinterpret_cast<const double2*>(ga + 2 * h);
+        pb[h] = *reinterpret_cast<const double2*>(gb + 2 * h);
+    }
     for (int ks = 0; ks < CB; ks += KS) {
-        // 128 rows x 32 cols per operand: 256 threads x 8 doubles (4 x double2)
+        __syncthreads();
 #pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const int idx = tid + p * 256;         // 512 (row, quad) pairs
-            const int r = idx >> 2, c = (idx & 3) * 8;
-            const double* pa = ga + r * ld + ks + c;
-            const double* pb = gb + r * ld + ks + c;
-#pragma unroll
-            for (int h = 0; h < 8; h += 2) {
-                const double2 va = *reinterpret_cast<const double2*>(pa + h);
-                const double2 vb = *reinterpret_cast<const double2*>(pb + h);
-                As[r][c + h] = va.x; As[r][c + h + 1] = va.y;
-                Bs[r][c + h] = vb.x; Bs[r][c + h + 1] = vb.y;
-            }
+        for (int h = 0; h < 8; ++h) {
+            As[rr][cc + 2 * h] = pa[h].x; As[rr][cc + 2 * h + 1] = pa[h].y;
+            Bs[rr][cc + 2 * h] = pb[h].x; Bs[rr][cc + 2 * h + 1] = pb[h].y;
         }
         __syncthreads();
+        if (ks + KS < CB) {
+#pragma unroll
+            for (int h = 0; h < 8; ++h) {
+                pa[h] = *reinterpret_cast<const double2*>(ga + ks + KS + 2 * h);
+                pb[h] = *reinterpret_cast<const double2*>(gb + ks + KS + 2 * h);
+            }
+        }
 #pragma unroll
         for (int kk = 0; kk < KS; kk += 4) {
             double av[4], bv[4];
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                av[t] = As[wr + t * 16 + lr][kk + lk];
+                av[t] = -As[wr + t * 16 + lr][kk + lk];
                 bv[t] = Bs[wc + t * 16 + lr][kk + lk];
             }
 #pragma unroll
@@ -265,18 +284,85 @@ __global__ __launch_bounds__(256) void k_syrk128(double* __restrict__ S, int64_t
 #pragma unroll
                 for (int b = 0; b < 4; ++b) acc[a][b] = mfma(av[a], bv[b], acc[a][b]);
         }
-        __syncthreads();
     }
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t row = bi * CB + wr + a * 16 + lk + 4 * r;
-                const int64_t col = bj * CB + wc + b * 16 + lr;
-                S[row * ld + col] -= acc[a][b][r];
+            for (int r = 0; r < 4; ++r) Cp[(a * 16 + 4 * r) * ld + b * 16] = acc[a][b][r];
+}
+
+// k_syrk_col64: the critical-path update of block column kb+1 (rows (kb+1)*128 .. (nb+1)*128) with
+// 64x64 tiles, K = 128: 4x the workgroups of k_syrk128, a quarter of the latency each.
+// Tile q: sub-row q >> 1 (64 rows), sub-column q & 1 of the 128-wide block column.
+__global__ __launch_bounds__(256) void k_syrk_col64(double* __restrict__ S, int64_t ld, int64_t kb) {
+    const int64_t r0 = (kb + 1) * CB + (int64_t)(blockIdx.x >> 1) * 64;
+    const int64_t c0 = (kb + 1) * CB + (int64_t)(blockIdx.x & 1) * 64;
+    __shared__ __attribute__((aligned(16))) double As[64][LDK];
+    __shared__ __attribute__((aligned(16))) double Bs[64][LDK];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int lr = lane & 15, lk = lane >> 4;
+    const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
+    const int64_t k0 = kb * CB;
+    double* Cp = S + (r0 + wr + lk) * ld + c0 + wc + lr;
+    dbl4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[a][b][r] = Cp[(a * 16 + 4 * r) * ld + b * 16];
+    const int rr = tid >> 2, cc = (tid & 3) * 8;
+    const double* ga = S + (r0 + rr) * ld + k0 + cc;
+    const double* gb = S + (c0 + rr) * ld + k0 + cc;
+    double2 pa[4], pb[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        pa[h] = *reinterpret_cast<const double2*>(ga + 2 * h);
+        pb[h] = *reinterpret_cast<const double2*>(gb + 2 * h);
+    }
+    for (int ks = 0; ks < CB; ks += KS) {
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            As[rr][cc + 2 * h] = pa[h].x; As[rr][cc + 2 * h + 1] = pa[h].y;
+            Bs[rr][cc + 2 * h] = pb[h].x; Bs[rr][cc + 2 * h + 1] = pb[h].y;
+        }
+        __syncthreads();
+        if (ks + KS < CB) {
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                pa[h] = *reinterpret_cast<const double2*>(ga + ks + KS + 2 * h);
+                pb[h] = *reinterpret_cast<const double2*>(gb + ks + KS + 2 * h);
             }
+        }
+#pragma unroll
+        for (int kk = 0; kk < KS; kk += 4) {
+            double av[2], bv[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                av[t] = -As[wr + t * 16 + lr][kk + lk];
+                bv[t] = Bs[wc + t * 16 + lr][kk + lk];
+            }
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) acc[a][b] = mfma(av[a], bv[b], acc[a][b]);
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Cp[(a * 16 + 4 * r) * ld + b * 16] = acc[a][b][r];
+}
+
+static inline int64_t syrk_tiles(int64_t nb, int64_t jlo, int64_t ncol) {
+    int64_t t = 0;
+    for (int64_t j = jlo; j < jlo + ncol; ++j) t += nb - j + 1;
+    return t;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -400,17 +486,30 @@ __global__ void k_neg_copy(const double* __restrict__ X, double* __restrict__ de
 }
 
 // ------------------------------------------------------------------------------------------------
+// Right-looking with depth-1 lookahead on two streams:
+//   stream A (critical path): potrf(k) -> trsm(k) -> [wait rest(k-1)] -> col(k) -> potrf(k+1) ...
+//   stream B (bulk):          [wait trsm(k)] -> rest(k)
+// col(k) updates block column k+1 (the next panel), rest(k) the columns >= k+2; so the bulk update
+// rest(k-1) runs concurrently with potrf(k) and trsm(k).
 int launch_cholesky(Ctx& c) {
     const int64_t ld = c.L.ld, nb = c.L.n_pad / CB;
-    const size_t lds_potrf = sizeof(double) * (CB * LDA + IB * 17);
+    const size_t lds_potrf = sizeof(double) * (CB * LDA + IB * 17 + IB);
+    hipStream_t A = c.stream, B = c.stream2;
     for (int64_t kb = 0; kb < nb; ++kb) {
-        k_potrf128<<<1, 256, lds_potrf, c.stream>>>(c.d_S, ld, kb * CB, c.d_dinv, c.d_scal);
+        k_potrf128<<<1, 256, lds_potrf, A>>>(c.d_S, ld, kb * CB, c.d_dinv, c.d_scal);
         // panel rows below the diagonal block, RHS block row included: (nb - kb) * 128 rows
-        k_trsm128<<<(unsigned)((nb - kb) * 2), 256, 0, c.stream>>>(c.d_S, ld, kb * CB, (kb + 1) * CB, c.d_dinv);
+        k_trsm128<<<(unsigned)((nb - kb) * 2), 256, 0, A>>>(c.d_S, ld, kb * CB, (kb + 1) * CB, c.d_dinv);
+        FBA_HIP(hipEventRecord(c.ev_trsm[kb], A));
         const int64_t m = nb - kb - 1;  // trailing block columns
+        if (m > 1) {
+            FBA_HIP(hipStreamWaitEvent(B, c.ev_trsm[kb], 0));
+            k_syrk128<<<(unsigned)syrk_tiles(nb, kb + 2, m - 1), 256, 0, B>>>(c.d_S, ld, kb, nb, kb + 2);
+            FBA_HIP(hipEventRecord(c.ev_rest[kb], B));
+        }
         if (m > 0) {
-            const int64_t tiles = m * (m + 1) / 2 + m;  // lower tiles + RHS block row
-            k_syrk128<<<(unsigned)tiles, 256, 0, c.stream>>>(c.d_S, ld, kb, nb, kb + 1, nb);
+            if (kb > 0 && nb - kb > 1) FBA_HIP(hipStreamWaitEvent(A, c.ev_rest[kb - 1], 0));
+            // block column kb+1: (nb - kb) block rows of 128 (RHS row included) x 2 sub-columns of 64
+            k_syrk_col64<<<(unsigned)((nb - kb) * 4), 256, 0, A>>>(c.d_S, ld, kb);
         }
     }
     FBA_HIP(hipGetLastError());
@@ -428,8 +527,16 @@ int launch_backward(Ctx& c) {
 }
 
 int chol_setup(Ctx& c) {
-    const size_t lds_potrf = sizeof(double) * (CB * LDA + IB * 17);
+    const size_t lds_potrf = sizeof(double) * (CB * LDA + IB * 17 + IB);
     FBA_HIP(hipFuncSetAttribute((const void*)k_potrf128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_potrf));
+    const int64_t nb = c.L.n_pad / CB;
+    FBA_HIP(hipStreamCreateWithFlags(&c.stream2, hipStreamNonBlocking));
+    c.ev_trsm.assign(nb, nullptr);
+    c.ev_rest.assign(nb, nullptr);
+    for (int64_t k = 0; k < nb; ++k) {
+        FBA_HIP(hipEventCreateWithFlags(&c.ev_trsm[k], hipEventDisableTiming));
+        FBA_HIP(hipEventCreateWithFlags(&c.ev_rest[k], hipEventDisableTiming));
+    }
     return FBA_OK;
 }
 

@@ -41,6 +41,8 @@ struct Ctx {
     fba_options opt{};
     Layout L;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;          // bulk trailing updates (Cholesky lookahead)
+    std::vector<hipEvent_t> ev_trsm, ev_rest;  // per Cholesky step
     bool own_stream = false;
     int device = 0;
 
