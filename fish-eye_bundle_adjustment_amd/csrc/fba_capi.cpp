@@ -160,7 +160,7 @@ static void destroy(Ctx* c) {
     void* ptrs[] = {c->d_chunk_obs, c->d_chunk_pt, c->d_xy, c->d_img, c->d_cam, c->d_pt, c->d_ctl, c->d_lp_tie, c->d_lp_start, c->d_lp_cam,
                     c->d_img_start, c->d_img_obs, c->d_cam_lp, c->d_cam_ctl, c->d_pair_e, c->d_pair_start,
                     c->d_pair_ij, c->d_xfull, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
-                    c->d_pt_tab, c->d_slab, c->d_S, c->d_X, c->d_dinv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
+                    c->d_pt_tab, c->d_slab, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
                     c->d_active, c->d_counted, c->d_obs_pho};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
@@ -391,6 +391,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         (rc = dalloc(&c->d_slab, (size_t)std::max(L.n_cam, 1) * NSLAB * npk)) ||
         (rc = dalloc(&c->d_S, (size_t)(L.n_pad + NB) * L.ld)) || (rc = dalloc(&c->d_X, (size_t)L.n_pad)) ||
         (rc = dalloc(&c->d_dinv, (size_t)(L.n_pad / NB) * 8 * 256)) ||
+        (rc = dalloc(&c->d_linv, (size_t)(L.n_pad / NB) * NB * NB)) ||
         (rc = dalloc(&c->d_scal, 16)) || (rc = dalloc(&c->d_part, (size_t)c->n_part)) ||
         (rc = dalloc(&c->d_res, (size_t)7 * std::max<int64_t>(c->n_obs, 1)))) {
         destroy(c);

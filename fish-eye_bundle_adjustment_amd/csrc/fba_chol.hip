@@ -17,7 +17,9 @@
 //   forward solve   the right-hand sides [r | G W^1/2] are stored as extra ROWS below M (one extra
 //                   block row), so the panel solves compute Y' = (L^-1 B)' as a by-product
 //   border combine  H = Z'Z, h = Z'y, k = -H^-1 h, y <- y + Z k      (Z, y = forward-solved G W^1/2, r)
-//   backward solve  L' x = y, one launch per block row (k_trsv_bwd128, blocked with the D_s)
+//   backward solve  L' x = y with the 128x128 diagonal-block inverses (k_trtri128, all blocks in
+//                   parallel), then one short launch per block row (k_bwd_step: two 128x128 GEMVs
+//                   on the critical workgroup)
 // so delta_c = -x = -M^-1 (r + G W^1/2 k) satisfies [S G; G' 0][delta; W^1/2 k] = [-r; 0] as the
 // reference's bordered system does.
 #include "fba_internal.h"
@@ -433,51 +435,110 @@ __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, 
 }
 
 // ------------------------------------------------------------------------------------------------
-// backward solve step kb: every workgroup solves L_kk^T x = y_kb (blocked with the D_s, 128 threads),
-// then workgroup jb < kb updates y_jb -= L_{kb,jb}^T x; workgroup kb stores x.
+// k_trtri128: inverse of every 128x128 diagonal block of L (one workgroup per block, all blocks in
+// parallel after the factorisation): block forward substitution on the 8x8 grid of 16x16 tiles,
+// X_ii = D_i, X_ij = -D_i sum_{k=j}^{i-1} L_ik X_kj, on v_mfma_f64_16x16x4_f64.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(128) void k_trsv_bwd128(double* __restrict__ S, int64_t ld, int64_t n_pad, int64_t kb,
-                                                     const double* __restrict__ dinv, double* __restrict__ X) {
+__global__ __launch_bounds__(256) void k_trtri128(const double* __restrict__ S, int64_t ld,
+                                                  const double* __restrict__ dinv, double* __restrict__ linv) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* X = smem;                   // [128][LDA]
+    double* Y = smem + CB * LDA;        // [4 waves][16][17]
+    const int kb = blockIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int lr = lane & 15, lk = lane >> 4;
+    const double* L = S + (int64_t)kb * CB * ld + (int64_t)kb * CB;
+    const double* Dk = dinv + (int64_t)kb * (CB / IB) * (IB * IB);
+    for (int idx = tid; idx < CB * CB; idx += 256) {
+        const int r = idx >> 7, c = idx & 127;
+        X[r * LDA + c] = ((r >> 4) == (c >> 4)) ? Dk[(r >> 4) * IB * IB + (r & 15) * IB + (c & 15)] : 0.0;
+    }
+    __syncthreads();
+    double* Yw = Y + wave * IB * 17;
+    for (int i = 1; i < CB / IB; ++i) {
+        for (int j = wave; j < i; j += 4) {
+            dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+            for (int k = j; k < i; ++k) {
+#pragma unroll
+                for (int kk = 0; kk < IB; kk += 4) {
+                    const double av = L[(int64_t)(IB * i + lr) * ld + IB * k + kk + lk];
+                    const double bv = X[(IB * k + kk + lk) * LDA + IB * j + lr];
+                    acc = mfma(av, bv, acc);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Yw[(lk + 4 * r) * 17 + lr] = acc[r];
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_wave_barrier();
+            dbl4 out = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int kk = 0; kk < IB; kk += 4) {
+                const double av = -Dk[i * IB * IB + lr * IB + kk + lk];
+                const double bv = Yw[(kk + lk) * 17 + lr];
+                out = mfma(av, bv, out);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) X[(IB * i + lk + 4 * r) * LDA + IB * j + lr] = out[r];
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_wave_barrier();
+        }
+        __syncthreads();
+    }
+    double* out = linv + (int64_t)kb * CB * CB;
+    for (int idx = tid; idx < CB * CB; idx += 256) out[idx] = X[(idx >> 7) * LDA + (idx & 127)];
+}
+
+// ------------------------------------------------------------------------------------------------
+// backward solve L' x = y with the diagonal-block inverses:
+//   k_bwd_first  x_{nb-1} = Linv_{nb-1}^T y_{nb-1}
+//   k_bwd_step   (kb): workgroup 0 (the critical one) y_{kb-1} -= L_{kb,kb-1}^T x_kb and then
+//                x_{kb-1} = Linv_{kb-1}^T y_{kb-1}; workgroup 1+j updates y_j -= L_{kb,j}^T x_kb
+// 256 threads = 128 columns x 2 halves of the 128 rows, halves summed in a fixed order.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ double gemv_t128(const double* __restrict__ M, int64_t ldm, const double* __restrict__ v,
+                                            int tid, double* red) {
+    const int c = tid & 127, h = tid >> 7;
+    double acc = 0.0;
+#pragma unroll 8
+    for (int r = h * 64; r < h * 64 + 64; ++r) acc += M[(int64_t)r * ldm + c] * v[r];
+    red[tid] = acc;
+    __syncthreads();
+    const double s = red[c] + red[128 + c];
+    __syncthreads();
+    return s;  // valid for every thread (column c = tid & 127)
+}
+
+__global__ __launch_bounds__(256) void k_bwd_first(const double* __restrict__ S, int64_t ld, int64_t n_pad, int64_t kb,
+                                                   const double* __restrict__ linv, double* __restrict__ X) {
+    __shared__ double ys[CB];
+    __shared__ double red[256];
+    const int tid = threadIdx.x;
+    if (tid < CB) ys[tid] = S[n_pad * ld + kb * CB + tid];
+    __syncthreads();
+    const double x = gemv_t128(linv + kb * CB * CB, CB, ys, tid, red);
+    if (tid < CB) X[kb * CB + tid] = x;
+}
+
+__global__ __launch_bounds__(256) void k_bwd_step(double* __restrict__ S, int64_t ld, int64_t n_pad, int64_t kb,
+                                                  const double* __restrict__ linv, double* __restrict__ X) {
     __shared__ double xs[CB];
-    __shared__ double part[8][IB];
+    __shared__ double ys[CB];
+    __shared__ double red[256];
     const int tid = threadIdx.x;
     const int64_t k0 = kb * CB;
     double* y = S + n_pad * ld;
-    xs[tid] = y[k0 + tid];
+    if (tid < CB) xs[tid] = X[k0 + tid];
     __syncthreads();
-    const double* L = S + k0 * ld + k0;
-    const double* Dk = dinv + kb * (CB / IB) * (IB * IB);
-    for (int s = CB / IB - 1; s >= 0; --s) {
-        const int c0 = s * IB;
-        // z_c = y_{c0+c} - sum_{r >= c0+16} L[r][c0+c] x_r : 8 threads per column, strided rows
-        const int c = tid & 15, g = tid >> 4;
-        double acc = 0.0;
-        for (int r = c0 + IB + g; r < CB; r += 8) acc += L[r * ld + c0 + c] * xs[r];
-        part[g][c] = acc;
-        __syncthreads();
-        if (tid < IB) {
-            double z = xs[c0 + tid];
-            for (int h = 0; h < 8; ++h) z -= part[h][tid];
-            part[0][tid] = z;  // reuse after the reads above (same thread wrote part[*][tid] reads only)
-        }
-        __syncthreads();
-        if (tid < IB) {
-            // x_c = sum_m D[m][c] z_m   (D_s^T z)
-            double v = 0.0;
-            for (int m = 0; m < IB; ++m) v += Dk[s * IB * IB + m * IB + tid] * part[0][m];
-            xs[c0 + tid] = v;
-        }
-        __syncthreads();
-    }
-    const int64_t jb = blockIdx.x;
-    if (jb == kb) {
-        X[k0 + tid] = xs[tid];
+    const int64_t j = blockIdx.x == 0 ? kb - 1 : (int64_t)blockIdx.x - 1;
+    const double u = gemv_t128(S + k0 * ld + j * CB, ld, xs, tid, red);
+    if (blockIdx.x != 0) {
+        if (tid < CB) y[j * CB + tid] -= u;
         return;
     }
-    double acc = 0.0;
-    const double* Lr = S + k0 * ld + jb * CB + tid;
-    for (int r = 0; r < CB; ++r) acc += Lr[r * ld] * xs[r];
-    y[jb * CB + tid] -= acc;
+    if (tid < CB) ys[tid] = y[j * CB + tid] - u;
+    __syncthreads();
+    const double x = gemv_t128(linv + j * CB * CB, CB, ys, tid, red);
+    if (tid < CB) X[j * CB + tid] = x;
 }
 
 __global__ void k_neg_copy(const double* __restrict__ X, double* __restrict__ delta, int64_t u_c) {
@@ -518,9 +579,12 @@ int launch_cholesky(Ctx& c) {
 
 int launch_backward(Ctx& c) {
     const int64_t ld = c.L.ld, nb = c.L.n_pad / CB;
+    const size_t lds_trtri = sizeof(double) * (CB * LDA + 4 * IB * 17);
     if (c.set.inner_constraints) k_border_combine<<<1, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad);
-    for (int64_t kb = nb - 1; kb >= 0; --kb)
-        k_trsv_bwd128<<<(unsigned)(kb + 1), 128, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, kb, c.d_dinv, c.d_X);
+    k_trtri128<<<(unsigned)nb, 256, lds_trtri, c.stream>>>(c.d_S, ld, c.d_dinv, c.d_linv);
+    k_bwd_first<<<1, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, nb - 1, c.d_linv, c.d_X);
+    for (int64_t kb = nb - 1; kb >= 1; --kb)
+        k_bwd_step<<<(unsigned)kb, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, kb, c.d_linv, c.d_X);
     k_neg_copy<<<(unsigned)((c.L.u_c + 255) / 256), 256, 0, c.stream>>>(c.d_X, c.d_delta, c.L.u_c);
     FBA_HIP(hipGetLastError());
     return FBA_OK;
@@ -529,6 +593,8 @@ int launch_backward(Ctx& c) {
 int chol_setup(Ctx& c) {
     const size_t lds_potrf = sizeof(double) * (CB * LDA + IB * 17 + IB);
     FBA_HIP(hipFuncSetAttribute((const void*)k_potrf128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_potrf));
+    const size_t lds_trtri = sizeof(double) * (CB * LDA + 4 * IB * 17);
+    FBA_HIP(hipFuncSetAttribute((const void*)k_trtri128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_trtri));
     const int64_t nb = c.L.n_pad / CB;
     FBA_HIP(hipStreamCreateWithFlags(&c.stream2, hipStreamNonBlocking));
     c.ev_trsm.assign(nb, nullptr);

@@ -97,6 +97,7 @@ struct Ctx {
     double* d_S = nullptr;       // [(n_pad+NB)*ld] normal matrix (lower) + RHS rows
     double* d_X = nullptr;       // [n_pad] solution of the bordered solve
     double* d_dinv = nullptr;    // [(n_pad/NB)*8*256] inverses of the 16x16 diagonal blocks of L
+    double* d_linv = nullptr;    // [(n_pad/NB)*128*128] inverses of the 128x128 diagonal blocks of L
     double* d_scal = nullptr;    // scalars: [1] Cholesky failure flag, [2] sumabs, [8..14] border weights
     double* d_part = nullptr;    // block partial sums
     int n_part = 0;
