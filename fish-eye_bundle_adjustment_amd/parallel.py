@@ -31,13 +31,21 @@ def device_view(ptr, n, device):
 
 
 class ShardedStep:
-    def __init__(self, ctx, group=None, device=None):
+    """One Gauss-Newton iteration across ranks.  ``ctx`` provides accumulate() / solve_update() (a
+    capi.Context); the reduce buffer is the context's device buffer unless ``buffer`` (a float64
+    tensor aliasing the same storage) is given."""
+
+    def __init__(self, ctx, group=None, device=None, buffer=None):
         import torch
         self.ctx = ctx
         self.group = group
-        self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-        ptr, n = ctx.reduce_buffer()
-        self.buf = device_view(ptr, n, self.device)
+        if buffer is None:
+            self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+            ptr, n = ctx.reduce_buffer()
+            self.buf = device_view(ptr, n, self.device)
+        else:
+            self.buf = buffer
+            self.device = buffer.device
         self.share = torch.zeros(1, dtype=torch.float64, device=self.device)
 
     def __call__(self):

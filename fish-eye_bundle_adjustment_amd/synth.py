@@ -72,10 +72,20 @@ def _project(typ, U, V, W, c, xp, yp, K, P):
     return x, y
 
 
+def camera_params(k):
+    """Intrinsics of camera k (k = 0 is the documented single camera)."""
+    return XP + 3.0 * k, YP - 2.0 * k, C0 * (1.0 + 0.02 * k)
+
+
 def generate(n_img, n_tie, seed, obs_per_point=10, noise=0.3, typ="fisheye", spacing=1000.0,
-             max_theta_deg=80.0):
-    """Returns a dict of arrays describing the scene (truth and initial values)."""
+             max_theta_deg=80.0, n_cam=1, n_control=0):
+    """Returns a dict of arrays describing the scene (truth and initial values).
+
+    n_cam > 1: image i uses camera i % n_cam (camera_params(k)); n_control > 0: the first
+    n_control points are control points (exact CNT coordinates, not in the .tie list)."""
     rng = np.random.default_rng(seed)
+    cam_of = np.arange(n_img) % n_cam
+    cxp, cyp, cc = (np.array(v) for v in zip(*[camera_params(k) for k in range(n_cam)]))
     obs_per_point = min(obs_per_point, n_img)
     g = int(math.ceil(math.sqrt(n_img)))
     ii = np.arange(n_img)
@@ -110,7 +120,8 @@ def generate(n_img, n_tie, seed, obs_per_point=10, noise=0.3, typ="fisheye", spa
         U, V, W = UVW[..., 0], UVW[..., 1], UVW[..., 2]
         dist = np.sqrt((d * d).sum(-1))
         with np.errstate(invalid="ignore", divide="ignore"):
-            x, y = _project(typ, U, V, W, C0, XP, YP, K0, P0)
+            kc = cam_of[cand]
+            x, y = _project(typ, U, V, W, cc[kc], cxp[kc], cyp[kc], K0, P0)
         ok = inside & (W < 0) & (-W >= cos_max * dist)
         ok &= (x > SENSOR[0] + 1) & (x < SENSOR[2] - 1) & (y > SENSOR[1] + 1) & (y < SENSOR[3] - 1)
         dist = np.where(ok, dist, np.inf)
@@ -133,8 +144,11 @@ def generate(n_img, n_tie, seed, obs_per_point=10, noise=0.3, typ="fisheye", spa
     C0v = C_true + rng.normal(0, 10.0, C_true.shape)
     ang0 = ang_true + rng.normal(0, math.radians(0.1), ang_true.shape)
     X0 = X_true + rng.normal(0, 10.0, X_true.shape)
+    control = np.zeros(n_tie, bool)
+    control[:n_control] = True
+    X0[control] = X_true[control]
     return dict(C_true=C_true, ang_true=ang_true, X_true=X_true, C0=C0v, ang0=ang0, X0=X0, img=img, pid=pid,
-                xy=xy, typ=typ)
+                xy=xy, typ=typ, cam=cam_of, control=control)
 
 
 def write_folder(scene, folder, name="synth", nk=5, cfg_overrides=None):
@@ -142,6 +156,9 @@ def write_folder(scene, folder, name="synth", nk=5, cfg_overrides=None):
     os.makedirs(folder, exist_ok=True)
     n_img = len(scene["C0"])
     n_tie = len(scene["X0"])
+    cam = scene.get("cam", np.zeros(n_img, np.int64))
+    control = scene.get("control", np.zeros(n_tie, bool))
+    n_cam = int(cam.max()) + 1
     img_ids = [str(1000 + i) for i in range(n_img)]
     wid = max(6, len(str(n_tie)))
     pt_ids = [f"P{j:0{wid}d}" for j in range(n_tie)]
@@ -152,21 +169,25 @@ def write_folder(scene, folder, name="synth", nk=5, cfg_overrides=None):
     with open(os.path.join(folder, name + ".ext"), "w") as fh:
         for i in range(n_img):
             c, a = scene["C0"][i], np.degrees(scene["ang0"][i])
-            fh.write(f"{img_ids[i]}\tfe0\t{c[0]:.17g}\t{c[1]:.17g}\t{c[2]:.17g}\t{a[0]:.17g}\t{a[1]:.17g}\t{a[2]:.17g}\n")
+            fh.write(f"{img_ids[i]}\tfe{cam[i]}\t{c[0]:.17g}\t{c[1]:.17g}\t{c[2]:.17g}\t{a[0]:.17g}\t{a[1]:.17g}\t{a[2]:.17g}\n")
     with open(os.path.join(folder, name + ".cnt"), "w") as fh:
         fh.writelines(f"{pt_ids[j]}\t{x[0]:.17g}\t{x[1]:.17g}\t{x[2]:.17g}\n" for j, x in enumerate(scene["X0"]))
     with open(os.path.join(folder, name + ".tie"), "w") as fh:
-        fh.writelines(f"{p}\n" for p in pt_ids)
+        fh.writelines(f"{p}\n" for j, p in enumerate(pt_ids) if not control[j])
     with open(os.path.join(folder, name + ".int"), "w") as fh:
-        fh.write(f"fe0\t{YDIR:g}\t{SENSOR[0]:g}\t{SENSOR[1]:g}\t{SENSOR[2]:g}\t{SENSOR[3]:g}\n")
         ks = "\t".join(["0"] * nk)
-        fh.write(f"{XP + 0.5:.17g}\t{YP + 0.5:.17g}\t{C0 + 1.0:.17g}\t{ks}\t0\t0\n")
+        for k in range(n_cam):
+            xp, yp, c = camera_params(k)
+            fh.write(f"fe{k}\t{YDIR:g}\t{SENSOR[0]:g}\t{SENSOR[1]:g}\t{SENSOR[2]:g}\t{SENSOR[3]:g}\n")
+            fh.write(f"{xp + 0.5:.17g}\t{yp + 0.5:.17g}\t{c + 1.0:.17g}\t{ks}\t0\t0\n")
     cfg = {
-        "Iteration_Cap": "20", "Threshold_Value": "0.000001", "Meas_std": "0.3", "Inner_Constraints": "1",
+        "Iteration_Cap": "20", "Threshold_Value": "0.000001", "Meas_std": "0.3",
+        "Inner_Constraints": "0" if control.any() else "1",
         "Estimate_Xc": "1", "Estimate_Yc": "1", "Estimate_Zc": "1", "Estimate_Omega": "1", "Estimate_Phi": "1",
         "Estimate_Kappa": "1", "Estimate_xp": "1", "Estimate_yp": "1", "Estimate_c": "1",
         "Estimate_Radial_Distortions": "1", "Num_Radial_Distortions": str(nk),
-        "Estimate_Decentering_Distortions": "1", "Estimate_tie": "1", "Estimate_AllGCP": "1",
+        "Estimate_Decentering_Distortions": "1", "Estimate_tie": "1",
+        "Estimate_AllGCP": "0" if control.any() else "1",
         "Type": f"'{scene['typ']}'", "Check_Points": "0", "Output_Filename": f"'{name}.out'",
     }
     if cfg_overrides:

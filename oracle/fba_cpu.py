@@ -1,0 +1,217 @@
+"""ctypes driver of oracle/libfbo.so (oracle/fba_cpu.c) -- TEST INFRASTRUCTURE ONLY.
+
+The block-sparse CPU restatement of main.m:407-494 for scenes the dense oracle cannot hold:
+``fbo_reduce`` (C/OpenMP) linearises and eliminates the tie points, the reduced camera system is
+solved here with LAPACK through SciPy, ``fbo_update`` (C) back-substitutes, de-scales and updates.
+
+Two solvers for the bordered system (main.m:432, inner constraints on):
+* ``"kkt"``  -- the reference's bordered matrix [S G; G' 0] solved directly (symmetric-indefinite
+  LAPACK solve); independent of the GPU's method, used by the parity tests.
+* ``"chol"`` -- the regularised border M = S + G W G' (W = equilibrated, as the GPU path) with a
+  Cholesky factorisation and a 7x7 border correction; the fastest CPU method, used as bench.py's
+  ``cpu_baseline``.
+
+Only ``tests/``, ``__graft_entry__`` and ``bench.py``'s ``cpu_baseline`` leg may import this.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import time
+
+import numpy as np
+import scipy.linalg as sla
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfbo.so")
+TYPES = ("fisheye", "pinhole", "equisolid", "orthographic", "stereographic")
+
+
+class Input(C.Structure):
+    _fields_ = [("n_pts", C.c_int64), ("n_img", C.c_int32), ("n_cam", C.c_int32), ("n_tie", C.c_int32),
+                ("nk", C.c_int32), ("type", C.c_int32), ("est", C.c_int32 * 11), ("ic", C.c_int32),
+                ("reserved", C.c_int32), ("sx", C.c_double), ("sy", C.c_double)] + [
+        (n, C.c_void_p) for n in ("x", "y", "img", "cam", "tie", "eop", "iop", "bounds", "xyz")]
+
+
+def build():
+    """Compile libfbo.so with the committed Makefile (gcc + OpenMP)."""
+    subprocess.run(["make", "-s", "-C", _HERE, "libfbo.so"], check=True)
+
+
+def _lib():
+    if not os.path.exists(LIB_PATH):
+        build()
+    lib = C.CDLL(LIB_PATH)
+    P = C.c_void_p
+    lib.fbo_create.argtypes = [P, C.c_int]
+    lib.fbo_create.restype = P
+    lib.fbo_destroy.argtypes = [P]
+    lib.fbo_sizes.argtypes = [P, P]
+    lib.fbo_reduce.argtypes = [P, P, P, P, P]
+    lib.fbo_reduce.restype = C.c_int
+    lib.fbo_update.argtypes = [P, P, P]
+    lib.fbo_update.restype = C.c_double
+    lib.fbo_set_shard.argtypes = [P, P, C.c_int]
+    lib.fbo_residuals.argtypes = [P, P]
+    lib.fbo_residuals.restype = C.c_double
+    return lib
+
+
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = _lib()
+    return _LIB
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def default_threads():
+    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return n if n > 0 else min(os.cpu_count() or 1, 16)
+
+
+class CpuAdjustment:
+    """One scene (an ``oracle.fba_oracle.Data``), iterated on the host."""
+
+    def __init__(self, data, threads=None, solver="kkt"):
+        from fba_oracle import buildxhat
+        s = data.settings
+        if s["type"] not in TYPES:
+            raise ValueError("BuildAwG, invalid type in data.settings.type")
+        nk = int(s["Num_Radial_Distortions"])
+        self.data, self.solver = data, solver
+        self.threads = threads or default_threads()
+        self._keep = dict(
+            x=np.ascontiguousarray(data.x, np.float64), y=np.ascontiguousarray(data.y, np.float64),
+            img=np.ascontiguousarray(data.ext_index, np.int64), cam=np.ascontiguousarray(data.cam_num, np.int64),
+            tie=np.ascontiguousarray(data.tie_index, np.int64),
+            eop=np.ascontiguousarray(data.eop_fixed, np.float64),
+            iop=np.ascontiguousarray(data.iop_fixed[:, :5 + nk], np.float64),
+            bounds=np.ascontiguousarray(data.bounds, np.float64),
+            xyz=np.ascontiguousarray(data.xyz_fixed, np.float64))
+        est = (C.c_int32 * 11)(*[int(s[k]) for k in (
+            "Estimate_Xc", "Estimate_Yc", "Estimate_Zc", "Estimate_w", "Estimate_p", "Estimate_k",
+            "Estimate_xp", "Estimate_yp", "Estimate_c", "Estimate_radial", "Estimate_decent")])
+        k = self._keep
+        self.inp = Input(len(data.x), data.numImg, data.numCam, data.numtie, nk, TYPES.index(s["type"]), est,
+                         int(s["Inner_Constraints"]), 0, float(s["Meas_std"]), float(s["Meas_std_y"]),
+                         *[_p(k[n]).value for n in ("x", "y", "img", "cam", "tie", "eop", "iop", "bounds", "xyz")])
+        self.h = lib().fbo_create(C.byref(self.inp), int(self.threads))
+        if not self.h:
+            raise ValueError("fbo_create: unsupported settings")
+        sz = np.zeros(4, np.int64)
+        lib().fbo_sizes(self.h, _p(sz))
+        self.u, self.u_c = int(sz[0]), int(sz[1])
+        self.ic = bool(s["Inner_Constraints"])
+        self.xhat, self.names = buildxhat(data)
+        assert len(self.xhat) == self.u
+        # S and r share one flat buffer: the unit a multi-rank caller all-reduces
+        self.flat = np.zeros(self.u_c * self.u_c + self.u_c)
+        self.S = self.flat[: self.u_c * self.u_c].reshape(self.u_c, self.u_c)
+        self.r = self.flat[self.u_c * self.u_c:]
+        self.G = np.zeros((self.u_c, 7)) if self.ic else None
+        self.deltasum = []
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().fbo_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def _solve(self):
+        S, r, G = self.S, self.r, self.G
+        if not self.ic:
+            return sla.cho_solve(sla.cho_factor(S, lower=True, overwrite_a=True, check_finite=False), -r,
+                                 check_finite=False)
+        if self.solver == "kkt":
+            K = np.zeros((self.u_c + 7, self.u_c + 7))
+            K[: self.u_c, : self.u_c] = S
+            K[: self.u_c, self.u_c:] = G
+            K[self.u_c:, : self.u_c] = G.T
+            rhs = np.concatenate([-r, np.zeros(7)])
+            return sla.solve(K, rhs, assume_a="sym", overwrite_a=True, check_finite=False)[: self.u_c]
+        # regularised border: M = S + G W G', M d = -r - G k, G'd = 0
+        dg = np.diag(S).copy()
+        wm = 1.0 / np.einsum("im,i->m", G * G, 1.0 / dg)
+        M = S
+        M += (G * wm) @ G.T
+        f = sla.cho_factor(M, lower=True, overwrite_a=True, check_finite=False)
+        X = sla.cho_solve(f, np.column_stack([-r, G]), check_finite=False)
+        x0, Y = X[:, 0], X[:, 1:]
+        k = np.linalg.solve(G.T @ Y, G.T @ x0)
+        return x0 - Y @ k
+
+    def set_shard(self, owned_obs, count_cam):
+        """Restrict to one rank's observations (fba_partition's split); see fbo_set_shard."""
+        self._owned = np.ascontiguousarray(owned_obs, dtype=np.uint8)
+        lib().fbo_set_shard(self.h, _p(self._owned), int(count_cam))
+
+    def accumulate(self):
+        """Linearise + point-reduce into ``self.flat`` (= [S | r])."""
+        rc = lib().fbo_reduce(self.h, _p(self.xhat), _p(self.S), _p(self.r), _p(self.G) if self.ic else None)
+        if rc != 0:
+            raise FloatingPointError("singular tie-point block")
+
+    def solve_update(self):
+        """Bordered solve of the (summed) reduced system, back-substitution, update; returns this
+        context's share of deltasum."""
+        dc = np.ascontiguousarray(self._solve())
+        return lib().fbo_update(self.h, _p(dc), _p(self.xhat))
+
+    def step(self):
+        """One pass of main.m:413-488; returns deltasum."""
+        self.accumulate()
+        d = self.solve_update()
+        self.deltasum.append(d)
+        return d
+
+    def adjust(self, max_iter=None):
+        """main.m:407-494: while deltasum > threshold, at most Iteration_Cap passes."""
+        s = self.data.settings
+        cap = s["Iteration_Cap"] if max_iter is None else min(s["Iteration_Cap"], max_iter)
+        d, it = 100.0, 0
+        while d > s["threshold"]:
+            it += 1
+            d = self.step()
+            if it >= cap:
+                break
+        return it
+
+    def residuals(self):
+        """main.m:569, :601: v and sigma0^2 from the last linearisation and de-scaled delta."""
+        v = np.zeros(2 * len(self.data.x))
+        vtpv = lib().fbo_residuals(self.h, _p(v))
+        return v, vtpv / (len(v) - self.u)
+
+
+def time_iterations(folder, seconds=20.0, threads=None, data=None):
+    """cpu_baseline: Gauss-Newton passes per second of the block-sparse CPU restatement
+    ("chol" solver, OpenMP + threaded LAPACK) on ``folder``'s scene, bounded to ~``seconds``."""
+    from threadpoolctl import threadpool_limits
+    import fba_oracle
+    if data is None:
+        data = fba_oracle.load_folder(folder)
+    threads = threads or default_threads()
+    with threadpool_limits(limits=threads):
+        adj = CpuAdjustment(data, threads=threads, solver="chol")
+        t0 = time.perf_counter()
+        n = 0
+        while True:
+            adj.step()
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= seconds or n >= 1000:
+                break
+        adj.close()
+    return {"value": n / el, "iterations": n, "seconds": el, "cores": threads,
+            "n_pts": len(data.x), "u": adj.u, "u_c": adj.u_c}

@@ -100,6 +100,18 @@ def distortion_scale(names, dist_scaling):
     return sc
 
 
+def dist_scaling_of(od):
+    """The rmax^(2j) columns of dist_scaling (BuildAwG.m:424-426) from the INT bounds, without
+    forming the dense A of a large scene (what distortion_scale reads)."""
+    nk = max(od.settings["Num_Radial_Distortions"], 1)
+    out = np.zeros((od.numCam, 2 + nk))
+    for k in range(od.numCam):
+        b = od.bounds[np.nonzero(od.cam_num == k)[0][0]]
+        rmax = np.sqrt(((b[3] - b[1]) * 0.5) ** 2 + ((b[4] - b[2]) * 0.5) ** 2)
+        out[k, 2:] = rmax ** (2 * np.arange(1, nk + 1))
+    return out
+
+
 def group_rel_err(a, b, names, dist_scaling=None):
     """max over parameter groups of max|a-b| / max|b| (distortion terms in the scaled units)."""
     a = np.asarray(a, dtype=np.float64)

@@ -1,0 +1,110 @@
+"""GPU parity at BASELINE.json's scene sizes (synthetic fish-eye configs 3-5, synth.py).
+
+* config 3 (200 images x 5,000 tie points, 50k image points) and a control-point scene: the whole
+  adjustment (main.m:407-494) against the C restatement oracle/fba_cpu.c solving the reference's
+  bordered system directly ("kkt") -- same iteration count, xhat <= 1e-9 relative per parameter
+  group (distortion terms in scaled units), sigma0^2 <= 1e-9.
+* config 4 (1,000 x 50,000, the bench workload): the first two Gauss-Newton passes against the
+  same oracle -- deltasum <= 1e-9 of the first correction, xhat <= 1e-9 per group.
+* config 5 (4,000 x 200,000, 2M image points; too large for a CPU oracle within a test): size-
+  independent properties -- bit-identical repeat runs, monotone convergence below Threshold_Value
+  within Iteration_Cap, and sigma0^2 = 1 +- 5% (the generator's noise equals Meas_std, so the a
+  posteriori variance factor of a correct adjustment is ~1).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import dist_scaling_of, group_rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fbo():
+    import fba_cpu
+    fba_cpu.build()
+    return fba_cpu
+
+
+def _scene(config, root, **kw):
+    from fba_amd import synth
+    folder = os.path.join(root, f"c{config}")
+    if not os.path.exists(os.path.join(folder, ".done")):
+        synth.make_config(config, folder, **kw)
+        open(os.path.join(folder, ".done"), "w").close()
+    return folder
+
+
+@pytest.fixture(scope="module")
+def scenes(tmp_path_factory):
+    return str(tmp_path_factory.mktemp("fullsize"))
+
+
+def _ctx(fba, ds):
+    return fba.capi.Context(ds.pack(), fba.capi.make_settings(ds.settings))
+
+
+def _check_adjust(fba, fbo, oracle, folder):
+    ds = fba.load_folder(folder)
+    od = oracle.load_folder(folder)
+    ref = fbo.CpuAdjustment(od, solver="kkt")
+    it = ref.adjust()
+    _, s02 = ref.residuals()
+    res = fba.adjust(ds)
+    assert res.iterations == it
+    dsc = dist_scaling_of(od)
+    err = group_rel_err(res.xhat, ref.xhat, ref.names, dsc)
+    assert max(err.values()) <= 1e-9, err
+    assert abs(res.sigma02 - s02) <= 1e-9 * s02
+    np.testing.assert_allclose(res.deltasum, ref.deltasum, rtol=0, atol=1e-9 * ref.deltasum[0])
+
+
+def test_config3_adjust_matches_oracle(fba, fbo, oracle, scenes):
+    _check_adjust(fba, fbo, oracle, _scene(3, scenes))
+
+
+def test_control_points_adjust_matches_oracle(fba, fbo, oracle, tmp_path):
+    """No inner constraints: 40 control points fix the datum (the cam0 configuration, at scale)."""
+    from fba_amd import synth
+    folder = synth.write_folder(synth.generate(120, 3000, seed=21, n_control=40), str(tmp_path / "ctl"))
+    _check_adjust(fba, fbo, oracle, folder)
+
+
+def test_config4_first_iterations_match_oracle(fba, fbo, oracle, scenes):
+    folder = _scene(4, scenes)
+    ds = fba.load_folder(folder)
+    od = oracle.load_folder(folder)
+    ref = fbo.CpuAdjustment(od, solver="kkt")
+    ctx = _ctx(fba, ds)
+    try:
+        for _ in range(2):
+            d_ref = ref.step()
+            d = ctx.step()
+            assert abs(d - d_ref) <= 1e-9 * ref.deltasum[0]
+        x = ctx.get_xhat()
+    finally:
+        ctx.close()
+    dsc = dist_scaling_of(od)
+    err = group_rel_err(x, ref.xhat, ref.names, dsc)
+    assert max(err.values()) <= 1e-9, err
+
+
+def test_config5_properties(fba, scenes):
+    folder = _scene(5, scenes)
+    ds = fba.load_folder(folder)
+    runs = []
+    for _ in range(2):
+        ctx = _ctx(fba, ds)
+        try:
+            runs.append(([ctx.step() for _ in range(2)], ctx.get_xhat()))
+        finally:
+            ctx.close()
+    assert runs[0][0] == runs[1][0] and np.array_equal(runs[0][1], runs[1][1])  # deterministic
+    res = fba.adjust(ds)
+    d = np.array(res.deltasum)
+    assert d[-1] <= ds.settings["threshold"] and res.iterations < ds.settings["Iteration_Cap"]
+    assert (np.diff(d[:3]) < 0).all()
+    assert abs(res.sigma02 - 1.0) <= 0.05, res.sigma02
+    assert np.isfinite(res.xhat).all()

@@ -1,0 +1,119 @@
+"""CPU: the C/OpenMP block-sparse restatement (oracle/fba_cpu.c) against the dense NumPy oracle, and
+the observation-shard algebra the multi-GPU path relies on.
+
+oracle/fba_cpu.c is the checker for scenes too large for the dense oracle (the GPU full-size parity
+tests) and bench.py's cpu_baseline, so it is pinned here against the dense oracle, which is itself
+pinned by the reference-expression goldens (tests/test_oracle.py).
+
+Tolerances: xhat 1e-9 relative per parameter group (north_star bar) and sigma0^2 1e-9 on every
+scene whose reference restatement is not path-sensitive (conftest.solver_spread: the pinhole cam0
+variants and the synthetic scenes); the first deltasum 1e-8 (its own 1-ulp-of-w spread is ~2e-9
+on cam0).
+"""
+import numpy as np
+import pytest
+
+from conftest import CAM0_VARIANTS, dist_scaling_of, group_rel_err
+
+PINHOLE = sorted(k for k in CAM0_VARIANTS if "pinhole" in k)
+
+
+@pytest.fixture(scope="module")
+def fbo():
+    import fba_cpu
+    fba_cpu.build()
+    return fba_cpu
+
+
+def _compare(ca, ro, dtol=1e-8):
+    err = group_rel_err(ca.xhat, ro.xhat, ro.names, ro.dist_scaling)
+    assert max(err.values()) <= 1e-9, err
+    v, s02 = ca.residuals()
+    assert abs(s02 - ro.sigma02) <= 1e-9 * ro.sigma02
+    assert np.abs(v - ro.v).max() <= 1e-9 * np.abs(ro.v).max()
+    assert abs(ca.deltasum[0] - ro.deltasum[0]) <= dtol * ro.deltasum[0]
+
+
+@pytest.mark.parametrize("variant", PINHOLE)
+@pytest.mark.parametrize("solver", ["kkt", "chol"])
+def test_cam0_matches_dense_oracle(fbo, oracle, cam0_folders, variant, solver):
+    od = oracle.load_folder(cam0_folders[variant])
+    ro = oracle.adjust(od)
+    ca = fbo.CpuAdjustment(od, threads=2, solver=solver)
+    assert ca.adjust() == ro.iterations
+    _compare(ca, ro)
+
+
+@pytest.mark.parametrize("typ", ["fisheye", "pinhole", "equisolid", "orthographic", "stereographic"])
+def test_synthetic_matches_dense_oracle(fba, fbo, oracle, tmp_path, typ):
+    from fba_amd import synth
+    folder = synth.write_folder(synth.generate(12, 240, seed=17, typ=typ), str(tmp_path / typ))
+    od = oracle.load_folder(folder)
+    ro = oracle.adjust(od)
+    ca = fbo.CpuAdjustment(od, threads=2)
+    assert ca.adjust() == ro.iterations
+    _compare(ca, ro, dtol=1e-9)
+
+
+def test_chol_border_matches_kkt(fba, fbo, oracle, tmp_path):
+    """The regularised-border Cholesky (the GPU's method, and cpu_baseline's) against the direct
+    bordered solve, on a scene with several cameras."""
+    from fba_amd import synth
+    folder = synth.write_folder(synth.generate(30, 900, seed=5, n_cam=3), str(tmp_path / "s"))
+    od = oracle.load_folder(folder)
+    a, b = (fbo.CpuAdjustment(od, threads=2, solver=s) for s in ("kkt", "chol"))
+    d_first = None
+    for _ in range(3):
+        da, db = a.step(), b.step()
+        d_first = d_first or da
+        # once converging, deltasum is a difference of nearly equal iterates: compare on the scale
+        # of the first correction
+        assert abs(da - db) <= 1e-9 * d_first
+    err = group_rel_err(a.xhat, b.xhat, a.names)
+    assert max(err.values()) <= 1e-10, err
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shard_reduced_systems_sum_to_full(fba, fbo, oracle, tmp_path, world):
+    """fba_partition's split: the reduced camera systems of the shards sum to the full one, and the
+    deltasum shares to the full deltasum -- the identity the RCCL all-reduce relies on."""
+    from fba_amd import synth
+    folder = synth.write_folder(synth.generate(16, 400, seed=3, n_control=12), str(tmp_path / "s"))
+    ds = fba.load_folder(folder)
+    od = oracle.load_folder(folder)
+    tie_owner, ctl_owner = fba.capi.partition(ds.pack(), world)
+    tie = od.tie_index
+    owner = np.where(tie >= 0, tie_owner[np.maximum(tie, 0)], ctl_owner)
+    assert (owner >= 0).all() and (owner < world).all()
+    full = fbo.CpuAdjustment(od, threads=2)
+    full.accumulate()
+    ranks = []
+    for r in range(world):
+        c = fbo.CpuAdjustment(od, threads=2)
+        c.set_shard(owner == r, count_cam=(r == 0))
+        c.accumulate()
+        ranks.append(c)
+    total = sum(c.flat for c in ranks)
+    scale = np.abs(full.flat).max()
+    assert np.abs(total - full.flat).max() <= 1e-12 * scale
+    # the all-reduced system is what every rank (and, here, the single context) solves
+    for c in ranks + [full]:
+        c.flat[:] = total
+    shares = [c.solve_update() for c in ranks]
+    d = full.solve_update()
+    assert abs(sum(shares) - d) <= 1e-10 * d
+    dsc = dist_scaling_of(od)  # distortion terms compared in scaled units
+    assert np.array_equal(dsc[:, 2:], oracle.build_awg(od, full.xhat)[3][:, 2:])
+    xr = full.xhat.copy()
+    u_c = full.u_c
+    xr[u_c:] = 0
+    for r, c in enumerate(ranks):
+        own_pts = np.unique(tie[(owner == r) & (tie >= 0)])
+        for j in range(3):
+            xr[u_c + 3 * own_pts + j] = c.xhat[u_c + 3 * own_pts + j]
+        cx = c.xhat.copy()
+        cx[u_c:] = full.xhat[u_c:]
+        err = group_rel_err(cx, full.xhat, full.names, dsc)
+        assert max(err.values()) == 0.0, err
+    err = group_rel_err(xr, full.xhat, full.names, dsc)
+    assert max(err.values()) == 0.0, err
