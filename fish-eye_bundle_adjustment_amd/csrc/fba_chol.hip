@@ -24,6 +24,9 @@
 // reference's bordered system does.
 #include "fba_internal.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace fba {
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
@@ -51,163 +54,292 @@ __device__ __forceinline__ dbl4 mfma(double a, double b, dbl4 c) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_potrf128: factor the 128x128 diagonal block at (k0, k0); 256 threads
+// k_potrf128: factor the 128x128 diagonal block at (k0, k0); 256 threads.
+// Eight 16-column leaves.  A leaf is factored in registers by wave 0 (lane i = row i) with
+// v_mov_b64_dpp row_newbcast broadcasts: every broadcast L[l][j] feeds both the rank-1 update of the
+// leaf and the forward substitution of its inverse D_s = L_ss^-1 (lane c = column c), so the leaf
+// factor and its inverse cost one pass.  In-block lookahead: after the panel solve of leaf s, wave 0
+// updates the next diagonal tile and factors leaf s+1 while waves 1-3 apply the rest of the update.
 // ------------------------------------------------------------------------------------------------
+template <int L>
+__device__ __forceinline__ double bc16(double v) {
+    return __builtin_amdgcn_mov_dpp(v, 0x150 + L, 0xF, 0xF, true);
+}
+
+// lane index known after unrolling: resolved at compile time
+__device__ __forceinline__ double bcl(double v, int l) {
+    switch (l) {
+        case 0: return bc16<0>(v);
+        case 1: return bc16<1>(v);
+        case 2: return bc16<2>(v);
+        case 3: return bc16<3>(v);
+        case 4: return bc16<4>(v);
+        case 5: return bc16<5>(v);
+        case 6: return bc16<6>(v);
+        case 7: return bc16<7>(v);
+        case 8: return bc16<8>(v);
+        case 9: return bc16<9>(v);
+        case 10: return bc16<10>(v);
+        case 11: return bc16<11>(v);
+        case 12: return bc16<12>(v);
+        case 13: return bc16<13>(v);
+        case 14: return bc16<14>(v);
+        case 15: return bc16<15>(v);
+        default: return v;
+    }
+}
+
+// lane i (< 16) of a wave holds row i of a 16x16 SPD block in a[]; on return a[] holds row i of L
+// (lower part) and x[] COLUMN i of L^-1 (x[r] = (L^-1)[r][i]).  Every broadcast L[l][j] feeds both
+// the rank-1 update of the factor and the forward substitution of the inverse's columns.
+// Returns false if a pivot was not positive.
+__device__ __forceinline__ bool leaf_factor(double (&a)[IB], double (&x)[IB], int lane16) {
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < IB; ++r) x[r] = (r == lane16) ? 1.0 : 0.0;
+#pragma unroll
+    for (int j = 0; j < IB; ++j) {
+        double d = bcl(a[j], j);
+        if (!(d > 0.0)) { ok = false; d = 1.0; }
+        const double inv = rsqrt_d(d);
+        a[j] *= inv;       // lane j: d * inv = sqrt(d); lanes > j: L[i][j]; lanes < j: unused
+        x[j] *= inv;       // (L^-1)[j][c] final
+#pragma unroll
+        for (int l = j + 1; l < IB; ++l) {
+            const double t = bcl(a[j], l);  // L[l][j]
+            a[l] -= a[j] * t;
+            x[l] -= t * x[j];
+        }
+    }
+    return ok;
+}
+
 __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_t ld, int64_t k0,
                                                   double* __restrict__ dinv, double* __restrict__ scal) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* A = smem;                  // [128][LDA]
     double* Dl = smem + CB * LDA;      // [16][17] current inverse D_s
-    double* rd = Dl + IB * 17;         // [16] reciprocal diagonal of the current L_ss
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    for (int idx = tid; idx < CB * CB / 2; idx += 256) {
-        const int r = idx >> 6, c = (idx & 63) * 2;
-        const double2 v = *reinterpret_cast<const double2*>(S + (k0 + r) * ld + k0 + c);
-        A[r * LDA + c] = v.x;
-        A[r * LDA + c + 1] = v.y;
+    const int lr = lane & 15, lk = lane >> 4;
+    {
+        // 128 x 128 block: thread -> row tid >> 1, 64 columns; 2 batches of 16 double2
+        const int r = tid >> 1, cb = (tid & 1) * 64;
+        const double* g = S + (k0 + r) * ld + k0 + cb;
+        double2 v[32];
+#pragma unroll
+        for (int q = 0; q < 32; ++q) v[q] = *reinterpret_cast<const double2*>(g + 2 * q);
+#pragma unroll
+        for (int q = 0; q < 32; ++q) {
+            A[r * LDA + cb + 2 * q] = v[q].x;
+            A[r * LDA + cb + 2 * q + 1] = v[q].y;
+        }
     }
     __syncthreads();
-    const int lr = lane & 15, lk = lane >> 4;
+    const int64_t dbase = (k0 / CB) * (CB / IB) * (IB * IB);
+    bool ok = true;
+    // leaf 0 (wave 0)
+    if (wave == 0) {
+        double a[IB], x[IB];
+#pragma unroll
+        for (int c = 0; c < IB; ++c) a[c] = A[lr * LDA + c];
+        ok = leaf_factor(a, x, lr);
+        if (lane < IB) {
+#pragma unroll
+            for (int c = 0; c < IB; ++c) {
+                if (c <= lane) A[lane * LDA + c] = a[c];
+                const double v = (c >= lane) ? x[c] : 0.0;  // (L^-1)[c][lane]
+                Dl[c * 17 + lane] = v;
+                dinv[dbase + c * IB + lane] = v;
+            }
+        }
+    }
     for (int s = 0; s < CB / IB; ++s) {
         const int c0 = s * IB;
+        __syncthreads();  // B1: L_ss, D_s in LDS; column s updated
+        if (s == CB / IB - 1) break;
+        // panel solve X_t = A_ts D_s^T: wave 0 tile s+1, waves 1..3 tiles s+2..7
+        {
+            const int t0 = (wave == 0) ? s + 1 : s + 1 + wave;
+            const int step = (wave == 0) ? CB : 3;
+            for (int t = t0; t < CB / IB; t += step) {
+                const int r0 = t * IB;
+                dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int kk = 0; kk < IB; kk += 4)
+                    acc = mfma(A[(r0 + lr) * LDA + c0 + kk + lk], Dl[lr * 17 + kk + lk], acc);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) A[(r0 + lk + 4 * r) * LDA + c0 + lr] = acc[r];
+            }
+        }
+        __syncthreads();  // B2: panel column s solved
+        const int m = CB / IB - 1 - s;  // tiles (ti, tj), s < tj <= ti
         if (wave == 0) {
-            // (a) 16x16 factor: lane i (< 16) holds row c0+i of the sub-block in registers
-            double a[IB];
-#pragma unroll
-            for (int c = 0; c < IB; ++c) a[c] = (lane < IB) ? A[(c0 + lane) * LDA + c0 + c] : 0.0;
-            bool bad = false;
-#pragma unroll
-            for (int j = 0; j < IB; ++j) {
-                double d = readlane_d(a[j], j);
-                if (!(d > 0.0)) { bad = true; d = 1.0; }
-                const double inv = rsqrt_d(d), sd = d * inv;
-                if (lane == 0) rd[j] = inv;
-                a[j] = (lane == j) ? sd : (lane > j ? a[j] * inv : a[j]);
-#pragma unroll
-                for (int l = j + 1; l < IB; ++l) a[l] -= a[j] * readlane_d(a[j], l);
-            }
-            if (bad && lane == 0 && scal[1] == 0.0) scal[1] = (double)(k0 + c0 + 1);
-            if (lane < IB) {
-#pragma unroll
-                for (int c = 0; c < IB; ++c)
-                    if (c <= lane) A[(c0 + lane) * LDA + c0 + c] = a[c];
-            }
-            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the block's L is in LDS
-            __builtin_amdgcn_wave_barrier();
-            // (b) D_s = L_ss^-1: lane c (< 16) computes column c by forward substitution
-            double x[IB];
-#pragma unroll
-            for (int i = 0; i < IB; ++i) {
-                double acc = (i == lane) ? 1.0 : 0.0;
-#pragma unroll
-                for (int m = 0; m < i; ++m) acc -= A[(c0 + i) * LDA + c0 + m] * x[m];
-                x[i] = acc * rd[i];
-            }
-            if (lane < IB) {
-#pragma unroll
-                for (int i = 0; i < IB; ++i) {
-                    const double v = (i >= lane) ? x[i] : 0.0;
-                    Dl[i * 17 + lane] = v;
-                    dinv[((k0 / CB) * (CB / IB) + s) * (IB * IB) + i * IB + lane] = v;
-                }
-            }
-        }
-        __syncthreads();
-        // (c) in-block panel solve: rows below the sub-block, X = A_s D_s^T  (16-row tiles)
-        for (int t = s + 1 + wave; t < CB / IB; t += 4) {
-            const int r0 = t * IB;
-            dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int kk = 0; kk < IB; kk += 4) {
-                const double av = A[(r0 + lr) * LDA + c0 + kk + lk];
-                const double bv = Dl[lr * 17 + kk + lk];  // B[k][n] = D[n][k]
-                acc = mfma(av, bv, acc);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) A[(r0 + lk + 4 * r) * LDA + c0 + lr] = acc[r];
-        }
-        __syncthreads();
-        // (d) in-block trailing update of the lower tiles (ti >= tj > s), K = 16
-        const int m = CB / IB - 1 - s;
-        const int ntile = m * (m + 1) / 2;
-        for (int q = wave; q < ntile; q += 4) {
-            int ti = 0, rem = q;
-            while (rem > ti) { rem -= ti + 1; ++ti; }
-            const int tj = rem;
-            const int R = (s + 1 + ti) * IB, C = (s + 1 + tj) * IB;
+            // next diagonal tile, then its leaf factor
+            const int R = c0 + IB;
             dbl4 acc;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc[r] = A[(R + lk + 4 * r) * LDA + C + lr];
+            for (int r = 0; r < 4; ++r) acc[r] = A[(R + lk + 4 * r) * LDA + R + lr];
 #pragma unroll
-            for (int kk = 0; kk < IB; kk += 4) {
-                const double av = -A[(R + lr) * LDA + c0 + kk + lk];
-                const double bv = A[(C + lr) * LDA + c0 + kk + lk];
-                acc = mfma(av, bv, acc);
+            for (int kk = 0; kk < IB; kk += 4)
+                acc = mfma(-A[(R + lr) * LDA + c0 + kk + lk], A[(R + lr) * LDA + c0 + kk + lk], acc);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) A[(R + lk + 4 * r) * LDA + R + lr] = acc[r];
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_wave_barrier();
+            double a[IB], x[IB];
+#pragma unroll
+            for (int c = 0; c < IB; ++c) a[c] = A[(R + lr) * LDA + R + c];
+            ok &= leaf_factor(a, x, lr);
+            if (lane < IB) {
+#pragma unroll
+                for (int c = 0; c < IB; ++c) {
+                    if (c <= lane) A[(R + lane) * LDA + R + c] = a[c];
+                    const double v = (c >= lane) ? x[c] : 0.0;  // (L^-1)[c][lane]
+                    Dl[c * 17 + lane] = v;  // safe: every wave finished reading D_s before B2
+                    dinv[dbase + (s + 1) * IB * IB + c * IB + lane] = v;
+                }
             }
+        } else {
+            const int ntile = m * (m + 1) / 2;
+            for (int q = 1 + (wave - 1); q < ntile; q += 3) {
+                int ti = 0, rem = q;
+                while (rem > ti) { rem -= ti + 1; ++ti; }
+                const int tj = rem;
+                const int R = (s + 1 + ti) * IB, C = (s + 1 + tj) * IB;
+                dbl4 acc;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) A[(R + lk + 4 * r) * LDA + C + lr] = acc[r];
+                for (int r = 0; r < 4; ++r) acc[r] = A[(R + lk + 4 * r) * LDA + C + lr];
+#pragma unroll
+                for (int kk = 0; kk < IB; kk += 4)
+                    acc = mfma(-A[(R + lr) * LDA + c0 + kk + lk], A[(C + lr) * LDA + c0 + kk + lk], acc);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) A[(R + lk + 4 * r) * LDA + C + lr] = acc[r];
+            }
         }
-        __syncthreads();
     }
-    for (int idx = tid; idx < CB * CB; idx += 256) {
-        const int r = idx >> 7, c = idx & 127;
-        if (c <= r) S[(k0 + r) * ld + k0 + c] = A[r * LDA + c];
+    if (!ok && lane == 0 && scal[1] == 0.0) scal[1] = (double)(k0 + 1);
+    {
+        const int r = tid >> 1, cb = (tid & 1) * 64;
+        double* g = S + (k0 + r) * ld + k0 + cb;
+#pragma unroll
+        for (int q = 0; q < 32; ++q) {
+            const int c = cb + 2 * q;
+            if (c + 1 <= r) {
+                double2 v;
+                v.x = A[r * LDA + c];
+                v.y = A[r * LDA + c + 1];
+                *reinterpret_cast<double2*>(g + 2 * q) = v;
+            } else if (c == r) {
+                g[2 * q] = A[r * LDA + c];
+            }
+        }
     }
 }
+
 
 // ------------------------------------------------------------------------------------------------
 // k_trsm128: rows [row0, row0 + 64*gridDim.x) of the panel at columns [k0, k0+128):
 //   X = A L^-T by blocked substitution, X_s = (A_s - sum_{t<s} X_t L_st^T) D_s^T.
-// 256 threads = 4 waves x 16 rows; each wave works on its own rows (no barriers).
+// 256 threads = 4 waves x 16 rows.  L_kk was just written by another CU, so its reads are far-cache
+// latency bound: the whole workgroup stages the 28 off-diagonal 16x16 tiles of L_kk and the eight
+// D_s into LDS with one round of loads (issued together with the panel rows), after which each wave
+// runs its eight sub-steps out of LDS only.
 // ------------------------------------------------------------------------------------------------
+constexpr int TRSM_NT = (CB / IB) * (CB / IB - 1) / 2;  // 28 off-diagonal tiles
+constexpr size_t TRSM_LDS = sizeof(double) * (4 * IB * LDA + 4 * IB * 17 + (TRSM_NT + CB / IB) * IB * 17);
+
 __global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t ld, int64_t k0, int64_t row0,
                                                  const double* __restrict__ dinv) {
-    __shared__ __attribute__((aligned(16))) double X[4][IB][LDA];
-    __shared__ __attribute__((aligned(16))) double T[4][IB][17];
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* X = smem;                       // [4][IB][LDA]   panel rows of each wave
+    double* T = X + 4 * IB * LDA;           // [4][IB][17]    per-wave 16x16 staging
+    double* Lt = T + 4 * IB * 17;           // [28][IB][17]   L_st, p = s(s-1)/2 + t
+    double* Dt = Lt + TRSM_NT * IB * 17;    // [8][IB][17]    D_s
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int lr = lane & 15, lk = lane >> 4;
     const int64_t rbase = row0 + (int64_t)blockIdx.x * 64 + wave * IB;
-    double* Xw = &X[wave][0][0];
-    double* Tw = &T[wave][0][0];
-    // load the wave's 16 x 128 panel rows
-    for (int idx = lane; idx < IB * CB / 2; idx += 64) {
-        const int r = idx >> 6, c = (idx & 63) * 2;
-        const double2 v = *reinterpret_cast<const double2*>(S + (rbase + r) * ld + k0 + c);
-        Xw[r * LDA + c] = v.x;
-        Xw[r * LDA + c + 1] = v.y;
-    }
+    double* Xw = X + wave * IB * LDA;
+    double* Tw = T + wave * IB * 17;
     const double* L = S + k0 * ld + k0;
     const double* Dk = dinv + (k0 / CB) * (CB / IB) * (IB * IB);
+    {
+        double2 v[16], lv[14], dv[4];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int idx = lane + 64 * q, r = idx >> 6, c = (idx & 63) * 2;
+            v[q] = *reinterpret_cast<const double2*>(S + (rbase + r) * ld + k0 + c);
+        }
+        // off-diagonal tiles: item i -> tile p = i >> 7, row n = (i >> 3) & 15, columns 2*(i & 7)
+#pragma unroll
+        for (int q = 0; q < 14; ++q) {
+            const int i = tid + 256 * q, p = i >> 7, n = (i >> 3) & 15, kc = (i & 7) * 2;
+            int sr = 1, pp = p;
+            while (pp >= sr) { pp -= sr; ++sr; }
+            lv[q] = *reinterpret_cast<const double2*>(L + (int64_t)(sr * IB + n) * ld + pp * IB + kc);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dv[q] = *reinterpret_cast<const double2*>(Dk + 2 * (tid + 256 * q));
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int idx = lane + 64 * q, r = idx >> 6, c = (idx & 63) * 2;
+            Xw[r * LDA + c] = v[q].x;
+            Xw[r * LDA + c + 1] = v[q].y;
+        }
+#pragma unroll
+        for (int q = 0; q < 14; ++q) {
+            const int i = tid + 256 * q, p = i >> 7, n = (i >> 3) & 15, kc = (i & 7) * 2;
+            Lt[(p * IB + n) * 17 + kc] = lv[q].x;
+            Lt[(p * IB + n) * 17 + kc + 1] = lv[q].y;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = 2 * (tid + 256 * q), sd = e >> 8, n = (e >> 4) & 15, kc = e & 15;
+            Dt[(sd * IB + n) * 17 + kc] = dv[q].x;
+            Dt[(sd * IB + n) * 17 + kc + 1] = dv[q].y;
+        }
+    }
+    __syncthreads();
+#pragma unroll
     for (int s = 0; s < CB / IB; ++s) {
         const int c0 = s * IB;
-        // Z = A_s - sum_{t<s} X_t L_st^T : output 16x16, K = 16 s
+        // Z = A_s - sum_{t<s} X_t L_st^T : output 16x16, K = 16 s.  All operands of the step are read
+        // from LDS in one batch, then two independent MFMA chains.
+        double av[CB / 4], bv[CB / 4];
+#pragma unroll
+        for (int t = 0; t < s; ++t) {
+            const double* Lst = Lt + (s * (s - 1) / 2 + t) * IB * 17;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {  // B[k][n] = L[c0+n][t*16+k]
+                av[4 * t + kk] = Xw[lr * LDA + t * IB + 4 * kk + lk];
+                bv[4 * t + kk] = Lst[lr * 17 + 4 * kk + lk];
+            }
+        }
+        dbl4 p0 = dbl4{0.0, 0.0, 0.0, 0.0}, p1 = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < 4 * s; q += 2) {
+            p0 = mfma(av[q], bv[q], p0);
+            p1 = mfma(av[q + 1], bv[q + 1], p1);
+        }
         dbl4 acc;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r] = Xw[(lk + 4 * r) * LDA + c0 + lr];
-        for (int kk = 0; kk < c0; kk += 4) {
-            const double av = -Xw[lr * LDA + kk + lk];
-            const double bv = L[(c0 + lr) * ld + kk + lk];  // B[k][n] = L[c0+n][k]
-            acc = mfma(av, bv, acc);
-        }
+        for (int r = 0; r < 4; ++r) acc[r] = Xw[(lk + 4 * r) * LDA + c0 + lr] - (p0[r] + p1[r]);
         // Z (D layout) -> LDS, then X_s = Z D_s^T
 #pragma unroll
         for (int r = 0; r < 4; ++r) Tw[(lk + 4 * r) * 17 + lr] = acc[r];
         __builtin_amdgcn_s_waitcnt(0xC07F);
         __builtin_amdgcn_wave_barrier();
         dbl4 out = dbl4{0.0, 0.0, 0.0, 0.0};
+        const double* Ds = Dt + s * IB * 17;
 #pragma unroll
-        for (int kk = 0; kk < IB; kk += 4) {
-            const double av = Tw[lr * 17 + kk + lk];
-            const double bv = Dk[s * IB * IB + lr * IB + kk + lk];  // B[k][n] = D[n][k]
-            out = mfma(av, bv, out);
-        }
+        for (int kk = 0; kk < IB; kk += 4) out = mfma(Tw[lr * 17 + kk + lk], Ds[lr * 17 + kk + lk], out);
 #pragma unroll
         for (int r = 0; r < 4; ++r) Xw[(lk + 4 * r) * LDA + c0 + lr] = out[r];
         __builtin_amdgcn_s_waitcnt(0xC07F);
         __builtin_amdgcn_wave_barrier();
     }
-    for (int idx = lane; idx < IB * CB / 2; idx += 64) {
-        const int r = idx >> 6, c = (idx & 63) * 2;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int idx = lane + 64 * q, r = idx >> 6, c = (idx & 63) * 2;
         double2 v;
         v.x = Xw[r * LDA + c];
         v.y = Xw[r * LDA + c + 1];
@@ -226,16 +358,17 @@ constexpr int KS = 32;
 constexpr int LDK = 34;   // LDS stride of a 32-deep slice: bank = (4r + 2k) mod 64, conflict-free
 
 __global__ __launch_bounds__(256) void k_syrk128(double* __restrict__ S, int64_t ld, int64_t kb, int64_t nb,
-                                                 int64_t jlo) {
-    int64_t q = blockIdx.x, bj = jlo, bi = 0;
+                                                 int64_t jlo, int64_t ntiles) {
+    __shared__ __attribute__((aligned(16))) double As[CB][LDK];
+    __shared__ __attribute__((aligned(16))) double Bs[CB][LDK];
+    for (int64_t q0 = blockIdx.x; q0 < ntiles; q0 += gridDim.x) {
+    int64_t q = q0, bj = jlo, bi = 0;
     for (;;) {
         const int64_t cnt = nb - bj + 1;
         if (q < cnt) { bi = bj + q; break; }
         q -= cnt;
         ++bj;
     }
-    __shared__ __attribute__((aligned(16))) double As[CB][LDK];
-    __shared__ __attribute__((aligned(16))) double Bs[CB][LDK];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int lr = lane & 15, lk = lane >> 4;
     const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
@@ -293,6 +426,8 @@ __global__ __launch_bounds__(256) void k_syrk128(double* __restrict__ S, int64_t
         for (int b = 0; b < 4; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) Cp[(a * 16 + 4 * r) * ld + b * 16] = acc[a][b][r];
+    __syncthreads();  // LDS reuse by the next tile
+    }
 }
 
 // k_syrk_col64: the critical-path update of block column kb+1 (rows (kb+1)*128 .. (nb+1)*128) with
@@ -559,12 +694,14 @@ int launch_cholesky(Ctx& c) {
     for (int64_t kb = 0; kb < nb; ++kb) {
         k_potrf128<<<1, 256, lds_potrf, A>>>(c.d_S, ld, kb * CB, c.d_dinv, c.d_scal);
         // panel rows below the diagonal block, RHS block row included: (nb - kb) * 128 rows
-        k_trsm128<<<(unsigned)((nb - kb) * 2), 256, 0, A>>>(c.d_S, ld, kb * CB, (kb + 1) * CB, c.d_dinv);
+        k_trsm128<<<(unsigned)((nb - kb) * 2), 256, TRSM_LDS, A>>>(c.d_S, ld, kb * CB, (kb + 1) * CB, c.d_dinv);
         FBA_HIP(hipEventRecord(c.ev_trsm[kb], A));
         const int64_t m = nb - kb - 1;  // trailing block columns
         if (m > 1) {
             FBA_HIP(hipStreamWaitEvent(B, c.ev_trsm[kb], 0));
-            k_syrk128<<<(unsigned)syrk_tiles(nb, kb + 2, m - 1), 256, 0, B>>>(c.d_S, ld, kb, nb, kb + 2);
+            const int64_t nt = syrk_tiles(nb, kb + 2, m - 1);
+            const int64_t grid = c.syrk_cap > 0 && nt > c.syrk_cap ? c.syrk_cap : nt;
+            k_syrk128<<<(unsigned)grid, 256, 0, B>>>(c.d_S, ld, kb, nb, kb + 2, nt);
             FBA_HIP(hipEventRecord(c.ev_rest[kb], B));
         }
         if (m > 0) {
@@ -593,10 +730,24 @@ int launch_backward(Ctx& c) {
 int chol_setup(Ctx& c) {
     const size_t lds_potrf = sizeof(double) * (CB * LDA + IB * 17 + IB);
     FBA_HIP(hipFuncSetAttribute((const void*)k_potrf128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_potrf));
+    FBA_HIP(hipFuncSetAttribute((const void*)k_trsm128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRSM_LDS));
     const size_t lds_trtri = sizeof(double) * (CB * LDA + 4 * IB * 17);
     FBA_HIP(hipFuncSetAttribute((const void*)k_trtri128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_trtri));
     const int64_t nb = c.L.n_pad / CB;
-    FBA_HIP(hipStreamCreateWithFlags(&c.stream2, hipStreamNonBlocking));
+    // bulk trailing updates on a low-priority stream: the latency-bound critical-path kernels of
+    // the main stream get the compute units first as workgroups retire
+    int prio_least = 0, prio_greatest = 0;
+    FBA_HIP(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
+    const char* pe = getenv("FBA_PRIO");
+    const int prio_mode = pe ? atoi(pe) : 1;
+    if (prio_mode == 1)
+        FBA_HIP(hipStreamCreateWithPriority(&c.stream2, hipStreamNonBlocking, prio_least));
+    else
+        FBA_HIP(hipStreamCreateWithFlags(&c.stream2, hipStreamNonBlocking));
+    const char* ce = getenv("FBA_SYRK_CAP");
+    c.syrk_cap = ce ? atoi(ce) : 0;
+    if (c.opt.verbose) fprintf(stderr, "[fba] stream priorities least %d greatest %d, bulk mode %d, syrk cap %d\n",
+                           prio_least, prio_greatest, prio_mode, c.syrk_cap);
     c.ev_trsm.assign(nb, nullptr);
     c.ev_rest.assign(nb, nullptr);
     for (int64_t k = 0; k < nb; ++k) {
