@@ -341,6 +341,9 @@ __global__ __launch_bounds__(256) void k_lin_point(
 //   21 <= q < 27      reduced RHS r_e
 //   27 <= q < 27+6CW  image-camera block (camera row c, image column a)
 // Two thread groups split the staged observations; their sums are added in a fixed order.
+// The gathers are software-pipelined: the observation/point indices of chunk c+1 are fetched before
+// chunk c is published to LDS, and its rows are loaded into registers (all loads of a thread in
+// flight together) while chunk c is reduced.
 // ------------------------------------------------------------------------------------------------
 __constant__ int c_tri_a[21] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 4, 5, 5, 5, 5, 5, 5};
 __constant__ int c_tri_b[21] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4, 0, 1, 2, 3, 4, 5};
@@ -353,12 +356,16 @@ __global__ __launch_bounds__(256) void k_image(const double* __restrict__ J, con
                                                int64_t n_pad, int n_img, double px, double py) {
     using LY = Lay<NK>;
     constexpr int CW = LY::CW, NJ = LY::NJ, JS = LY::JS, PS = LY::PS;
-    constexpr int F = JS + 36 + 3 + 3 * CW;  // J row | W,T | vb | Wc
+    constexpr int NP = 3 + 3 * CW;           // vb | Wc
+    constexpr int F = JS + 36 + NP;          // J row | W,T | vb | Wc
     constexpr int CH = 32;
     constexpr int NOUT = 27 + 6 * CW;
+    constexpr int NJ2 = JS / 2, NW2 = 18;
+    constexpr int RJ = (CH * NJ2 + 255) / 256, RW = (CH * NW2 + 255) / 256, RP = (CH * NP + 255) / 256;
+    static_assert(JS % 2 == 0, "J rows are read as double2");
     __shared__ double st[CH][F + 1];
     __shared__ double part[128];
-    __shared__ int so[CH];
+    __shared__ int so[2][CH], sp[2][CH];
     const int e = blockIdx.x;
     const int tid = threadIdx.x;
     const int g = tid >> 7, q = tid & 127;
@@ -368,30 +375,71 @@ __global__ __launch_bounds__(256) void k_image(const double* __restrict__ J, con
     if (q < 21) { kind = 0; a = c_tri_a[q]; b = c_tri_b[q]; }
     else if (q < 27) { kind = 1; a = q - 21; }
     else if (q < NOUT) { kind = 2; a = (q - 27) % 6; b = (q - 27) / 6; }
-    double acc = 0.0;
-    for (int base = i0; base < i1; base += CH) {
-        const int n = min(CH, i1 - base);
-        if (tid < n) so[tid] = img_obs[base + tid];
-        __syncthreads();
-        for (int idx = tid; idx < n * F; idx += 256) {
-            const int k = idx / F, f = idx - k * F;
-            const int o = so[k];
-            double v;
-            if (f < JS) v = J[(int64_t)o * JS + f];
-            else if (f < JS + 36) v = WT[(int64_t)o * 36 + (f - JS)];
-            else {
-                const int p = pt[o];
-                const int ff = f - JS - 36;  // 0..2 vb, 3.. Wc
-                v = (p < 0) ? 0.0 : PT[(int64_t)p * PS + (ff < 3 ? 6 + ff : 12 + ff - 3)];
-            }
-            st[k][f] = v;
+    const double2* J2 = reinterpret_cast<const double2*>(J);
+    const double2* W2 = reinterpret_cast<const double2*>(WT);
+    double2 rj[RJ], rw[RW];
+    double rp[RP];
+    auto fetch_idx = [&](int base, int buf) {
+        if (tid < CH) {
+            const int o = (base + tid < i1) ? img_obs[base + tid] : 0;
+            so[buf][tid] = o;
+            sp[buf][tid] = (base + tid < i1) ? pt[o] : -1;
         }
+    };
+    auto fetch_rows = [&](int buf, int n) {
+#pragma unroll
+        for (int r = 0; r < RJ; ++r) {
+            const int idx = tid + 256 * r, k = idx / NJ2, f = idx - k * NJ2;
+            if (idx < n * NJ2) rj[r] = J2[(int64_t)so[buf][k] * NJ2 + f];
+        }
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+            const int idx = tid + 256 * r, k = idx / NW2, f = idx - k * NW2;
+            if (idx < n * NW2) rw[r] = W2[(int64_t)so[buf][k] * NW2 + f];
+        }
+#pragma unroll
+        for (int r = 0; r < RP; ++r) {
+            const int idx = tid + 256 * r, k = idx / NP, f = idx - k * NP;
+            if (idx < n * NP) {
+                const int p = sp[buf][k];
+                rp[r] = (p < 0) ? 0.0 : PT[(int64_t)p * PS + (f < 3 ? 6 + f : 12 + f - 3)];
+            }
+        }
+    };
+    auto publish = [&](int n) {
+#pragma unroll
+        for (int r = 0; r < RJ; ++r) {
+            const int idx = tid + 256 * r, k = idx / NJ2, f = idx - k * NJ2;
+            if (idx < n * NJ2) { st[k][2 * f] = rj[r].x; st[k][2 * f + 1] = rj[r].y; }
+        }
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+            const int idx = tid + 256 * r, k = idx / NW2, f = idx - k * NW2;
+            if (idx < n * NW2) { st[k][JS + 2 * f] = rw[r].x; st[k][JS + 2 * f + 1] = rw[r].y; }
+        }
+#pragma unroll
+        for (int r = 0; r < RP; ++r) {
+            const int idx = tid + 256 * r, k = idx / NP, f = idx - k * NP;
+            if (idx < n * NP) st[k][JS + 36 + f] = rp[r];
+        }
+    };
+    fetch_idx(i0, 0);
+    __syncthreads();
+    fetch_rows(0, min(CH, i1 - i0));
+    double acc = 0.0;
+    int buf = 0;
+    for (int base = i0; base < i1; base += CH, buf ^= 1) {
+        const int n = min(CH, i1 - base);
+        const bool more = base + CH < i1;
+        if (more) fetch_idx(base + CH, buf ^ 1);
+        publish(n);
         __syncthreads();
+        if (more) fetch_rows(buf ^ 1, min(CH, i1 - base - CH));
         if (q < NOUT) {
             for (int k = g; k < n; k += 2) {
                 const double* r = st[k];
                 const double ea0 = r[a], ea1 = r[NJ + a];
-                const bool tie = pt[so[k]] >= 0;
+                const bool tie = sp[buf][k] >= 0;
                 if (kind == 0) {
                     acc += px * ea0 * r[b] + py * ea1 * r[NJ + b];
                     if (tie) {
