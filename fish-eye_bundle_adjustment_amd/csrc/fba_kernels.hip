@@ -487,8 +487,13 @@ __global__ __launch_bounds__(256) void k_image(const double* __restrict__ J, con
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_pairs(const double* __restrict__ WT, const int32_t* __restrict__ pair_e,
                                               const int32_t* __restrict__ pair_start, const int32_t* __restrict__ pair_ij,
-                                              double* __restrict__ S, int64_t ld) {
-    const int64_t pr = blockIdx.x;
+                                              double* __restrict__ S, int64_t ld, int64_t n_pairs) {
+    // XCD-aware: workgroups are dealt round-robin over the 8 XCDs, so block b works on pair
+    // (b % 8) * per + b / 8 -- each XCD walks a contiguous run of the (e1, e2)-sorted pair list and
+    // the W/T rows of an image's observations are re-read from that XCD's L2
+    const int64_t per = (n_pairs + 7) / 8;
+    const int64_t pr = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+    if (pr >= n_pairs) return;
     const int q = threadIdx.x;
     if (q >= 36) return;
     const int a = q / 6, b = q % 6;
@@ -554,37 +559,74 @@ __global__ __launch_bounds__(128) void k_cam_stage1(const double* __restrict__ J
     const int64_t q0 = cam_ctl[k], q1 = cam_ctl[k + 1];
     const int64_t nq = q1 - q0;
     const int64_t b0 = q0 + nq * s / NSLAB, b1 = q0 + nq * (s + 1) / NSLAB;
-    // direct terms over the observations: tie observations of points [a0,a1), then control ones
+    // direct terms over the observations: tie observations of points [a0,a1), then control ones.
+    // Chunks of 32 observations; the rows of chunk c+1 are loaded into registers while chunk c is
+    // reduced from LDS.
     const int64_t oa0 = (a0 < a1) ? lp_start[a0] : 0, oa1 = (a0 < a1) ? lp_start[a1] : 0;
-    for (int pass = 0; pass < 2; ++pass) {
-        const int64_t lo = pass == 0 ? oa0 : n_obs_tie + b0;
-        const int64_t hi = pass == 0 ? oa1 : n_obs_tie + b1;
-        for (int64_t base = lo; base < hi; base += CH) {
-            const int n = (int)min((int64_t)CH, hi - base);
-            for (int idx = q; idx < n * (2 * CW + 2); idx += 128) {
-                const int kk = idx / (2 * CW + 2), f = idx - kk * (2 * CW + 2);
-                const double* r = J + (base + kk) * JS;
-                so[kk][f] = (f < CW) ? r[6 + f] : (f < 2 * CW ? r[NJ + 6 + f - CW] : r[2 * NJ + f - 2 * CW]);
+    const int64_t ob0 = n_obs_tie + b0, ob1 = n_obs_tie + b1;
+    const int nc0 = (int)((oa1 - oa0 + CH - 1) / CH), nc1 = (int)((ob1 - ob0 + CH - 1) / CH);
+    constexpr int FO = 2 * CW + 2;
+    constexpr int RO = (CH * FO + 127) / 128, RPT = (CH * FP + 127) / 128;
+    auto chunk = [&](int c, int64_t& base) -> int {
+        if (c < nc0) { base = oa0 + (int64_t)c * CH; return (int)min((int64_t)CH, oa1 - base); }
+        base = ob0 + (int64_t)(c - nc0) * CH;
+        return (int)min((int64_t)CH, ob1 - base);
+    };
+    double ro[RO];
+    auto fetch_o = [&](int c) {
+        int64_t base;
+        const int n = chunk(c, base);
+#pragma unroll
+        for (int r = 0; r < RO; ++r) {
+            const int idx = q + 128 * r, kk = idx / FO, f = idx - kk * FO;
+            if (idx < n * FO) {
+                const double* row = J + (base + kk) * JS;
+                ro[r] = (f < CW) ? row[6 + f] : (f < 2 * CW ? row[NJ + 6 + f - CW] : row[2 * NJ + f - 2 * CW]);
             }
-            __syncthreads();
-            if (act)
-                for (int kk = 0; kk < n; ++kk) {
-                    const double* r = so[kk];
-                    const double s0 = (c2 >= 0) ? r[c2] : r[2 * CW];
-                    const double s1 = (c2 >= 0) ? r[CW + c2] : r[2 * CW + 1];
-                    acc += px * r[c1] * s0 + py * r[CW + c1] * s1;
-                }
-            __syncthreads();
         }
-    }
-    // Schur terms of the points [a0, a1)
-    for (int64_t base = a0; base < a1; base += CH) {
-        const int n = (int)min((int64_t)CH, a1 - base);
-        for (int idx = q; idx < n * FP; idx += 128) {
-            const int kk = idx / FP, f = idx - kk * FP;
-            sp[kk][f] = PT[(base + kk) * PS + 6 + (f < 3 ? f : f + 3)];
+        return n;
+    };
+    const int nco = nc0 + nc1;
+    int n_cur = nco > 0 ? fetch_o(0) : 0;
+    for (int c = 0; c < nco; ++c) {
+        const int n = n_cur;
+#pragma unroll
+        for (int r = 0; r < RO; ++r) {
+            const int idx = q + 128 * r, kk = idx / FO, f = idx - kk * FO;
+            if (idx < n * FO) so[kk][f] = ro[r];
         }
         __syncthreads();
+        if (c + 1 < nco) n_cur = fetch_o(c + 1);
+        if (act)
+            for (int kk = 0; kk < n; ++kk) {
+                const double* r = so[kk];
+                const double s0 = (c2 >= 0) ? r[c2] : r[2 * CW];
+                const double s1 = (c2 >= 0) ? r[CW + c2] : r[2 * CW + 1];
+                acc += px * r[c1] * s0 + py * r[CW + c1] * s1;
+            }
+        __syncthreads();
+    }
+    // Schur terms of the points [a0, a1), pipelined the same way
+    double rpt[RPT];
+    auto fetch_p = [&](int64_t base) {
+        const int n = (int)min((int64_t)CH, a1 - base);
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+            const int idx = q + 128 * r, kk = idx / FP, f = idx - kk * FP;
+            if (idx < n * FP) rpt[r] = PT[(base + kk) * PS + 6 + (f < 3 ? f : f + 3)];
+        }
+        return n;
+    };
+    n_cur = a0 < a1 ? fetch_p(a0) : 0;
+    for (int64_t base = a0; base < a1; base += CH) {
+        const int n = n_cur;
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+            const int idx = q + 128 * r, kk = idx / FP, f = idx - kk * FP;
+            if (idx < n * FP) sp[kk][f] = rpt[r];
+        }
+        __syncthreads();
+        if (base + CH < a1) n_cur = fetch_p(base + CH);
         if (act)
             for (int kk = 0; kk < n; ++kk) {
                 const double* r = sp[kk];  // vb 0..2, Wc 3.., Tc 3+3CW..
@@ -945,7 +987,8 @@ int launch_accumulate(Ctx& c) {
 #undef IMG
     FBA_HIP(hipGetLastError());
     if (c.n_pairs > 0) {
-        k_pairs<<<(unsigned)c.n_pairs, 64, 0, c.stream>>>(c.d_WT, c.d_pair_e, c.d_pair_start, c.d_pair_ij, c.d_S, L.ld);
+        k_pairs<<<(unsigned)(8 * ((c.n_pairs + 7) / 8)), 64, 0, c.stream>>>(c.d_WT, c.d_pair_e, c.d_pair_start,
+                                                                       c.d_pair_ij, c.d_S, L.ld, c.n_pairs);
         FBA_HIP(hipGetLastError());
     }
     dim3 g1(NSLAB, L.n_cam);
