@@ -53,14 +53,6 @@ __device__ __forceinline__ dbl4 mfma(double a, double b, dbl4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// ------------------------------------------------------------------------------------------------
-// k_potrf128: factor the 128x128 diagonal block at (k0, k0); 256 threads.
-// Eight 16-column leaves.  A leaf is factored in registers by wave 0 (lane i = row i) with
-// v_mov_b64_dpp row_newbcast broadcasts: every broadcast L[l][j] feeds both the rank-1 update of the
-// leaf and the forward substitution of its inverse D_s = L_ss^-1 (lane c = column c), so the leaf
-// factor and its inverse cost one pass.  In-block lookahead: after the panel solve of leaf s, wave 0
-// updates the next diagonal tile and factors leaf s+1 while waves 1-3 apply the rest of the update.
-// ------------------------------------------------------------------------------------------------
 template <int L>
 __device__ __forceinline__ double bc16(double v) {
     return __builtin_amdgcn_mov_dpp(v, 0x150 + L, 0xF, 0xF, true);
@@ -89,10 +81,54 @@ __device__ __forceinline__ double bcl(double v, int l) {
     }
 }
 
+// d += s[lane l of this row] * m, one v_fmac_f64_dpp (row_newbcast:l); l known after unrolling.
+// The first use of a freshly written s carries the 2-wait-state VALU-write -> DPP-read gap itself
+// (inline asm is opaque to the compiler's hazard recognizer).
+__device__ __forceinline__ void fmac_bc_first(double& d, double s, double m, int l) {
+    switch (l) {
+        case 1: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:1 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 2: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:2 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 3: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:3 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 4: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:4 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 5: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:5 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 6: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:6 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 7: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:7 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 8: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:8 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 9: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:9 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 10: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:10 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 11: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:11 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 12: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:12 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 13: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:13 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 14: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:14 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 15: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:15 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        default: break;
+    }
+}
+__device__ __forceinline__ void fmac_bc(double& d, double s, double m, int l) {
+    switch (l) {
+        case 1: asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:1 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 2: asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:2 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 3: asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:3 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 4: asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:4 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 5: asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:5 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 6: asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:6 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 7: asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:7 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 8: asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:8 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 9: asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:9 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 10: asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:10 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 11: asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:11 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 12: asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:12 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 13: asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:13 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 14: asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:14 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 15: asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:15 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        default: break;
+    }
+}
+
 // lane i (< 16) of a wave holds row i of a 16x16 SPD block in a[]; on return a[] holds row i of L
 // (lower part) and x[] COLUMN i of L^-1 (x[r] = (L^-1)[r][i]).  Every broadcast L[l][j] feeds both
-// the rank-1 update of the factor and the forward substitution of the inverse's columns.
-// Returns false if a pivot was not positive.
+// the rank-1 update of the factor and the forward substitution of the inverse's columns, each as
+// one v_fmac_f64_dpp.  Returns false if a pivot was not positive.
 __device__ __forceinline__ bool leaf_factor(double (&a)[IB], double (&x)[IB], int lane16) {
     bool ok = true;
 #pragma unroll
@@ -104,52 +140,102 @@ __device__ __forceinline__ bool leaf_factor(double (&a)[IB], double (&x)[IB], in
         const double inv = rsqrt_d(d);
         a[j] *= inv;       // lane j: d * inv = sqrt(d); lanes > j: L[i][j]; lanes < j: unused
         x[j] *= inv;       // (L^-1)[j][c] final
+        const double na = -a[j], nx = -x[j];
 #pragma unroll
         for (int l = j + 1; l < IB; ++l) {
-            const double t = bcl(a[j], l);  // L[l][j]
-            a[l] -= a[j] * t;
-            x[l] -= t * x[j];
+            if (l == j + 1) fmac_bc_first(a[l], a[j], na, l);  // a[l] -= L[i][j] L[l][j]
+            else fmac_bc(a[l], a[j], na, l);
         }
+#pragma unroll
+        for (int l = j + 1; l < IB; ++l) fmac_bc(x[l], a[j], nx, l);  // x[l] -= L[l][j] x[j]
     }
     return ok;
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_potrf128: factor the 128x128 diagonal block at (k0, k0); 256 threads.
+// Eight 16-column leaves.  A leaf is factored in registers by wave 0 (lane i = row i) with
+// row_newbcast DPP broadcasts: every broadcast L[l][j] feeds both the rank-1 update of the
+// leaf and the forward substitution of its inverse D_s = L_ss^-1 (lane c = column c), so the leaf
+// factor and its inverse cost one pass.  In-block lookahead: after the panel solve of leaf s, wave 0
+// updates the next diagonal tile and factors leaf s+1 while waves 1-3 apply the rest of the update.
+// ------------------------------------------------------------------------------------------------
+
+constexpr int POTRF_NT = (CB / IB) * (CB / IB + 1) / 2;  // 36 lower tiles
+constexpr size_t POTRF_LDS = sizeof(double) * (POTRF_NT + 1) * IB * 17;
+
 __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_t ld, int64_t k0,
                                                   double* __restrict__ dinv, double* __restrict__ scal) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    double* A = smem;                  // [128][LDA]
-    double* Dl = smem + CB * LDA;      // [16][17] current inverse D_s
+    // lower-triangle tiles only (80 KB, so the kernel fits beside a bulk-update workgroup on a CU):
+    // element (r, c), r/16 >= c/16, at tile (r/16)(r/16+1)/2 + c/16, row r%16 (stride 17), col c%16
+#define AT(r, c) smem[(((r) >> 4) * (((r) >> 4) + 1) / 2 + ((c) >> 4)) * (IB * 17) + ((r) & 15) * 17 + ((c) & 15)]
+    double* Dl = smem + POTRF_NT * IB * 17;  // [16][17] current inverse D_s
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int lr = lane & 15, lk = lane >> 4;
-    {
-        // 128 x 128 block: thread -> row tid >> 1, 64 columns; 2 batches of 16 double2
-        const int r = tid >> 1, cb = (tid & 1) * 64;
-        const double* g = S + (k0 + r) * ld + k0 + cb;
-        double2 v[32];
-#pragma unroll
-        for (int q = 0; q < 32; ++q) v[q] = *reinterpret_cast<const double2*>(g + 2 * q);
-#pragma unroll
-        for (int q = 0; q < 32; ++q) {
-            A[r * LDA + cb + 2 * q] = v[q].x;
-            A[r * LDA + cb + 2 * q + 1] = v[q].y;
-        }
-    }
-    __syncthreads();
     const int64_t dbase = (k0 / CB) * (CB / IB) * (IB * IB);
     bool ok = true;
-    // leaf 0 (wave 0)
-    if (wave == 0) {
+    // store the final tiles (t, sc), t >= sc, of block column sc (diagonal tile: lower part only);
+    // item i -> tile row t = sc + (i >> 7), row (i >> 3) & 15, columns 2 (i & 7)
+    auto store_col = [&](int sc, int t0, int nthr) {
+        for (int i = t0; i < (CB / IB - sc) * 128; i += nthr) {
+            const int ti = sc + (i >> 7), n = (i >> 3) & 15, m = (i & 7) * 2;
+            double* g = S + (k0 + ti * IB + n) * ld + k0 + sc * IB + m;
+            const double* t = smem + (ti * (ti + 1) / 2 + sc) * IB * 17 + n * 17 + m;
+            if (ti > sc || m + 1 <= n) {
+                double2 v;
+                v.x = t[0];
+                v.y = t[1];
+                *reinterpret_cast<double2*>(g) = v;
+            } else if (m == n) {
+                g[0] = t[0];
+            }
+        }
+    };
+    {
+        // wave 0 reads the rows of diagonal tile 0 straight into registers (issued first, so leaf 0
+        // starts after one load latency); the other 35 lower tiles go through LDS: item i -> tile
+        // p = 1 + (i >> 7), row (i >> 3) & 15, columns 2 (i & 7), all of a thread's loads in flight
         double a[IB], x[IB];
+        if (wave == 0) {
 #pragma unroll
-        for (int c = 0; c < IB; ++c) a[c] = A[lr * LDA + c];
-        ok = leaf_factor(a, x, lr);
-        if (lane < IB) {
+            for (int h = 0; h < IB / 2; ++h) {
+                const double2 v = *reinterpret_cast<const double2*>(S + (k0 + lr) * ld + k0 + 2 * h);
+                a[2 * h] = v.x;
+                a[2 * h + 1] = v.y;
+            }
+        }
+        constexpr int NQ = ((POTRF_NT - 1) * 128 + 255) / 256;  // 18
+        double2 v[NQ];
+        int off[NQ];
 #pragma unroll
-            for (int c = 0; c < IB; ++c) {
-                if (c <= lane) A[lane * LDA + c] = a[c];
-                const double v = (c >= lane) ? x[c] : 0.0;  // (L^-1)[c][lane]
-                Dl[c * 17 + lane] = v;
-                dinv[dbase + c * IB + lane] = v;
+        for (int q = 0; q < NQ; ++q) {
+            const int i = tid + 256 * q, p = 1 + (i >> 7), n = (i >> 3) & 15, m = (i & 7) * 2;
+            int ti = 0, pp = p;
+            while (pp > ti) { pp -= ti + 1; ++ti; }
+            off[q] = -1;
+            if (p < POTRF_NT) {
+                v[q] = *reinterpret_cast<const double2*>(S + (k0 + ti * IB + n) * ld + k0 + pp * IB + m);
+                off[q] = p * IB * 17 + n * 17 + m;
+            }
+        }
+        if (wave == 0) {
+            ok = leaf_factor(a, x, lr);
+            if (lane < IB) {
+#pragma unroll
+                for (int c = 0; c < IB; ++c) {
+                    if (c <= lane) AT(lane, c) = a[c];
+                    const double d = (c >= lane) ? x[c] : 0.0;  // (L^-1)[c][lane]
+                    Dl[c * 17 + lane] = d;
+                    dinv[dbase + c * IB + lane] = d;
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            if (off[q] >= 0) {
+                smem[off[q]] = v[q].x;
+                smem[off[q] + 1] = v[q].y;
             }
         }
     }
@@ -166,9 +252,9 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
                 dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
                 for (int kk = 0; kk < IB; kk += 4)
-                    acc = mfma(A[(r0 + lr) * LDA + c0 + kk + lk], Dl[lr * 17 + kk + lk], acc);
+                    acc = mfma(AT((r0 + lr), c0 + kk + lk), Dl[lr * 17 + kk + lk], acc);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) A[(r0 + lk + 4 * r) * LDA + c0 + lr] = acc[r];
+                for (int r = 0; r < 4; ++r) AT((r0 + lk + 4 * r), c0 + lr) = acc[r];
             }
         }
         __syncthreads();  // B2: panel column s solved
@@ -178,22 +264,22 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
             const int R = c0 + IB;
             dbl4 acc;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc[r] = A[(R + lk + 4 * r) * LDA + R + lr];
+            for (int r = 0; r < 4; ++r) acc[r] = AT((R + lk + 4 * r), R + lr);
 #pragma unroll
             for (int kk = 0; kk < IB; kk += 4)
-                acc = mfma(-A[(R + lr) * LDA + c0 + kk + lk], A[(R + lr) * LDA + c0 + kk + lk], acc);
+                acc = mfma(-AT((R + lr), c0 + kk + lk), AT((R + lr), c0 + kk + lk), acc);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) A[(R + lk + 4 * r) * LDA + R + lr] = acc[r];
+            for (int r = 0; r < 4; ++r) AT((R + lk + 4 * r), R + lr) = acc[r];
             __builtin_amdgcn_s_waitcnt(0xC07F);
             __builtin_amdgcn_wave_barrier();
             double a[IB], x[IB];
 #pragma unroll
-            for (int c = 0; c < IB; ++c) a[c] = A[(R + lr) * LDA + R + c];
+            for (int c = 0; c < IB; ++c) a[c] = AT((R + lr), R + c);
             ok &= leaf_factor(a, x, lr);
             if (lane < IB) {
 #pragma unroll
                 for (int c = 0; c < IB; ++c) {
-                    if (c <= lane) A[(R + lane) * LDA + R + c] = a[c];
+                    if (c <= lane) AT((R + lane), R + c) = a[c];
                     const double v = (c >= lane) ? x[c] : 0.0;  // (L^-1)[c][lane]
                     Dl[c * 17 + lane] = v;  // safe: every wave finished reading D_s before B2
                     dinv[dbase + (s + 1) * IB * IB + c * IB + lane] = v;
@@ -208,32 +294,19 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
                 const int R = (s + 1 + ti) * IB, C = (s + 1 + tj) * IB;
                 dbl4 acc;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc[r] = A[(R + lk + 4 * r) * LDA + C + lr];
+                for (int r = 0; r < 4; ++r) acc[r] = AT((R + lk + 4 * r), C + lr);
 #pragma unroll
                 for (int kk = 0; kk < IB; kk += 4)
-                    acc = mfma(-A[(R + lr) * LDA + c0 + kk + lk], A[(C + lr) * LDA + c0 + kk + lk], acc);
+                    acc = mfma(-AT((R + lr), c0 + kk + lk), AT((C + lr), c0 + kk + lk), acc);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) A[(R + lk + 4 * r) * LDA + C + lr] = acc[r];
+                for (int r = 0; r < 4; ++r) AT((R + lk + 4 * r), C + lr) = acc[r];
             }
+            store_col(s, tid - 64, 192);  // block column s is final: write it out behind the update
         }
     }
     if (!ok && lane == 0 && scal[1] == 0.0) scal[1] = (double)(k0 + 1);
-    {
-        const int r = tid >> 1, cb = (tid & 1) * 64;
-        double* g = S + (k0 + r) * ld + k0 + cb;
-#pragma unroll
-        for (int q = 0; q < 32; ++q) {
-            const int c = cb + 2 * q;
-            if (c + 1 <= r) {
-                double2 v;
-                v.x = A[r * LDA + c];
-                v.y = A[r * LDA + c + 1];
-                *reinterpret_cast<double2*>(g + 2 * q) = v;
-            } else if (c == r) {
-                g[2 * q] = A[r * LDA + c];
-            }
-        }
-    }
+    store_col(CB / IB - 1, tid, 256);
+#undef AT
 }
 
 
@@ -689,10 +762,9 @@ __global__ void k_neg_copy(const double* __restrict__ X, double* __restrict__ de
 // rest(k-1) runs concurrently with potrf(k) and trsm(k).
 int launch_cholesky(Ctx& c) {
     const int64_t ld = c.L.ld, nb = c.L.n_pad / CB;
-    const size_t lds_potrf = sizeof(double) * (CB * LDA + IB * 17 + IB);
     hipStream_t A = c.stream, B = c.stream2;
     for (int64_t kb = 0; kb < nb; ++kb) {
-        k_potrf128<<<1, 256, lds_potrf, A>>>(c.d_S, ld, kb * CB, c.d_dinv, c.d_scal);
+        k_potrf128<<<1, 256, POTRF_LDS, A>>>(c.d_S, ld, kb * CB, c.d_dinv, c.d_scal);
         // panel rows below the diagonal block, RHS block row included: (nb - kb) * 128 rows
         k_trsm128<<<(unsigned)((nb - kb) * 2), 256, TRSM_LDS, A>>>(c.d_S, ld, kb * CB, (kb + 1) * CB, c.d_dinv);
         FBA_HIP(hipEventRecord(c.ev_trsm[kb], A));
@@ -728,8 +800,7 @@ int launch_backward(Ctx& c) {
 }
 
 int chol_setup(Ctx& c) {
-    const size_t lds_potrf = sizeof(double) * (CB * LDA + IB * 17 + IB);
-    FBA_HIP(hipFuncSetAttribute((const void*)k_potrf128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_potrf));
+    FBA_HIP(hipFuncSetAttribute((const void*)k_potrf128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)POTRF_LDS));
     FBA_HIP(hipFuncSetAttribute((const void*)k_trsm128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRSM_LDS));
     const size_t lds_trtri = sizeof(double) * (CB * LDA + 4 * IB * 17);
     FBA_HIP(hipFuncSetAttribute((const void*)k_trtri128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_trtri));

@@ -19,5 +19,8 @@ for step in "$@"; do
     benchq) run bench 600 python bench.py --steps 5 --warmup 1 --no-cpu --verbose ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
           run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
+    pmc) cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+          run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$PWD/gpurun_out/pmc_fetch" -o run -- python bench.py --steps 2 --warmup 1 --no-cpu
+          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$PWD/gpurun_out/pmc_write" -o run -- python bench.py --steps 2 --warmup 1 --no-cpu ;;
   esac
 done

@@ -244,6 +244,136 @@ __global__ __launch_bounds__(256) void k_trsm_prof(double* __restrict__ S, int64
 #undef TT
 }
 
+// previous (full 128x130 LDS block) version, for the contention comparison
+__global__ __launch_bounds__(256) void k_potrf_old(double* __restrict__ S, int64_t ld, int64_t k0,
+                                                  double* __restrict__ dinv, double* __restrict__ scal) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* A = smem;                  // [128][LDA]
+    double* Dl = smem + CB * LDA;      // [16][17] current inverse D_s
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int lr = lane & 15, lk = lane >> 4;
+    {
+        // 128 x 128 block: thread -> row tid >> 1, 64 columns; 2 batches of 16 double2
+        const int r = tid >> 1, cb = (tid & 1) * 64;
+        const double* g = S + (k0 + r) * ld + k0 + cb;
+        double2 v[32];
+#pragma unroll
+        for (int q = 0; q < 32; ++q) v[q] = *reinterpret_cast<const double2*>(g + 2 * q);
+#pragma unroll
+        for (int q = 0; q < 32; ++q) {
+            A[r * LDA + cb + 2 * q] = v[q].x;
+            A[r * LDA + cb + 2 * q + 1] = v[q].y;
+        }
+    }
+    __syncthreads();
+    const int64_t dbase = (k0 / CB) * (CB / IB) * (IB * IB);
+    bool ok = true;
+    // leaf 0 (wave 0)
+    if (wave == 0) {
+        double a[IB], x[IB];
+#pragma unroll
+        for (int c = 0; c < IB; ++c) a[c] = A[lr * LDA + c];
+        ok = leaf_factor(a, x, lr);
+        if (lane < IB) {
+#pragma unroll
+            for (int c = 0; c < IB; ++c) {
+                if (c <= lane) A[lane * LDA + c] = a[c];
+                const double v = (c >= lane) ? x[c] : 0.0;  // (L^-1)[c][lane]
+                Dl[c * 17 + lane] = v;
+                dinv[dbase + c * IB + lane] = v;
+            }
+        }
+    }
+    for (int s = 0; s < CB / IB; ++s) {
+        const int c0 = s * IB;
+        __syncthreads();  // B1: L_ss, D_s in LDS; column s updated
+        if (s == CB / IB - 1) break;
+        // panel solve X_t = A_ts D_s^T: wave 0 tile s+1, waves 1..3 tiles s+2..7
+        {
+            const int t0 = (wave == 0) ? s + 1 : s + 1 + wave;
+            const int step = (wave == 0) ? CB : 3;
+            for (int t = t0; t < CB / IB; t += step) {
+                const int r0 = t * IB;
+                dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int kk = 0; kk < IB; kk += 4)
+                    acc = mfma(A[(r0 + lr) * LDA + c0 + kk + lk], Dl[lr * 17 + kk + lk], acc);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) A[(r0 + lk + 4 * r) * LDA + c0 + lr] = acc[r];
+            }
+        }
+        __syncthreads();  // B2: panel column s solved
+        const int m = CB / IB - 1 - s;  // tiles (ti, tj), s < tj <= ti
+        if (wave == 0) {
+            // next diagonal tile, then its leaf factor
+            const int R = c0 + IB;
+            dbl4 acc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] = A[(R + lk + 4 * r) * LDA + R + lr];
+#pragma unroll
+            for (int kk = 0; kk < IB; kk += 4)
+                acc = mfma(-A[(R + lr) * LDA + c0 + kk + lk], A[(R + lr) * LDA + c0 + kk + lk], acc);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) A[(R + lk + 4 * r) * LDA + R + lr] = acc[r];
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_wave_barrier();
+            double a[IB], x[IB];
+#pragma unroll
+            for (int c = 0; c < IB; ++c) a[c] = A[(R + lr) * LDA + R + c];
+            ok &= leaf_factor(a, x, lr);
+            if (lane < IB) {
+#pragma unroll
+                for (int c = 0; c < IB; ++c) {
+                    if (c <= lane) A[(R + lane) * LDA + R + c] = a[c];
+                    const double v = (c >= lane) ? x[c] : 0.0;  // (L^-1)[c][lane]
+                    Dl[c * 17 + lane] = v;  // safe: every wave finished reading D_s before B2
+                    dinv[dbase + (s + 1) * IB * IB + c * IB + lane] = v;
+                }
+            }
+        } else {
+            const int ntile = m * (m + 1) / 2;
+            for (int q = 1 + (wave - 1); q < ntile; q += 3) {
+                int ti = 0, rem = q;
+                while (rem > ti) { rem -= ti + 1; ++ti; }
+                const int tj = rem;
+                const int R = (s + 1 + ti) * IB, C = (s + 1 + tj) * IB;
+                dbl4 acc;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[r] = A[(R + lk + 4 * r) * LDA + C + lr];
+#pragma unroll
+                for (int kk = 0; kk < IB; kk += 4)
+                    acc = mfma(-A[(R + lr) * LDA + c0 + kk + lk], A[(C + lr) * LDA + c0 + kk + lk], acc);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) A[(R + lk + 4 * r) * LDA + C + lr] = acc[r];
+            }
+        }
+    }
+    if (!ok && lane == 0 && scal[1] == 0.0) scal[1] = (double)(k0 + 1);
+    {
+        const int r = tid >> 1, cb = (tid & 1) * 64;
+        double* g = S + (k0 + r) * ld + k0 + cb;
+#pragma unroll
+        for (int q = 0; q < 32; ++q) {
+            const int c = cb + 2 * q;
+            if (c + 1 <= r) {
+                double2 v;
+                v.x = A[r * LDA + c];
+                v.y = A[r * LDA + c + 1];
+                *reinterpret_cast<double2*>(g + 2 * q) = v;
+            } else if (c == r) {
+                g[2 * q] = A[r * LDA + c];
+            }
+        }
+    }
+}
+
+
+
+__global__ void k_spin(long long cycles) {
+    const long long t0 = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - t0 < cycles) __builtin_amdgcn_s_sleep(2);
+}
+
 static double check(const std::vector<double>& L, const std::vector<double>& A0, int n, int ld) {
     // || L L' - A0 ||_max / ||A0||_max over the lower triangle
     double err = 0, mx = 0;
@@ -296,10 +426,10 @@ int main() {
     CK(hipMalloc(&dts, 64 * 8));
     CK(hipMemset(scal, 0, 16 * 8));
     const size_t lds = sizeof(double) * (CB * LDA + IB * 17 + IB);
-    CK(hipFuncSetAttribute((const void*)k_potrf128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    CK(hipFuncSetAttribute((const void*)k_potrf128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)POTRF_LDS));
     CK(hipFuncSetAttribute((const void*)k_potrf_prof, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     std::vector<double> L(A0.size());
-    float t = time_kernel([&] { k_potrf128<<<1, 256, lds>>>(dS, ld, 0, dinv, scal); }, dS, A0, 20);
+    float t = time_kernel([&] { k_potrf128<<<1, 256, POTRF_LDS>>>(dS, ld, 0, dinv, scal); }, dS, A0, 20);
     CK(hipMemcpy(L.data(), dS, L.size() * 8, hipMemcpyDeviceToHost));
     printf("k_potrf128        %8.2f us  err %.2e\n", t, check(L, A0, n, ld));
     t = time_kernel([&] { k_potrf_prof<<<1, 256, lds>>>(dS, ld, 0, dinv, scal, dts); }, dS, A0, 20);
@@ -307,7 +437,7 @@ int main() {
     printf("k_potrf_prof      %8.2f us  err %.2e\n", t, check(L, A0, n, ld));
     unsigned long long ts[64];
     CK(hipMemcpy(ts, dts, sizeof ts, hipMemcpyDeviceToHost));
-    printf("  load %llu cycles\n", ts[1] - ts[0]);
+    printf("  load %llu cycles; alone: %llu cycles over %.2f us = %.2f GHz\n", ts[1] - ts[0], ts[40] - ts[0], t, (ts[40] - ts[0]) / (1e3 * t));
     unsigned long long fa = 0, fb = 0, fc = 0, fd = 0;
     for (int q = 0; q < 8; ++q) {
         unsigned long long a = ts[2 + 4 * q] - (q ? ts[1 + 4 * q] : ts[1]);
@@ -330,7 +460,7 @@ int main() {
         CK(hipMalloc(&dP, P.size() * 8));
         CK(hipMemcpy(dP, P.data(), P.size() * 8, hipMemcpyHostToDevice));
         CK(hipFuncSetAttribute((const void*)k_trsm128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRSM_LDS));
-        k_potrf128<<<1, 256, lds>>>(dP, N, 0, dinv, scal);
+        k_potrf128<<<1, 256, POTRF_LDS>>>(dP, N, 0, dinv, scal);
         CK(hipDeviceSynchronize());
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0));
@@ -353,6 +483,49 @@ int main() {
         printf("  trsm wg5: load %llu compute %llu store %llu\n", tt[1] - tt[0], tt[2] - tt[1], tt[3] - tt[2]);
         printf("k_trsm128 (%lld rows)  %8.2f us (best of 10, repeated in place)\n", (long long)(nb * CB), 1e3f * best);
         CK(hipFree(dP));
+    }
+    // contention: a bulk k_syrk128 grid on a low-priority stream, potrf on a high-priority one
+    {
+        const int64_t N = 6144, nb = N / CB - 1;
+        double* dM;
+        CK(hipMalloc(&dM, (size_t)(N + CB) * N * 8));
+        CK(hipMemset(dM, 0, (size_t)(N + CB) * N * 8));
+        for (int i = 0; i < CB; ++i) CK(hipMemcpy(dM + (size_t)i * N, A0.data() + i * ld, CB * 8, hipMemcpyHostToDevice));
+        int lo, hi;
+        CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        hipStream_t sA, sB;
+        CK(hipStreamCreateWithPriority(&sA, hipStreamNonBlocking, hi));
+        CK(hipStreamCreateWithPriority(&sB, hipStreamNonBlocking, lo));
+        CK(hipFuncSetAttribute((const void*)k_potrf_old, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(sizeof(double) * (CB * LDA + IB * 17 + IB))));
+        hipEvent_t a0, a1, b0, b1;
+        CK(hipEventCreate(&a0)); CK(hipEventCreate(&a1)); CK(hipEventCreate(&b0)); CK(hipEventCreate(&b1));
+        int64_t nt = 0;
+        for (int64_t j = 2; j < nb; ++j) nt += nb - j + 1;
+        CK(hipFuncSetAttribute((const void*)k_potrf_prof, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(sizeof(double) * (CB * LDA + IB * 17 + IB))));
+        for (int variant = 0; variant < 3; ++variant) {
+            for (int rep = 0; rep < 3; ++rep) {
+                CK(hipDeviceSynchronize());
+                CK(hipEventRecord(b0, sB));
+                k_syrk128<<<(unsigned)nt, 256, 0, sB>>>(dM, N, 0, nb, 2, nt);
+                CK(hipEventRecord(b1, sB));
+                // give the bulk grid a head start, then the critical kernel
+                k_spin<<<1, 64, 0, sA>>>(20000);
+                CK(hipEventRecord(a0, sA));
+                if (variant == 0) k_potrf_old<<<1, 256, sizeof(double) * (CB * LDA + IB * 17 + IB), sA>>>(dM, N, 0, dinv, scal);
+                else if (variant == 1) k_potrf128<<<1, 256, POTRF_LDS, sA>>>(dM, N, 0, dinv, scal);
+                else k_potrf_prof<<<1, 256, sizeof(double) * (CB * LDA + IB * 17 + IB), sA>>>(dM, N, 0, dinv, scal, dts);
+                CK(hipEventRecord(a1, sA));
+                CK(hipDeviceSynchronize());
+                float ta, tb;
+                CK(hipEventElapsedTime(&ta, a0, a1));
+                CK(hipEventElapsedTime(&tb, b0, b1));
+                unsigned long long tq[64];
+                CK(hipMemcpy(tq, dts, sizeof tq, hipMemcpyDeviceToHost));
+                printf("  contention %s: potrf %.1f us, bulk syrk (%lld tiles) %.1f us%s", variant == 0 ? "old(135KB)" : variant == 1 ? "new(80KB)" : "prof", 1e3f * ta, (long long)nt, 1e3f * tb, variant == 2 ? "" : "\n");
+                if (variant == 2) printf("  -> %llu shader cycles = %.2f GHz over the kernel\n", tq[40] - tq[0], (tq[40] - tq[0]) / (1e3 * ta));
+            }
+        }
+        CK(hipFree(dM));
     }
     {
         const int nn = 1 << 20;
