@@ -579,32 +579,55 @@ static inline int64_t syrk_tiles(int64_t nb, int64_t jlo, int64_t ncol) {
 // border combine (inner constraints): RHS rows n_pad + 0 (y) and n_pad + 1..7 (Z), length n
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, int64_t ld, int64_t n_pad) {
-    __shared__ double red[8][256];
+    __shared__ double red[4][35];
     __shared__ double H[7][8];
     __shared__ double kk[7];
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const double* y = S + n_pad * ld;
-    for (int a = 0; a < 7; ++a) {
-        const double* za = S + (n_pad + 1 + a) * ld;
-        double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int64_t i = tid; i < n_pad; i += 256) {
-            const double z = za[i];
-            acc[0] += z * y[i];
-            for (int b = a; b < 7; ++b) acc[1 + b] += z * S[(n_pad + 1 + b) * ld + i];
+    const double* z = S + (n_pad + 1) * ld;
+    // one pass: h_a = z_a . y (7) and the upper triangle of H = Z'Z (28), all in registers
+    double acc[35];
+#pragma unroll
+    for (int q = 0; q < 35; ++q) acc[q] = 0.0;
+    for (int64_t i = tid; i < n_pad; i += 256) {
+        double zv[7];
+#pragma unroll
+        for (int m = 0; m < 7; ++m) zv[m] = z[m * ld + i];
+        const double yv = y[i];
+        int q = 7;
+#pragma unroll
+        for (int m = 0; m < 7; ++m) {
+            acc[m] += zv[m] * yv;
+#pragma unroll
+            for (int b = m; b < 7; ++b) acc[q++] += zv[m] * zv[b];
         }
-        for (int b = 0; b < 8; ++b) red[b][tid] = acc[b];
-        __syncthreads();
-        for (int w = 128; w > 0; w >>= 1) {
-            if (tid < w)
-                for (int b = 0; b < 8; ++b) red[b][tid] += red[b][tid + w];
-            __syncthreads();
-        }
-        if (tid == 0) {
-            H[a][0] = red[0][0];
-            for (int b = a; b < 7; ++b) { H[a][1 + b] = red[1 + b][0]; H[b][1 + a] = red[1 + b][0]; }
-        }
-        __syncthreads();
     }
+    // fixed-order reduction: butterfly within each wave, then the four waves in order
+#pragma unroll
+    for (int q = 0; q < 35; ++q) {
+        double v = acc[q];
+#pragma unroll
+        for (int w = 32; w > 0; w >>= 1) v += __shfl_xor(v, w, 64);
+        acc[q] = v;
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < 35; ++q) red[wave][q] = acc[q];
+    __syncthreads();
+    if (tid < 35) {
+        const double v = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+        if (tid < 7) {
+            H[tid][0] = v;
+        } else {
+            int q = 7, am = 0, bm = 0;
+            for (int m = 0; m < 7; ++m)
+                for (int b = m; b < 7; ++b, ++q)
+                    if (q == tid) { am = m; bm = b; }
+            H[am][1 + bm] = v;
+            H[bm][1 + am] = v;
+        }
+    }
+    __syncthreads();
     if (tid == 0) {
         // solve H[:,1..7] k = -H[:,0]  (SPD 7x7; Gaussian elimination with partial pivoting)
         double A[7][8];
@@ -705,13 +728,23 @@ __global__ __launch_bounds__(256) void k_trtri128(const double* __restrict__ S, 
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ double gemv_t128(const double* __restrict__ M, int64_t ldm, const double* __restrict__ v,
                                             int tid, double* red) {
-    const int c = tid & 127, h = tid >> 7;
-    double acc = 0.0;
-#pragma unroll 8
-    for (int r = h * 64; r < h * 64 + 64; ++r) acc += M[(int64_t)r * ldm + c] * v[r];
-    red[tid] = acc;
+    // thread -> columns 2 (tid & 63) + {0,1}, rows 32 (tid >> 6) .. +32: all 32 double2 loads in flight
+    const int c2 = tid & 63, h = tid >> 6;
+    double2 m[32];
+#pragma unroll
+    for (int r = 0; r < 32; ++r) m[r] = *reinterpret_cast<const double2*>(M + (int64_t)(h * 32 + r) * ldm + 2 * c2);
+    double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+    for (int r = 0; r < 32; ++r) {
+        const double vr = v[h * 32 + r];
+        a0 += m[r].x * vr;
+        a1 += m[r].y * vr;
+    }
+    red[h * 128 + 2 * c2] = a0;
+    red[h * 128 + 2 * c2 + 1] = a1;
     __syncthreads();
-    const double s = red[c] + red[128 + c];
+    const int c = tid & 127;
+    const double s = (red[c] + red[128 + c]) + (red[256 + c] + red[384 + c]);
     __syncthreads();
     return s;  // valid for every thread (column c = tid & 127)
 }
@@ -719,7 +752,7 @@ __device__ __forceinline__ double gemv_t128(const double* __restrict__ M, int64_
 __global__ __launch_bounds__(256) void k_bwd_first(const double* __restrict__ S, int64_t ld, int64_t n_pad, int64_t kb,
                                                    const double* __restrict__ linv, double* __restrict__ X) {
     __shared__ double ys[CB];
-    __shared__ double red[256];
+    __shared__ double red[512];
     const int tid = threadIdx.x;
     if (tid < CB) ys[tid] = S[n_pad * ld + kb * CB + tid];
     __syncthreads();
@@ -731,7 +764,7 @@ __global__ __launch_bounds__(256) void k_bwd_step(double* __restrict__ S, int64_
                                                   const double* __restrict__ linv, double* __restrict__ X) {
     __shared__ double xs[CB];
     __shared__ double ys[CB];
-    __shared__ double red[256];
+    __shared__ double red[512];
     const int tid = threadIdx.x;
     const int64_t k0 = kb * CB;
     double* y = S + n_pad * ld;
