@@ -258,7 +258,6 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
             }
         }
         __syncthreads();  // B2: panel column s solved
-        const int m = CB / IB - 1 - s;  // tiles (ti, tj), s < tj <= ti
         if (wave == 0) {
             // next diagonal tile, then its leaf factor
             const int R = c0 + IB;
@@ -286,20 +285,34 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
                 }
             }
         } else {
-            const int ntile = m * (m + 1) / 2;
-            for (int q = 1 + (wave - 1); q < ntile; q += 3) {
-                int ti = 0, rem = q;
-                while (rem > ti) { rem -= ti + 1; ++ti; }
-                const int tj = rem;
-                const int R = (s + 1 + ti) * IB, C = (s + 1 + tj) * IB;
-                dbl4 acc;
+            // waves 1-3: the rest of the trailing update, by tile rows s+2 .. 7 dealt in snake order
+            // (largest first) for balance; the tiles of a row go in pairs sharing the A operand,
+            // two independent MFMA chains
+            const int nrows = CB / IB - 2 - s;
+            for (int i = 0; i < nrows; ++i) {
+                const int w = ((i / 3) & 1) ? 3 - (i % 3) : 1 + (i % 3);
+                if (w != wave) continue;
+                const int R = (CB / IB - 1 - i) * IB;
+                for (int C = c0 + IB; C <= R; C += 2 * IB) {
+                    const bool two = C + IB <= R;
+                    dbl4 acc1, acc2 = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc[r] = AT((R + lk + 4 * r), C + lr);
+                    for (int r = 0; r < 4; ++r) acc1[r] = AT((R + lk + 4 * r), C + lr);
+                    if (two)
 #pragma unroll
-                for (int kk = 0; kk < IB; kk += 4)
-                    acc = mfma(-AT((R + lr), c0 + kk + lk), AT((C + lr), c0 + kk + lk), acc);
+                        for (int r = 0; r < 4; ++r) acc2[r] = AT((R + lk + 4 * r), C + IB + lr);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) AT((R + lk + 4 * r), C + lr) = acc[r];
+                    for (int kk = 0; kk < IB; kk += 4) {
+                        const double av = -AT((R + lr), c0 + kk + lk);
+                        acc1 = mfma(av, AT((C + lr), c0 + kk + lk), acc1);
+                        if (two) acc2 = mfma(av, AT((C + IB + lr), c0 + kk + lk), acc2);
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) AT((R + lk + 4 * r), C + lr) = acc1[r];
+                    if (two)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) AT((R + lk + 4 * r), C + IB + lr) = acc2[r];
+                }
             }
             store_col(s, tid - 64, 192);  // block column s is final: write it out behind the update
         }
@@ -503,12 +516,9 @@ __global__ __launch_bounds__(256) void k_syrk128(double* __restrict__ S, int64_t
     }
 }
 
-// k_syrk_col64: the critical-path update of block column kb+1 (rows (kb+1)*128 .. (nb+1)*128) with
-// 64x64 tiles, K = 128: 4x the workgroups of k_syrk128, a quarter of the latency each.
-// Tile q: sub-row q >> 1 (64 rows), sub-column q & 1 of the 128-wide block column.
-__global__ __launch_bounds__(256) void k_syrk_col64(double* __restrict__ S, int64_t ld, int64_t kb) {
-    const int64_t r0 = (kb + 1) * CB + (int64_t)(blockIdx.x >> 1) * 64;
-    const int64_t c0 = (kb + 1) * CB + (int64_t)(blockIdx.x & 1) * 64;
+// C(r0.., c0..) -= X_r X_c^T for one 64x64 tile, K = 128 (the panel at columns k0.. = kb*128):
+// 4 waves of 32x32 (2x2 MFMA tiles), K staged through LDS in 32-deep slices.
+__device__ __forceinline__ void tile64_update(double* __restrict__ S, int64_t ld, int64_t kb, int64_t r0, int64_t c0) {
     __shared__ __attribute__((aligned(16))) double As[64][LDK];
     __shared__ __attribute__((aligned(16))) double Bs[64][LDK];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -567,6 +577,31 @@ __global__ __launch_bounds__(256) void k_syrk_col64(double* __restrict__ S, int6
         for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) Cp[(a * 16 + 4 * r) * ld + b * 16] = acc[a][b][r];
+}
+
+
+// k_syrk_col64: the critical-path update of block column kb+1 (rows (kb+1)*128 .. (nb+1)*128) with
+// 64x64 tiles, K = 128: 4x the workgroups of k_syrk128, a quarter of the latency each.
+// Tile q: sub-row q >> 1 (64 rows), sub-column q & 1 of the 128-wide block column.
+__global__ __launch_bounds__(256) void k_syrk_col64(double* __restrict__ S, int64_t ld, int64_t kb) {
+    tile64_update(S, ld, kb, (kb + 1) * CB + (int64_t)(blockIdx.x >> 1) * 64,
+                  (kb + 1) * CB + (int64_t)(blockIdx.x & 1) * 64);
+}
+
+// k_syrk_q64: the trailing tiles [tile0, tile0 + gridDim.x/4) of k_syrk128's list, as quarters (the
+// partial last round of the bulk update: four short workgroups per tile instead of one long one).
+__global__ __launch_bounds__(256) void k_syrk_q64(double* __restrict__ S, int64_t ld, int64_t kb, int64_t nb,
+                                                  int64_t jlo, int64_t tile0) {
+    int64_t q = tile0 + blockIdx.x / 4, bj = jlo, bi = 0;
+    for (;;) {
+        const int64_t cnt = nb - bj + 1;
+        if (q < cnt) { bi = bj + q; break; }
+        q -= cnt;
+        ++bj;
+    }
+    const int qr = (blockIdx.x >> 1) & 1, qc = blockIdx.x & 1;
+    if (bi == bj && qr == 0 && qc == 1) return;  // strictly upper quarter of a diagonal block
+    tile64_update(S, ld, kb, bi * CB + qr * 64, bj * CB + qc * 64);
 }
 
 static inline int64_t syrk_tiles(int64_t nb, int64_t jlo, int64_t ncol) {
@@ -804,9 +839,12 @@ int launch_cholesky(Ctx& c) {
         const int64_t m = nb - kb - 1;  // trailing block columns
         if (m > 1) {
             FBA_HIP(hipStreamWaitEvent(B, c.ev_trsm[kb], 0));
+            // optional whole rounds of 128x128 tiles (bulk_slots resident workgroups), the rest as
+            // 64x64 quarters: four short workgroups per tile keep the last round short
             const int64_t nt = syrk_tiles(nb, kb + 2, m - 1);
-            const int64_t grid = c.syrk_cap > 0 && nt > c.syrk_cap ? c.syrk_cap : nt;
-            k_syrk128<<<(unsigned)grid, 256, 0, B>>>(c.d_S, ld, kb, nb, kb + 2, nt);
+            const int64_t nfull = c.bulk_slots > 0 ? (nt / c.bulk_slots) * c.bulk_slots : 0;
+            if (nfull > 0) k_syrk128<<<(unsigned)nfull, 256, 0, B>>>(c.d_S, ld, kb, nb, kb + 2, nfull);
+            if (nt > nfull) k_syrk_q64<<<(unsigned)((nt - nfull) * 4), 256, 0, B>>>(c.d_S, ld, kb, nb, kb + 2, nfull);
             FBA_HIP(hipEventRecord(c.ev_rest[kb], B));
         }
         if (m > 0) {
@@ -848,10 +886,16 @@ int chol_setup(Ctx& c) {
         FBA_HIP(hipStreamCreateWithPriority(&c.stream2, hipStreamNonBlocking, prio_least));
     else
         FBA_HIP(hipStreamCreateWithFlags(&c.stream2, hipStreamNonBlocking));
-    const char* ce = getenv("FBA_SYRK_CAP");
-    c.syrk_cap = ce ? atoi(ce) : 0;
-    if (c.opt.verbose) fprintf(stderr, "[fba] stream priorities least %d greatest %d, bulk mode %d, syrk cap %d\n",
-                           prio_least, prio_greatest, prio_mode, c.syrk_cap);
+    const char* ce = getenv("FBA_BULK_SLOTS");
+    int dev = 0;
+    FBA_HIP(hipGetDevice(&dev));
+    hipDeviceProp_t prop;
+    FBA_HIP(hipGetDeviceProperties(&prop, dev));
+    // measured (config 4): 64x64 quarter tiles throughout beat whole rounds of 128x128 tiles + a
+    // quarter-tile remainder (4.02 vs 4.10-4.24 ms), so by default no whole rounds are used
+    c.bulk_slots = ce ? atoi(ce) : 0;
+    if (c.opt.verbose) fprintf(stderr, "[fba] stream priorities least %d greatest %d, bulk mode %d, bulk slots %d\n",
+                           prio_least, prio_greatest, prio_mode, c.bulk_slots);
     c.ev_trsm.assign(nb, nullptr);
     c.ev_rest.assign(nb, nullptr);
     for (int64_t k = 0; k < nb; ++k) {

@@ -374,6 +374,259 @@ __global__ void k_spin(long long cycles) {
     while (__builtin_amdgcn_s_memtime() - t0 < cycles) __builtin_amdgcn_s_sleep(2);
 }
 
+// instrumented copy of k_potrf128
+__global__ __launch_bounds__(256) void k_potrf_ts(double* __restrict__ S, int64_t ld, int64_t k0,
+                                                  double* __restrict__ dinv, double* __restrict__ scal, unsigned long long* ts) {
+#define T0(i) do { if (threadIdx.x == 0) ts[i] = __builtin_amdgcn_s_memtime(); } while (0)
+    T0(0);
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    // lower-triangle tiles only (80 KB, so the kernel fits beside a bulk-update workgroup on a CU):
+    // element (r, c), r/16 >= c/16, at tile (r/16)(r/16+1)/2 + c/16, row r%16 (stride 17), col c%16
+#define AT_(r, c) smem[(((r) >> 4) * (((r) >> 4) + 1) / 2 + ((c) >> 4)) * (IB * 17) + ((r) & 15) * 17 + ((c) & 15)]
+    double* Dl = smem + POTRF_NT * IB * 17;  // [16][17] current inverse D_s
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int lr = lane & 15, lk = lane >> 4;
+    const int64_t dbase = (k0 / CB) * (CB / IB) * (IB * IB);
+    bool ok = true;
+    // store the final tiles (t, sc), t >= sc, of block column sc (diagonal tile: lower part only);
+    // item i -> tile row t = sc + (i >> 7), row (i >> 3) & 15, columns 2 (i & 7)
+    auto store_col = [&](int sc, int t0, int nthr) {
+        for (int i = t0; i < (CB / IB - sc) * 128; i += nthr) {
+            const int ti = sc + (i >> 7), n = (i >> 3) & 15, m = (i & 7) * 2;
+            double* g = S + (k0 + ti * IB + n) * ld + k0 + sc * IB + m;
+            const double* t = smem + (ti * (ti + 1) / 2 + sc) * IB * 17 + n * 17 + m;
+            if (ti > sc || m + 1 <= n) {
+                double2 v;
+                v.x = t[0];
+                v.y = t[1];
+                *reinterpret_cast<double2*>(g) = v;
+            } else if (m == n) {
+                g[0] = t[0];
+            }
+        }
+    };
+    {
+        // wave 0 reads the rows of diagonal tile 0 straight into registers (issued first, so leaf 0
+        // starts after one load latency); the other 35 lower tiles go through LDS: item i -> tile
+        // p = 1 + (i >> 7), row (i >> 3) & 15, columns 2 (i & 7), all of a thread's loads in flight
+        double a[IB], x[IB];
+        if (wave == 0) {
+#pragma unroll
+            for (int h = 0; h < IB / 2; ++h) {
+                const double2 v = *reinterpret_cast<const double2*>(S + (k0 + lr) * ld + k0 + 2 * h);
+                a[2 * h] = v.x;
+                a[2 * h + 1] = v.y;
+            }
+        }
+        constexpr int NQ = ((POTRF_NT - 1) * 128 + 255) / 256;  // 18
+        double2 v[NQ];
+        int off[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int i = tid + 256 * q, p = 1 + (i >> 7), n = (i >> 3) & 15, m = (i & 7) * 2;
+            int ti = 0, pp = p;
+            while (pp > ti) { pp -= ti + 1; ++ti; }
+            off[q] = -1;
+            if (p < POTRF_NT) {
+                v[q] = *reinterpret_cast<const double2*>(S + (k0 + ti * IB + n) * ld + k0 + pp * IB + m);
+                off[q] = p * IB * 17 + n * 17 + m;
+            }
+        }
+        if (wave == 0) {
+            T0(1);
+            ok = leaf_factor(a, x, lr);
+            T0(2);
+            if (lane < IB) {
+#pragma unroll
+                for (int c = 0; c < IB; ++c) {
+                    if (c <= lane) AT_(lane, c) = a[c];
+                    const double d = (c >= lane) ? x[c] : 0.0;  // (L^-1)[c][lane]
+                    Dl[c * 17 + lane] = d;
+                    dinv[dbase + c * IB + lane] = d;
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            if (off[q] >= 0) {
+                smem[off[q]] = v[q].x;
+                smem[off[q] + 1] = v[q].y;
+            }
+        }
+    }
+    for (int s = 0; s < CB / IB; ++s) {
+        const int c0 = s * IB;
+        __syncthreads();  // B1: L_ss, D_s in LDS; column s updated
+        T0(3 + 4 * s);
+        if (s == CB / IB - 1) break;
+        // panel solve X_t = A_ts D_s^T: wave 0 tile s+1, waves 1..3 tiles s+2..7
+        {
+            const int t0 = (wave == 0) ? s + 1 : s + 1 + wave;
+            const int step = (wave == 0) ? CB : 3;
+            for (int t = t0; t < CB / IB; t += step) {
+                const int r0 = t * IB;
+                dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int kk = 0; kk < IB; kk += 4)
+                    acc = mfma(AT_((r0 + lr), c0 + kk + lk), Dl[lr * 17 + kk + lk], acc);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) AT_((r0 + lk + 4 * r), c0 + lr) = acc[r];
+            }
+        }
+        __syncthreads();  // B2: panel column s solved
+        T0(4 + 4 * s);
+        if (wave == 0) {
+            // next diagonal tile, then its leaf factor
+            const int R = c0 + IB;
+            dbl4 acc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] = AT_((R + lk + 4 * r), R + lr);
+#pragma unroll
+            for (int kk = 0; kk < IB; kk += 4)
+                acc = mfma(-AT_((R + lr), c0 + kk + lk), AT_((R + lr), c0 + kk + lk), acc);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) AT_((R + lk + 4 * r), R + lr) = acc[r];
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_wave_barrier();
+            double a[IB], x[IB];
+#pragma unroll
+            for (int c = 0; c < IB; ++c) a[c] = AT_((R + lr), R + c);
+            T0(5 + 4 * s);
+            ok &= leaf_factor(a, x, lr);
+            T0(6 + 4 * s);
+            if (lane < IB) {
+#pragma unroll
+                for (int c = 0; c < IB; ++c) {
+                    if (c <= lane) AT_((R + lane), R + c) = a[c];
+                    const double v = (c >= lane) ? x[c] : 0.0;  // (L^-1)[c][lane]
+                    Dl[c * 17 + lane] = v;  // safe: every wave finished reading D_s before B2
+                    dinv[dbase + (s + 1) * IB * IB + c * IB + lane] = v;
+                }
+            }
+        } else {
+            // waves 1-3: the rest of the trailing update, by tile rows s+2 .. 7 dealt in snake order
+            // (largest first) for balance; the tiles of a row go in pairs sharing the A operand,
+            // two independent MFMA chains
+            const int nrows = CB / IB - 2 - s;
+            for (int i = 0; i < nrows; ++i) {
+                const int w = ((i / 3) & 1) ? 3 - (i % 3) : 1 + (i % 3);
+                if (w != wave) continue;
+                const int R = (CB / IB - 1 - i) * IB;
+                for (int C = c0 + IB; C <= R; C += 2 * IB) {
+                    const bool two = C + IB <= R;
+                    dbl4 acc1, acc2 = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc1[r] = AT_((R + lk + 4 * r), C + lr);
+                    if (two)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) acc2[r] = AT_((R + lk + 4 * r), C + IB + lr);
+#pragma unroll
+                    for (int kk = 0; kk < IB; kk += 4) {
+                        const double av = -AT_((R + lr), c0 + kk + lk);
+                        acc1 = mfma(av, AT_((C + lr), c0 + kk + lk), acc1);
+                        if (two) acc2 = mfma(av, AT_((C + IB + lr), c0 + kk + lk), acc2);
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) AT_((R + lk + 4 * r), C + lr) = acc1[r];
+                    if (two)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) AT_((R + lk + 4 * r), C + IB + lr) = acc2[r];
+                }
+            }
+            store_col(s, tid - 64, 192);  // block column s is final: write it out behind the update
+        }
+    }
+    if (!ok && lane == 0 && scal[1] == 0.0) scal[1] = (double)(k0 + 1);
+    store_col(CB / IB - 1, tid, 256);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    T0(40);
+#undef AT_
+#undef T0
+}
+
+
+
+
+// experimental: VALU (v_fma_f64) trailing update, same tile list and semantics as k_syrk128.
+// 256 threads = 16 x 16, each an 8 x 8 micro-tile of the 128 x 128 C tile; K staged in 32-deep
+// slices, k-major in LDS so that a thread's 8 A (B) values are two ds_read_b128 broadcasts.
+constexpr int VK = 32, VLD = 128 + 4;
+__global__ __launch_bounds__(256) void k_syrk_valu(double* __restrict__ S, int64_t ld, int64_t kb, int64_t nb,
+                                                   int64_t jlo, int64_t ntiles) {
+    __shared__ __attribute__((aligned(16))) double As[VK][VLD];
+    __shared__ __attribute__((aligned(16))) double Bs[VK][VLD];
+    const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+    const int64_t k0 = kb * CB;
+    for (int64_t q0 = blockIdx.x; q0 < ntiles; q0 += gridDim.x) {
+        int64_t q = q0, bj = jlo, bi = 0;
+        for (;;) {
+            const int64_t cnt = nb - bj + 1;
+            if (q < cnt) { bi = bj + q; break; }
+            q -= cnt;
+            ++bj;
+        }
+        double acc[8][8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[i][j] = 0.0;
+        // staging: thread -> row rr (0..127), 16 k-values at cc (0 or 16) of the 32-deep slice
+        const int rr = tid >> 1, cc = (tid & 1) * 16;
+        const double* ga = S + (bi * CB + rr) * ld + k0 + cc;
+        const double* gb = S + (bj * CB + rr) * ld + k0 + cc;
+        double2 pa[8], pb[8];
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+            pa[h] = *reinterpret_cast<const double2*>(ga + 2 * h);
+            pb[h] = *reinterpret_cast<const double2*>(gb + 2 * h);
+        }
+        for (int ks = 0; ks < CB; ks += VK) {
+            __syncthreads();
+#pragma unroll
+            for (int h = 0; h < 8; ++h) {
+                As[cc + 2 * h][rr] = pa[h].x; As[cc + 2 * h + 1][rr] = pa[h].y;
+                Bs[cc + 2 * h][rr] = pb[h].x; Bs[cc + 2 * h + 1][rr] = pb[h].y;
+            }
+            __syncthreads();
+            if (ks + VK < CB) {
+#pragma unroll
+                for (int h = 0; h < 8; ++h) {
+                    pa[h] = *reinterpret_cast<const double2*>(ga + ks + VK + 2 * h);
+                    pb[h] = *reinterpret_cast<const double2*>(gb + ks + VK + 2 * h);
+                }
+            }
+#pragma unroll 4
+            for (int k = 0; k < VK; ++k) {
+                double a[8], b[8];
+                const double2* ap = reinterpret_cast<const double2*>(&As[k][ty * 8]);
+                const double2* bp = reinterpret_cast<const double2*>(&Bs[k][tx * 8]);
+#pragma unroll
+                for (int h = 0; h < 4; ++h) {
+                    const double2 va = ap[h], vb = bp[h];
+                    a[2 * h] = va.x; a[2 * h + 1] = va.y;
+                    b[2 * h] = vb.x; b[2 * h + 1] = vb.y;
+                }
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) acc[i][j] = fma(a[i], b[j], acc[i][j]);
+            }
+        }
+        double* Cp = S + (bi * CB + ty * 8) * ld + bj * CB + tx * 8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; j += 2) {
+                double2 c = *reinterpret_cast<double2*>(Cp + i * ld + j);
+                c.x -= acc[i][j];
+                c.y -= acc[i][j + 1];
+                *reinterpret_cast<double2*>(Cp + i * ld + j) = c;
+            }
+        __syncthreads();
+    }
+}
+
 static double check(const std::vector<double>& L, const std::vector<double>& A0, int n, int ld) {
     // || L L' - A0 ||_max / ||A0||_max over the lower triangle
     double err = 0, mx = 0;
@@ -449,6 +702,18 @@ int main() {
     }
     printf("  totals factor %llu inverse %llu panel %llu update %llu store %llu  all %llu\n", fa, fb, fc, fd,
            ts[40] - ts[33], ts[40] - ts[0]);
+    {
+        CK(hipFuncSetAttribute((const void*)k_potrf_ts, hipFuncAttributeMaxDynamicSharedMemorySize, (int)POTRF_LDS));
+        float tt = time_kernel([&] { k_potrf_ts<<<1, 256, POTRF_LDS>>>(dS, ld, 0, dinv, scal, dts); }, dS, A0, 5);
+        unsigned long long q[64];
+        CK(hipMemcpy(q, dts, sizeof q, hipMemcpyDeviceToHost));
+        printf("potrf_ts %.2f us: load->leaf0 start %llu, leaf0 %llu, to B1 %llu\n", tt, q[1] - q[0], q[2] - q[1], q[3] - q[2]);
+        for (int s = 0; s < 7; ++s)
+            printf("  s%d: B1->B2 (panel) %llu | B2->leaf start (diag upd) %llu | leaf %llu | leaf end->B1 %llu\n", s,
+                   q[4 + 4 * s] - q[3 + 4 * s], q[5 + 4 * s] - q[4 + 4 * s], q[6 + 4 * s] - q[5 + 4 * s],
+                   q[7 + 4 * s] - q[6 + 4 * s]);
+        printf("  end (store + drain) %llu, total %llu cycles\n", q[40] - q[31], q[40] - q[0]);
+    }
     // k_trsm128 on a tall panel (config-4 size): rows 128 .. 6144 of a 6144-wide matrix
     {
         const int64_t N = 6144, nb = N / CB;
@@ -524,6 +789,22 @@ int main() {
                 printf("  contention %s: potrf %.1f us, bulk syrk (%lld tiles) %.1f us%s", variant == 0 ? "old(135KB)" : variant == 1 ? "new(80KB)" : "prof", 1e3f * ta, (long long)nt, 1e3f * tb, variant == 2 ? "" : "\n");
                 if (variant == 2) printf("  -> %llu shader cycles = %.2f GHz over the kernel\n", tq[40] - tq[0], (tq[40] - tq[0]) / (1e3 * ta));
             }
+        }
+        // bulk update alone: MFMA k_syrk128 vs VALU k_syrk_valu over the same 1080 tiles
+        for (int variant = 0; variant < 2; ++variant) {
+            float best = 1e9f;
+            for (int rep = 0; rep < 5; ++rep) {
+                CK(hipEventRecord(b0, sB));
+                if (variant == 0) k_syrk128<<<(unsigned)nt, 256, 0, sB>>>(dM, N, 0, nb, 2, nt);
+                else k_syrk_valu<<<(unsigned)nt, 256, 0, sB>>>(dM, N, 0, nb, 2, nt);
+                CK(hipEventRecord(b1, sB));
+                CK(hipEventSynchronize(b1));
+                float tb;
+                CK(hipEventElapsedTime(&tb, b0, b1));
+                best = fminf(best, tb);
+            }
+            const double fl = 2.0 * 128 * 128 * 128 * (double)nt;
+            printf("  bulk %s: %.1f us  %.1f TFLOP/s\n", variant ? "VALU k_syrk_valu" : "MFMA k_syrk128", 1e3f * best, fl / (1e-3 * best) / 1e12);
         }
         CK(hipFree(dM));
     }
