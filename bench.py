@@ -52,6 +52,20 @@ def phase_roofline(ds, ms_phase, n_steps):
     return t, chol_flops, lin_bytes
 
 
+def pmc_traffic(config, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this workload
+    (profiles/*pmc_config<N>.json, made by scripts/pmc_summary.py: FETCH_SIZE x2 per the gfx950
+    correction + WRITE_SIZE), or None."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_config{config}.json")), reverse=True):
+        with open(f) as fh:
+            d = json.load(fh)
+        k = d.get("kernels", {}).get(kernel)
+        if k:
+            return k["hbm_bytes_per_launch"]
+    return None
+
+
 def cpu_baseline(folder, seconds):
     """The oracle (test infrastructure) timed on the host: a bounded sample of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -129,17 +143,24 @@ def main():
     names = ["linearize", "point", "accumulate", "border", "cholesky", "backward", "update", "total"]
     ms = {n: float(v) for n, v in zip(names, phases)}
     t, chol_flops, lin_bytes = phase_roofline(ds, ms, args.steps)
-    dominant = max(names[:-1], key=lambda k: t[k])
-    if dominant in ("cholesky",):
-        roof = {"bound": "mfma",
-                "kernel": "cholesky phase (k_potrf128+k_trsm128+k_syrk128+k_syrk_col64, 2 streams)",
-                "achieved": chol_flops / (t["cholesky"] * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
-                "unit": "TFLOP/s"}
-    else:
-        roof = {"bound": "hbm", "kernel": dominant, "achieved": lin_bytes / (t[dominant] * 1e-3) / 1e9,
-                "peak": HBM_PEAK_GBS, "unit": "GB/s"}
-    roof["frac"] = roof["achieved"] / roof["peak"]
-    roof["traffic"] = None
+
+    # roofline of the dominant kernel, outside the timed region: one more step with HIP events
+    # around every launch of the Cholesky bulk update (k_syrk_q64) on the stream it runs on
+    ctx.set_probe(True)
+    step()
+    pr = ctx.probe_stats()
+    ctx.set_probe(False)
+    avg_s = pr["ms"] * 1e-3 / max(pr["launches"], 1)
+    flops_launch = pr["flops"] / max(pr["launches"], 1)
+    traffic = pmc_traffic(args.config, "k_syrk_q64")
+    roof = {"bound": "mfma", "kernel": "k_syrk_q64 (Cholesky bulk trailing update, 64x64x128 f64 MFMA tiles)",
+            "achieved": flops_launch / avg_s / 1e12 if avg_s > 0 else None, "peak": FP64_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "launches": pr["launches"], "avg_launch_us": avg_s * 1e6,
+            "flops_per_launch": flops_launch,
+            "traffic": traffic}
+    roof["frac"] = roof["achieved"] / roof["peak"] if roof["achieved"] else None
+    phase_roof = {"cholesky_TFLOPs": chol_flops / (t["cholesky"] * 1e-3) / 1e12,
+                  "linearize_accumulate_GBs": lin_bytes / ((t["linearize"] + t["accumulate"]) * 1e-3) / 1e9}
     value = args.steps / dt
     out = {
         "metric": "Gauss-Newton iter/sec (BuildAwG+solve) and image-point obs/sec",
@@ -154,6 +175,7 @@ def main():
         "phase_ms": {k: t[k] for k in names},
         "deltasum_last": dsum[-1] if dsum else None,
         "roofline": roof,
+        "phase_roofline": phase_roof,
     }
     ctx.close()
     if rank == 0 and world == 1 and not args.no_cpu:

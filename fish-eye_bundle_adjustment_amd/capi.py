@@ -22,7 +22,8 @@ EXPORTS = (
     "fba_last_error", "fba_abi_version", "fba_count_unknowns", "fba_partition", "fba_create",
     "fba_destroy", "fba_buildxhat", "fba_set_xhat", "fba_get_xhat", "fba_build_awg",
     "fba_accumulate", "fba_reduce_buffer", "fba_synchronize", "fba_solve_update", "fba_step", "fba_adjust",
-    "fba_residuals", "fba_finish_stats", "fba_last_timings", "fba_set_timing",
+    "fba_residuals", "fba_finish_stats", "fba_last_timings", "fba_set_timing", "fba_set_probe",
+    "fba_probe_stats",
 )
 
 
@@ -78,6 +79,8 @@ def _load():
         "fba_finish_stats": ([P, P, P, D, P], C.c_int),
         "fba_last_timings": ([P, P], C.c_int),
         "fba_set_timing": ([P, I], C.c_int),
+        "fba_set_probe": ([P, I], C.c_int),
+        "fba_probe_stats": ([P, P], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -230,6 +233,14 @@ class Context:
 
     def set_timing(self, on=True):
         check(lib.fba_set_timing(self.h, int(on)))
+
+    def set_probe(self, on=True):
+        check(lib.fba_set_probe(self.h, int(on)))
+
+    def probe_stats(self):
+        out = np.zeros(4)
+        check(lib.fba_probe_stats(self.h, ptr(out)))
+        return {"launches": int(out[0]), "ms": float(out[1]), "flops": float(out[2])}
 
     def timings(self):
         ms = np.zeros(8)

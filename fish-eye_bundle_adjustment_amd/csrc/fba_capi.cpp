@@ -169,6 +169,8 @@ static void destroy(Ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (auto e : c->ev_trsm)
         if (e) (void)hipEventDestroy(e);
+    for (auto e : c->probe_ev)
+        if (e) (void)hipEventDestroy(e);
     for (auto e : c->ev_rest)
         if (e) (void)hipEventDestroy(e);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
@@ -708,6 +710,33 @@ int fba_last_timings(fba_ctx* ctx, double* ms) {
     Ctx* c = reinterpret_cast<Ctx*>(ctx);
     if (!c || !ms) { set_error("NULL argument"); return FBA_ERR_ARG; }
     for (int i = 0; i < 8; ++i) ms[i] = c->last_ms[i];
+    return FBA_OK;
+}
+
+int fba_set_probe(fba_ctx* ctx, int32_t enabled) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }
+    c->probe = enabled != 0;
+    c->probe_n = 0;
+    c->probe_flops = 0.0;
+    return FBA_OK;
+}
+
+int fba_probe_stats(fba_ctx* ctx, double* out) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c || !out) { set_error("NULL argument"); return FBA_ERR_ARG; }
+    FBA_HIP(hipStreamSynchronize(c->stream));
+    FBA_HIP(hipStreamSynchronize(c->stream2));
+    double ms = 0.0;
+    for (int i = 0; i < c->probe_n; ++i) {
+        float t = 0.f;
+        FBA_HIP(hipEventElapsedTime(&t, c->probe_ev[2 * i], c->probe_ev[2 * i + 1]));
+        ms += t;
+    }
+    out[0] = c->probe_n;
+    out[1] = ms;
+    out[2] = c->probe_flops;
+    out[3] = 0.0;
     return FBA_OK;
 }
 

@@ -844,7 +844,18 @@ int launch_cholesky(Ctx& c) {
             const int64_t nt = syrk_tiles(nb, kb + 2, m - 1);
             const int64_t nfull = c.bulk_slots > 0 ? (nt / c.bulk_slots) * c.bulk_slots : 0;
             if (nfull > 0) k_syrk128<<<(unsigned)nfull, 256, 0, B>>>(c.d_S, ld, kb, nb, kb + 2, nfull);
-            if (nt > nfull) k_syrk_q64<<<(unsigned)((nt - nfull) * 4), 256, 0, B>>>(c.d_S, ld, kb, nb, kb + 2, nfull);
+            if (nt > nfull) {
+                const bool pr = c.probe && c.probe_n < (int)c.probe_ev.size() / 2;
+                if (pr) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], B));
+                k_syrk_q64<<<(unsigned)((nt - nfull) * 4), 256, 0, B>>>(c.d_S, ld, kb, nb, kb + 2, nfull);
+                if (pr) {
+                    FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], B));
+                    // quarters computed (strictly upper quarters of diagonal blocks skipped) x 2*64*64*128
+                    const int64_t ndiag = (nfull == 0) ? (m - 1) : 0;  // tiles are column-major: diagonal ones
+                    c.probe_flops += (double)(4 * (nt - nfull) - ndiag) * 2.0 * 64 * 64 * CB;
+                    ++c.probe_n;
+                }
+            }
             FBA_HIP(hipEventRecord(c.ev_rest[kb], B));
         }
         if (m > 0) {
@@ -896,6 +907,8 @@ int chol_setup(Ctx& c) {
     c.bulk_slots = ce ? atoi(ce) : 0;
     if (c.opt.verbose) fprintf(stderr, "[fba] stream priorities least %d greatest %d, bulk mode %d, bulk slots %d\n",
                            prio_least, prio_greatest, prio_mode, c.bulk_slots);
+    c.probe_ev.assign(2 * nb, nullptr);
+    for (auto& e : c.probe_ev) FBA_HIP(hipEventCreate(&e));
     c.ev_trsm.assign(nb, nullptr);
     c.ev_rest.assign(nb, nullptr);
     for (int64_t k = 0; k < nb; ++k) {

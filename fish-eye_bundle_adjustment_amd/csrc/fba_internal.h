@@ -114,6 +114,11 @@ struct Ctx {
     bool have_delta = false;
     int iterations = 0;
     bool timing = false;
+    // kernel probe (fba_set_probe): HIP events around every bulk trailing-update launch
+    bool probe = false;
+    std::vector<hipEvent_t> probe_ev;  // [2*nb]
+    int probe_n = 0;
+    double probe_flops = 0.0;
     hipEvent_t ev[9] = {};
     double last_ms[8] = {0};
 };
