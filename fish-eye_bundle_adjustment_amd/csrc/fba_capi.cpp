@@ -158,7 +158,7 @@ static void partition(const fba_problem* p, int world, std::vector<int32_t>& tie
 static void destroy(Ctx* c) {
     if (!c) return;
     void* ptrs[] = {c->d_chunk_obs, c->d_chunk_pt, c->d_xy, c->d_img, c->d_cam, c->d_pt, c->d_ctl, c->d_lp_tie, c->d_lp_start, c->d_lp_cam,
-                    c->d_img_start, c->d_img_obs, c->d_cam_lp, c->d_cam_ctl, c->d_pair_e, c->d_pair_start,
+                    c->d_img_start, c->d_img_obs, c->d_cam_lp, c->d_cam_ctl, c->d_pair_e, c->d_pair_start, c->d_gpairs, c->d_red,
                     c->d_pair_ij, c->d_xfull, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
                     c->d_pt_tab, c->d_slab, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
                     c->d_active, c->d_counted, c->d_obs_pho};
@@ -344,6 +344,29 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     }
     pair_start.push_back((int32_t)terms.size());
     c->n_pairs = (int64_t)pair_e.size() / 2;
+    // ranks > 1: the co-visible image pairs of ALL tie points (identical on every rank), for the
+    // compact reduce buffer
+    std::vector<int32_t> gpairs;
+    if (opt.world > 1) {
+        std::vector<std::pair<int32_t, int32_t>> pi;  // (tie, image)
+        for (int64_t i = 0; i < p->n_pts; ++i)
+            if (p->tie[i] >= 0) pi.emplace_back(p->tie[i], p->img[i]);
+        std::sort(pi.begin(), pi.end());
+        std::vector<std::pair<int32_t, int32_t>> gp;
+        for (size_t a = 0; a < pi.size();) {
+            size_t b = a;
+            while (b < pi.size() && pi[b].first == pi[a].first) ++b;
+            for (size_t x = a; x < b; ++x)
+                for (size_t y = a; y < b; ++y)
+                    if (pi[x].second > pi[y].second) gp.emplace_back(pi[x].second, pi[y].second);
+            a = b;
+        }
+        std::sort(gp.begin(), gp.end());
+        gp.erase(std::unique(gp.begin(), gp.end()), gp.end());
+        for (auto& q : gp) { gpairs.push_back(q.first); gpairs.push_back(q.second); }
+        c->n_gpairs = (int64_t)gp.size();
+        c->n_red = 36 * (c->n_gpairs + L.n_img) + (int64_t)L.cw * L.n_cam * L.n_pad + L.n_pad;
+    }
     c->n_pair_terms = (int64_t)terms.size();
     terms.clear();
     terms.shrink_to_fit();
@@ -375,7 +398,8 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         (rc = upload(&c->d_pair_ij, pair_ij)) || (rc = upload(&c->d_xfull, c->xfull0)) ||
         (rc = upload(&c->d_caminfo, caminfo)) || (rc = upload(&c->d_active, active)) ||
         (rc = upload(&c->d_counted, counted)) || (rc = upload(&c->d_obs_pho, pho)) ||
-        (rc = upload(&c->d_chunk_obs, chunk_obs)) || (rc = upload(&c->d_chunk_pt, chunk_pt))) {
+        (rc = upload(&c->d_chunk_obs, chunk_obs)) || (rc = upload(&c->d_chunk_pt, chunk_pt)) ||
+        (opt.world > 1 && ((rc = upload(&c->d_gpairs, gpairs)) || (rc = dalloc(&c->d_red, (size_t)c->n_red))))) {
         destroy(c);
         return rc;
     }
@@ -435,6 +459,7 @@ static int accumulate(Ctx* c) {
     if ((rc = launch_point(*c))) return rc;
     mark(c, 2);
     if ((rc = launch_accumulate(*c))) return rc;
+    if (c->opt.world > 1 && (rc = launch_pack(*c, 0))) return rc;
     mark(c, 3);
     c->have_lin = true;
     return FBA_OK;
@@ -444,6 +469,7 @@ static int solve_update(Ctx* c, double* dsum) {
     int rc;
     const Layout& L = c->L;
     if (!c->have_lin) { set_error("fba_solve_update before fba_accumulate"); return FBA_ERR_ARG; }
+    if (c->opt.world > 1 && (rc = launch_pack(*c, 1))) return rc;
     if ((rc = launch_border(*c))) return rc;
     mark(c, 4);
     if ((rc = launch_cholesky(*c))) return rc;
@@ -605,8 +631,13 @@ int fba_accumulate(fba_ctx* ctx) {
 int fba_reduce_buffer(fba_ctx* ctx, void** dev_ptr, int64_t* n_doubles) {
     Ctx* c = reinterpret_cast<Ctx*>(ctx);
     if (!c || !dev_ptr || !n_doubles) { set_error("NULL argument"); return FBA_ERR_ARG; }
-    *dev_ptr = c->d_S;
-    *n_doubles = (c->L.n_pad + 1) * c->L.ld;  // lower normal matrix + RHS row 0
+    if (c->opt.world > 1) {  // compact: only the entries any rank writes (~6 MB at config 4)
+        *dev_ptr = c->d_red;
+        *n_doubles = c->n_red;
+    } else {
+        *dev_ptr = c->d_S;
+        *n_doubles = (c->L.n_pad + 1) * c->L.ld;  // lower normal matrix + RHS row 0
+    }
     return FBA_OK;
 }
 

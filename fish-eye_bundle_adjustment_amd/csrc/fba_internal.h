@@ -80,6 +80,11 @@ struct Ctx {
     int64_t n_pairs = 0, n_pair_terms = 0;
     int32_t* d_pair_e = nullptr;     // [2*n_pairs] (e1,e2) with e1 > e2
     int32_t* d_pair_start = nullptr; // [n_pairs+1]
+    // multi-rank compact reduce buffer: the entries of S that any rank can write (global co-visible
+    // image pairs, diagonal blocks, camera rows, RHS row), packed after fba_accumulate
+    int64_t n_gpairs = 0, n_red = 0;
+    int32_t* d_gpairs = nullptr;     // [2*n_gpairs] (e1,e2), e1 > e2, over ALL tie points
+    double* d_red = nullptr;         // [n_red]
     int32_t* d_pair_ij = nullptr;    // [2*n_pair_terms] (obs in e1, obs in e2)
 
     double* d_xfull = nullptr;   // [u_full]
@@ -141,7 +146,8 @@ int launch_linearize(Ctx& c);
 int launch_point(Ctx& c);
 int launch_accumulate(Ctx& c);   // zero S, image, pair, camera blocks, unit diagonal for unused
 int launch_border(Ctx& c);       // alpha, G G^T border, RHS rows
-int chol_setup(Ctx& c);          // one-time kernel attributes
+int chol_setup(Ctx& c);          // one-time kernel attributes, streams, events
+int launch_pack(Ctx& c, int dir);  // multi-rank compact reduce buffer: 0 = S -> buffer, 1 = buffer -> S
 int launch_cholesky(Ctx& c);     // factor + forward solve of RHS rows
 int launch_backward(Ctx& c);     // border combine + backward solve -> delta_c
 int launch_backsub_update(Ctx& c);

@@ -1066,4 +1066,40 @@ int launch_dense_awg(Ctx& c, double* dA, double* dW, const int64_t* d_map, int64
     return FBA_OK;
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// multi-rank compact reduce buffer: [global pair blocks 6x6 | diagonal blocks 6x6 | camera rows | RHS row]
+// dir 0: red <- S (after the accumulation), dir 1: S <- red (after the all-reduce)
+// ------------------------------------------------------------------------------------------------
+__global__ void k_pack(double* __restrict__ S, int64_t ld, double* __restrict__ red, const int32_t* __restrict__ gp,
+                       int64_t n_gp, int n_img, int64_t n_camrows, int64_t n_pad, int dir) {
+    const int64_t n_blk = 36 * (n_gp + n_img), n_cam = n_camrows * n_pad;
+    const int64_t total = n_blk + n_cam + n_pad;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
+        int64_t pos;
+        if (q < n_blk) {
+            const int64_t b = q / 36;
+            const int a = (int)(q % 36) / 6, c = (int)(q % 6);
+            const int64_t e1 = b < n_gp ? gp[2 * b] : b - n_gp, e2 = b < n_gp ? gp[2 * b + 1] : b - n_gp;
+            pos = (6 * e1 + a) * ld + 6 * e2 + c;
+        } else if (q < n_blk + n_cam) {
+            const int64_t r = (q - n_blk) / n_pad, col = (q - n_blk) % n_pad;
+            pos = (6 * (int64_t)n_img + r) * ld + col;
+        } else {
+            pos = n_pad * ld + (q - n_blk - n_cam);
+        }
+        if (dir == 0) red[q] = S[pos];
+        else S[pos] = red[q];
+    }
+}
+
+int launch_pack(Ctx& c, int dir) {
+    const int64_t ncr = (int64_t)c.L.cw * c.L.n_cam;
+    const int64_t total = c.n_red;
+    const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
+    k_pack<<<grid, 256, 0, c.stream>>>(c.d_S, c.L.ld, c.d_red, c.d_gpairs, c.n_gpairs, c.L.n_img, ncr, c.L.n_pad, dir);
+    FBA_HIP(hipGetLastError());
+    return FBA_OK;
+}
+
 }  // namespace fba
