@@ -828,34 +828,54 @@ __global__ void k_neg_copy(const double* __restrict__ X, double* __restrict__ de
 //   stream B (bulk):          [wait trsm(k)] -> rest(k)
 // col(k) updates block column k+1 (the next panel), rest(k) the columns >= k+2; so the bulk update
 // rest(k-1) runs concurrently with potrf(k) and trsm(k).
+// The bulk update with its event record (and the kernel probe) on stream st.
+static int bulk_update(Ctx& c, hipStream_t st, int64_t kb, int64_t jlo, int64_t ncol) {
+    const int64_t ld = c.L.ld, nb = c.L.n_pad / CB;
+    // optional whole rounds of 128x128 tiles (bulk_slots resident workgroups), the rest as 64x64
+    // quarters: four short workgroups per tile keep the last round short
+    const int64_t nt = syrk_tiles(nb, jlo, ncol);
+    const int64_t nfull = c.bulk_slots > 0 ? (nt / c.bulk_slots) * c.bulk_slots : 0;
+    if (nfull > 0) k_syrk128<<<(unsigned)nfull, 256, 0, st>>>(c.d_S, ld, kb, nb, jlo, nfull);
+    if (nt > nfull) {
+        const bool pr = c.probe && c.probe_n < (int)c.probe_ev.size() / 2;
+        if (pr) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], st));
+        k_syrk_q64<<<(unsigned)((nt - nfull) * 4), 256, 0, st>>>(c.d_S, ld, kb, nb, jlo, nfull);
+        if (pr) {
+            FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], st));
+            // quarters computed (strictly upper quarters of diagonal blocks skipped) x 2*64*64*128;
+            // the list is column-major with one diagonal tile per column
+            const int64_t ndiag = (nfull == 0) ? ncol : 0;
+            c.probe_flops += (double)(4 * (nt - nfull) - ndiag) * 2.0 * 64 * 64 * CB;
+            ++c.probe_n;
+        }
+    }
+    return FBA_OK;
+}
+
 int launch_cholesky(Ctx& c) {
     const int64_t ld = c.L.ld, nb = c.L.n_pad / CB;
     hipStream_t A = c.stream, B = c.stream2;
+    bool single = false;
     for (int64_t kb = 0; kb < nb; ++kb) {
         k_potrf128<<<1, 256, POTRF_LDS, A>>>(c.d_S, ld, kb * CB, c.d_dinv, c.d_scal);
         // panel rows below the diagonal block, RHS block row included: (nb - kb) * 128 rows
         k_trsm128<<<(unsigned)((nb - kb) * 2), 256, TRSM_LDS, A>>>(c.d_S, ld, kb * CB, (kb + 1) * CB, c.d_dinv);
-        FBA_HIP(hipEventRecord(c.ev_trsm[kb], A));
         const int64_t m = nb - kb - 1;  // trailing block columns
+        // once the whole trailing update of a step is small, the cross-stream hand-offs (~10 us each)
+        // cost more than the overlap gains: the rest of the factorisation runs on one stream, one
+        // trailing-update launch per step (next panel column included)
+        if (!single && syrk_tiles(nb, kb + 1, m) <= c.switch_tiles) {
+            single = true;
+            if (kb > 0 && nb - kb > 1) FBA_HIP(hipStreamWaitEvent(A, c.ev_rest[kb - 1], 0));
+        }
+        if (single) {
+            if (m > 0) bulk_update(c, A, kb, kb + 1, m);
+            continue;
+        }
+        FBA_HIP(hipEventRecord(c.ev_trsm[kb], A));
         if (m > 1) {
             FBA_HIP(hipStreamWaitEvent(B, c.ev_trsm[kb], 0));
-            // optional whole rounds of 128x128 tiles (bulk_slots resident workgroups), the rest as
-            // 64x64 quarters: four short workgroups per tile keep the last round short
-            const int64_t nt = syrk_tiles(nb, kb + 2, m - 1);
-            const int64_t nfull = c.bulk_slots > 0 ? (nt / c.bulk_slots) * c.bulk_slots : 0;
-            if (nfull > 0) k_syrk128<<<(unsigned)nfull, 256, 0, B>>>(c.d_S, ld, kb, nb, kb + 2, nfull);
-            if (nt > nfull) {
-                const bool pr = c.probe && c.probe_n < (int)c.probe_ev.size() / 2;
-                if (pr) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], B));
-                k_syrk_q64<<<(unsigned)((nt - nfull) * 4), 256, 0, B>>>(c.d_S, ld, kb, nb, kb + 2, nfull);
-                if (pr) {
-                    FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], B));
-                    // quarters computed (strictly upper quarters of diagonal blocks skipped) x 2*64*64*128
-                    const int64_t ndiag = (nfull == 0) ? (m - 1) : 0;  // tiles are column-major: diagonal ones
-                    c.probe_flops += (double)(4 * (nt - nfull) - ndiag) * 2.0 * 64 * 64 * CB;
-                    ++c.probe_n;
-                }
-            }
+            bulk_update(c, B, kb, kb + 2, m - 1);
             FBA_HIP(hipEventRecord(c.ev_rest[kb], B));
         }
         if (m > 0) {
@@ -905,6 +925,8 @@ int chol_setup(Ctx& c) {
     // measured (config 4): 64x64 quarter tiles throughout beat whole rounds of 128x128 tiles + a
     // quarter-tile remainder (4.02 vs 4.10-4.24 ms), so by default no whole rounds are used
     c.bulk_slots = ce ? atoi(ce) : 0;
+    const char* se = getenv("FBA_SWITCH_TILES");
+    c.switch_tiles = se ? atoll(se) : 600;  // measured at config 4: 300 -> 3.73 ms, 600 -> 3.70, 1200 -> 3.73
     if (c.opt.verbose) fprintf(stderr, "[fba] stream priorities least %d greatest %d, bulk mode %d, bulk slots %d\n",
                            prio_least, prio_greatest, prio_mode, c.bulk_slots);
     c.probe_ev.assign(2 * nb, nullptr);

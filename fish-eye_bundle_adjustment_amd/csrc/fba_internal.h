@@ -42,6 +42,7 @@ struct Ctx {
     Layout L;
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;          // bulk trailing updates (Cholesky lookahead)
+    int64_t switch_tiles = 600;             // trailing tiles below which the factorisation runs on one stream
     int bulk_slots = 0;                     // resident k_syrk128 workgroups (whole rounds of the bulk update)
     std::vector<hipEvent_t> ev_trsm, ev_rest;  // per Cholesky step
     bool own_stream = false;

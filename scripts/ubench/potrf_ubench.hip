@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256) void k_potrf_ts(double* __restrict__ S, int64_
     // lower-triangle tiles only (80 KB, so the kernel fits beside a bulk-update workgroup on a CU):
     // element (r, c), r/16 >= c/16, at tile (r/16)(r/16+1)/2 + c/16, row r%16 (stride 17), col c%16
 #define AT_(r, c) smem[(((r) >> 4) * (((r) >> 4) + 1) / 2 + ((c) >> 4)) * (IB * 17) + ((r) & 15) * 17 + ((c) & 15)]
-    double* Dl = smem + POTRF_NT * IB * 17;  // [16][17] current inverse D_s
+    double* Dt = smem + POTRF_NT * IB * 17;  // [16][18] current inverse, transposed: Dt[c][i] = D_s[i][c]
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int lr = lane & 15, lk = lane >> 4;
     const int64_t dbase = (k0 / CB) * (CB / IB) * (IB * IB);
@@ -436,15 +436,7 @@ __global__ __launch_bounds__(256) void k_potrf_ts(double* __restrict__ S, int64_
             T0(1);
             ok = leaf_factor(a, x, lr);
             T0(2);
-            if (lane < IB) {
-#pragma unroll
-                for (int c = 0; c < IB; ++c) {
-                    if (c <= lane) AT_(lane, c) = a[c];
-                    const double d = (c >= lane) ? x[c] : 0.0;  // (L^-1)[c][lane]
-                    Dl[c * 17 + lane] = d;
-                    dinv[dbase + c * IB + lane] = d;
-                }
-            }
+            if (lane < IB) put_leaf(smem, Dt, 0, lane, a, x);
         }
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
@@ -459,6 +451,7 @@ __global__ __launch_bounds__(256) void k_potrf_ts(double* __restrict__ S, int64_
         __syncthreads();  // B1: L_ss, D_s in LDS; column s updated
         T0(3 + 4 * s);
         if (s == CB / IB - 1) break;
+        if (wave > 0) copy_dinv(dinv + dbase + s * IB * IB, Dt, tid - 64, 192);  // D_s -> global
         // panel solve X_t = A_ts D_s^T: wave 0 tile s+1, waves 1..3 tiles s+2..7
         {
             const int t0 = (wave == 0) ? s + 1 : s + 1 + wave;
@@ -468,7 +461,7 @@ __global__ __launch_bounds__(256) void k_potrf_ts(double* __restrict__ S, int64_
                 dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
                 for (int kk = 0; kk < IB; kk += 4)
-                    acc = mfma(AT_((r0 + lr), c0 + kk + lk), Dl[lr * 17 + kk + lk], acc);
+                    acc = mfma(AT_((r0 + lr), c0 + kk + lk), Dt[(kk + lk) * 18 + lr], acc);  // B[k][n] = D[n][k]
 #pragma unroll
                 for (int r = 0; r < 4; ++r) AT_((r0 + lk + 4 * r), c0 + lr) = acc[r];
             }
@@ -494,15 +487,7 @@ __global__ __launch_bounds__(256) void k_potrf_ts(double* __restrict__ S, int64_
             T0(5 + 4 * s);
             ok &= leaf_factor(a, x, lr);
             T0(6 + 4 * s);
-            if (lane < IB) {
-#pragma unroll
-                for (int c = 0; c < IB; ++c) {
-                    if (c <= lane) AT_((R + lane), R + c) = a[c];
-                    const double v = (c >= lane) ? x[c] : 0.0;  // (L^-1)[c][lane]
-                    Dl[c * 17 + lane] = v;  // safe: every wave finished reading D_s before B2
-                    dinv[dbase + (s + 1) * IB * IB + c * IB + lane] = v;
-                }
-            }
+            if (lane < IB) put_leaf(smem, Dt, s + 1, lane, a, x);  // D_s was last read before B2
         } else {
             // waves 1-3: the rest of the trailing update, by tile rows s+2 .. 7 dealt in snake order
             // (largest first) for balance; the tiles of a row go in pairs sharing the A operand,
@@ -541,92 +526,14 @@ __global__ __launch_bounds__(256) void k_potrf_ts(double* __restrict__ S, int64_
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     T0(40);
+    copy_dinv(dinv + dbase + (CB / IB - 1) * IB * IB, Dt, tid, 256);
 #undef AT_
 #undef T0
 }
 
 
 
-
-// experimental: VALU (v_fma_f64) trailing update, same tile list and semantics as k_syrk128.
-// 256 threads = 16 x 16, each an 8 x 8 micro-tile of the 128 x 128 C tile; K staged in 32-deep
-// slices, k-major in LDS so that a thread's 8 A (B) values are two ds_read_b128 broadcasts.
-constexpr int VK = 32, VLD = 128 + 4;
-__global__ __launch_bounds__(256) void k_syrk_valu(double* __restrict__ S, int64_t ld, int64_t kb, int64_t nb,
-                                                   int64_t jlo, int64_t ntiles) {
-    __shared__ __attribute__((aligned(16))) double As[VK][VLD];
-    __shared__ __attribute__((aligned(16))) double Bs[VK][VLD];
-    const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
-    const int64_t k0 = kb * CB;
-    for (int64_t q0 = blockIdx.x; q0 < ntiles; q0 += gridDim.x) {
-        int64_t q = q0, bj = jlo, bi = 0;
-        for (;;) {
-            const int64_t cnt = nb - bj + 1;
-            if (q < cnt) { bi = bj + q; break; }
-            q -= cnt;
-            ++bj;
-        }
-        double acc[8][8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) acc[i][j] = 0.0;
-        // staging: thread -> row rr (0..127), 16 k-values at cc (0 or 16) of the 32-deep slice
-        const int rr = tid >> 1, cc = (tid & 1) * 16;
-        const double* ga = S + (bi * CB + rr) * ld + k0 + cc;
-        const double* gb = S + (bj * CB + rr) * ld + k0 + cc;
-        double2 pa[8], pb[8];
-#pragma unroll
-        for (int h = 0; h < 8; ++h) {
-            pa[h] = *reinterpret_cast<const double2*>(ga + 2 * h);
-            pb[h] = *reinterpret_cast<const double2*>(gb + 2 * h);
-        }
-        for (int ks = 0; ks < CB; ks += VK) {
-            __syncthreads();
-#pragma unroll
-            for (int h = 0; h < 8; ++h) {
-                As[cc + 2 * h][rr] = pa[h].x; As[cc + 2 * h + 1][rr] = pa[h].y;
-                Bs[cc + 2 * h][rr] = pb[h].x; Bs[cc + 2 * h + 1][rr] = pb[h].y;
-            }
-            __syncthreads();
-            if (ks + VK < CB) {
-#pragma unroll
-                for (int h = 0; h < 8; ++h) {
-                    pa[h] = *reinterpret_cast<const double2*>(ga + ks + VK + 2 * h);
-                    pb[h] = *reinterpret_cast<const double2*>(gb + ks + VK + 2 * h);
-                }
-            }
-#pragma unroll 4
-            for (int k = 0; k < VK; ++k) {
-                double a[8], b[8];
-                const double2* ap = reinterpret_cast<const double2*>(&As[k][ty * 8]);
-                const double2* bp = reinterpret_cast<const double2*>(&Bs[k][tx * 8]);
-#pragma unroll
-                for (int h = 0; h < 4; ++h) {
-                    const double2 va = ap[h], vb = bp[h];
-                    a[2 * h] = va.x; a[2 * h + 1] = va.y;
-                    b[2 * h] = vb.x; b[2 * h + 1] = vb.y;
-                }
-#pragma unroll
-                for (int i = 0; i < 8; ++i)
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) acc[i][j] = fma(a[i], b[j], acc[i][j]);
-            }
-        }
-        double* Cp = S + (bi * CB + ty * 8) * ld + bj * CB + tx * 8;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; j += 2) {
-                double2 c = *reinterpret_cast<double2*>(Cp + i * ld + j);
-                c.x -= acc[i][j];
-                c.y -= acc[i][j + 1];
-                *reinterpret_cast<double2*>(Cp + i * ld + j) = c;
-            }
-        __syncthreads();
-    }
-}
-
+// end of instrumented copy
 static double check(const std::vector<double>& L, const std::vector<double>& A0, int n, int ld) {
     // || L L' - A0 ||_max / ||A0||_max over the lower triangle
     double err = 0, mx = 0;
@@ -789,22 +696,6 @@ int main() {
                 printf("  contention %s: potrf %.1f us, bulk syrk (%lld tiles) %.1f us%s", variant == 0 ? "old(135KB)" : variant == 1 ? "new(80KB)" : "prof", 1e3f * ta, (long long)nt, 1e3f * tb, variant == 2 ? "" : "\n");
                 if (variant == 2) printf("  -> %llu shader cycles = %.2f GHz over the kernel\n", tq[40] - tq[0], (tq[40] - tq[0]) / (1e3 * ta));
             }
-        }
-        // bulk update alone: MFMA k_syrk128 vs VALU k_syrk_valu over the same 1080 tiles
-        for (int variant = 0; variant < 2; ++variant) {
-            float best = 1e9f;
-            for (int rep = 0; rep < 5; ++rep) {
-                CK(hipEventRecord(b0, sB));
-                if (variant == 0) k_syrk128<<<(unsigned)nt, 256, 0, sB>>>(dM, N, 0, nb, 2, nt);
-                else k_syrk_valu<<<(unsigned)nt, 256, 0, sB>>>(dM, N, 0, nb, 2, nt);
-                CK(hipEventRecord(b1, sB));
-                CK(hipEventSynchronize(b1));
-                float tb;
-                CK(hipEventElapsedTime(&tb, b0, b1));
-                best = fminf(best, tb);
-            }
-            const double fl = 2.0 * 128 * 128 * 128 * (double)nt;
-            printf("  bulk %s: %.1f us  %.1f TFLOP/s\n", variant ? "VALU k_syrk_valu" : "MFMA k_syrk128", 1e3f * best, fl / (1e-3 * best) / 1e12);
         }
         CK(hipFree(dM));
     }

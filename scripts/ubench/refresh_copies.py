@@ -19,6 +19,6 @@ k = k.replace("        __syncthreads();  // B2: panel column s solved\n", "     
 k = k.replace("            ok &= leaf_factor(a, x, lr);", "            T0(5 + 4 * s);\n            ok &= leaf_factor(a, x, lr);\n            T0(6 + 4 * s);")
 k = k.replace("    store_col(CB / IB - 1, tid, 256);\n", "    store_col(CB / IB - 1, tid, 256);\n    __builtin_amdgcn_s_waitcnt(0);\n    __syncthreads();\n    T0(40);\n")
 s0 = u.index("// instrumented copy of k_potrf128\n")
-s1 = u.index("static double check(", s0)
+s1 = u.index("// end of instrumented copy", s0)
 u = u[:s0] + "// instrumented copy of k_potrf128\n" + k + "\n" + u[s1:]
 open(U, "w").write(u)
