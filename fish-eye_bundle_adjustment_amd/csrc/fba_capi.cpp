@@ -216,7 +216,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     std::vector<int32_t> ctl_owner;
     partition(p, opt.world, c->tie_owner, ctl_owner);
 
-    // local tie points sorted by (camera, tie index); their observations in PHO order
+    // local tie points sorted by camera; their observations in PHO order
     std::vector<std::vector<int64_t>> tie_obs(L.n_tie);
     std::vector<int32_t> tie_cam(L.n_tie, 0);
     for (int64_t i = 0; i < p->n_pts; ++i)
@@ -227,7 +227,40 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     std::vector<int32_t> lps;
     for (int t = 0; t < L.n_tie; ++t)
         if (c->tie_owner[t] == opt.rank && !tie_obs[t].empty()) lps.push_back(t);
-    std::stable_sort(lps.begin(), lps.end(), [&](int32_t a, int32_t b) { return tie_cam[a] < tie_cam[b]; });
+    // within a camera, points in Morton (Z-curve) order of their initial coordinates: the points two
+    // co-visible images share -- and so the W/T and Jacobian rows a pair or an image gathers -- sit
+    // close together in memory
+    std::vector<uint64_t> zkey(L.n_tie, 0);
+    {
+        double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+        for (int32_t t : lps)
+            for (int d = 0; d < 3; ++d) {
+                lo[d] = std::min(lo[d], p->tie0[3 * (int64_t)t + d]);
+                hi[d] = std::max(hi[d], p->tie0[3 * (int64_t)t + d]);
+            }
+        auto spread = [](uint64_t v) {  // 21 bits -> every third bit
+            v &= 0x1fffff;
+            v = (v | v << 32) & 0x1f00000000ffffULL;
+            v = (v | v << 16) & 0x1f0000ff0000ffULL;
+            v = (v | v << 8) & 0x100f00f00f00f00fULL;
+            v = (v | v << 4) & 0x10c30c30c30c30c3ULL;
+            v = (v | v << 2) & 0x1249249249249249ULL;
+            return v;
+        };
+        for (int32_t t : lps) {
+            uint64_t k = 0;
+            for (int d = 0; d < 3; ++d) {
+                const double span = hi[d] > lo[d] ? hi[d] - lo[d] : 1.0;
+                double f = (p->tie0[3 * (int64_t)t + d] - lo[d]) / span;
+                f = std::isfinite(f) ? std::min(std::max(f, 0.0), 1.0) : 0.0;
+                k |= spread((uint64_t)(f * 2097151.0)) << d;
+            }
+            zkey[t] = k;
+        }
+    }
+    std::stable_sort(lps.begin(), lps.end(), [&](int32_t a, int32_t b) {
+        return tie_cam[a] != tie_cam[b] ? tie_cam[a] < tie_cam[b] : zkey[a] < zkey[b];
+    });
     c->n_lp = (int64_t)lps.size();
 
     std::vector<double> xy;

@@ -482,8 +482,11 @@ __global__ __launch_bounds__(256) void k_image(const double* __restrict__ J, con
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_pairs: off-diagonal image-image blocks S(e1,e2) = -sum W_i Vinv W_j^T over shared tie points;
-// one wave per co-visible pair, lanes 0..35 own the 6x6 entries, 4 terms in flight.
+// k_pairs: off-diagonal image-image blocks S(e1,e2) = -sum W_i Vinv W_j^T = -sum T_i W_j^T over the tie
+// points the two images share; one wave per co-visible pair.  The (T_i, W_j) rows of 32 terms at a
+// time are gathered with 16-byte loads into LDS (9 per lane per chunk -- narrow per-entry loads made
+// this kernel bound by vector-memory instruction issue), the next chunk's rows and indices are in
+// flight while the current chunk is reduced; lanes 0..35 own the 6x6 entries, 4 partial sums each.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_pairs(const double* __restrict__ WT, const int32_t* __restrict__ pair_e,
                                               const int32_t* __restrict__ pair_start, const int32_t* __restrict__ pair_ij,
@@ -494,34 +497,73 @@ __global__ __launch_bounds__(64) void k_pairs(const double* __restrict__ WT, con
     const int64_t per = (n_pairs + 7) / 8;
     const int64_t pr = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
     if (pr >= n_pairs) return;
+    constexpr int CH = 32, RS = 18;  // terms per chunk, doubles per staged row
+    __shared__ __attribute__((aligned(16))) double rows[CH][2][RS];
+    __shared__ int2 idx[2][CH];
     const int q = threadIdx.x;
-    if (q >= 36) return;
     const int a = q / 6, b = q % 6;
     const int e1 = pair_e[2 * pr], e2 = pair_e[2 * pr + 1];
     const int t0 = pair_start[pr], t1 = pair_start[pr + 1];
+    const int nch = (t1 - t0 + CH - 1) / CH;
+    const int2* ij2 = reinterpret_cast<const int2*>(pair_ij);
+    const double2* WT2 = reinterpret_cast<const double2*>(WT);
+    // item it (< 2*9*CH): term it / 18, row (it / 9) & 1 (0: T_i = WT[i][18..36), 1: W_j = WT[j][0..18)),
+    // 16-byte part it % 9
+    constexpr int NR = (2 * 9 * CH + 63) / 64;  // 9 loads per lane
+    double2 rv[NR];
+    int2 iv = make_int2(0, 0);
+    auto fetch_rows = [&](int c, int buf) {
+        const int n = min(CH, t1 - t0 - c * CH);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int it = q + 64 * r, k = it / 18, row = (it / 9) & 1, part = it % 9;
+            if (k < n) {
+                const int2 t = idx[buf][k];
+                rv[r] = WT2[(int64_t)(row ? t.y : t.x) * 18 + (row ? 0 : 9) + part];
+            }
+        }
+    };
+    auto fetch_idx = [&](int c) {
+        if (q < CH && t0 + c * CH + q < t1) iv = ij2[t0 + c * CH + q];
+    };
+    fetch_idx(0);
+    if (q < CH) idx[0][q] = iv;
+    __syncthreads();
+    if (nch > 0) fetch_rows(0, 0);
+    if (nch > 1) fetch_idx(1);
     double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
-    int t = t0;
-    for (; t + 4 <= t1; t += 4) {
-        const int2 ij0 = *reinterpret_cast<const int2*>(pair_ij + 2 * t);
-        const int2 ij1 = *reinterpret_cast<const int2*>(pair_ij + 2 * t + 2);
-        const int2 ij2 = *reinterpret_cast<const int2*>(pair_ij + 2 * t + 4);
-        const int2 ij3 = *reinterpret_cast<const int2*>(pair_ij + 2 * t + 6);
-        const double* T0 = WT + (int64_t)ij0.x * 36 + 18 + 3 * a; const double* W0 = WT + (int64_t)ij0.y * 36 + 3 * b;
-        const double* T1 = WT + (int64_t)ij1.x * 36 + 18 + 3 * a; const double* W1 = WT + (int64_t)ij1.y * 36 + 3 * b;
-        const double* T2 = WT + (int64_t)ij2.x * 36 + 18 + 3 * a; const double* W2 = WT + (int64_t)ij2.y * 36 + 3 * b;
-        const double* T3 = WT + (int64_t)ij3.x * 36 + 18 + 3 * a; const double* W3 = WT + (int64_t)ij3.y * 36 + 3 * b;
-        acc0 -= T0[0] * W0[0] + T0[1] * W0[1] + T0[2] * W0[2];
-        acc1 -= T1[0] * W1[0] + T1[1] * W1[1] + T1[2] * W1[2];
-        acc2 -= T2[0] * W2[0] + T2[1] * W2[1] + T2[2] * W2[2];
-        acc3 -= T3[0] * W3[0] + T3[1] * W3[1] + T3[2] * W3[2];
+    for (int c = 0; c < nch; ++c) {
+        const int n = min(CH, t1 - t0 - c * CH);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int it = q + 64 * r, k = it / 18, row = (it / 9) & 1, part = it % 9;
+            if (k < n) *reinterpret_cast<double2*>(&rows[k][row][2 * part]) = rv[r];
+        }
+        if (c + 1 < nch && q < CH) idx[(c + 1) & 1][q] = iv;
+        __syncthreads();
+        if (c + 1 < nch) fetch_rows(c + 1, (c + 1) & 1);
+        if (c + 2 < nch) fetch_idx(c + 2);
+        if (q < 36) {
+            int k = 0;
+            for (; k + 4 <= n; k += 4) {
+                const double* T0 = rows[k][0] + 3 * a; const double* W0 = rows[k][1] + 3 * b;
+                const double* T1 = rows[k + 1][0] + 3 * a; const double* W1 = rows[k + 1][1] + 3 * b;
+                const double* T2 = rows[k + 2][0] + 3 * a; const double* W2 = rows[k + 2][1] + 3 * b;
+                const double* T3 = rows[k + 3][0] + 3 * a; const double* W3 = rows[k + 3][1] + 3 * b;
+                acc0 -= T0[0] * W0[0] + T0[1] * W0[1] + T0[2] * W0[2];
+                acc1 -= T1[0] * W1[0] + T1[1] * W1[1] + T1[2] * W1[2];
+                acc2 -= T2[0] * W2[0] + T2[1] * W2[1] + T2[2] * W2[2];
+                acc3 -= T3[0] * W3[0] + T3[1] * W3[1] + T3[2] * W3[2];
+            }
+            for (; k < n; ++k) {
+                const double* T = rows[k][0] + 3 * a;
+                const double* W = rows[k][1] + 3 * b;
+                acc0 -= T[0] * W[0] + T[1] * W[1] + T[2] * W[2];
+            }
+        }
+        __syncthreads();
     }
-    for (; t < t1; ++t) {
-        const int i = pair_ij[2 * t], j = pair_ij[2 * t + 1];
-        const double* T = WT + (int64_t)i * 36 + 18 + 3 * a;
-        const double* W = WT + (int64_t)j * 36 + 3 * b;
-        acc0 -= T[0] * W[0] + T[1] * W[1] + T[2] * W[2];
-    }
-    S[(int64_t)(6 * e1 + a) * ld + 6 * e2 + b] = (acc0 + acc1) + (acc2 + acc3);
+    if (q < 36) S[(int64_t)(6 * e1 + a) * ld + 6 * e2 + b] = (acc0 + acc1) + (acc2 + acc3);
 }
 
 // ------------------------------------------------------------------------------------------------
