@@ -64,19 +64,21 @@ static void compute_layout(const fba_problem* p, const fba_settings* s, Layout& 
     L.u_full = L.u_c + 3 * (int64_t)L.n_tie;
     L.n_pad = round_up(std::max<int64_t>(L.u_c, 1), NB);
     L.ld = L.n_pad;
-    L.nrhs = s->inner_constraints ? 8 : 1;
+    L.nrhs = s->inner_constraints ? 15 : 1;
     L.u_img = s->est_Xc + s->est_Yc + s->est_Zc + s->est_omega + s->est_phi + s->est_kappa;
     L.u_cam = s->est_c + s->est_xp + s->est_yp + s->est_radial * s->num_radial + s->est_decent * 2;
     L.u_ref = (int64_t)L.u_img * L.n_img + (int64_t)L.u_cam * L.n_cam + 3 * (int64_t)L.n_tie;
 }
 
-static void full_to_ref_map(const fba_settings* s, const Layout& L, std::vector<int64_t>& map) {
+// full (internal) index -> the reference's xhat index.  Internal image e is EXT row img_ord[e].
+static void full_to_ref_map(const fba_settings* s, const Layout& L, const std::vector<int32_t>& img_ord,
+                            std::vector<int64_t>& map) {
     map.assign(L.u_full, -1);
     const int ee[6] = {s->est_Xc, s->est_Yc, s->est_Zc, s->est_omega, s->est_phi, s->est_kappa};
     for (int e = 0; e < L.n_img; ++e) {
         int cnt = 0;
         for (int a = 0; a < 6; ++a)
-            if (ee[a]) map[6 * (int64_t)e + a] = (int64_t)e * L.u_img + cnt++;
+            if (ee[a]) map[6 * (int64_t)e + a] = (int64_t)img_ord[e] * L.u_img + cnt++;
     }
     std::vector<int> ce(L.cw, 0);
     ce[0] = s->est_xp;
@@ -178,6 +180,77 @@ static void destroy(Ctx* c) {
     delete c;
 }
 
+// Reverse Cuthill-McKee order of the images on their co-visibility graph (images sharing a tie point),
+// over ALL tie points so that every rank derives the same order.  Returns ord[new] = old.
+static std::vector<int32_t> image_order(const fba_problem* p) {
+    const int n = p->n_img;
+    std::vector<std::pair<int32_t, int32_t>> ti;  // (tie, image)
+    for (int64_t i = 0; i < p->n_pts; ++i)
+        if (p->tie[i] >= 0) ti.emplace_back(p->tie[i], p->img[i]);
+    std::sort(ti.begin(), ti.end());
+    std::vector<std::pair<int32_t, int32_t>> edges;
+    for (size_t a = 0; a < ti.size();) {
+        size_t b = a;
+        while (b < ti.size() && ti[b].first == ti[a].first) ++b;
+        for (size_t x = a; x < b; ++x)
+            for (size_t y = a; y < b; ++y)
+                if (ti[x].second != ti[y].second) edges.emplace_back(ti[x].second, ti[y].second);
+        a = b;
+    }
+    std::sort(edges.begin(), edges.end());
+    edges.erase(std::unique(edges.begin(), edges.end()), edges.end());
+    std::vector<int32_t> start(n + 1, 0), adj(edges.size());
+    for (auto& e : edges) start[e.first + 1]++;
+    for (int v = 0; v < n; ++v) start[v + 1] += start[v];
+    for (size_t q = 0; q < edges.size(); ++q) adj[q] = edges[q].second;
+    auto deg = [&](int v) { return start[v + 1] - start[v]; };
+    std::vector<int32_t> order;
+    order.reserve(n);
+    std::vector<char> seen(n, 0);
+    for (;;) {
+        int root = -1;  // unvisited image of minimum degree (lowest index on ties)
+        for (int v = 0; v < n; ++v)
+            if (!seen[v] && (root < 0 || deg(v) < deg(root))) root = v;
+        if (root < 0) break;
+        size_t head = order.size();
+        order.push_back(root);
+        seen[root] = 1;
+        while (head < order.size()) {
+            const int v = order[head++];
+            std::vector<int32_t> nb(adj.begin() + start[v], adj.begin() + start[v + 1]);
+            std::stable_sort(nb.begin(), nb.end(), [&](int32_t a, int32_t b) { return deg(a) < deg(b); });
+            for (int32_t w : nb)
+                if (!seen[w]) { seen[w] = 1; order.push_back(w); }
+        }
+    }
+    std::reverse(order.begin(), order.end());
+    return order;
+}
+
+// Envelope of the reduced system by 128-row block: first[i] = first nonzero block column of block row
+// i (image-image blocks of co-visible pairs, the local border block, the dense camera rows).
+static void block_envelope(const Layout& L, const std::vector<std::pair<int32_t, int32_t>>& pairs_new, int n_loc,
+                           std::vector<int32_t>& first) {
+    const int64_t nb = L.n_pad / NB;
+    first.assign(nb, 0);
+    for (int64_t i = 0; i < nb; ++i) first[i] = (int32_t)i;
+    // an image's 6 rows may straddle two blocks: its rows reach back to the first block of the
+    // other image (and of itself)
+    auto touch = [&](int64_t e1, int64_t e2) {
+        const int64_t bj = 6 * e2 / NB;
+        for (int64_t bi = 6 * e1 / NB; bi <= (6 * e1 + 5) / NB && bi < nb; ++bi)
+            first[bi] = std::min<int32_t>(first[bi], (int32_t)bj);
+    };
+    for (auto& q : pairs_new) touch(q.first, q.second);  // (e1, e2), e1 > e2
+    for (int64_t e = 0; e < L.n_img; ++e) touch(e, e);
+    if (n_loc > 0) {
+        const int64_t bl = (6 * (int64_t)n_loc - 1) / NB;
+        for (int64_t i = 0; i <= bl; ++i) first[i] = 0;
+    }
+    // block rows holding camera rows (and everything after) are dense
+    for (int64_t i = (6 * (int64_t)L.n_img) / NB; i < nb; ++i) first[i] = 0;
+}
+
 static int create(const fba_problem* p, const fba_settings* s, const fba_options* o, Ctx** out) {
     int rc = check_settings(s);
     if (rc) return rc;
@@ -195,7 +268,11 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     c->n_pts = p->n_pts;
     Layout& L = c->L;
     compute_layout(p, s, L);
-    full_to_ref_map(s, L, c->full_to_ref);
+    // camera-side order of the images: reverse Cuthill-McKee, so the reduced system is banded
+    c->img_ord = image_order(p);
+    c->img_new.assign(L.n_img, 0);
+    for (int e = 0; e < L.n_img; ++e) c->img_new[c->img_ord[e]] = e;
+    full_to_ref_map(s, L, c->img_ord, c->full_to_ref);
 
     FBA_HIP(hipSetDevice(opt.device));
     c->device = opt.device;
@@ -208,7 +285,8 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
 
     // initial full-space parameters
     c->xfull0.assign(L.u_full, 0.0);
-    for (int64_t i = 0; i < 6 * (int64_t)L.n_img; ++i) c->xfull0[i] = p->eop0[i];
+    for (int e = 0; e < L.n_img; ++e)
+        for (int a = 0; a < 6; ++a) c->xfull0[6 * (int64_t)e + a] = p->eop0[6 * (int64_t)c->img_ord[e] + a];
     for (int64_t i = 0; i < (int64_t)L.cw * L.n_cam; ++i) c->xfull0[6 * (int64_t)L.n_img + i] = p->iop0[i];
     for (int64_t i = 0; i < 3 * (int64_t)L.n_tie; ++i) c->xfull0[L.u_c + i] = p->tie0[i];
 
@@ -274,7 +352,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
             pho.push_back(i);
             xy.push_back(p->xy[2 * i]);
             xy.push_back(p->xy[2 * i + 1]);
-            img.push_back(p->img[i]);
+            img.push_back(c->img_new[p->img[i]]);
             cam.push_back(p->cam[i]);
             pt.push_back((int32_t)lp);
         }
@@ -293,7 +371,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         pho.push_back(i);
         xy.push_back(p->xy[2 * i]);
         xy.push_back(p->xy[2 * i + 1]);
-        img.push_back(p->img[i]);
+        img.push_back(c->img_new[p->img[i]]);
         cam.push_back(p->cam[i]);
         pt.push_back(-1 - (int32_t)q);
         for (int m = 0; m < 3; ++m) ctl.push_back(p->xyz_fixed[3 * i + m]);
@@ -377,13 +455,16 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     }
     pair_start.push_back((int32_t)terms.size());
     c->n_pairs = (int64_t)pair_e.size() / 2;
-    // ranks > 1: the co-visible image pairs of ALL tie points (identical on every rank), for the
-    // compact reduce buffer
+    c->n_pair_terms = (int64_t)terms.size();
+    terms.clear();
+    terms.shrink_to_fit();
+    // the co-visible image pairs of ALL tie points (identical on every rank): the compact reduce
+    // buffer of ranks > 1 and the block envelope of the reduced system
     std::vector<int32_t> gpairs;
-    if (opt.world > 1) {
-        std::vector<std::pair<int32_t, int32_t>> pi;  // (tie, image)
+    {
+        std::vector<std::pair<int32_t, int32_t>> pi;  // (tie, internal image)
         for (int64_t i = 0; i < p->n_pts; ++i)
-            if (p->tie[i] >= 0) pi.emplace_back(p->tie[i], p->img[i]);
+            if (p->tie[i] >= 0) pi.emplace_back(p->tie[i], c->img_new[p->img[i]]);
         std::sort(pi.begin(), pi.end());
         std::vector<std::pair<int32_t, int32_t>> gp;
         for (size_t a = 0; a < pi.size();) {
@@ -396,13 +477,16 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         }
         std::sort(gp.begin(), gp.end());
         gp.erase(std::unique(gp.begin(), gp.end()), gp.end());
-        for (auto& q : gp) { gpairs.push_back(q.first); gpairs.push_back(q.second); }
-        c->n_gpairs = (int64_t)gp.size();
-        c->n_red = 36 * (c->n_gpairs + L.n_img) + (int64_t)L.cw * L.n_cam * L.n_pad + L.n_pad;
+        // inner constraints: the border is applied on the first n_loc images only (local border,
+        // DESIGN.md section 2), so M keeps the band structure
+        c->n_loc = s->inner_constraints ? std::min<int>(L.n_img, (int)(NB / 6)) : 0;
+        block_envelope(L, gp, c->n_loc, c->env_first);
+        if (opt.world > 1) {
+            for (auto& q : gp) { gpairs.push_back(q.first); gpairs.push_back(q.second); }
+            c->n_gpairs = (int64_t)gp.size();
+            c->n_red = 36 * (c->n_gpairs + L.n_img) + (int64_t)L.cw * L.n_cam * L.n_pad + L.n_pad;
+        }
     }
-    c->n_pair_terms = (int64_t)terms.size();
-    terms.clear();
-    terms.shrink_to_fit();
 
     // which full-space entries are estimated / owned / counted
     std::vector<uint8_t> active(L.n_pad, 0), counted(L.u_full, 0);
@@ -451,7 +535,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         (rc = dalloc(&c->d_S, (size_t)(L.n_pad + NB) * L.ld)) || (rc = dalloc(&c->d_X, (size_t)L.n_pad)) ||
         (rc = dalloc(&c->d_dinv, (size_t)(L.n_pad / NB) * 8 * 256)) ||
         (rc = dalloc(&c->d_linv, (size_t)(L.n_pad / NB) * NB * NB)) ||
-        (rc = dalloc(&c->d_scal, 16)) || (rc = dalloc(&c->d_part, (size_t)c->n_part)) ||
+        (rc = dalloc(&c->d_scal, 32 + 256)) || (rc = dalloc(&c->d_part, (size_t)c->n_part)) ||
         (rc = dalloc(&c->d_res, (size_t)7 * std::max<int64_t>(c->n_obs, 1)))) {
         destroy(c);
         return rc;

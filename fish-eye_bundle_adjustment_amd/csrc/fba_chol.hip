@@ -1,27 +1,32 @@
-// fba_chol.hip -- dense fp64 Cholesky of the reduced camera system on gfx950 (MI355X).
+// fba_chol.hip -- fp64 envelope Cholesky of the reduced camera system on gfx950 (MI355X).
 //
 // The reference inverts the bordered normal matrix explicitly, Cx = [N G; G' 0]^-1
 // (main.m:428-440).  Here the tie points have already been eliminated (Schur complement), the
-// border is folded in as M = S + G W G' (SPD whenever the bordered matrix is nonsingular; W = one
-// equilibrating weight per constraint column, fba_kernels.hip k_border_weights), and
+// images are in reverse Cuthill-McKee order (fba_capi.cpp image_order), so the image-image part of
+// the reduced system S is banded, and the border is folded in LOCALLY as M = S + A A' with A =
+// G_l W^1/2 restricted to the first n_loc images (SPD whenever the bordered matrix is nonsingular
+// and those images fix the datum; W = one equilibrating weight per constraint column,
+// fba_kernels.hip k_border_weights) -- so M keeps the band, and
 //
-//   M = L L'        right-looking blocked Cholesky, NB = 128, depth-1 lookahead on two streams:
+//   M = L L'        right-looking blocked Cholesky over the block envelope, NB = 128:
 //     k_potrf128    the 128x128 diagonal block, LDS-resident in one workgroup: 8 sub-panels of 16
-//                   (16x16 factor in registers with v_readlane broadcasts, its 16x16 inverse, then
-//                   the in-block panel solve and trailing update on v_mfma_f64_16x16x4_f64); writes
+//                   (16x16 factor in registers with DPP broadcasts, its 16x16 inverse, then the
+//                   in-block panel solve and trailing update on v_mfma_f64_16x16x4_f64); writes
 //                   L_kk and the eight 16x16 inverses D_s = L_ss^-1 used by the solves below
-//     k_trsm128     the panel below, X = A L_kk^-T by blocked substitution
+//     k_trsm128     the panel rows of the envelope, X = A L_kk^-T by blocked substitution
 //                   X_s = (A_s - sum_{t<s} X_t L_st^T) D_s^T: all MFMA, 16 rows per wave
-//     k_syrk128     trailing update C -= X_i X_j^T, 128x128 tiles (4 waves x 64x64), K = 128
-//                   staged through LDS in 32-deep slices, v_mfma_f64_16x16x4_f64
-//   forward solve   the right-hand sides [r | G W^1/2] are stored as extra ROWS below M (one extra
-//                   block row), so the panel solves compute Y' = (L^-1 B)' as a by-product
-//   border combine  H = Z'Z, h = Z'y, k = -H^-1 h, y <- y + Z k      (Z, y = forward-solved G W^1/2, r)
-//   backward solve  L' x = y with the 128x128 diagonal-block inverses (k_trtri128, all blocks in
+//     k_syrk_env    trailing update C -= X_i X_j^T over the envelope, 64x64 tiles, K = 128 staged
+//                   through LDS in 32-deep slices, v_mfma_f64_16x16x4_f64
+//   forward solve   the right-hand sides [r | A | B] (B = G D, D an equilibration over all images)
+//                   are stored as extra ROWS below M (one extra block row), so the panel solves
+//                   compute Y' = (L^-1 [r A B])' as a by-product
+//   border combine  the 14x14 system of k_border_combine restores the exact bordered solution:
+//                   u = y + A~ z + B~ k with z = A~'u and B~'u = 0
+//   backward solve  L' x = u with the 128x128 diagonal-block inverses (k_trtri128, all blocks in
 //                   parallel), then one short launch per block row (k_bwd_step: two 128x128 GEMVs
 //                   on the critical workgroup)
-// so delta_c = -x = -M^-1 (r + G W^1/2 k) satisfies [S G; G' 0][delta; W^1/2 k] = [-r; 0] as the
-// reference's bordered system does.
+// so delta_c = -x satisfies [S G; G' 0][delta; lambda] = [-r; 0] as the reference's bordered
+// system does.
 #include "fba_internal.h"
 
 #include <cstdio>
@@ -51,6 +56,10 @@ __device__ __forceinline__ double rsqrt_d(double d) {
 
 __device__ __forceinline__ dbl4 mfma(double a, double b, dbl4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+__host__ __device__ __forceinline__ int64_t rmap(int64_t x, int64_t a0, int64_t n1, int64_t b0) {
+    return x < n1 ? a0 + x : b0 + (x - n1);
 }
 
 template <int L>
@@ -334,8 +343,8 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
 constexpr int TRSM_NT = (CB / IB) * (CB / IB - 1) / 2;  // 28 off-diagonal tiles
 constexpr size_t TRSM_LDS = sizeof(double) * (4 * IB * LDA + 4 * IB * 17 + (TRSM_NT + CB / IB) * IB * 17);
 
-__global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t ld, int64_t k0, int64_t row0,
-                                                 const double* __restrict__ dinv) {
+__global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t ld, int64_t k0, int64_t a0,
+                                                 int64_t n1, int64_t b0, const double* __restrict__ dinv) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* X = smem;                       // [4][IB][LDA]   panel rows of each wave
     double* T = X + 4 * IB * LDA;           // [4][IB][17]    per-wave 16x16 staging
@@ -343,7 +352,7 @@ __global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t
     double* Dt = Lt + TRSM_NT * IB * 17;    // [8][IB][17]    D_s
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int lr = lane & 15, lk = lane >> 4;
-    const int64_t rbase = row0 + (int64_t)blockIdx.x * 64 + wave * IB;
+    const int64_t rbase = rmap(blockIdx.x >> 1, a0, n1, b0) * CB + (blockIdx.x & 1) * 64 + wave * IB;
     double* Xw = X + wave * IB * LDA;
     double* Tw = T + wave * IB * 17;
     const double* L = S + k0 * ld + k0;
@@ -434,87 +443,14 @@ __global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_syrk128: trailing update C(bi,bj) -= X_bi X_bj^T, 128x128 tiles, K = 128 in 32-deep slices.
-// Tiles: block columns bj in [jlo, jlo + ncol), block rows bi in [bj, nb] (bi == nb: RHS block row).
-// 4 waves, each a 64x64 quadrant = 4x4 MFMA tiles.  The accumulators start from C (its loads overlap
-// the first slice), each next slice is prefetched into registers while the MFMAs of the current one
-// run, and the epilogue is a plain store.
+// Trailing updates, 64x64 output tiles, K = 128 staged through LDS in 32-deep slices.
+// Envelope: at step kb the panel rows are the block rows R_kb = {a0 .. a0+n1-1} u {b0 .. nb} (the
+// image block rows whose envelope reaches column kb, then the dense camera rows and the RHS block
+// row nb); rmap(x) is the x-th block of that list.  Blocks outside the envelope are zero and stay
+// zero (no fill outside the profile), so they are never touched.
 // ------------------------------------------------------------------------------------------------
 constexpr int KS = 32;
 constexpr int LDK = 34;   // LDS stride of a 32-deep slice: bank = (4r + 2k) mod 64, conflict-free
-
-__global__ __launch_bounds__(256) void k_syrk128(double* __restrict__ S, int64_t ld, int64_t kb, int64_t nb,
-                                                 int64_t jlo, int64_t ntiles) {
-    __shared__ __attribute__((aligned(16))) double As[CB][LDK];
-    __shared__ __attribute__((aligned(16))) double Bs[CB][LDK];
-    for (int64_t q0 = blockIdx.x; q0 < ntiles; q0 += gridDim.x) {
-    int64_t q = q0, bj = jlo, bi = 0;
-    for (;;) {
-        const int64_t cnt = nb - bj + 1;
-        if (q < cnt) { bi = bj + q; break; }
-        q -= cnt;
-        ++bj;
-    }
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int lr = lane & 15, lk = lane >> 4;
-    const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
-    const int64_t k0 = kb * CB;
-    double* Cp = S + (bi * CB + wr + lk) * ld + bj * CB + wc + lr;
-    dbl4 acc[4][4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) acc[a][b][r] = Cp[(a * 16 + 4 * r) * ld + b * 16];
-    // staging: thread -> (row rr, 16 columns at cc) of the 128 x 32 slice, for A and B
-    const int rr = tid >> 1, cc = (tid & 1) * 16;
-    const double* ga = S + (bi * CB + rr) * ld + k0 + cc;
-    const double* gb = S + (bj * CB + rr) * ld + k0 + cc;
-    double2 pa[8], pb[8];
-#pragma unroll
-    for (int h = 0; h < 8; ++h) {
-        pa[h] = *reinterpret_cast<const double2*>(ga + 2 * h);
-        pb[h] = *reinterpret_cast<const double2*>(gb + 2 * h);
-    }
-    for (int ks = 0; ks < CB; ks += KS) {
-        __syncthreads();
-#pragma unroll
-        for (int h = 0; h < 8; ++h) {
-            As[rr][cc + 2 * h] = pa[h].x; As[rr][cc + 2 * h + 1] = pa[h].y;
-            Bs[rr][cc + 2 * h] = pb[h].x; Bs[rr][cc + 2 * h + 1] = pb[h].y;
-        }
-        __syncthreads();
-        if (ks + KS < CB) {
-#pragma unroll
-            for (int h = 0; h < 8; ++h) {
-                pa[h] = *reinterpret_cast<const double2*>(ga + ks + KS + 2 * h);
-                pb[h] = *reinterpret_cast<const double2*>(gb + ks + KS + 2 * h);
-            }
-        }
-#pragma unroll
-        for (int kk = 0; kk < KS; kk += 4) {
-            double av[4], bv[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                av[t] = -As[wr + t * 16 + lr][kk + lk];
-                bv[t] = Bs[wc + t * 16 + lr][kk + lk];
-            }
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int b = 0; b < 4; ++b) acc[a][b] = mfma(av[a], bv[b], acc[a][b]);
-        }
-    }
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) Cp[(a * 16 + 4 * r) * ld + b * 16] = acc[a][b][r];
-    __syncthreads();  // LDS reuse by the next tile
-    }
-}
 
 // C(r0.., c0..) -= X_r X_c^T for one 64x64 tile, K = 128 (the panel at columns k0.. = kb*128):
 // 4 waves of 32x32 (2x2 MFMA tiles), K staged through LDS in 32-deep slices.
@@ -580,122 +516,121 @@ __device__ __forceinline__ void tile64_update(double* __restrict__ S, int64_t ld
 }
 
 
-// k_syrk_col64: the critical-path update of block column kb+1 (rows (kb+1)*128 .. (nb+1)*128) with
-// 64x64 tiles, K = 128: 4x the workgroups of k_syrk128, a quarter of the latency each.
-// Tile q: sub-row q >> 1 (64 rows), sub-column q & 1 of the 128-wide block column.
-__global__ __launch_bounds__(256) void k_syrk_col64(double* __restrict__ S, int64_t ld, int64_t kb) {
-    tile64_update(S, ld, kb, (kb + 1) * CB + (int64_t)(blockIdx.x >> 1) * 64,
-                  (kb + 1) * CB + (int64_t)(blockIdx.x & 1) * 64);
-}
-
-// k_syrk_q64: the trailing tiles [tile0, tile0 + gridDim.x/4) of k_syrk128's list, as quarters (the
-// partial last round of the bulk update: four short workgroups per tile instead of one long one).
-__global__ __launch_bounds__(256) void k_syrk_q64(double* __restrict__ S, int64_t ld, int64_t kb, int64_t nb,
-                                                  int64_t jlo, int64_t tile0) {
-    int64_t q = tile0 + blockIdx.x / 4, bj = jlo, bi = 0;
+// k_syrk_env: tiles [tile0, tile0 + gridDim.x/4) of the step's list, as 64x64 quarters: block
+// columns by list position pj = pj0, pj0+1, ..., rows by position pi in [pj, nr) (column-major;
+// the strictly upper quarter of a diagonal block is skipped)
+__global__ __launch_bounds__(256) void k_syrk_env(double* __restrict__ S, int64_t ld, int64_t kb, int64_t a0,
+                                                  int64_t n1, int64_t b0, int64_t nr, int64_t pj0, int64_t tile0) {
+    int64_t q = tile0 + blockIdx.x / 4, pj = pj0, pi = 0;
     for (;;) {
-        const int64_t cnt = nb - bj + 1;
-        if (q < cnt) { bi = bj + q; break; }
+        const int64_t cnt = nr - pj;
+        if (q < cnt) { pi = pj + q; break; }
         q -= cnt;
-        ++bj;
+        ++pj;
     }
     const int qr = (blockIdx.x >> 1) & 1, qc = blockIdx.x & 1;
-    if (bi == bj && qr == 0 && qc == 1) return;  // strictly upper quarter of a diagonal block
-    tile64_update(S, ld, kb, bi * CB + qr * 64, bj * CB + qc * 64);
+    if (pi == pj && qr == 0 && qc == 1) return;
+    tile64_update(S, ld, kb, rmap(pi, a0, n1, b0) * CB + qr * 64, rmap(pj, a0, n1, b0) * CB + qc * 64);
 }
 
-static inline int64_t syrk_tiles(int64_t nb, int64_t jlo, int64_t ncol) {
-    int64_t t = 0;
-    for (int64_t j = jlo; j < jlo + ncol; ++j) t += nb - j + 1;
-    return t;
+// panel block rows of step kb (see rmap)
+struct PanelRows {
+    int64_t a0, n1, b0, nr;
+    int64_t tiles(int64_t pj0, int64_t ncol) const {
+        int64_t t = 0;
+        for (int64_t j = pj0; j < pj0 + ncol; ++j) t += nr - j;
+        return t;
+    }
+};
+
+static PanelRows panel_rows(const Ctx& c, int64_t kb) {
+    const int64_t nb = c.L.n_pad / CB;
+    const int64_t T = std::min<int64_t>((6 * (int64_t)c.L.n_img) / CB, nb);  // first dense block row
+    PanelRows r;
+    r.a0 = kb + 1;
+    int64_t lb = kb;
+    if ((int64_t)c.env_first.size() == nb) {
+        for (int64_t i = kb + 1; i < T; ++i)
+            if (c.env_first[i] <= kb) lb = i;
+    } else {
+        lb = std::max<int64_t>(kb, T - 1);
+    }
+    r.n1 = lb - kb;
+    r.b0 = std::max<int64_t>(T, kb + 1);
+    r.nr = r.n1 + (nb - r.b0 + 1);
+    return r;
 }
 
 // ------------------------------------------------------------------------------------------------
 // border combine (inner constraints): RHS rows n_pad + 0 (y) and n_pad + 1..7 (Z), length n
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, int64_t ld, int64_t n_pad) {
-    __shared__ double red[4][35];
-    __shared__ double H[7][8];
-    __shared__ double kk[7];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const double* y = S + n_pad * ld;
-    const double* z = S + (n_pad + 1) * ld;
-    // one pass: h_a = z_a . y (7) and the upper triangle of H = Z'Z (28), all in registers
-    double acc[35];
+// Gram matrix of the 15 forward-solved RHS rows [y | A (7) | B (7)] (row a per workgroup, fixed-order
+// reductions), into scal[32 + 15a + b]
+__global__ __launch_bounds__(256) void k_border_gram(const double* __restrict__ S, int64_t ld, int64_t n_pad,
+                                                     double* __restrict__ scal) {
+    __shared__ double red[4][15];
+    const int a = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const double* ra = S + (n_pad + a) * ld;
+    double acc[15];
 #pragma unroll
-    for (int q = 0; q < 35; ++q) acc[q] = 0.0;
+    for (int b = 0; b < 15; ++b) acc[b] = 0.0;
     for (int64_t i = tid; i < n_pad; i += 256) {
-        double zv[7];
+        const double v = ra[i];
 #pragma unroll
-        for (int m = 0; m < 7; ++m) zv[m] = z[m * ld + i];
-        const double yv = y[i];
-        int q = 7;
-#pragma unroll
-        for (int m = 0; m < 7; ++m) {
-            acc[m] += zv[m] * yv;
-#pragma unroll
-            for (int b = m; b < 7; ++b) acc[q++] += zv[m] * zv[b];
-        }
+        for (int b = 0; b < 15; ++b) acc[b] += v * S[(n_pad + b) * ld + i];
     }
-    // fixed-order reduction: butterfly within each wave, then the four waves in order
 #pragma unroll
-    for (int q = 0; q < 35; ++q) {
-        double v = acc[q];
+    for (int b = 0; b < 15; ++b) {
+        double v = acc[b];
 #pragma unroll
         for (int w = 32; w > 0; w >>= 1) v += __shfl_xor(v, w, 64);
-        acc[q] = v;
+        acc[b] = v;
     }
     if (lane == 0)
 #pragma unroll
-        for (int q = 0; q < 35; ++q) red[wave][q] = acc[q];
+        for (int b = 0; b < 15; ++b) red[wave][b] = acc[b];
     __syncthreads();
-    if (tid < 35) {
-        const double v = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
-        if (tid < 7) {
-            H[tid][0] = v;
-        } else {
-            int q = 7, am = 0, bm = 0;
-            for (int m = 0; m < 7; ++m)
-                for (int b = m; b < 7; ++b, ++q)
-                    if (q == tid) { am = m; bm = b; }
-            H[am][1 + bm] = v;
-            H[bm][1 + am] = v;
+    if (tid < 15) scal[32 + 15 * a + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+}
+
+// Solve [[A'A - I, A'B], [B'A, B'B]] [z; k] = -[A'y; B'y] (14x14, partial pivoting) and form
+// u = y + A z + B k in the RHS row (derivation in fba_kernels.hip, border section)
+__global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, int64_t ld, int64_t n_pad,
+                                                        const double* __restrict__ scal) {
+    __shared__ double coef[14];
+    if (threadIdx.x == 0) {
+        double H[14][15];
+        const double* g = scal + 32;  // g[15a + b], index 0 = y, 1..7 = A, 8..14 = B
+        for (int r = 0; r < 14; ++r) {
+            for (int q = 0; q < 14; ++q) H[r][q] = g[15 * (1 + r) + (1 + q)] - ((r == q && r < 7) ? 1.0 : 0.0);
+            H[r][14] = -g[15 * (1 + r)];
         }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        // solve H[:,1..7] k = -H[:,0]  (SPD 7x7; Gaussian elimination with partial pivoting)
-        double A[7][8];
-        for (int a = 0; a < 7; ++a) {
-            for (int b = 0; b < 7; ++b) A[a][b] = H[a][b + 1];
-            A[a][7] = -H[a][0];
-        }
-        for (int col = 0; col < 7; ++col) {
+        for (int col = 0; col < 14; ++col) {
             int piv = col;
-            for (int r = col + 1; r < 7; ++r)
-                if (fabs(A[r][col]) > fabs(A[piv][col])) piv = r;
+            for (int r = col + 1; r < 14; ++r)
+                if (fabs(H[r][col]) > fabs(H[piv][col])) piv = r;
             if (piv != col)
-                for (int b = 0; b < 8; ++b) {
-                    const double t = A[col][b];
-                    A[col][b] = A[piv][b];
-                    A[piv][b] = t;
+                for (int q = 0; q < 15; ++q) {
+                    const double t = H[col][q];
+                    H[col][q] = H[piv][q];
+                    H[piv][q] = t;
                 }
-            for (int r = col + 1; r < 7; ++r) {
-                const double f = A[r][col] / A[col][col];
-                for (int b = col; b < 8; ++b) A[r][b] -= f * A[col][b];
+            for (int r = col + 1; r < 14; ++r) {
+                const double f = H[r][col] / H[col][col];
+                for (int q = col; q < 15; ++q) H[r][q] -= f * H[col][q];
             }
         }
-        for (int r = 6; r >= 0; --r) {
-            double s = A[r][7];
-            for (int b = r + 1; b < 7; ++b) s -= A[r][b] * kk[b];
-            kk[r] = s / A[r][r];
+        for (int r = 13; r >= 0; --r) {
+            double v = H[r][14];
+            for (int q = r + 1; q < 14; ++q) v -= H[r][q] * coef[q];
+            coef[r] = v / H[r][r];
         }
     }
     __syncthreads();
     double* yw = S + n_pad * ld;
-    for (int64_t i = tid; i < n_pad; i += 256) {
+    for (int64_t i = threadIdx.x; i < n_pad; i += 256) {
         double v = yw[i];
-        for (int m = 0; m < 7; ++m) v += S[(n_pad + 1 + m) * ld + i] * kk[m];
+        for (int m = 0; m < 14; ++m) v += S[(n_pad + 1 + m) * ld + i] * coef[m];
         yw[i] = v;
     }
 }
@@ -823,31 +758,27 @@ __global__ void k_neg_copy(const double* __restrict__ X, double* __restrict__ de
 }
 
 // ------------------------------------------------------------------------------------------------
-// Right-looking with depth-1 lookahead on two streams:
+// Right-looking over the envelope.  While a step's trailing update is large: depth-1 lookahead on
+// two streams,
 //   stream A (critical path): potrf(k) -> trsm(k) -> [wait rest(k-1)] -> col(k) -> potrf(k+1) ...
 //   stream B (bulk):          [wait trsm(k)] -> rest(k)
-// col(k) updates block column k+1 (the next panel), rest(k) the columns >= k+2; so the bulk update
-// rest(k-1) runs concurrently with potrf(k) and trsm(k).
-// The bulk update with its event record (and the kernel probe) on stream st.
-static int bulk_update(Ctx& c, hipStream_t st, int64_t kb, int64_t jlo, int64_t ncol) {
-    const int64_t ld = c.L.ld, nb = c.L.n_pad / CB;
-    // optional whole rounds of 128x128 tiles (bulk_slots resident workgroups), the rest as 64x64
-    // quarters: four short workgroups per tile keep the last round short
-    const int64_t nt = syrk_tiles(nb, jlo, ncol);
-    const int64_t nfull = c.bulk_slots > 0 ? (nt / c.bulk_slots) * c.bulk_slots : 0;
-    if (nfull > 0) k_syrk128<<<(unsigned)nfull, 256, 0, st>>>(c.d_S, ld, kb, nb, jlo, nfull);
-    if (nt > nfull) {
-        const bool pr = c.probe && c.probe_n < (int)c.probe_ev.size() / 2;
-        if (pr) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], st));
-        k_syrk_q64<<<(unsigned)((nt - nfull) * 4), 256, 0, st>>>(c.d_S, ld, kb, nb, jlo, nfull);
-        if (pr) {
-            FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], st));
-            // quarters computed (strictly upper quarters of diagonal blocks skipped) x 2*64*64*128;
-            // the list is column-major with one diagonal tile per column
-            const int64_t ndiag = (nfull == 0) ? ncol : 0;
-            c.probe_flops += (double)(4 * (nt - nfull) - ndiag) * 2.0 * 64 * 64 * CB;
-            ++c.probe_n;
-        }
+// col(k) updates block column k+1 (the next panel), rest(k) the other columns of the step, so the
+// bulk update rest(k-1) runs concurrently with potrf(k) and trsm(k).  Once the trailing update is
+// small (always, for a banded camera system), the cross-stream hand-offs (~10 us each) cost more
+// than the overlap gains and each step is potrf -> trsm -> one update launch on one stream.
+// ------------------------------------------------------------------------------------------------
+// The update of list columns [pj0, pj0 + ncol) of step kb on stream st (with the kernel probe)
+static int bulk_update(Ctx& c, hipStream_t st, int64_t kb, const PanelRows& R, int64_t pj0, int64_t ncol) {
+    const int64_t nt = R.tiles(pj0, ncol);
+    if (nt <= 0) return FBA_OK;
+    const bool pr = c.probe && c.probe_n < (int)c.probe_ev.size() / 2;
+    if (pr) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], st));
+    k_syrk_env<<<(unsigned)(nt * 4), 256, 0, st>>>(c.d_S, c.L.ld, kb, R.a0, R.n1, R.b0, R.nr, pj0, 0);
+    if (pr) {
+        FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], st));
+        // quarters computed (one skipped per diagonal tile, one diagonal tile per column) x 2*64*64*128
+        c.probe_flops += (double)(4 * nt - ncol) * 2.0 * 64 * 64 * CB;
+        ++c.probe_n;
     }
     return FBA_OK;
 }
@@ -857,32 +788,29 @@ int launch_cholesky(Ctx& c) {
     hipStream_t A = c.stream, B = c.stream2;
     bool single = false;
     for (int64_t kb = 0; kb < nb; ++kb) {
+        const PanelRows R = panel_rows(c, kb);
         k_potrf128<<<1, 256, POTRF_LDS, A>>>(c.d_S, ld, kb * CB, c.d_dinv, c.d_scal);
-        // panel rows below the diagonal block, RHS block row included: (nb - kb) * 128 rows
-        k_trsm128<<<(unsigned)((nb - kb) * 2), 256, TRSM_LDS, A>>>(c.d_S, ld, kb * CB, (kb + 1) * CB, c.d_dinv);
-        const int64_t m = nb - kb - 1;  // trailing block columns
-        // once the whole trailing update of a step is small, the cross-stream hand-offs (~10 us each)
-        // cost more than the overlap gains: the rest of the factorisation runs on one stream, one
-        // trailing-update launch per step (next panel column included)
-        if (!single && syrk_tiles(nb, kb + 1, m) <= c.switch_tiles) {
+        // panel rows: nr block rows (RHS block row included) of 2 x 64
+        k_trsm128<<<(unsigned)(R.nr * 2), 256, TRSM_LDS, A>>>(c.d_S, ld, kb * CB, R.a0, R.n1, R.b0, c.d_dinv);
+        const int64_t m = R.nr - 1;  // trailing block columns of the step
+        if (!single && R.tiles(0, m) <= c.switch_tiles) {
             single = true;
             if (kb > 0 && nb - kb > 1) FBA_HIP(hipStreamWaitEvent(A, c.ev_rest[kb - 1], 0));
         }
         if (single) {
-            if (m > 0) bulk_update(c, A, kb, kb + 1, m);
+            bulk_update(c, A, kb, R, 0, m);
             continue;
         }
+        const bool next = m > 0 && rmap(0, R.a0, R.n1, R.b0) == kb + 1;  // block column kb+1 in the list
+        const int64_t p0 = next ? 1 : 0;
         FBA_HIP(hipEventRecord(c.ev_trsm[kb], A));
-        if (m > 1) {
+        if (m > p0) {
             FBA_HIP(hipStreamWaitEvent(B, c.ev_trsm[kb], 0));
-            bulk_update(c, B, kb, kb + 2, m - 1);
-            FBA_HIP(hipEventRecord(c.ev_rest[kb], B));
+            bulk_update(c, B, kb, R, p0, m - p0);
         }
-        if (m > 0) {
-            if (kb > 0 && nb - kb > 1) FBA_HIP(hipStreamWaitEvent(A, c.ev_rest[kb - 1], 0));
-            // block column kb+1: (nb - kb) block rows of 128 (RHS row included) x 2 sub-columns of 64
-            k_syrk_col64<<<(unsigned)((nb - kb) * 4), 256, 0, A>>>(c.d_S, ld, kb);
-        }
+        FBA_HIP(hipEventRecord(c.ev_rest[kb], B));
+        if (kb > 0 && nb - kb > 1) FBA_HIP(hipStreamWaitEvent(A, c.ev_rest[kb - 1], 0));
+        if (next) k_syrk_env<<<(unsigned)(R.nr * 4), 256, 0, A>>>(c.d_S, ld, kb, R.a0, R.n1, R.b0, R.nr, 0, 0);
     }
     FBA_HIP(hipGetLastError());
     return FBA_OK;
@@ -891,7 +819,10 @@ int launch_cholesky(Ctx& c) {
 int launch_backward(Ctx& c) {
     const int64_t ld = c.L.ld, nb = c.L.n_pad / CB;
     const size_t lds_trtri = sizeof(double) * (CB * LDA + 4 * IB * 17);
-    if (c.set.inner_constraints) k_border_combine<<<1, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad);
+    if (c.set.inner_constraints) {
+        k_border_gram<<<15, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_scal);
+        k_border_combine<<<1, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_scal);
+    }
     k_trtri128<<<(unsigned)nb, 256, lds_trtri, c.stream>>>(c.d_S, ld, c.d_dinv, c.d_linv);
     k_bwd_first<<<1, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, nb - 1, c.d_linv, c.d_X);
     for (int64_t kb = nb - 1; kb >= 1; --kb)
@@ -917,18 +848,10 @@ int chol_setup(Ctx& c) {
         FBA_HIP(hipStreamCreateWithPriority(&c.stream2, hipStreamNonBlocking, prio_least));
     else
         FBA_HIP(hipStreamCreateWithFlags(&c.stream2, hipStreamNonBlocking));
-    const char* ce = getenv("FBA_BULK_SLOTS");
-    int dev = 0;
-    FBA_HIP(hipGetDevice(&dev));
-    hipDeviceProp_t prop;
-    FBA_HIP(hipGetDeviceProperties(&prop, dev));
-    // measured (config 4): 64x64 quarter tiles throughout beat whole rounds of 128x128 tiles + a
-    // quarter-tile remainder (4.02 vs 4.10-4.24 ms), so by default no whole rounds are used
-    c.bulk_slots = ce ? atoi(ce) : 0;
     const char* se = getenv("FBA_SWITCH_TILES");
     c.switch_tiles = se ? atoll(se) : 600;  // measured at config 4: 300 -> 3.73 ms, 600 -> 3.70, 1200 -> 3.73
-    if (c.opt.verbose) fprintf(stderr, "[fba] stream priorities least %d greatest %d, bulk mode %d, bulk slots %d\n",
-                           prio_least, prio_greatest, prio_mode, c.bulk_slots);
+    if (c.opt.verbose) fprintf(stderr, "[fba] stream priorities least %d greatest %d, bulk mode %d\n",
+                           prio_least, prio_greatest, prio_mode);
     c.probe_ev.assign(2 * nb, nullptr);
     for (auto& e : c.probe_ev) FBA_HIP(hipEventCreate(&e));
     c.ev_trsm.assign(nb, nullptr);

@@ -30,7 +30,7 @@ struct Layout {
     int64_t u_full = 0;   // u_c + 3*n_tie
     int64_t n_pad = 0;    // u_c rounded up to NB
     int64_t ld = 0;       // leading dimension of the normal matrix (row-major)
-    int nrhs = 1;         // 1 (+7 with inner constraints)
+    int nrhs = 1;         // 1 (+14 with inner constraints: local border + constraint columns)
     int64_t u_ref = 0;    // the reference's u
     int u_img = 0, u_cam = 0;
 };
@@ -43,7 +43,6 @@ struct Ctx {
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;          // bulk trailing updates (Cholesky lookahead)
     int64_t switch_tiles = 600;             // trailing tiles below which the factorisation runs on one stream
-    int bulk_slots = 0;                     // resident k_syrk128 workgroups (whole rounds of the bulk update)
     std::vector<hipEvent_t> ev_trsm, ev_rest;  // per Cholesky step
     bool own_stream = false;
     int device = 0;
@@ -84,6 +83,10 @@ struct Ctx {
     // multi-rank compact reduce buffer: the entries of S that any rank can write (global co-visible
     // image pairs, diagonal blocks, camera rows, RHS row), packed after fba_accumulate
     int64_t n_gpairs = 0, n_red = 0;
+    // camera-side image order (reverse Cuthill-McKee) and the block envelope of the reduced system
+    std::vector<int32_t> img_ord, img_new;  // internal -> EXT row, EXT row -> internal
+    std::vector<int32_t> env_first;         // [n_pad/NB] first nonzero block column of each block row
+    int n_loc = 0;                          // images carrying the (local) inner-constraint border
     int32_t* d_gpairs = nullptr;     // [2*n_gpairs] (e1,e2), e1 > e2, over ALL tie points
     double* d_red = nullptr;         // [n_red]
     int32_t* d_pair_ij = nullptr;    // [2*n_pair_terms] (obs in e1, obs in e2)

@@ -706,59 +706,66 @@ __global__ void k_cam_stage2(const double* __restrict__ slab, double* __restrict
 }
 
 // ------------------------------------------------------------------------------------------------
-// border: M = S + G W G^T with one weight per constraint column, w_m = 1 / sum_i G_im^2 / S_ii
-// (EOP rows).  The constraints G^T delta = 0 are invariant to the column weights; this choice
-// equilibrates the added curvature against S row by row, so the Cholesky of M keeps S's precision
-// (a single trace-based weight put 1e7 x S_ii on the translation rows of cam0 and lost 7 digits).
-// scal layout: [1] Cholesky failure flag, [2] sumabs, [8..14] w_m
+// border (inner constraints, main.m:428-436).  The reference solves [S G; G' 0].  Here
+//   M = S + G_l W_l G_l'   with G_l = the rows of G of the first n_loc images only (local border:
+//                           M stays banded), w_m = 1 / sum_{i in loc} G_im^2 / S_ii (equilibrated)
+// and the exact bordered solution follows from the forward-solved right-hand sides
+//   r | A = G_l W_l^1/2 | B = G D   (D = the same equilibration over all images; B'x = 0 <=> G'x = 0)
+// in k_border_combine.  scal: [1] Cholesky failure flag, [2] sumabs, [8..14] W_l, [16..22] D^2.
 // ------------------------------------------------------------------------------------------------
 __global__ void k_border_weights(const double* __restrict__ S, const double* __restrict__ G,
-                                 double* __restrict__ scal, int64_t ld, int n_img, int ic) {
-    __shared__ double red[7][256];
-    double a[7] = {0, 0, 0, 0, 0, 0, 0};
+                                 double* __restrict__ scal, int64_t ld, int n_img, int n_loc, int ic) {
+    __shared__ double red[14][256];
+    double a[14];
+#pragma unroll
+    for (int m = 0; m < 14; ++m) a[m] = 0.0;
     if (ic) {
         for (int64_t i = threadIdx.x; i < 6 * (int64_t)n_img; i += blockDim.x) {
             const double sii = S[i * ld + i];
             if (!(sii > 0.0)) continue;
             const double* g = G + (i / 6) * 42 + (i % 6) * 7;
-            for (int m = 0; m < 7; ++m) a[m] += g[m] * g[m] / sii;
+            const bool loc = i < 6 * (int64_t)n_loc;
+#pragma unroll
+            for (int m = 0; m < 7; ++m) {
+                const double v = g[m] * g[m] / sii;
+                a[7 + m] += v;
+                if (loc) a[m] += v;
+            }
         }
     }
-    for (int m = 0; m < 7; ++m) red[m][threadIdx.x] = a[m];
+#pragma unroll
+    for (int m = 0; m < 14; ++m) red[m][threadIdx.x] = a[m];
     __syncthreads();
     for (int w = blockDim.x / 2; w > 0; w >>= 1) {
         if (threadIdx.x < w)
-            for (int m = 0; m < 7; ++m) red[m][threadIdx.x] += red[m][threadIdx.x + w];
+            for (int m = 0; m < 14; ++m) red[m][threadIdx.x] += red[m][threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x < 7) scal[8 + threadIdx.x] = red[threadIdx.x][0] > 0.0 ? 1.0 / red[threadIdx.x][0] : 1.0;
+    if (threadIdx.x < 7) {
+        scal[8 + threadIdx.x] = red[threadIdx.x][0] > 0.0 ? 1.0 / red[threadIdx.x][0] : 1.0;
+        scal[16 + threadIdx.x] = red[7 + threadIdx.x][0] > 0.0 ? 1.0 / red[7 + threadIdx.x][0] : 1.0;
+    }
     if (threadIdx.x == 0) scal[1] = 0.0;  // Cholesky failure flag
 }
 
+// M += G_l W_l G_l' on the 6 n_loc x 6 n_loc block (lower part)
 __global__ void k_border(double* __restrict__ S, const double* __restrict__ G, const double* __restrict__ scal,
-                         int64_t ld, int n_img, int ic) {
-    // 2D grid of 64x64 tiles over the EOP rows; lower tiles only
-    const int64_t i = (int64_t)blockIdx.y * 64 + threadIdx.y;
-    const int64_t jb = (int64_t)blockIdx.x * 64;
-    if (blockIdx.x > blockIdx.y) return;
-    const int64_t n = 6 * (int64_t)n_img;
-    if (!ic || i >= n) return;
-    const double* gi = G + (i / 6) * 42 + (i % 6) * 7;
-    double g[7];
-    for (int m = 0; m < 7; ++m) g[m] = gi[m] * scal[8 + m];
-    for (int jj = threadIdx.x; jj < 64; jj += blockDim.x) {
-        const int64_t j = jb + jj;
-        if (j > i || j >= n) continue;
+                         int64_t ld, int n_loc) {
+    const int64_t n = 6 * (int64_t)n_loc;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n * n; q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = q / n, j = q % n;
+        if (j > i) continue;
+        const double* gi = G + (i / 6) * 42 + (i % 6) * 7;
         const double* gj = G + (j / 6) * 42 + (j % 6) * 7;
         double acc = 0.0;
-        for (int m = 0; m < 7; ++m) acc += g[m] * gj[m];
+        for (int m = 0; m < 7; ++m) acc += gi[m] * scal[8 + m] * gj[m];
         S[i * ld + j] += acc;
     }
 }
 
 __global__ void k_finish_rhs(double* __restrict__ S, const double* __restrict__ G, const double* __restrict__ scal,
                              const uint8_t* __restrict__ active, int64_t ld, int64_t n_pad, int64_t u_c, int n_img,
-                             int ic) {
+                             int n_loc, int ic) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_pad) return;
     if (i >= u_c || !active[i]) {
@@ -767,9 +774,11 @@ __global__ void k_finish_rhs(double* __restrict__ S, const double* __restrict__ 
         S[n_pad * ld + i] = 0.0;
     }
     if (ic) {
-        for (int m = 0; m < 7; ++m)
-            S[(n_pad + 1 + m) * ld + i] =
-                (i < 6 * (int64_t)n_img) ? sqrt(scal[8 + m]) * G[(i / 6) * 42 + (i % 6) * 7 + m] : 0.0;
+        const double* g = G + (i / 6) * 42 + (i % 6) * 7;
+        for (int m = 0; m < 7; ++m) {
+            S[(n_pad + 1 + m) * ld + i] = (i < 6 * (int64_t)n_loc) ? sqrt(scal[8 + m]) * g[m] : 0.0;   // A
+            S[(n_pad + 8 + m) * ld + i] = (i < 6 * (int64_t)n_img) ? sqrt(scal[16 + m]) * g[m] : 0.0;  // B
+        }
     }
 }
 
@@ -1047,15 +1056,15 @@ int launch_accumulate(Ctx& c) {
 int launch_border(Ctx& c) {
     const Layout& L = c.L;
     const int ic = c.set.inner_constraints;
-    k_border_weights<<<1, 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, L.ld, L.n_img, ic);
+    k_border_weights<<<1, 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, L.ld, L.n_img, c.n_loc, ic);
     FBA_HIP(hipGetLastError());
-    if (ic) {
-        const int nb = (int)((6 * (int64_t)L.n_img + 63) / 64);
-        k_border<<<dim3(nb, nb), dim3(16, 64), 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, L.ld, L.n_img, ic);
+    if (ic && c.n_loc > 0) {
+        const int64_t n = 6 * (int64_t)c.n_loc;
+        k_border<<<(unsigned)((n * n + 255) / 256), 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, L.ld, c.n_loc);
         FBA_HIP(hipGetLastError());
     }
     k_finish_rhs<<<(unsigned)((L.n_pad + 255) / 256), 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, c.d_active,
-                                                                           L.ld, L.n_pad, L.u_c, L.n_img, ic);
+                                                                           L.ld, L.n_pad, L.u_c, L.n_img, c.n_loc, ic);
     FBA_HIP(hipGetLastError());
     return FBA_OK;
 }
