@@ -145,21 +145,23 @@ def main():
     t, chol_flops, lin_bytes = phase_roofline(ds, ms, args.steps)
 
     # roofline of the dominant kernel, outside the timed region: one more step with HIP events
-    # around every launch of the Cholesky bulk update (k_syrk_q64) on the stream it runs on
+    # around every launch of the Cholesky trailing update (k_syrk_multi, one per elimination-tree
+    # level) on the stream it runs on
     ctx.set_probe(True)
     step()
     pr = ctx.probe_stats()
     ctx.set_probe(False)
     avg_s = pr["ms"] * 1e-3 / max(pr["launches"], 1)
     flops_launch = pr["flops"] / max(pr["launches"], 1)
-    traffic = pmc_traffic(args.config, "k_syrk_q64")
-    roof = {"bound": "mfma", "kernel": "k_syrk_q64 (Cholesky bulk trailing update, 64x64x128 f64 MFMA tiles)",
+    traffic = pmc_traffic(args.config, "k_syrk_multi")
+    roof = {"bound": "mfma", "kernel": "k_syrk_multi (Cholesky trailing update of one tree level, 64x64 f64 MFMA "
+                                       "tiles, K = 128 per source column)",
             "achieved": flops_launch / avg_s / 1e12 if avg_s > 0 else None, "peak": FP64_PEAK_TFLOPS,
             "unit": "TFLOP/s", "launches": pr["launches"], "avg_launch_us": avg_s * 1e6,
             "flops_per_launch": flops_launch,
             "traffic": traffic}
     roof["frac"] = roof["achieved"] / roof["peak"] if roof["achieved"] else None
-    phase_roof = {"cholesky_TFLOPs": chol_flops / (t["cholesky"] * 1e-3) / 1e12,
+    phase_roof = {"cholesky_dense_equiv_TFLOPs": chol_flops / (t["cholesky"] * 1e-3) / 1e12,
                   "linearize_accumulate_GBs": lin_bytes / ((t["linearize"] + t["accumulate"]) * 1e-3) / 1e9}
     value = args.steps / dt
     out = {

@@ -54,8 +54,10 @@ static int check_settings(const fba_settings* s) {
     return FBA_OK;
 }
 
-static void compute_layout(const fba_problem* p, const fba_settings* s, Layout& L) {
-    L.n_img = p->n_img;
+// n_slots: internal image slots (the EXT images in camera order plus padding slots, fba_order.cpp)
+static void compute_layout(const fba_problem* p, const fba_settings* s, Layout& L, int n_slots) {
+    L.n_img = n_slots;
+    L.n_img_ref = p->n_img;
     L.n_cam = p->n_cam;
     L.n_tie = p->n_tie;
     L.nk = s->num_radial;
@@ -67,15 +69,17 @@ static void compute_layout(const fba_problem* p, const fba_settings* s, Layout& 
     L.nrhs = s->inner_constraints ? 15 : 1;
     L.u_img = s->est_Xc + s->est_Yc + s->est_Zc + s->est_omega + s->est_phi + s->est_kappa;
     L.u_cam = s->est_c + s->est_xp + s->est_yp + s->est_radial * s->num_radial + s->est_decent * 2;
-    L.u_ref = (int64_t)L.u_img * L.n_img + (int64_t)L.u_cam * L.n_cam + 3 * (int64_t)L.n_tie;
+    L.u_ref = (int64_t)L.u_img * L.n_img_ref + (int64_t)L.u_cam * L.n_cam + 3 * (int64_t)L.n_tie;
 }
 
-// full (internal) index -> the reference's xhat index.  Internal image e is EXT row img_ord[e].
+// full (internal) index -> the reference's xhat index.  Internal image slot e is EXT row img_ord[e]
+// (-1: a padding slot, no reference unknowns).
 static void full_to_ref_map(const fba_settings* s, const Layout& L, const std::vector<int32_t>& img_ord,
                             std::vector<int64_t>& map) {
     map.assign(L.u_full, -1);
     const int ee[6] = {s->est_Xc, s->est_Yc, s->est_Zc, s->est_omega, s->est_phi, s->est_kappa};
     for (int e = 0; e < L.n_img; ++e) {
+        if (img_ord[e] < 0) continue;
         int cnt = 0;
         for (int a = 0; a < 6; ++a)
             if (ee[a]) map[6 * (int64_t)e + a] = (int64_t)img_ord[e] * L.u_img + cnt++;
@@ -89,9 +93,9 @@ static void full_to_ref_map(const fba_settings* s, const Layout& L, const std::v
     for (int k = 0; k < L.n_cam; ++k) {
         int cnt = 0;
         for (int c = 0; c < L.cw; ++c)
-            if (ce[c]) map[6 * (int64_t)L.n_img + (int64_t)k * L.cw + c] = (int64_t)L.u_img * L.n_img + (int64_t)k * L.u_cam + cnt++;
+            if (ce[c]) map[6 * (int64_t)L.n_img + (int64_t)k * L.cw + c] = (int64_t)L.u_img * L.n_img_ref + (int64_t)k * L.u_cam + cnt++;
     }
-    const int64_t tb = (int64_t)L.u_img * L.n_img + (int64_t)L.u_cam * L.n_cam;
+    const int64_t tb = (int64_t)L.u_img * L.n_img_ref + (int64_t)L.u_cam * L.n_cam;
     for (int64_t t = 0; t < 3 * (int64_t)L.n_tie; ++t) map[L.u_c + t] = tb + t;
 }
 
@@ -163,92 +167,16 @@ static void destroy(Ctx* c) {
                     c->d_img_start, c->d_img_obs, c->d_cam_lp, c->d_cam_ctl, c->d_pair_e, c->d_pair_start, c->d_gpairs, c->d_red,
                     c->d_pair_ij, c->d_xfull, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
                     c->d_pt_tab, c->d_slab, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
-                    c->d_active, c->d_counted, c->d_obs_pho};
+                    c->d_active, c->d_counted, c->d_obs_pho, c->d_sched};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
-    for (auto e : c->ev_trsm)
-        if (e) (void)hipEventDestroy(e);
     for (auto e : c->probe_ev)
         if (e) (void)hipEventDestroy(e);
-    for (auto e : c->ev_rest)
-        if (e) (void)hipEventDestroy(e);
-    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
-}
-
-// Reverse Cuthill-McKee order of the images on their co-visibility graph (images sharing a tie point),
-// over ALL tie points so that every rank derives the same order.  Returns ord[new] = old.
-static std::vector<int32_t> image_order(const fba_problem* p) {
-    const int n = p->n_img;
-    std::vector<std::pair<int32_t, int32_t>> ti;  // (tie, image)
-    for (int64_t i = 0; i < p->n_pts; ++i)
-        if (p->tie[i] >= 0) ti.emplace_back(p->tie[i], p->img[i]);
-    std::sort(ti.begin(), ti.end());
-    std::vector<std::pair<int32_t, int32_t>> edges;
-    for (size_t a = 0; a < ti.size();) {
-        size_t b = a;
-        while (b < ti.size() && ti[b].first == ti[a].first) ++b;
-        for (size_t x = a; x < b; ++x)
-            for (size_t y = a; y < b; ++y)
-                if (ti[x].second != ti[y].second) edges.emplace_back(ti[x].second, ti[y].second);
-        a = b;
-    }
-    std::sort(edges.begin(), edges.end());
-    edges.erase(std::unique(edges.begin(), edges.end()), edges.end());
-    std::vector<int32_t> start(n + 1, 0), adj(edges.size());
-    for (auto& e : edges) start[e.first + 1]++;
-    for (int v = 0; v < n; ++v) start[v + 1] += start[v];
-    for (size_t q = 0; q < edges.size(); ++q) adj[q] = edges[q].second;
-    auto deg = [&](int v) { return start[v + 1] - start[v]; };
-    std::vector<int32_t> order;
-    order.reserve(n);
-    std::vector<char> seen(n, 0);
-    for (;;) {
-        int root = -1;  // unvisited image of minimum degree (lowest index on ties)
-        for (int v = 0; v < n; ++v)
-            if (!seen[v] && (root < 0 || deg(v) < deg(root))) root = v;
-        if (root < 0) break;
-        size_t head = order.size();
-        order.push_back(root);
-        seen[root] = 1;
-        while (head < order.size()) {
-            const int v = order[head++];
-            std::vector<int32_t> nb(adj.begin() + start[v], adj.begin() + start[v + 1]);
-            std::stable_sort(nb.begin(), nb.end(), [&](int32_t a, int32_t b) { return deg(a) < deg(b); });
-            for (int32_t w : nb)
-                if (!seen[w]) { seen[w] = 1; order.push_back(w); }
-        }
-    }
-    std::reverse(order.begin(), order.end());
-    return order;
-}
-
-// Envelope of the reduced system by 128-row block: first[i] = first nonzero block column of block row
-// i (image-image blocks of co-visible pairs, the local border block, the dense camera rows).
-static void block_envelope(const Layout& L, const std::vector<std::pair<int32_t, int32_t>>& pairs_new, int n_loc,
-                           std::vector<int32_t>& first) {
-    const int64_t nb = L.n_pad / NB;
-    first.assign(nb, 0);
-    for (int64_t i = 0; i < nb; ++i) first[i] = (int32_t)i;
-    // an image's 6 rows may straddle two blocks: its rows reach back to the first block of the
-    // other image (and of itself)
-    auto touch = [&](int64_t e1, int64_t e2) {
-        const int64_t bj = 6 * e2 / NB;
-        for (int64_t bi = 6 * e1 / NB; bi <= (6 * e1 + 5) / NB && bi < nb; ++bi)
-            first[bi] = std::min<int32_t>(first[bi], (int32_t)bj);
-    };
-    for (auto& q : pairs_new) touch(q.first, q.second);  // (e1, e2), e1 > e2
-    for (int64_t e = 0; e < L.n_img; ++e) touch(e, e);
-    if (n_loc > 0) {
-        const int64_t bl = (6 * (int64_t)n_loc - 1) / NB;
-        for (int64_t i = 0; i <= bl; ++i) first[i] = 0;
-    }
-    // block rows holding camera rows (and everything after) are dense
-    for (int64_t i = (6 * (int64_t)L.n_img) / NB; i < nb; ++i) first[i] = 0;
 }
 
 static int create(const fba_problem* p, const fba_settings* s, const fba_options* o, Ctx** out) {
@@ -267,11 +195,12 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     c->opt = opt;
     c->n_pts = p->n_pts;
     Layout& L = c->L;
-    compute_layout(p, s, L);
-    // camera-side order of the images: reverse Cuthill-McKee, so the reduced system is banded
-    c->img_ord = image_order(p);
-    c->img_new.assign(L.n_img, 0);
-    for (int e = 0; e < L.n_img; ++e) c->img_new[c->img_ord[e]] = e;
+    // camera-side order of the images: nested dissection with padding slots (fba_order.cpp)
+    c->img_ord = camera_order(p);
+    compute_layout(p, s, L, (int)c->img_ord.size());
+    c->img_new.assign(L.n_img_ref, 0);
+    for (int e = 0; e < L.n_img; ++e)
+        if (c->img_ord[e] >= 0) c->img_new[c->img_ord[e]] = e;
     full_to_ref_map(s, L, c->img_ord, c->full_to_ref);
 
     FBA_HIP(hipSetDevice(opt.device));
@@ -286,7 +215,8 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     // initial full-space parameters
     c->xfull0.assign(L.u_full, 0.0);
     for (int e = 0; e < L.n_img; ++e)
-        for (int a = 0; a < 6; ++a) c->xfull0[6 * (int64_t)e + a] = p->eop0[6 * (int64_t)c->img_ord[e] + a];
+        if (c->img_ord[e] >= 0)
+            for (int a = 0; a < 6; ++a) c->xfull0[6 * (int64_t)e + a] = p->eop0[6 * (int64_t)c->img_ord[e] + a];
     for (int64_t i = 0; i < (int64_t)L.cw * L.n_cam; ++i) c->xfull0[6 * (int64_t)L.n_img + i] = p->iop0[i];
     for (int64_t i = 0; i < 3 * (int64_t)L.n_tie; ++i) c->xfull0[L.u_c + i] = p->tie0[i];
 
@@ -477,10 +407,10 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         }
         std::sort(gp.begin(), gp.end());
         gp.erase(std::unique(gp.begin(), gp.end()), gp.end());
-        // inner constraints: the border is applied on the first n_loc images only (local border,
-        // DESIGN.md section 2), so M keeps the band structure
+        // inner constraints: the border is applied on the first n_loc image slots only (local
+        // border), so M keeps the sparsity of S
         c->n_loc = s->inner_constraints ? std::min<int>(L.n_img, (int)(NB / 6)) : 0;
-        block_envelope(L, gp, c->n_loc, c->env_first);
+        build_schedule(*c, gp);
         if (opt.world > 1) {
             for (auto& q : gp) { gpairs.push_back(q.first); gpairs.push_back(q.second); }
             c->n_gpairs = (int64_t)gp.size();
@@ -516,6 +446,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         (rc = upload(&c->d_caminfo, caminfo)) || (rc = upload(&c->d_active, active)) ||
         (rc = upload(&c->d_counted, counted)) || (rc = upload(&c->d_obs_pho, pho)) ||
         (rc = upload(&c->d_chunk_obs, chunk_obs)) || (rc = upload(&c->d_chunk_pt, chunk_pt)) ||
+        (rc = upload(&c->d_sched, c->sched.buf)) ||
         (opt.world > 1 && ((rc = upload(&c->d_gpairs, gpairs)) || (rc = dalloc(&c->d_red, (size_t)c->n_red))))) {
         destroy(c);
         return rc;
@@ -633,10 +564,6 @@ int fba_abi_version(void) { return FBA_ABI_VERSION; }
 
 int fba_count_unknowns(const fba_problem* p, const fba_settings* s, int64_t* u_out) {
     if (!p || !s || !u_out) { set_error("NULL argument"); return FBA_ERR_ARG; }
-    Layout L;
-    fba_settings s2 = *s;
-    if (s2.num_radial < 1) s2.num_radial = 1;
-    compute_layout(p, &s2, L);
     *u_out = (int64_t)(s->est_Xc + s->est_Yc + s->est_Zc + s->est_omega + s->est_phi + s->est_kappa) * p->n_img +
              (int64_t)(s->est_c + s->est_xp + s->est_yp + s->est_radial * s->num_radial + s->est_decent * 2) * p->n_cam +
              3 * (int64_t)p->n_tie;
@@ -720,6 +647,7 @@ int fba_build_awg(fba_ctx* ctx, const double* xhat, double* A, double* w, double
         for (int e = 0; e < L.n_img; ++e)
             for (int a = 0; a < 6; ++a) {
                 const int64_t r = c->full_to_ref[6 * (int64_t)e + a];
+                if (r < 0) continue;  // padding slot
                 for (int m = 0; m < 7; ++m) G[r + m * u] = g[(size_t)e * 42 + a * 7 + m];
             }
     }
@@ -874,7 +802,6 @@ int fba_probe_stats(fba_ctx* ctx, double* out) {
     Ctx* c = reinterpret_cast<Ctx*>(ctx);
     if (!c || !out) { set_error("NULL argument"); return FBA_ERR_ARG; }
     FBA_HIP(hipStreamSynchronize(c->stream));
-    FBA_HIP(hipStreamSynchronize(c->stream2));
     double ms = 0.0;
     for (int i = 0; i < c->probe_n; ++i) {
         float t = 0.f;

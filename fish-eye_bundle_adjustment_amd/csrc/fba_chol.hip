@@ -1,34 +1,35 @@
-// fba_chol.hip -- fp64 envelope Cholesky of the reduced camera system on gfx950 (MI355X).
+// fba_chol.hip -- fp64 sparse (block) Cholesky of the reduced camera system on gfx950 (MI355X).
 //
 // The reference inverts the bordered normal matrix explicitly, Cx = [N G; G' 0]^-1
 // (main.m:428-440).  Here the tie points have already been eliminated (Schur complement), the
-// images are in reverse Cuthill-McKee order (fba_capi.cpp image_order), so the image-image part of
-// the reduced system S is banded, and the border is folded in LOCALLY as M = S + A A' with A =
-// G_l W^1/2 restricted to the first n_loc images (SPD whenever the bordered matrix is nonsingular
-// and those images fix the datum; W = one equilibrating weight per constraint column,
-// fba_kernels.hip k_border_weights) -- so M keeps the band, and
+// images are in nested-dissection order (fba_order.cpp), so the image-image part of the reduced
+// system S is block sparse, and the border is folded in LOCALLY as M = S + A A' with A = G_l W^1/2
+// restricted to the first n_loc image slots (SPD whenever the bordered matrix is nonsingular and
+// those images fix the datum; W = one equilibrating weight per constraint column, fba_kernels.hip
+// k_border_weights) -- so M keeps the sparsity of S, and
 //
-//   M = L L'        right-looking blocked Cholesky over the block envelope, NB = 128:
-//     k_potrf128    the 128x128 diagonal block, LDS-resident in one workgroup: 8 sub-panels of 16
-//                   (16x16 factor in registers with DPP broadcasts, its 16x16 inverse, then the
-//                   in-block panel solve and trailing update on v_mfma_f64_16x16x4_f64); writes
-//                   L_kk and the eight 16x16 inverses D_s = L_ss^-1 used by the solves below
-//     k_trsm128     the panel rows of the envelope, X = A L_kk^-T by blocked substitution
+//   M = L L'        right-looking block Cholesky, NB = 128, one batched step per level of the
+//                   elimination tree (the columns of a level are independent):
+//     k_potrf128    the level's 128x128 diagonal blocks, one LDS-resident workgroup each: 8
+//                   sub-panels of 16 (16x16 factor in registers with DPP broadcasts, its 16x16
+//                   inverse, then the in-block panel solve and trailing update on
+//                   v_mfma_f64_16x16x4_f64); writes L_kk and the eight 16x16 inverses D_s = L_ss^-1
+//     k_trsm128     the panel blocks of those columns, X = A L_kk^-T by blocked substitution
 //                   X_s = (A_s - sum_{t<s} X_t L_st^T) D_s^T: all MFMA, 16 rows per wave
-//     k_syrk_env    trailing update C -= X_i X_j^T over the envelope, 64x64 tiles, K = 128 staged
-//                   through LDS in 32-deep slices, v_mfma_f64_16x16x4_f64
+//     k_syrk_multi  the trailing updates of the level, C -= sum_k X_ik X_jk^T, 64x64 tiles, K = 128
+//                   per source column staged through LDS in 32-deep slices
 //   forward solve   the right-hand sides [r | A | B] (B = G D, D an equilibration over all images)
-//                   are stored as extra ROWS below M (one extra block row), so the panel solves
-//                   compute Y' = (L^-1 [r A B])' as a by-product
+//                   are stored as extra ROWS below M (one extra block row, in every panel), so the
+//                   panel solves compute Y' = (L^-1 [r A B])' as a by-product
 //   border combine  the 14x14 system of k_border_combine restores the exact bordered solution:
 //                   u = y + A~ z + B~ k with z = A~'u and B~'u = 0
 //   backward solve  L' x = u with the 128x128 diagonal-block inverses (k_trtri128, all blocks in
-//                   parallel), then one short launch per block row (k_bwd_step: two 128x128 GEMVs
-//                   on the critical workgroup)
+//                   parallel), then one launch per level, top down (k_bwd_wave)
 // so delta_c = -x satisfies [S G; G' 0][delta; lambda] = [-r; 0] as the reference's bordered
 // system does.
 #include "fba_internal.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -56,10 +57,6 @@ __device__ __forceinline__ double rsqrt_d(double d) {
 
 __device__ __forceinline__ dbl4 mfma(double a, double b, dbl4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-}
-
-__host__ __device__ __forceinline__ int64_t rmap(int64_t x, int64_t a0, int64_t n1, int64_t b0) {
-    return x < n1 ? a0 + x : b0 + (x - n1);
 }
 
 template <int L>
@@ -173,8 +170,9 @@ __device__ __forceinline__ bool leaf_factor(double (&a)[IB], double (&x)[IB], in
 constexpr int POTRF_NT = (CB / IB) * (CB / IB + 1) / 2;  // 36 lower tiles
 constexpr size_t POTRF_LDS = sizeof(double) * (POTRF_NT + 1) * IB * 17;
 
-__global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_t ld, int64_t k0,
+__global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ cols,
                                                   double* __restrict__ dinv, double* __restrict__ scal) {
+    const int64_t k0 = (int64_t)cols[blockIdx.x] * CB;  // one diagonal block per workgroup (one level)
     extern __shared__ __attribute__((aligned(16))) double smem[];
     // lower-triangle tiles only (80 KB, so the kernel fits beside a bulk-update workgroup on a CU):
     // element (r, c), r/16 >= c/16, at tile (r/16)(r/16+1)/2 + c/16, row r%16 (stride 17), col c%16
@@ -333,7 +331,7 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
 
 
 // ------------------------------------------------------------------------------------------------
-// k_trsm128: rows [row0, row0 + 64*gridDim.x) of the panel at columns [k0, k0+128):
+// k_trsm128: one (column k, block row r) task per 2 workgroups, r in the panel rows of column k:
 //   X = A L^-T by blocked substitution, X_s = (A_s - sum_{t<s} X_t L_st^T) D_s^T.
 // 256 threads = 4 waves x 16 rows.  L_kk was just written by another CU, so its reads are far-cache
 // latency bound: the whole workgroup stages the 28 off-diagonal 16x16 tiles of L_kk and the eight
@@ -343,8 +341,8 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
 constexpr int TRSM_NT = (CB / IB) * (CB / IB - 1) / 2;  // 28 off-diagonal tiles
 constexpr size_t TRSM_LDS = sizeof(double) * (4 * IB * LDA + 4 * IB * 17 + (TRSM_NT + CB / IB) * IB * 17);
 
-__global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t ld, int64_t k0, int64_t a0,
-                                                 int64_t n1, int64_t b0, const double* __restrict__ dinv) {
+__global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ tasks,
+                                                 const double* __restrict__ dinv) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* X = smem;                       // [4][IB][LDA]   panel rows of each wave
     double* T = X + 4 * IB * LDA;           // [4][IB][17]    per-wave 16x16 staging
@@ -352,7 +350,9 @@ __global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t
     double* Dt = Lt + TRSM_NT * IB * 17;    // [8][IB][17]    D_s
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int lr = lane & 15, lk = lane >> 4;
-    const int64_t rbase = rmap(blockIdx.x >> 1, a0, n1, b0) * CB + (blockIdx.x & 1) * 64 + wave * IB;
+    // task (column k, block row r): 2 workgroups of 64 rows each
+    const int64_t k0 = (int64_t)tasks[2 * (blockIdx.x >> 1)] * CB;
+    const int64_t rbase = (int64_t)tasks[2 * (blockIdx.x >> 1) + 1] * CB + (blockIdx.x & 1) * 64 + wave * IB;
     double* Xw = X + wave * IB * LDA;
     double* Tw = T + wave * IB * 17;
     const double* L = S + k0 * ld + k0;
@@ -443,24 +443,29 @@ __global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t
 }
 
 // ------------------------------------------------------------------------------------------------
-// Trailing updates, 64x64 output tiles, K = 128 staged through LDS in 32-deep slices.
-// Envelope: at step kb the panel rows are the block rows R_kb = {a0 .. a0+n1-1} u {b0 .. nb} (the
-// image block rows whose envelope reaches column kb, then the dense camera rows and the RHS block
-// row nb); rmap(x) is the x-th block of that list.  Blocks outside the envelope are zero and stay
-// zero (no fill outside the profile), so they are never touched.
+// k_syrk_multi: the trailing updates of one level, C(i,j) -= sum_k X_ik X_jk^T over the level's
+// columns k whose panel holds both block rows i and j (ascending k, in one workgroup: the result does
+// not depend on the schedule).  64x64 output quarters (4 workgroups per 128x128 target, the
+// strictly upper quarter of a diagonal target skipped), K = 128 per source column staged through LDS
+// in 32-deep slices, the next slice prefetched into registers while the MFMAs of the current one run.
 // ------------------------------------------------------------------------------------------------
 constexpr int KS = 32;
 constexpr int LDK = 34;   // LDS stride of a 32-deep slice: bank = (4r + 2k) mod 64, conflict-free
 
-// C(r0.., c0..) -= X_r X_c^T for one 64x64 tile, K = 128 (the panel at columns k0.. = kb*128):
-// 4 waves of 32x32 (2x2 MFMA tiles), K staged through LDS in 32-deep slices.
-__device__ __forceinline__ void tile64_update(double* __restrict__ S, int64_t ld, int64_t kb, int64_t r0, int64_t c0) {
+__global__ __launch_bounds__(256) void k_syrk_multi(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ tiles,
+                                                    const int32_t* __restrict__ src_start,
+                                                    const int32_t* __restrict__ src) {
     __shared__ __attribute__((aligned(16))) double As[64][LDK];
     __shared__ __attribute__((aligned(16))) double Bs[64][LDK];
+    const int t = blockIdx.x >> 2, qr = (blockIdx.x >> 1) & 1, qc = blockIdx.x & 1;
+    const int64_t bi = tiles[2 * t], bj = tiles[2 * t + 1];
+    if (bi == bj && qr == 0 && qc == 1) return;
+    const int s0 = src_start[t], nsl = 4 * (src_start[t + 1] - s0);
+    const int32_t* ks_src = src + s0;
+    const int64_t r0 = bi * CB + qr * 64, c0 = bj * CB + qc * 64;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int lr = lane & 15, lk = lane >> 4;
     const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
-    const int64_t k0 = kb * CB;
     double* Cp = S + (r0 + wr + lk) * ld + c0 + wc + lr;
     dbl4 acc[2][2];
 #pragma unroll
@@ -470,15 +475,18 @@ __device__ __forceinline__ void tile64_update(double* __restrict__ S, int64_t ld
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[a][b][r] = Cp[(a * 16 + 4 * r) * ld + b * 16];
     const int rr = tid >> 2, cc = (tid & 3) * 8;
-    const double* ga = S + (r0 + rr) * ld + k0 + cc;
-    const double* gb = S + (c0 + rr) * ld + k0 + cc;
+    const double* ga = S + (r0 + rr) * ld + cc;
+    const double* gb = S + (c0 + rr) * ld + cc;
     double2 pa[4], pb[4];
+    {
+        const int64_t kc = (int64_t)ks_src[0] * CB;
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
-        pa[h] = *reinterpret_cast<const double2*>(ga + 2 * h);
-        pb[h] = *reinterpret_cast<const double2*>(gb + 2 * h);
+        for (int h = 0; h < 4; ++h) {
+            pa[h] = *reinterpret_cast<const double2*>(ga + kc + 2 * h);
+            pb[h] = *reinterpret_cast<const double2*>(gb + kc + 2 * h);
+        }
     }
-    for (int ks = 0; ks < CB; ks += KS) {
+    for (int sl = 0; sl < nsl; ++sl) {
         __syncthreads();
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
@@ -486,20 +494,21 @@ __device__ __forceinline__ void tile64_update(double* __restrict__ S, int64_t ld
             Bs[rr][cc + 2 * h] = pb[h].x; Bs[rr][cc + 2 * h + 1] = pb[h].y;
         }
         __syncthreads();
-        if (ks + KS < CB) {
+        if (sl + 1 < nsl) {
+            const int64_t kc = (int64_t)ks_src[(sl + 1) >> 2] * CB + ((sl + 1) & 3) * KS;
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
-                pa[h] = *reinterpret_cast<const double2*>(ga + ks + KS + 2 * h);
-                pb[h] = *reinterpret_cast<const double2*>(gb + ks + KS + 2 * h);
+                pa[h] = *reinterpret_cast<const double2*>(ga + kc + 2 * h);
+                pb[h] = *reinterpret_cast<const double2*>(gb + kc + 2 * h);
             }
         }
 #pragma unroll
         for (int kk = 0; kk < KS; kk += 4) {
             double av[2], bv[2];
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                av[t] = -As[wr + t * 16 + lr][kk + lk];
-                bv[t] = Bs[wc + t * 16 + lr][kk + lk];
+            for (int q = 0; q < 2; ++q) {
+                av[q] = -As[wr + q * 16 + lr][kk + lk];
+                bv[q] = Bs[wc + q * 16 + lr][kk + lk];
             }
 #pragma unroll
             for (int a = 0; a < 2; ++a)
@@ -513,52 +522,6 @@ __device__ __forceinline__ void tile64_update(double* __restrict__ S, int64_t ld
         for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) Cp[(a * 16 + 4 * r) * ld + b * 16] = acc[a][b][r];
-}
-
-
-// k_syrk_env: tiles [tile0, tile0 + gridDim.x/4) of the step's list, as 64x64 quarters: block
-// columns by list position pj = pj0, pj0+1, ..., rows by position pi in [pj, nr) (column-major;
-// the strictly upper quarter of a diagonal block is skipped)
-__global__ __launch_bounds__(256) void k_syrk_env(double* __restrict__ S, int64_t ld, int64_t kb, int64_t a0,
-                                                  int64_t n1, int64_t b0, int64_t nr, int64_t pj0, int64_t tile0) {
-    int64_t q = tile0 + blockIdx.x / 4, pj = pj0, pi = 0;
-    for (;;) {
-        const int64_t cnt = nr - pj;
-        if (q < cnt) { pi = pj + q; break; }
-        q -= cnt;
-        ++pj;
-    }
-    const int qr = (blockIdx.x >> 1) & 1, qc = blockIdx.x & 1;
-    if (pi == pj && qr == 0 && qc == 1) return;
-    tile64_update(S, ld, kb, rmap(pi, a0, n1, b0) * CB + qr * 64, rmap(pj, a0, n1, b0) * CB + qc * 64);
-}
-
-// panel block rows of step kb (see rmap)
-struct PanelRows {
-    int64_t a0, n1, b0, nr;
-    int64_t tiles(int64_t pj0, int64_t ncol) const {
-        int64_t t = 0;
-        for (int64_t j = pj0; j < pj0 + ncol; ++j) t += nr - j;
-        return t;
-    }
-};
-
-static PanelRows panel_rows(const Ctx& c, int64_t kb) {
-    const int64_t nb = c.L.n_pad / CB;
-    const int64_t T = std::min<int64_t>((6 * (int64_t)c.L.n_img) / CB, nb);  // first dense block row
-    PanelRows r;
-    r.a0 = kb + 1;
-    int64_t lb = kb;
-    if ((int64_t)c.env_first.size() == nb) {
-        for (int64_t i = kb + 1; i < T; ++i)
-            if (c.env_first[i] <= kb) lb = i;
-    } else {
-        lb = std::max<int64_t>(kb, T - 1);
-    }
-    r.n1 = lb - kb;
-    r.b0 = std::max<int64_t>(T, kb + 1);
-    r.nr = r.n1 + (nb - r.b0 + 1);
-    return r;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -719,37 +682,41 @@ __device__ __forceinline__ double gemv_t128(const double* __restrict__ M, int64_
     return s;  // valid for every thread (column c = tid & 127)
 }
 
-__global__ __launch_bounds__(256) void k_bwd_first(const double* __restrict__ S, int64_t ld, int64_t n_pad, int64_t kb,
-                                                   const double* __restrict__ linv, double* __restrict__ X) {
+// k_bwd_wave: one level of the backward solve (levels run top down).  Workgroup b < nsrc: column
+// i = srcs[b] of the level, x_i = Linv_i' y_i (y_i is final: its contributions came from higher
+// levels).  Workgroup nsrc + t: target column j = tgts[t], y_j -= sum_i L(i,j)' x_i over its sources
+// (ascending; x_i recomputed locally from y_i, one 128x128 GEMV, instead of a second launch).
+__global__ __launch_bounds__(256) void k_bwd_wave(double* __restrict__ S, int64_t ld, int64_t n_pad,
+                                                  const double* __restrict__ linv, double* __restrict__ X,
+                                                  const int32_t* __restrict__ srcs, int nsrc,
+                                                  const int32_t* __restrict__ tgts, const int32_t* __restrict__ tstart,
+                                                  const int32_t* __restrict__ tsrc) {
     __shared__ double ys[CB];
-    __shared__ double red[512];
-    const int tid = threadIdx.x;
-    if (tid < CB) ys[tid] = S[n_pad * ld + kb * CB + tid];
-    __syncthreads();
-    const double x = gemv_t128(linv + kb * CB * CB, CB, ys, tid, red);
-    if (tid < CB) X[kb * CB + tid] = x;
-}
-
-__global__ __launch_bounds__(256) void k_bwd_step(double* __restrict__ S, int64_t ld, int64_t n_pad, int64_t kb,
-                                                  const double* __restrict__ linv, double* __restrict__ X) {
     __shared__ double xs[CB];
-    __shared__ double ys[CB];
     __shared__ double red[512];
     const int tid = threadIdx.x;
-    const int64_t k0 = kb * CB;
     double* y = S + n_pad * ld;
-    if (tid < CB) xs[tid] = X[k0 + tid];
-    __syncthreads();
-    const int64_t j = blockIdx.x == 0 ? kb - 1 : (int64_t)blockIdx.x - 1;
-    const double u = gemv_t128(S + k0 * ld + j * CB, ld, xs, tid, red);
-    if (blockIdx.x != 0) {
-        if (tid < CB) y[j * CB + tid] -= u;
+    if ((int)blockIdx.x < nsrc) {
+        const int64_t i = srcs[blockIdx.x];
+        if (tid < CB) ys[tid] = y[i * CB + tid];
+        __syncthreads();
+        const double x = gemv_t128(linv + i * CB * CB, CB, ys, tid, red);
+        if (tid < CB) X[i * CB + tid] = x;
         return;
     }
-    if (tid < CB) ys[tid] = y[j * CB + tid] - u;
-    __syncthreads();
-    const double x = gemv_t128(linv + j * CB * CB, CB, ys, tid, red);
-    if (tid < CB) X[j * CB + tid] = x;
+    const int t = blockIdx.x - nsrc;
+    const int64_t j = tgts[t];
+    double acc = 0.0;
+    for (int q = tstart[t]; q < tstart[t + 1]; ++q) {
+        const int64_t i = tsrc[q];
+        if (tid < CB) ys[tid] = y[i * CB + tid];
+        __syncthreads();
+        const double x = gemv_t128(linv + i * CB * CB, CB, ys, tid, red);
+        if (tid < CB) xs[tid] = x;
+        __syncthreads();
+        acc += gemv_t128(S + i * CB * ld + j * CB, ld, xs, tid, red);
+    }
+    if (tid < CB) y[j * CB + tid] -= acc;
 }
 
 __global__ void k_neg_copy(const double* __restrict__ X, double* __restrict__ delta, int64_t u_c) {
@@ -758,59 +725,27 @@ __global__ void k_neg_copy(const double* __restrict__ X, double* __restrict__ de
 }
 
 // ------------------------------------------------------------------------------------------------
-// Right-looking over the envelope.  While a step's trailing update is large: depth-1 lookahead on
-// two streams,
-//   stream A (critical path): potrf(k) -> trsm(k) -> [wait rest(k-1)] -> col(k) -> potrf(k+1) ...
-//   stream B (bulk):          [wait trsm(k)] -> rest(k)
-// col(k) updates block column k+1 (the next panel), rest(k) the other columns of the step, so the
-// bulk update rest(k-1) runs concurrently with potrf(k) and trsm(k).  Once the trailing update is
-// small (always, for a banded camera system), the cross-stream hand-offs (~10 us each) cost more
-// than the overlap gains and each step is potrf -> trsm -> one update launch on one stream.
+// One batched step per elimination-tree level (fba_order.cpp): potrf of the level's diagonal blocks,
+// the panel solves of their columns (RHS block row included: the forward solve), the trailing
+// updates they cause.  Three launches per level on one stream.
 // ------------------------------------------------------------------------------------------------
-// The update of list columns [pj0, pj0 + ncol) of step kb on stream st (with the kernel probe)
-static int bulk_update(Ctx& c, hipStream_t st, int64_t kb, const PanelRows& R, int64_t pj0, int64_t ncol) {
-    const int64_t nt = R.tiles(pj0, ncol);
-    if (nt <= 0) return FBA_OK;
-    const bool pr = c.probe && c.probe_n < (int)c.probe_ev.size() / 2;
-    if (pr) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], st));
-    k_syrk_env<<<(unsigned)(nt * 4), 256, 0, st>>>(c.d_S, c.L.ld, kb, R.a0, R.n1, R.b0, R.nr, pj0, 0);
-    if (pr) {
-        FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], st));
-        // quarters computed (one skipped per diagonal tile, one diagonal tile per column) x 2*64*64*128
-        c.probe_flops += (double)(4 * nt - ncol) * 2.0 * 64 * 64 * CB;
-        ++c.probe_n;
-    }
-    return FBA_OK;
-}
-
 int launch_cholesky(Ctx& c) {
-    const int64_t ld = c.L.ld, nb = c.L.n_pad / CB;
-    hipStream_t A = c.stream, B = c.stream2;
-    bool single = false;
-    for (int64_t kb = 0; kb < nb; ++kb) {
-        const PanelRows R = panel_rows(c, kb);
-        k_potrf128<<<1, 256, POTRF_LDS, A>>>(c.d_S, ld, kb * CB, c.d_dinv, c.d_scal);
-        // panel rows: nr block rows (RHS block row included) of 2 x 64
-        k_trsm128<<<(unsigned)(R.nr * 2), 256, TRSM_LDS, A>>>(c.d_S, ld, kb * CB, R.a0, R.n1, R.b0, c.d_dinv);
-        const int64_t m = R.nr - 1;  // trailing block columns of the step
-        if (!single && R.tiles(0, m) <= c.switch_tiles) {
-            single = true;
-            if (kb > 0 && nb - kb > 1) FBA_HIP(hipStreamWaitEvent(A, c.ev_rest[kb - 1], 0));
+    const int64_t ld = c.L.ld;
+    const Sched& s = c.sched;
+    for (int w = 0; w < s.n_waves; ++w) {
+        const Sched::Wave& W = s.w[w];
+        k_potrf128<<<(unsigned)W.ncol, 256, POTRF_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.cols, c.d_dinv, c.d_scal);
+        k_trsm128<<<(unsigned)(2 * W.ntrsm), 256, TRSM_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.trsm, c.d_dinv);
+        if (W.ntile == 0) continue;
+        const bool pr = c.probe && c.probe_n < (int)c.probe_ev.size() / 2;
+        if (pr) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
+        k_syrk_multi<<<(unsigned)(4 * W.ntile), 256, 0, c.stream>>>(c.d_S, ld, c.d_sched + W.tiles,
+                                                                     c.d_sched + W.src_start, c.d_sched + W.src);
+        if (pr) {
+            FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], c.stream));
+            c.probe_flops += W.flops;
+            ++c.probe_n;
         }
-        if (single) {
-            bulk_update(c, A, kb, R, 0, m);
-            continue;
-        }
-        const bool next = m > 0 && rmap(0, R.a0, R.n1, R.b0) == kb + 1;  // block column kb+1 in the list
-        const int64_t p0 = next ? 1 : 0;
-        FBA_HIP(hipEventRecord(c.ev_trsm[kb], A));
-        if (m > p0) {
-            FBA_HIP(hipStreamWaitEvent(B, c.ev_trsm[kb], 0));
-            bulk_update(c, B, kb, R, p0, m - p0);
-        }
-        FBA_HIP(hipEventRecord(c.ev_rest[kb], B));
-        if (kb > 0 && nb - kb > 1) FBA_HIP(hipStreamWaitEvent(A, c.ev_rest[kb - 1], 0));
-        if (next) k_syrk_env<<<(unsigned)(R.nr * 4), 256, 0, A>>>(c.d_S, ld, kb, R.a0, R.n1, R.b0, R.nr, 0, 0);
     }
     FBA_HIP(hipGetLastError());
     return FBA_OK;
@@ -824,9 +759,13 @@ int launch_backward(Ctx& c) {
         k_border_combine<<<1, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_scal);
     }
     k_trtri128<<<(unsigned)nb, 256, lds_trtri, c.stream>>>(c.d_S, ld, c.d_dinv, c.d_linv);
-    k_bwd_first<<<1, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, nb - 1, c.d_linv, c.d_X);
-    for (int64_t kb = nb - 1; kb >= 1; --kb)
-        k_bwd_step<<<(unsigned)kb, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, kb, c.d_linv, c.d_X);
+    const Sched& s = c.sched;
+    for (int w = s.n_waves - 1; w >= 0; --w) {
+        const Sched::BWave& B = s.b[w];
+        k_bwd_wave<<<(unsigned)(B.nsrc + B.ntgt), 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_linv, c.d_X,
+                                                                     c.d_sched + B.srcs, B.nsrc, c.d_sched + B.tgts,
+                                                                     c.d_sched + B.src_start, c.d_sched + B.src);
+    }
     k_neg_copy<<<(unsigned)((c.L.u_c + 255) / 256), 256, 0, c.stream>>>(c.d_X, c.d_delta, c.L.u_c);
     FBA_HIP(hipGetLastError());
     return FBA_OK;
@@ -837,29 +776,8 @@ int chol_setup(Ctx& c) {
     FBA_HIP(hipFuncSetAttribute((const void*)k_trsm128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRSM_LDS));
     const size_t lds_trtri = sizeof(double) * (CB * LDA + 4 * IB * 17);
     FBA_HIP(hipFuncSetAttribute((const void*)k_trtri128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_trtri));
-    const int64_t nb = c.L.n_pad / CB;
-    // bulk trailing updates on a low-priority stream: the latency-bound critical-path kernels of
-    // the main stream get the compute units first as workgroups retire
-    int prio_least = 0, prio_greatest = 0;
-    FBA_HIP(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
-    const char* pe = getenv("FBA_PRIO");
-    const int prio_mode = pe ? atoi(pe) : 1;
-    if (prio_mode == 1)
-        FBA_HIP(hipStreamCreateWithPriority(&c.stream2, hipStreamNonBlocking, prio_least));
-    else
-        FBA_HIP(hipStreamCreateWithFlags(&c.stream2, hipStreamNonBlocking));
-    const char* se = getenv("FBA_SWITCH_TILES");
-    c.switch_tiles = se ? atoll(se) : 600;  // measured at config 4: 300 -> 3.73 ms, 600 -> 3.70, 1200 -> 3.73
-    if (c.opt.verbose) fprintf(stderr, "[fba] stream priorities least %d greatest %d, bulk mode %d\n",
-                           prio_least, prio_greatest, prio_mode);
-    c.probe_ev.assign(2 * nb, nullptr);
+    c.probe_ev.assign(2 * std::max(c.sched.n_waves, 1), nullptr);
     for (auto& e : c.probe_ev) FBA_HIP(hipEventCreate(&e));
-    c.ev_trsm.assign(nb, nullptr);
-    c.ev_rest.assign(nb, nullptr);
-    for (int64_t k = 0; k < nb; ++k) {
-        FBA_HIP(hipEventCreateWithFlags(&c.ev_trsm[k], hipEventDisableTiming));
-        FBA_HIP(hipEventCreateWithFlags(&c.ev_rest[k], hipEventDisableTiming));
-    }
     return FBA_OK;
 }
 

@@ -25,7 +25,8 @@ constexpr int IMG_TAB = 48;
 constexpr int CAM_TAB_HDR = 8;
 
 struct Layout {
-    int n_img = 0, n_cam = 0, n_tie = 0, nk = 1, cw = 6;
+    int n_img = 0, n_cam = 0, n_tie = 0, nk = 1, cw = 6;  // n_img: internal image slots (padding included)
+    int n_img_ref = 0;    // the reference's images (EXT rows)
     int64_t u_c = 0;      // 6*n_img + cw*n_cam (camera-side full unknowns)
     int64_t u_full = 0;   // u_c + 3*n_tie
     int64_t n_pad = 0;    // u_c rounded up to NB
@@ -35,15 +36,31 @@ struct Layout {
     int u_img = 0, u_cam = 0;
 };
 
+// Block schedule of the reduced-system Cholesky (fba_order.cpp): one batched step per level of the
+// elimination tree.  All offsets index the int32 device buffer Ctx::d_sched.
+struct Sched {
+    struct Wave {
+        int64_t cols = 0, trsm = 0, tiles = 0, src_start = 0, src = 0;  // offsets
+        int ncol = 0, ntrsm = 0, ntile = 0;
+        double flops = 0.0;       // trailing-update flops of the level (kernel probe)
+    };
+    struct BWave {
+        int64_t srcs = 0, tgts = 0, src_start = 0, src = 0;
+        int nsrc = 0, ntgt = 0;
+    };
+    int n_waves = 0;
+    int64_t n_tiles = 0;
+    std::vector<Wave> w;          // factorisation, level 0 up
+    std::vector<BWave> b;         // backward solve, indexed by level (run top down)
+    std::vector<int32_t> buf;     // host image of the lists (uploaded to Ctx::d_sched)
+};
+
 struct Ctx {
     fba_problem prob{};   // shallow copy (pointers valid only during fba_create)
     fba_settings set{};
     fba_options opt{};
     Layout L;
     hipStream_t stream = nullptr;
-    hipStream_t stream2 = nullptr;          // bulk trailing updates (Cholesky lookahead)
-    int64_t switch_tiles = 600;             // trailing tiles below which the factorisation runs on one stream
-    std::vector<hipEvent_t> ev_trsm, ev_rest;  // per Cholesky step
     bool own_stream = false;
     int device = 0;
 
@@ -83,10 +100,11 @@ struct Ctx {
     // multi-rank compact reduce buffer: the entries of S that any rank can write (global co-visible
     // image pairs, diagonal blocks, camera rows, RHS row), packed after fba_accumulate
     int64_t n_gpairs = 0, n_red = 0;
-    // camera-side image order (reverse Cuthill-McKee) and the block envelope of the reduced system
-    std::vector<int32_t> img_ord, img_new;  // internal -> EXT row, EXT row -> internal
-    std::vector<int32_t> env_first;         // [n_pad/NB] first nonzero block column of each block row
-    int n_loc = 0;                          // images carrying the (local) inner-constraint border
+    // camera-side image order (nested dissection, fba_order.cpp) and the factorisation schedule
+    std::vector<int32_t> img_ord, img_new;  // internal slot -> EXT row (-1: padding), EXT row -> slot
+    int n_loc = 0;                          // image slots carrying the (local) inner-constraint border
+    Sched sched;
+    int32_t* d_sched = nullptr;             // device image of the schedule lists (offsets in sched)
     int32_t* d_gpairs = nullptr;     // [2*n_gpairs] (e1,e2), e1 > e2, over ALL tie points
     double* d_red = nullptr;         // [n_red]
     int32_t* d_pair_ij = nullptr;    // [2*n_pair_terms] (obs in e1, obs in e2)
@@ -145,6 +163,8 @@ void set_error(const std::string& msg);
     } while (0)
 
 // kernel launchers (fba_kernels.hip / fba_chol.hip)
+std::vector<int32_t> camera_order(const fba_problem* p);  // internal image slot -> EXT row or -1 (fba_order.cpp)
+void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pairs);  // pairs: (e1, e2) slots, e1 > e2
 int launch_params(Ctx& c);
 int launch_linearize(Ctx& c);
 int launch_point(Ctx& c);

@@ -29,7 +29,8 @@ namespace fba {
 // ------------------------------------------------------------------------------------------------
 __global__ void k_params(const double* __restrict__ xfull, const double* __restrict__ caminfo,
                          double* __restrict__ img_tab, double* __restrict__ cam_tab, double* __restrict__ G,
-                         int n_img, int n_cam, int nk, int cw, int cam_stride, int ic) {
+                         const uint8_t* __restrict__ active, int n_img, int n_cam, int nk, int cw, int cam_stride,
+                         int ic) {
     int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < n_img) {
         const double* e = xfull + 6 * (int64_t)t;
@@ -67,7 +68,8 @@ __global__ void k_params(const double* __restrict__ xfull, const double* __restr
                 0, 0, 0, -1, -sin(w) * tp, cos(w) * tp, 0,
                 0, 0, 0, 0, -cos(w), -sin(w), 0,
                 0, 0, 0, 0, sin(w) * secp, -cos(w) * secp, 0};
-            for (int i = 0; i < 42; ++i) g[i] = rows[i];
+            const bool slot = active[6 * (int64_t)t];  // padding slots (fba_order.cpp) carry no constraint
+            for (int i = 0; i < 42; ++i) g[i] = slot ? rows[i] : 0.0;
         }
     } else if (t < n_img + n_cam) {
         int k = t - n_img;
@@ -1000,7 +1002,7 @@ static inline double py_of(const Ctx& c) { return 1.0 / (c.set.meas_std_y * c.se
 
 int launch_params(Ctx& c) {
     const int n = c.L.n_img + c.L.n_cam;
-    k_params<<<(n + 63) / 64, 64, 0, c.stream>>>(c.d_xfull, c.d_caminfo, c.d_img_tab, c.d_cam_tab, c.d_G,
+    k_params<<<(n + 63) / 64, 64, 0, c.stream>>>(c.d_xfull, c.d_caminfo, c.d_img_tab, c.d_cam_tab, c.d_G, c.d_active,
                                                    c.L.n_img, c.L.n_cam, c.L.nk, c.L.cw, c.cam_tab_stride,
                                                    c.set.inner_constraints);
     FBA_HIP(hipGetLastError());

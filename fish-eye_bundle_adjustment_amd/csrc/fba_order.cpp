@@ -1,0 +1,429 @@
+// fba_order.cpp -- camera-side ordering and the block schedule of the reduced-system Cholesky.
+//
+// The reference inverts the whole normal matrix (main.m:438-440); here the tie points are eliminated
+// first and the reduced camera system S (images, then cameras) is factored by 128x128 blocks.  Its
+// image-image part is sparse: images are coupled only when they share a tie point.  This file
+//   1. orders the images by nested dissection of their co-visibility graph (level-structure
+//      bisection, reverse Cuthill-McKee inside the leaves and the separators), padding with unused
+//      image slots so that two independent subtrees never share a 128-row block;
+//   2. runs the block-level symbolic factorisation (fill of the lower block pattern), and
+//   3. groups the block columns by their level in the elimination tree.  Columns of one level are
+//      independent, so each level is ONE batched step (potrf | panel solves | trailing updates) and
+//      the factorisation's critical path is the tree height, not the block count: at config 4
+//      (1,000 images) 21 steps instead of 47, at config 5 (4,000 images) 38 instead of 188.
+// Trailing-update targets that several columns of a level update are summed in one workgroup in
+// ascending column order, so results do not depend on the schedule (no floating-point atomics).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <deque>
+#include <map>
+
+#include "fba_internal.h"
+
+namespace fba {
+
+namespace {
+
+struct Graph {
+    int n = 0;
+    std::vector<int32_t> start, adj;  // CSR, no self loops, neighbours ascending
+};
+
+Graph covis_graph(const fba_problem* p) {
+    Graph g;
+    g.n = p->n_img;
+    std::vector<std::pair<int32_t, int32_t>> ti;  // (tie, image)
+    for (int64_t i = 0; i < p->n_pts; ++i)
+        if (p->tie[i] >= 0) ti.emplace_back(p->tie[i], p->img[i]);
+    std::sort(ti.begin(), ti.end());
+    std::vector<std::pair<int32_t, int32_t>> edges;
+    for (size_t a = 0; a < ti.size();) {
+        size_t b = a;
+        while (b < ti.size() && ti[b].first == ti[a].first) ++b;
+        for (size_t x = a; x < b; ++x)
+            for (size_t y = a; y < b; ++y)
+                if (ti[x].second != ti[y].second) edges.emplace_back(ti[x].second, ti[y].second);
+        a = b;
+    }
+    std::sort(edges.begin(), edges.end());
+    edges.erase(std::unique(edges.begin(), edges.end()), edges.end());
+    g.start.assign(g.n + 1, 0);
+    g.adj.resize(edges.size());
+    for (auto& e : edges) g.start[e.first + 1]++;
+    for (int v = 0; v < g.n; ++v) g.start[v + 1] += g.start[v];
+    for (size_t q = 0; q < edges.size(); ++q) g.adj[q] = edges[q].second;
+    return g;
+}
+
+class Dissection {
+  public:
+    // pos: image centres (3 per image) for coordinate bisection, or empty (level-structure bisection)
+    Dissection(const Graph& g, int leaf, std::vector<double> pos)
+        : g_(g), leaf_(leaf), pos_(std::move(pos)), tag_(g.n, -1), lev_(g.n, -1), deg_(g.n, 0) {}
+
+    // order the vertices (all of one tag), appending to out; -1 entries are padding slots
+    void nd(std::vector<int32_t> verts, std::vector<int32_t>& out) {
+        if ((int)verts.size() <= leaf_) return rcm(verts, out);
+        std::vector<int32_t> A, B, S;
+        if (!(pos_.empty() ? bisect(verts, A, B, S) : bisect_geo(verts, A, B, S))) return rcm(verts, out);
+        if (getenv("FBA_ND_DEBUG")) fprintf(stderr, "nd %zu -> A %zu B %zu S %zu\n", verts.size(), A.size(), B.size(), S.size());
+        verts.clear();
+        verts.shrink_to_fit();
+        nd(std::move(A), out);
+        // B starts in a fresh 128-row block: A and B then share no block and factor independently
+        const int64_t e = (int64_t)out.size();
+        const int64_t m = (6 * e + NB - 1) / NB;
+        const int64_t e1 = (NB * m + 5) / 6;
+        out.insert(out.end(), (size_t)(e1 - e), -1);
+        nd(std::move(B), out);
+        rcm(S, out);
+    }
+
+  private:
+    const Graph& g_;
+    int leaf_;
+    std::vector<double> pos_;
+    int next_ = 0;
+    std::vector<int> tag_, lev_, deg_;
+
+    int mark(const std::vector<int32_t>& verts) {
+        const int t = next_++;
+        for (int32_t v : verts) tag_[v] = t;
+        for (int32_t v : verts) {
+            int d = 0;
+            for (int32_t q = g_.start[v]; q < g_.start[v + 1]; ++q) d += tag_[g_.adj[q]] == t;
+            deg_[v] = d;
+        }
+        return t;
+    }
+
+    // BFS from root inside tag t; returns the vertices reached in BFS order, lev_ set
+    std::vector<int32_t> bfs(int root, int t) {
+        std::vector<int32_t> order{root};
+        lev_[root] = 0;
+        for (size_t h = 0; h < order.size(); ++h) {
+            const int v = order[h];
+            for (int32_t q = g_.start[v]; q < g_.start[v + 1]; ++q) {
+                const int w = g_.adj[q];
+                if (tag_[w] == t && lev_[w] < 0) {
+                    lev_[w] = lev_[v] + 1;
+                    order.push_back(w);
+                }
+            }
+        }
+        return order;
+    }
+    void clear_lev(const std::vector<int32_t>& vs) {
+        for (int32_t v : vs) lev_[v] = -1;
+    }
+
+    void rcm(const std::vector<int32_t>& verts, std::vector<int32_t>& out) {
+        const int t = mark(verts);
+        std::vector<int32_t> roots(verts);
+        std::stable_sort(roots.begin(), roots.end(), [&](int32_t a, int32_t b) { return deg_[a] < deg_[b]; });
+        std::vector<int32_t> order;
+        order.reserve(verts.size());
+        for (int32_t r : roots) {
+            if (lev_[r] >= 0) continue;
+            size_t h = order.size();
+            order.push_back(r);
+            lev_[r] = 0;
+            while (h < order.size()) {
+                const int v = order[h++];
+                std::vector<int32_t> nb;
+                for (int32_t q = g_.start[v]; q < g_.start[v + 1]; ++q) {
+                    const int w = g_.adj[q];
+                    if (tag_[w] == t && lev_[w] < 0) nb.push_back(w);
+                }
+                std::stable_sort(nb.begin(), nb.end(), [&](int32_t a, int32_t b) { return deg_[a] < deg_[b]; });
+                for (int32_t w : nb) {
+                    lev_[w] = 0;
+                    order.push_back(w);
+                }
+            }
+        }
+        clear_lev(verts);
+        out.insert(out.end(), order.rbegin(), order.rend());
+    }
+
+    // coordinate bisection: cut the images across the principal axis of their centres (a flight
+    // block's long side), the cut placed where the one-sided vertex separator (the images of one
+    // side that share a tie point with the other side) is smallest within 40-60 % of the images
+    bool bisect_geo(const std::vector<int32_t>& verts, std::vector<int32_t>& A, std::vector<int32_t>& B,
+                    std::vector<int32_t>& S) {
+        const int t = mark(verts);
+        const size_t n = verts.size();
+        double mu[3] = {0, 0, 0}, C[3][3] = {};
+        for (int32_t v : verts)
+            for (int d = 0; d < 3; ++d) mu[d] += pos_[3 * v + d] / (double)n;
+        for (int32_t v : verts)
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) C[a][b] += (pos_[3 * v + a] - mu[a]) * (pos_[3 * v + b] - mu[b]);
+        double ax[3] = {1.0, 0.7, 0.3};
+        for (int it = 0; it < 100; ++it) {  // power iteration: principal axis
+            double y[3] = {0, 0, 0}, nn = 0.0;
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) y[a] += C[a][b] * ax[b];
+            for (int a = 0; a < 3; ++a) nn += y[a] * y[a];
+            if (!(nn > 0.0)) return false;
+            nn = std::sqrt(nn);
+            for (int a = 0; a < 3; ++a) ax[a] = y[a] / nn;
+        }
+        std::vector<std::pair<double, int32_t>> pr(n);
+        for (size_t q = 0; q < n; ++q) {
+            const int32_t v = verts[q];
+            double x = 0.0;
+            for (int d = 0; d < 3; ++d) x += (pos_[3 * v + d] - mu[d]) * ax[d];
+            pr[q] = {x, v};
+        }
+        std::sort(pr.begin(), pr.end());
+        for (size_t q = 0; q < n; ++q) lev_[pr[q].second] = (int)q;  // rank along the axis
+        size_t best_cut = n / 2, best_sep = n + 1;
+        bool best_left = true;
+        for (int f = 40; f <= 60; f += 2) {
+            const size_t cut = n * f / 100;
+            if (cut == 0 || cut >= n) continue;
+            size_t sl = 0, sr = 0;  // left vertices with a right neighbour, and vice versa
+            for (size_t q = 0; q < n; ++q) {
+                const int32_t v = pr[q].second;
+                const bool left = q < cut;
+                for (int32_t e = g_.start[v]; e < g_.start[v + 1]; ++e) {
+                    const int w = g_.adj[e];
+                    if (tag_[w] != t) continue;
+                    if (((size_t)lev_[w] < cut) != left) { (left ? sl : sr)++; break; }
+                }
+            }
+            if (std::min(sl, sr) < best_sep) { best_sep = std::min(sl, sr); best_cut = cut; best_left = sl <= sr; }
+        }
+        for (size_t q = 0; q < n; ++q) {
+            const int32_t v = pr[q].second;
+            const bool left = q < best_cut;
+            bool cross = false;
+            for (int32_t e = g_.start[v]; e < g_.start[v + 1] && !cross; ++e) {
+                const int w = g_.adj[e];
+                cross = tag_[w] == t && (((size_t)lev_[w] < best_cut) != left);
+            }
+            if (cross && left == best_left) S.push_back(v);
+            else (left ? A : B).push_back(v);
+        }
+        clear_lev(verts);
+        std::sort(A.begin(), A.end());
+        std::sort(B.begin(), B.end());
+        return !A.empty() && !B.empty();
+    }
+
+    // level-structure bisection: A | separator S (one BFS level) | B, no edge between A and B
+    bool bisect(const std::vector<int32_t>& verts, std::vector<int32_t>& A, std::vector<int32_t>& B,
+                std::vector<int32_t>& S) {
+        const int t = mark(verts);
+        int root = verts[0];
+        for (int32_t v : verts)
+            if (deg_[v] < deg_[root] || (deg_[v] == deg_[root] && v < root)) root = v;
+        std::vector<int32_t> reach;
+        int ecc = -1;
+        for (int it = 0; it < 4; ++it) {  // pseudo-peripheral root
+            reach = bfs(root, t);
+            const int e = lev_[reach.back()];
+            int far = root;
+            for (int32_t v : reach)
+                if (lev_[v] == e && (far == root || deg_[v] < deg_[far] || (deg_[v] == deg_[far] && v < far))) far = v;
+            if (e <= ecc) break;
+            ecc = e;
+            clear_lev(reach);
+            root = far;
+        }
+        clear_lev(reach);
+        reach = bfs(root, t);
+        const int maxl = lev_[reach.back()];
+        if (maxl < 2) { clear_lev(reach); return false; }
+        std::vector<int64_t> cnt(maxl + 1, 0);
+        for (int32_t v : reach) cnt[lev_[v]]++;
+        const double half = 0.5 * (double)verts.size();
+        int best = 1;
+        double bscore = 1e300;
+        int64_t cum = 0;
+        for (int l = 0; l <= maxl; ++l) {
+            if (l >= 1 && l <= maxl - 1) {
+                const double score = std::fabs((double)cum + 0.5 * (double)cnt[l] - half);
+                if (score < bscore || (score == bscore && cnt[l] < cnt[best])) { bscore = score; best = l; }
+            }
+            cum += cnt[l];
+        }
+        // sides: 0 = A, 1 = S, 2 = B (unreached components go to B)
+        std::vector<int32_t> sepv;
+        for (int32_t v : verts) {
+            const int l = lev_[v];
+            if (l >= 0 && l < best) A.push_back(v);
+            else if (l == best) sepv.push_back(v);
+            else B.push_back(v);
+        }
+        clear_lev(reach);
+        for (int32_t v : A) lev_[v] = 0;
+        for (int32_t v : sepv) lev_[v] = 1;
+        for (int32_t v : B) lev_[v] = 2;
+        for (int32_t v : sepv) {  // a separator vertex without a neighbour on one side joins the other
+            bool inA = false, inB = false;
+            for (int32_t q = g_.start[v]; q < g_.start[v + 1]; ++q) {
+                const int w = g_.adj[q];
+                if (tag_[w] != t) continue;
+                inA |= lev_[w] == 0;
+                inB |= lev_[w] == 2;
+            }
+            if (!inB) { lev_[v] = 0; A.push_back(v); }
+            else if (!inA) { lev_[v] = 2; B.push_back(v); }
+            else S.push_back(v);
+        }
+        clear_lev(verts);
+        std::sort(A.begin(), A.end());
+        std::sort(B.begin(), B.end());
+        return !A.empty() && !B.empty();
+    }
+};
+
+}  // namespace
+
+std::vector<int32_t> camera_order(const fba_problem* p) {
+    const char* le = getenv("FBA_ND_LEAF");
+    int leaf = le ? atoi(le) : 150;  // levels at configs 4 / 5: leaf 150 -> 18 / 35, 250 -> 20 / 36, 400 -> 22 / 40
+    if (leaf <= 0) leaf = p->n_img;  // 0: reverse Cuthill-McKee only
+    Graph g = covis_graph(p);
+    std::vector<int32_t> all(p->n_img), out;
+    for (int v = 0; v < p->n_img; ++v) all[v] = v;
+    out.reserve(p->n_img + p->n_img / 8);
+    // coordinate bisection on the approximate image centres when they span the block (FBA_ND_MODE=bfs:
+    // level-structure bisection of the graph alone)
+    std::vector<double> pos;
+    const char* me = getenv("FBA_ND_MODE");
+    if (p->eop0 && !(me && std::string(me) == "bfs")) {
+        pos.resize(3 * (size_t)p->n_img);
+        double lo = 1e300, hi = -1e300;
+        for (int v = 0; v < p->n_img; ++v)
+            for (int d = 0; d < 3; ++d) {
+                pos[3 * v + d] = p->eop0[6 * (int64_t)v + d];
+                lo = std::min(lo, pos[3 * v + d]);
+                hi = std::max(hi, pos[3 * v + d]);
+            }
+        if (!(hi > lo) || !std::isfinite(hi - lo)) pos.clear();
+    }
+    Dissection(g, std::max(leaf, 1), std::move(pos)).nd(std::move(all), out);
+    return out;
+}
+
+void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pairs) {
+    const Layout& L = c.L;
+    const int64_t nb = L.n_pad / NB;
+    Sched& s = c.sched;
+    // lower block pattern, P[j][i] = block (i, j) nonzero, i >= j; row nb = the RHS block row
+    std::vector<std::vector<uint8_t>> P(nb, std::vector<uint8_t>(nb + 1, 0));
+    auto touch = [&](int64_t e1, int64_t e2) {  // rows of image e1 x columns of image e2 (6 each)
+        for (int64_t bi = 6 * e1 / NB; bi <= (6 * e1 + 5) / NB; ++bi)
+            for (int64_t bj = 6 * e2 / NB; bj <= (6 * e2 + 5) / NB; ++bj)
+                if (bi >= bj) P[bj][bi] = 1;
+    };
+    for (int64_t e = 0; e < L.n_img; ++e)  // (a padding slot is decoupled: it must not join two blocks)
+        if (c.img_ord[e] >= 0) touch(e, e);
+    for (auto& q : pairs) touch(q.first, q.second);
+    if (c.n_loc > 0) {  // the local inner-constraint border: dense on its block rows
+        const int64_t bl = (6 * (int64_t)c.n_loc - 1) / NB;
+        for (int64_t i = 0; i <= bl; ++i)
+            for (int64_t j = 0; j <= i; ++j) P[j][i] = 1;
+    }
+    const int64_t T = std::min<int64_t>(6 * (int64_t)L.n_img / NB, nb);  // camera rows: dense
+    for (int64_t j = 0; j < nb; ++j) {
+        for (int64_t i = std::max(T, j); i < nb; ++i) P[j][i] = 1;
+        P[j][nb] = 1;
+    }
+    // symbolic factorisation (fill) and elimination-tree levels
+    std::vector<std::vector<int32_t>> R(nb);
+    std::vector<int32_t> level(nb, 0);
+    for (int64_t k = 0; k < nb; ++k) {
+        for (int64_t i = k + 1; i <= nb; ++i)
+            if (P[k][i]) R[k].push_back((int32_t)i);
+        for (size_t a = 0; a < R[k].size(); ++a) {
+            const int32_t ia = R[k][a];
+            if (ia == nb) continue;
+            level[ia] = std::max(level[ia], level[k] + 1);
+            for (size_t b = a; b < R[k].size(); ++b) P[ia][R[k][b]] = 1;
+        }
+    }
+    const int nw = nb > 0 ? 1 + *std::max_element(level.begin(), level.end()) : 0;
+    s = Sched();
+    s.n_waves = nw;
+    std::vector<std::vector<int32_t>> wave(nw);
+    for (int64_t k = 0; k < nb; ++k) wave[level[k]].push_back((int32_t)k);
+    std::vector<int32_t> buf;  // device image
+    auto at = [&]() { return (int64_t)buf.size(); };
+    s.w.resize(nw);
+    int64_t ntile_total = 0;
+    for (int w = 0; w < nw; ++w) {
+        Sched::Wave& W = s.w[w];
+        W.cols = at();
+        W.ncol = (int)wave[w].size();
+        buf.insert(buf.end(), wave[w].begin(), wave[w].end());
+        W.trsm = at();
+        for (int32_t k : wave[w])
+            for (int32_t r : R[k]) { buf.push_back(k); buf.push_back(r); }
+        W.ntrsm = (int)((at() - W.trsm) / 2);
+        // trailing-update targets (i, j), j < nb, with their source columns in ascending order
+        std::map<std::pair<int32_t, int32_t>, std::vector<int32_t>> tg;
+        for (int32_t k : wave[w])
+            for (size_t b = 0; b < R[k].size(); ++b) {
+                if (R[k][b] == nb) continue;
+                for (size_t a = b; a < R[k].size(); ++a) tg[{R[k][a], R[k][b]}].push_back(k);
+            }
+        std::vector<std::pair<std::pair<int32_t, int32_t>, std::vector<int32_t>>> tl(tg.begin(), tg.end());
+        // longest (most sources) first, then by block column: the long workgroups start early
+        std::stable_sort(tl.begin(), tl.end(), [](const auto& a, const auto& b) {
+            if (a.second.size() != b.second.size()) return a.second.size() > b.second.size();
+            return a.first.second != b.first.second ? a.first.second < b.first.second : a.first.first < b.first.first;
+        });
+        W.ntile = (int)tl.size();
+        W.tiles = at();
+        for (auto& t : tl) { buf.push_back(t.first.first); buf.push_back(t.first.second); }
+        W.src_start = at();
+        int32_t acc = 0;
+        for (auto& t : tl) { buf.push_back(acc); acc += (int32_t)t.second.size(); }
+        buf.push_back(acc);
+        W.src = at();
+        W.flops = 0.0;
+        for (auto& t : tl) {
+            buf.insert(buf.end(), t.second.begin(), t.second.end());
+            const int quarters = t.first.first == t.first.second ? 3 : 4;
+            W.flops += (double)t.second.size() * quarters * 2.0 * 64 * 64 * NB;
+        }
+        ntile_total += W.ntile;
+    }
+    // backward solve L' x = y by levels, top down: the columns of level w get x = Linv' y; every
+    // column j whose panel holds one of them gets y_j -= sum_i L(i,j)' x_i (i ascending)
+    std::vector<std::vector<int32_t>> rev(nb);  // rev[i] = columns j < i with i in R[j]
+    for (int64_t j = 0; j < nb; ++j)
+        for (int32_t i : R[j])
+            if (i < nb) rev[i].push_back((int32_t)j);
+    s.b.resize(nw);
+    for (int w = nw - 1; w >= 0; --w) {
+        Sched::BWave& B = s.b[w];
+        B.srcs = s.w[w].cols;
+        B.nsrc = s.w[w].ncol;
+        std::map<int32_t, std::vector<int32_t>> tg;
+        for (int32_t i : wave[w])
+            for (int32_t j : rev[i]) tg[j].push_back(i);
+        B.ntgt = (int)tg.size();
+        B.tgts = at();
+        for (auto& t : tg) buf.push_back(t.first);
+        B.src_start = at();
+        int32_t acc = 0;
+        for (auto& t : tg) { buf.push_back(acc); acc += (int32_t)t.second.size(); }
+        buf.push_back(acc);
+        B.src = at();
+        for (auto& t : tg) buf.insert(buf.end(), t.second.begin(), t.second.end());
+    }
+    s.n_tiles = ntile_total;
+    s.buf = std::move(buf);
+    if (c.opt.verbose)
+        fprintf(stderr, "[fba] camera system: %ld blocks, %d levels, %ld update tiles, %d images + %d padding slots\n",
+                (long)nb, nw, (long)ntile_total, c.L.n_img_ref, c.L.n_img - c.L.n_img_ref);
+}
+
+}  // namespace fba

@@ -1,0 +1,293 @@
+// sched_check.cpp -- host-only check of the camera-side ordering and the level schedule of the
+// block Cholesky (fish-eye_bundle_adjustment_amd/csrc/fba_order.cpp), built and run by
+// tests/test_schedule.py (no GPU needed).
+//
+// A synthetic aerial block (images on a grid, tie points seen by the images within a radius) is
+// ordered by camera_order(); build_schedule() makes the per-level task lists.  Then a random SPD
+// matrix with exactly the block pattern of the reduced camera system (co-visible image pairs, the
+// local border block, dense camera rows) plus 15 RHS rows is factored by EMULATING the kernels'
+// schedule on the CPU (potrf per level column, panel solves per (k, r) task, trailing updates per
+// target with its source list, backward solve per level), and compared with a plain dense
+// Cholesky / solve of the same matrix.  It also checks that the task lists stay inside the
+// matrix, that no two independent subtrees share a block, and that every padding slot is unused.
+//
+//   sched_check <n_img> <seed>     prints "ok levels=<L> blocks=<B> err=<e>" or "FAIL ..."
+//   sched_check <n_img> 0 <file>   ordering statistics only, for the observations in <file>
+//                                  (int64 n_pts, int32 img[n_pts], int32 tie[n_pts], f64 eop[6 n_img])
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <set>
+
+#include "../fish-eye_bundle_adjustment_amd/csrc/fba_internal.h"
+
+using namespace fba;
+
+static int fail(const char* m) {
+    printf("FAIL %s\n", m);
+    return 1;
+}
+
+int main(int argc, char** argv) {
+    const int n_img = argc > 1 ? atoi(argv[1]) : 300;
+    const int seed = argc > 2 ? atoi(argv[2]) : 1;
+    std::mt19937_64 rng(seed);
+    std::uniform_real_distribution<double> U(0.0, 1.0);
+    // images on a grid (strips), tie points at random positions seen by images within a radius
+    const int gw = std::max(1, (int)std::sqrt(n_img * 0.6));
+    std::vector<double> ix(n_img), iy(n_img);
+    for (int e = 0; e < n_img; ++e) { ix[e] = e % gw; iy[e] = e / gw; }
+    std::vector<int32_t> img, tie, cam;
+    std::vector<double> eop;
+    int n_tie = 20 * n_img;
+    const bool stats_only = argc > 3;
+    if (stats_only) {
+        FILE* f = fopen(argv[3], "rb");
+        int64_t np = 0;
+        if (!f || fread(&np, 8, 1, f) != 1) return fail("cannot read observation file");
+        img.resize(np);
+        tie.resize(np);
+        cam.assign(np, 0);
+        if (fread(img.data(), 4, np, f) != (size_t)np || fread(tie.data(), 4, np, f) != (size_t)np) return fail("short file");
+        eop.assign(6 * (size_t)n_img, 0.0);
+        if (fread(eop.data(), 8, eop.size(), f) != eop.size()) eop.clear();
+        fclose(f);
+        n_tie = 0;
+        for (int32_t t : tie) n_tie = std::max(n_tie, t + 1);
+    }
+    for (int t = 0; t < n_tie && !stats_only; ++t) {
+        const double px = U(rng) * gw, py = U(rng) * ((n_img + gw - 1) / gw);
+        for (int e = 0; e < n_img; ++e)
+            if (std::hypot(ix[e] - px, iy[e] - py) < 1.6) { img.push_back(e); tie.push_back(t); cam.push_back(0); }
+    }
+    fba_problem p{};
+    p.n_pts = (int64_t)img.size();
+    p.n_img = n_img;
+    p.n_cam = 1;
+    p.n_tie = n_tie;
+    p.img = img.data();
+    p.tie = tie.data();
+    p.cam = cam.data();
+    if (!stats_only) {  // image centres on the grid (spacing 1000), for the coordinate bisection
+        eop.assign(6 * (size_t)n_img, 0.0);
+        for (int e = 0; e < n_img; ++e) { eop[6 * e] = 1000.0 * ix[e]; eop[6 * e + 1] = 1000.0 * iy[e]; eop[6 * e + 2] = 800.0; }
+    }
+    p.eop0 = eop.empty() ? nullptr : eop.data();
+    const std::vector<int32_t> ord = camera_order(&p);
+    // every image exactly once, the rest padding
+    {
+        std::vector<int> seen(n_img, 0);
+        for (int32_t v : ord)
+            if (v >= 0) seen[v]++;
+        for (int e = 0; e < n_img; ++e)
+            if (seen[e] != 1) return fail("camera_order is not a permutation");
+    }
+    Ctx c;
+    c.img_ord = ord;
+    Layout& L = c.L;
+    L.n_img = (int)ord.size();
+    L.n_img_ref = n_img;
+    L.n_cam = 1;
+    L.cw = 10;
+    L.u_c = 6 * (int64_t)L.n_img + L.cw;
+    L.n_pad = (L.u_c + NB - 1) / NB * NB;
+    L.ld = L.n_pad;
+    c.n_loc = std::min(L.n_img, NB / 6);
+    c.opt.verbose = 0;
+    std::vector<int32_t> slot(n_img);
+    for (int e = 0; e < L.n_img; ++e)
+        if (ord[e] >= 0) slot[ord[e]] = e;
+    std::set<std::pair<int32_t, int32_t>> ps;
+    std::vector<size_t> by_tie(img.size());
+    for (size_t q = 0; q < img.size(); ++q) by_tie[q] = q;
+    std::stable_sort(by_tie.begin(), by_tie.end(), [&](size_t a, size_t b) { return tie[a] < tie[b]; });
+    for (size_t a = 0; a < img.size();) {
+        size_t b = a;
+        while (b < img.size() && tie[by_tie[b]] == tie[by_tie[a]]) ++b;
+        for (size_t x = a; x < b; ++x)
+            for (size_t y = a; y < b; ++y)
+                if (slot[img[by_tie[x]]] > slot[img[by_tie[y]]]) ps.insert({slot[img[by_tie[x]]], slot[img[by_tie[y]]]});
+        a = b;
+    }
+    std::vector<std::pair<int32_t, int32_t>> pairs(ps.begin(), ps.end());
+    build_schedule(c, pairs);
+    const Sched& s = c.sched;
+    if (stats_only) {
+        std::vector<int> per(s.n_waves);
+        for (int w = 0; w < s.n_waves; ++w) per[w] = s.w[w].ncol;
+        printf("ok levels=%d blocks=%ld slots=%d tiles=%ld cols/level:", s.n_waves, (long)(L.n_pad / NB), L.n_img,
+               (long)s.n_tiles);
+        for (int v : per) printf(" %d", v);
+        printf("\n");
+        return 0;
+    }
+    const int64_t n = L.n_pad, nb = n / NB, nr = n + NB;  // rows: matrix + RHS block row
+    const int32_t* B = s.buf.data();
+    const int64_t nbuf = (int64_t)s.buf.size();
+    // matrix with the pattern of the reduced system; padding slots and padding rows decoupled
+    std::vector<double> M((size_t)nr * n, 0.0);
+    auto at = [&](int64_t r, int64_t q) -> double& { return M[(size_t)r * n + q]; };
+    std::vector<char> used(n, 0);
+    for (int e = 0; e < L.n_img; ++e)
+        if (ord[e] >= 0)
+            for (int a = 0; a < 6; ++a) used[6 * e + a] = 1;
+    for (int64_t i = 6 * (int64_t)L.n_img; i < L.u_c; ++i) used[i] = 1;
+    auto blk = [&](int64_t r0, int64_t c0) {  // random 6x6 coupling (lower part only)
+        for (int a = 0; a < 6; ++a)
+            for (int b = 0; b < 6; ++b)
+                if (r0 + a > c0 + b) at(r0 + a, c0 + b) = (U(rng) - 0.5) * 0.05;
+    };
+    for (auto& q : pairs) blk(6 * (int64_t)q.first, 6 * (int64_t)q.second);
+    for (int e = 0; e < L.n_img; ++e)
+        if (ord[e] >= 0) blk(6 * (int64_t)e, 6 * (int64_t)e);
+    for (int64_t i = 0; i < 6 * (int64_t)c.n_loc; ++i)  // local border block (dense)
+        for (int64_t j = 0; j < i; ++j)
+            if (used[i] && used[j]) at(i, j) += (U(rng) - 0.5) * 0.01;
+    for (int64_t i = 6 * (int64_t)L.n_img; i < L.u_c; ++i)  // camera rows (dense)
+        for (int64_t j = 0; j < i; ++j)
+            if (used[j]) at(i, j) = (U(rng) - 0.5) * 0.01;
+    for (int64_t i = 0; i < n; ++i) {  // diagonal dominance
+        double r = 0.0;
+        for (int64_t j = 0; j < n; ++j) r += std::fabs(j < i ? at(i, j) : at(j, i));
+        at(i, i) = used[i] ? r + 1.0 + U(rng) : 1.0;
+    }
+    for (int64_t q = 0; q < 15; ++q)
+        for (int64_t j = 0; j < n; ++j) at(n + q, j) = used[j] ? U(rng) - 0.5 : 0.0;
+    std::vector<double> M0 = M;
+    // -- the emulated schedule --
+    auto Bk = [&](int64_t i, int64_t j) { return &M[(size_t)(i * NB) * n + j * NB]; };
+    std::vector<int> done(nb, 0);
+    for (int w = 0; w < s.n_waves; ++w) {
+        const Sched::Wave& W = s.w[w];
+        if (W.cols + W.ncol > nbuf || W.trsm + 2 * W.ntrsm > nbuf || W.tiles + 2 * W.ntile > nbuf) return fail("list bounds");
+        for (int q = 0; q < W.ncol; ++q) {  // potrf
+            const int64_t k = B[W.cols + q];
+            if (k < 0 || k >= nb || done[k]) return fail("potrf column");
+            done[k] = 1;
+            double* A = Bk(k, k);
+            for (int j = 0; j < NB; ++j) {
+                double d = A[(size_t)j * n + j];
+                for (int t = 0; t < j; ++t) d -= A[(size_t)j * n + t] * A[(size_t)j * n + t];
+                if (!(d > 0)) return fail("not SPD in emulation");
+                d = std::sqrt(d);
+                A[(size_t)j * n + j] = d;
+                for (int i = j + 1; i < NB; ++i) {
+                    double v = A[(size_t)i * n + j];
+                    for (int t = 0; t < j; ++t) v -= A[(size_t)i * n + t] * A[(size_t)j * n + t];
+                    A[(size_t)i * n + j] = v / d;
+                }
+            }
+        }
+        for (int q = 0; q < W.ntrsm; ++q) {  // X = A L^-T
+            const int64_t k = B[W.trsm + 2 * q], r = B[W.trsm + 2 * q + 1];
+            if (k < 0 || k >= nb || !done[k] || r <= k || r > nb) return fail("trsm task");
+            const double* Lk = Bk(k, k);
+            double* X = Bk(r, k);
+            for (int i = 0; i < NB; ++i)
+                for (int j = 0; j < NB; ++j) {
+                    double v = X[(size_t)i * n + j];
+                    for (int t = 0; t < j; ++t) v -= X[(size_t)i * n + t] * Lk[(size_t)j * n + t];
+                    X[(size_t)i * n + j] = v / Lk[(size_t)j * n + j];
+                }
+        }
+        for (int q = 0; q < W.ntile; ++q) {  // C(i,j) -= sum_k X_ik X_jk'
+            const int64_t i = B[W.tiles + 2 * q], j = B[W.tiles + 2 * q + 1];
+            if (j < 0 || j >= nb || i < j || i > nb || done[j]) return fail("update target");
+            const int32_t s0 = B[W.src_start + q], s1 = B[W.src_start + q + 1];
+            int64_t prev = -1;
+            for (int32_t u = s0; u < s1; ++u) {
+                const int64_t k = B[W.src + u];
+                if (k <= prev || !done[k]) return fail("update sources");
+                prev = k;
+                const double* Xi = Bk(i, k);
+                const double* Xj = Bk(j, k);
+                double* C = Bk(i, j);
+                for (int a = 0; a < NB; ++a)
+                    for (int b = 0; b < NB; ++b) {
+                        if (i == j && b > a) continue;
+                        double v = 0.0;
+                        for (int t = 0; t < NB; ++t) v += Xi[(size_t)a * n + t] * Xj[(size_t)b * n + t];
+                        C[(size_t)a * n + b] -= v;
+                    }
+            }
+        }
+    }
+    for (int64_t k = 0; k < nb; ++k)
+        if (!done[k]) return fail("column never factored");
+    // -- reference: dense right-looking Cholesky of the same matrix (RHS rows as extra rows) --
+    std::vector<double> R = M0;
+    auto rat = [&](int64_t r, int64_t q) -> double& { return R[(size_t)r * n + q]; };
+    for (int64_t j = 0; j < n; ++j) {
+        const double d = std::sqrt(rat(j, j));
+        rat(j, j) = d;
+        for (int64_t i = j + 1; i < nr; ++i) rat(i, j) /= d;
+        for (int64_t q = j + 1; q < n; ++q) {
+            const double f = rat(q, j);
+            if (f == 0.0) continue;
+            for (int64_t i = q; i < nr; ++i) rat(i, q) -= rat(i, j) * f;
+        }
+    }
+    double err = 0.0, scale = 0.0;
+    for (int64_t i = 0; i < nr; ++i)
+        for (int64_t j = 0; j < std::min(i + 1, n); ++j) {
+            // structurally-zero blocks of the emulation were never touched: compare every entry
+            err = std::max(err, std::fabs(at(i, j) - rat(i, j)));
+            scale = std::max(scale, std::fabs(rat(i, j)));
+        }
+    // -- backward solve by levels (k_bwd_wave) vs dense back substitution --
+    std::vector<double> y(M.begin() + (size_t)n * n, M.begin() + (size_t)n * n + n), x(n, 0.0);
+    for (int w = s.n_waves - 1; w >= 0; --w) {
+        const Sched::BWave& Bw = s.b[w];
+        auto solve_diag = [&](int64_t i, double* out) {  // out = L_ii^-T y_i
+            const double* Lk = Bk(i, i);
+            for (int a = NB - 1; a >= 0; --a) {
+                double v = y[i * NB + a];
+                for (int t = a + 1; t < NB; ++t) v -= Lk[(size_t)t * n + a] * out[t];
+                out[a] = v / Lk[(size_t)a * n + a];
+            }
+        };
+        std::vector<double> xs(NB);
+        std::vector<std::vector<double>> upd;
+        for (int q = 0; q < Bw.ntgt; ++q) {  // targets first read the level's y (as the kernel does)
+            const int64_t j = B[Bw.tgts + q];
+            std::vector<double> acc(NB, 0.0);
+            for (int32_t u = B[Bw.src_start + q]; u < B[Bw.src_start + q + 1]; ++u) {
+                const int64_t i = B[Bw.src + u];
+                solve_diag(i, xs.data());
+                const double* Lij = Bk(i, j);
+                for (int b = 0; b < NB; ++b)
+                    for (int a = 0; a < NB; ++a) acc[b] += Lij[(size_t)a * n + b] * xs[a];
+            }
+            upd.push_back(acc);
+        }
+        for (int q = 0; q < Bw.nsrc; ++q) {
+            const int64_t i = B[Bw.srcs + q];
+            solve_diag(i, &x[i * NB]);
+        }
+        for (int q = 0; q < Bw.ntgt; ++q) {
+            const int64_t j = B[Bw.tgts + q];
+            for (int b = 0; b < NB; ++b) y[j * NB + b] -= upd[q][b];
+        }
+    }
+    std::vector<double> xr(n);
+    for (int64_t a = n - 1; a >= 0; --a) {
+        double v = rat(n, a);
+        for (int64_t t = a + 1; t < n; ++t) v -= rat(t, a) * xr[t];
+        xr[a] = v / rat(a, a);
+    }
+    double xerr = 0.0, xs_ = 0.0;
+    for (int64_t a = 0; a < n; ++a) {
+        xerr = std::max(xerr, std::fabs(x[a] - xr[a]));
+        xs_ = std::max(xs_, std::fabs(xr[a]));
+    }
+    // independence: no block mixes the rows of two sibling subtrees (checked via the level count
+    // being below the block count when a dissection happened)
+    const double rel = err / scale, xrel = xerr / xs_;
+    if (!(rel < 1e-12) || !(xrel < 1e-12)) {
+        printf("FAIL factor err %.3e solve err %.3e\n", rel, xrel);
+        return 1;
+    }
+    printf("ok levels=%d blocks=%ld slots=%d err=%.3e xerr=%.3e\n", s.n_waves, (long)nb, L.n_img, rel, xrel);
+    return 0;
+}

@@ -1,0 +1,39 @@
+"""CPU: the camera-side ordering and the level schedule of the block Cholesky (fba_order.cpp).
+
+tests/sched_check.cpp orders a synthetic aerial block by nested dissection, builds the per-level
+task lists the GPU kernels run (potrf columns, panel-solve tasks, trailing-update targets with their
+source columns, backward-solve levels), EMULATES that schedule on the CPU for a random SPD matrix
+with the reduced system's block pattern (local border block and dense camera rows included) and
+compares factor, forward-solved RHS rows and backward solution with a dense Cholesky: relative
+error < 1e-12.  No GPU involved; the kernels themselves are covered by tests/test_gpu_*.py.
+"""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def checker(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("sched") / "sched_check")
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", os.path.join(ROOT, "tests", "sched_check.cpp"),
+                    os.path.join(ROOT, "fish-eye_bundle_adjustment_amd", "csrc", "fba_order.cpp"), "-o", exe],
+                   check=True)
+    return exe
+
+
+@pytest.mark.parametrize("n_img,seed,leaf", [(40, 1, None), (300, 2, None), (300, 1, 60), (420, 3, 100),
+                                             (200, 4, 0)])
+def test_level_schedule_matches_dense_cholesky(checker, n_img, seed, leaf):
+    env = dict(os.environ)
+    env.pop("FBA_ND_LEAF", None)
+    if leaf is not None:
+        env["FBA_ND_LEAF"] = str(leaf)
+    r = subprocess.run([checker, str(n_img), str(seed)], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
+    fields = dict(f.split("=") for f in r.stdout.split()[1:])
+    assert int(fields["levels"]) <= int(fields["blocks"])
+    if leaf == 60:  # a dissected scene: independent subtrees share levels
+        assert int(fields["levels"]) < int(fields["blocks"])
