@@ -556,33 +556,46 @@ __global__ __launch_bounds__(256) void k_border_gram(const double* __restrict__ 
     if (tid < 15) scal[32 + 15 * a + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
 }
 
-// Solve [[A'A - I, A'B], [B'A, B'B]] [z; k] = -[A'y; B'y] (14x14, partial pivoting) and form
-// u = y + A z + B k in the RHS row (derivation in fba_kernels.hip, border section)
+// Solve [[A'A - I, A'B], [B'A, B'B]] [z; k] = -[A'y; B'y] (14x14, partial pivoting, in LDS with
+// the workgroup's threads) and form u = y + A z + B k in the RHS row (derivation in fba_kernels.hip,
+// border section)
 __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, int64_t ld, int64_t n_pad,
                                                         const double* __restrict__ scal) {
+    __shared__ double H[14][16];
+    __shared__ double f[14];
     __shared__ double coef[14];
-    if (threadIdx.x == 0) {
-        double H[14][15];
-        const double* g = scal + 32;  // g[15a + b], index 0 = y, 1..7 = A, 8..14 = B
-        for (int r = 0; r < 14; ++r) {
-            for (int q = 0; q < 14; ++q) H[r][q] = g[15 * (1 + r) + (1 + q)] - ((r == q && r < 7) ? 1.0 : 0.0);
-            H[r][14] = -g[15 * (1 + r)];
-        }
-        for (int col = 0; col < 14; ++col) {
-            int piv = col;
+    __shared__ int piv;
+    const int tid = threadIdx.x;
+    const double* g = scal + 32;  // g[15a + b], index 0 = y, 1..7 = A, 8..14 = B
+    if (tid < 14 * 15) {
+        const int r = tid / 15, q = tid % 15;
+        H[r][q] = (q < 14) ? g[15 * (1 + r) + (1 + q)] - ((r == q && r < 7) ? 1.0 : 0.0) : -g[15 * (1 + r)];
+    }
+    __syncthreads();
+    for (int col = 0; col < 14; ++col) {
+        if (tid == 0) {
+            int p = col;
             for (int r = col + 1; r < 14; ++r)
-                if (fabs(H[r][col]) > fabs(H[piv][col])) piv = r;
-            if (piv != col)
-                for (int q = 0; q < 15; ++q) {
-                    const double t = H[col][q];
-                    H[col][q] = H[piv][q];
-                    H[piv][q] = t;
-                }
-            for (int r = col + 1; r < 14; ++r) {
-                const double f = H[r][col] / H[col][col];
-                for (int q = col; q < 15; ++q) H[r][q] -= f * H[col][q];
-            }
+                if (fabs(H[r][col]) > fabs(H[p][col])) p = r;
+            piv = p;
         }
+        __syncthreads();
+        const int p = piv;
+        if (p != col && tid < 15) {
+            const double t = H[col][tid];
+            H[col][tid] = H[p][tid];
+            H[p][tid] = t;
+        }
+        __syncthreads();
+        if (tid > col && tid < 14) f[tid] = H[tid][col] / H[col][col];
+        __syncthreads();
+        if (tid < 14 * 15) {
+            const int r = tid / 15, q = tid % 15;
+            if (r > col && q >= col) H[r][q] -= f[r] * H[col][q];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
         for (int r = 13; r >= 0; --r) {
             double v = H[r][14];
             for (int q = r + 1; q < 14; ++q) v -= H[r][q] * coef[q];
@@ -591,8 +604,9 @@ __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, 
     }
     __syncthreads();
     double* yw = S + n_pad * ld;
-    for (int64_t i = threadIdx.x; i < n_pad; i += 256) {
+    for (int64_t i = tid; i < n_pad; i += 256) {
         double v = yw[i];
+#pragma unroll
         for (int m = 0; m < 14; ++m) v += S[(n_pad + 1 + m) * ld + i] * coef[m];
         yw[i] = v;
     }

@@ -715,39 +715,44 @@ __global__ void k_cam_stage2(const double* __restrict__ slab, double* __restrict
 //   r | A = G_l W_l^1/2 | B = G D   (D = the same equilibration over all images; B'x = 0 <=> G'x = 0)
 // in k_border_combine.  scal: [1] Cholesky failure flag, [2] sumabs, [8..14] W_l, [16..22] D^2.
 // ------------------------------------------------------------------------------------------------
-__global__ void k_border_weights(const double* __restrict__ S, const double* __restrict__ G,
-                                 double* __restrict__ scal, int64_t ld, int n_img, int n_loc, int ic) {
-    __shared__ double red[14][256];
+__global__ __launch_bounds__(1024) void k_border_weights(const double* __restrict__ S, const double* __restrict__ G,
+                                                         double* __restrict__ scal, int64_t ld, int n_img, int n_loc,
+                                                         int ic) {
+    __shared__ double red[16][14];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     double a[14];
 #pragma unroll
     for (int m = 0; m < 14; ++m) a[m] = 0.0;
     if (ic) {
-        for (int64_t i = threadIdx.x; i < 6 * (int64_t)n_img; i += blockDim.x) {
+        for (int64_t i = tid; i < 6 * (int64_t)n_img; i += 1024) {
             const double sii = S[i * ld + i];
-            if (!(sii > 0.0)) continue;
             const double* g = G + (i / 6) * 42 + (i % 6) * 7;
-            const bool loc = i < 6 * (int64_t)n_loc;
+            const bool ok = sii > 0.0, loc = i < 6 * (int64_t)n_loc;
+            const double inv = ok ? 1.0 / sii : 0.0;
 #pragma unroll
             for (int m = 0; m < 7; ++m) {
-                const double v = g[m] * g[m] / sii;
+                const double v = g[m] * g[m] * inv;
                 a[7 + m] += v;
                 if (loc) a[m] += v;
             }
         }
     }
 #pragma unroll
-    for (int m = 0; m < 14; ++m) red[m][threadIdx.x] = a[m];
+    for (int m = 0; m < 14; ++m) {
+        double v = a[m];
+#pragma unroll
+        for (int w = 32; w > 0; w >>= 1) v += __shfl_xor(v, w, 64);
+        if (lane == 0) red[wave][m] = v;
+    }
     __syncthreads();
-    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w)
-            for (int m = 0; m < 14; ++m) red[m][threadIdx.x] += red[m][threadIdx.x + w];
-        __syncthreads();
+    if (tid < 14) {
+        double v = 0.0;
+        for (int w = 0; w < 16; ++w) v += red[w][tid];
+        const int m = tid % 7;
+        if (tid < 7) scal[8 + m] = v > 0.0 ? 1.0 / v : 1.0;
+        else scal[16 + m] = v > 0.0 ? 1.0 / v : 1.0;
     }
-    if (threadIdx.x < 7) {
-        scal[8 + threadIdx.x] = red[threadIdx.x][0] > 0.0 ? 1.0 / red[threadIdx.x][0] : 1.0;
-        scal[16 + threadIdx.x] = red[7 + threadIdx.x][0] > 0.0 ? 1.0 / red[7 + threadIdx.x][0] : 1.0;
-    }
-    if (threadIdx.x == 0) scal[1] = 0.0;  // Cholesky failure flag
+    if (tid == 0) scal[1] = 0.0;  // Cholesky failure flag
 }
 
 // M += G_l W_l G_l' on the 6 n_loc x 6 n_loc block (lower part)
@@ -1058,7 +1063,7 @@ int launch_accumulate(Ctx& c) {
 int launch_border(Ctx& c) {
     const Layout& L = c.L;
     const int ic = c.set.inner_constraints;
-    k_border_weights<<<1, 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, L.ld, L.n_img, c.n_loc, ic);
+    k_border_weights<<<1, 1024, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, L.ld, L.n_img, c.n_loc, ic);
     FBA_HIP(hipGetLastError());
     if (ic && c.n_loc > 0) {
         const int64_t n = 6 * (int64_t)c.n_loc;
