@@ -7,7 +7,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <string>
 #include <numeric>
 #include <tuple>
 
@@ -164,9 +166,8 @@ static void partition(const fba_problem* p, int world, std::vector<int32_t>& tie
 static void destroy(Ctx* c) {
     if (!c) return;
     void* ptrs[] = {c->d_chunk_obs, c->d_chunk_pt, c->d_xy, c->d_img, c->d_cam, c->d_pt, c->d_ctl, c->d_lp_tie, c->d_lp_start, c->d_lp_cam,
-                    c->d_img_start, c->d_img_obs, c->d_cam_lp, c->d_cam_ctl, c->d_pair_e, c->d_pair_start, c->d_gpairs, c->d_red,
-                    c->d_pair_ij, c->d_xfull, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
-                    c->d_pt_tab, c->d_slab, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
+                    c->d_acc, c->d_ppart, c->d_ipart, c->d_cpart, c->d_lrprof, c->d_gpairs, c->d_red, c->d_xfull, c->d_xlin, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
+                    c->d_pt_tab, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
                     c->d_active, c->d_counted, c->d_obs_pho, c->d_sched};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
@@ -266,13 +267,30 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
             zkey[t] = k;
         }
     }
-    std::stable_sort(lps.begin(), lps.end(), [&](int32_t a, int32_t b) {
-        return tie_cam[a] != tie_cam[b] ? tie_cam[a] < tie_cam[b] : zkey[a] < zkey[b];
-    });
+    // default: lexicographic order of the points' (sorted) image sets -- consecutive points share most
+    // of their co-visible pairs, so the rows k_pairs gathers for one pair sit close together
+    // (FBA_POINT_ORDER=morton: the Z-curve order alone)
+    const char* po = getenv("FBA_POINT_ORDER");
+    if (po && std::string(po) == "morton") {
+        std::stable_sort(lps.begin(), lps.end(), [&](int32_t a, int32_t b) {
+            return tie_cam[a] != tie_cam[b] ? tie_cam[a] < tie_cam[b] : zkey[a] < zkey[b];
+        });
+    } else {
+        std::vector<std::vector<int32_t>> iset(L.n_tie);
+        for (int32_t t : lps) {
+            for (int64_t i : tie_obs[t]) iset[t].push_back(c->img_new[p->img[i]]);
+            std::sort(iset[t].begin(), iset[t].end());
+        }
+        std::stable_sort(lps.begin(), lps.end(), [&](int32_t a, int32_t b) {
+            if (tie_cam[a] != tie_cam[b]) return tie_cam[a] < tie_cam[b];
+            if (iset[a] != iset[b]) return iset[a] < iset[b];
+            return zkey[a] < zkey[b];
+        });
+    }
     c->n_lp = (int64_t)lps.size();
 
     std::vector<double> xy;
-    std::vector<int32_t> img, cam, pt, lp_start, lp_cam, cam_lp(L.n_cam + 1, 0), cam_ctl(L.n_cam + 1, 0);
+    std::vector<int32_t> img, cam, pt, lp_start, lp_cam;
     std::vector<double> ctl;
     std::vector<int64_t>& pho = c->obs_pho;
     lp_start.push_back(0);
@@ -288,7 +306,6 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         }
         lp_start.push_back((int32_t)pho.size());
         lp_cam.push_back(tie_cam[t]);
-        cam_lp[tie_cam[t] + 1]++;
     }
     c->n_obs_tie = (int64_t)pho.size();
     // control observations of this rank, sorted by camera (stable in PHO order)
@@ -305,89 +322,153 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         cam.push_back(p->cam[i]);
         pt.push_back(-1 - (int32_t)q);
         for (int m = 0; m < 3; ++m) ctl.push_back(p->xyz_fixed[3 * i + m]);
-        cam_ctl[p->cam[i] + 1]++;
-    }
-    for (int k = 0; k < L.n_cam; ++k) {
-        cam_lp[k + 1] += cam_lp[k];
-        cam_ctl[k + 1] += cam_ctl[k];
     }
     c->n_obs = (int64_t)pho.size();
     if (c->n_obs >= (int64_t)1 << 31) { set_error("too many observations per rank"); destroy(c); return FBA_ERR_UNSUPPORTED; }
     c->n_obs_pad = round_up(std::max<int64_t>(c->n_obs, 1), 64);
     c->n_lp_pad = round_up(std::max<int64_t>(c->n_lp, 1), 64);
 
-    // k_lin_point chunks: consecutive whole tie points with <= 256 observations, then control ones
+    // chunks (one k_lin_reduce / k_lin_point workgroup each): consecutive whole tie points of one
+    // camera, <= CHUNK_OBS observations and <= CHUNK_PTS points, then control observations of one
+    // camera, <= CHUNK_OBS at a time
     std::vector<int32_t> chunk_obs{0}, chunk_pt{0};
+    int64_t chunk_terms = 0;
     for (int64_t lp = 0; lp < c->n_lp; ++lp) {
-        if (lp_start[lp + 1] - lp_start[lp] > 256) {
+        if (lp_start[lp + 1] - lp_start[lp] > CHUNK_OBS) {
             set_error("a tie point with more than 256 observations: not implemented in this build");
             destroy(c);
             return FBA_ERR_UNSUPPORTED;
         }
-        if (lp_start[lp + 1] - chunk_obs.back() > 256) {
+        const int64_t n_lp_obs = lp_start[lp + 1] - lp_start[lp];
+        const int64_t lp_terms = n_lp_obs * (n_lp_obs - 1) / 2;
+        const bool split = lp > chunk_pt.back() &&
+                           (lp_start[lp + 1] - chunk_obs.back() > CHUNK_OBS || lp - chunk_pt.back() >= CHUNK_PTS ||
+                            lp_cam[lp] != lp_cam[lp - 1] || chunk_terms + lp_terms > CHUNK_TERMS);
+        if (split) {
             chunk_obs.push_back(lp_start[lp]);
             chunk_pt.push_back((int32_t)lp);
+            chunk_terms = 0;
         }
+        chunk_terms += lp_terms;
     }
     if (c->n_lp > 0) {
         chunk_obs.push_back(lp_start[c->n_lp]);
         chunk_pt.push_back((int32_t)c->n_lp);
     }
-    for (int64_t o = c->n_obs_tie; o < c->n_obs; o += 256) {
-        chunk_obs.push_back((int32_t)std::min<int64_t>(o + 256, c->n_obs));
+    for (int64_t o = c->n_obs_tie; o < c->n_obs;) {
+        int64_t e = o + 1;
+        while (e < c->n_obs && e - o < CHUNK_OBS && cam[e] == cam[o]) ++e;
+        chunk_obs.push_back((int32_t)e);
         chunk_pt.push_back((int32_t)c->n_lp);
+        o = e;
     }
     c->n_chunks = (int64_t)chunk_obs.size() - 1;
 
-    // per image CSR of local observations (PHO order within an image)
-    std::vector<int32_t> img_start(L.n_img + 1, 0), img_obs(c->n_obs);
-    {
-        std::vector<int64_t> ord(c->n_obs);
-        std::iota(ord.begin(), ord.end(), 0);
-        std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
-            return img[a] != img[b] ? img[a] < img[b] : pho[a] < pho[b];
-        });
-        for (int64_t q = 0; q < c->n_obs; ++q) {
-            img_obs[q] = (int32_t)ord[q];
-            img_start[img[ord[q]] + 1]++;
-        }
-        for (int e = 0; e < L.n_img; ++e) img_start[e + 1] += img_start[e];
-    }
-
-    // co-visible image pairs: for every local point, every pair of its observations in distinct images
-    std::vector<std::tuple<int32_t, int32_t, int32_t, int32_t>> terms;  // (e1, e2, i, j), e1 > e2
-    for (int64_t lp = 0; lp < c->n_lp; ++lp) {
-        const int a0 = lp_start[lp], a1 = lp_start[lp + 1];
-        for (int i = a0; i < a1; ++i)
-            for (int j = a0; j < a1; ++j) {
-                if (img[i] == img[j]) {
-                    if (i != j) {
-                        set_error("a tie point is measured twice in one image: not implemented in this build");
-                        destroy(c);
-                        return FBA_ERR_UNSUPPORTED;
+    // accumulation plan (k_lin_reduce): per chunk its co-visible pair keys with their (i, j)
+    // observation terms and its image keys with their observations; per pair / image / camera the
+    // partial slots the reduce kernels add up, in chunk order
+    AccPlan& A = c->acc;
+    std::vector<int32_t> ck_cam, ck_pk{0}, pk_t{0}, pk_term, ck_ik{0}, ik_o{0}, ik_obs;
+    std::vector<std::pair<int32_t, int32_t>> pk_key;
+    std::vector<int32_t> ik_img;
+    for (int64_t ch = 0; ch < c->n_chunks; ++ch) {
+        const int o0 = chunk_obs[ch], o1 = chunk_obs[ch + 1];
+        ck_cam.push_back(cam[o0]);
+        std::vector<std::tuple<int32_t, int32_t, int32_t>> tk;  // (e1, e2, term), e1 > e2, point order
+        for (int32_t lp = chunk_pt[ch]; lp < chunk_pt[ch + 1]; ++lp)
+            for (int i = lp_start[lp]; i < lp_start[lp + 1]; ++i)
+                for (int j = lp_start[lp]; j < lp_start[lp + 1]; ++j) {
+                    if (img[i] == img[j]) {
+                        if (i != j) {
+                            set_error("a tie point is measured twice in one image: not implemented in this build");
+                            destroy(c);
+                            return FBA_ERR_UNSUPPORTED;
+                        }
+                        continue;
                     }
-                    continue;
+                    if (img[i] > img[j]) tk.emplace_back(img[i], img[j], (i - o0) | ((j - o0) << 16));
                 }
-                if (img[i] > img[j]) terms.emplace_back(img[i], img[j], i, j);
+        std::stable_sort(tk.begin(), tk.end(), [](const auto& x, const auto& y) {
+            return std::get<0>(x) != std::get<0>(y) ? std::get<0>(x) < std::get<0>(y) : std::get<1>(x) < std::get<1>(y);
+        });
+        for (size_t q = 0; q < tk.size(); ++q) {
+            if (q == 0 || std::get<0>(tk[q]) != std::get<0>(tk[q - 1]) || std::get<1>(tk[q]) != std::get<1>(tk[q - 1])) {
+                if (q > 0) pk_t.push_back((int32_t)pk_term.size());
+                pk_key.emplace_back(std::get<0>(tk[q]), std::get<1>(tk[q]));
             }
-    }
-    std::sort(terms.begin(), terms.end());
-    std::vector<int32_t> pair_e, pair_start, pair_ij;
-    for (size_t q = 0; q < terms.size(); ++q) {
-        const auto& tq = terms[q];
-        if (q == 0 || std::get<0>(tq) != std::get<0>(terms[q - 1]) || std::get<1>(tq) != std::get<1>(terms[q - 1])) {
-            pair_e.push_back(std::get<0>(tq));
-            pair_e.push_back(std::get<1>(tq));
-            pair_start.push_back((int32_t)q);
+            pk_term.push_back(std::get<2>(tk[q]));
         }
-        pair_ij.push_back(std::get<2>(tq));
-        pair_ij.push_back(std::get<3>(tq));
+        if (!tk.empty()) pk_t.push_back((int32_t)pk_term.size());
+        ck_pk.push_back((int32_t)pk_key.size());
+        std::vector<std::pair<int32_t, int32_t>> io;  // (image, local obs)
+        for (int o = o0; o < o1; ++o) io.emplace_back(img[o], o - o0);
+        std::sort(io.begin(), io.end());
+        for (size_t q = 0; q < io.size(); ++q) {
+            if (q == 0 || io[q].first != io[q - 1].first) {
+                if (q > 0) ik_o.push_back((int32_t)ik_obs.size());
+                ik_img.push_back(io[q].first);
+            }
+            ik_obs.push_back(io[q].second);
+        }
+        if (!io.empty()) ik_o.push_back((int32_t)ik_obs.size());
+        ck_ik.push_back((int32_t)ik_img.size());
     }
-    pair_start.push_back((int32_t)terms.size());
-    c->n_pairs = (int64_t)pair_e.size() / 2;
-    c->n_pair_terms = (int64_t)terms.size();
-    terms.clear();
-    terms.shrink_to_fit();
+    // the local co-visible pairs and, per pair, its partial slots
+    std::vector<std::pair<int32_t, int32_t>> lpairs(pk_key);
+    std::sort(lpairs.begin(), lpairs.end());
+    lpairs.erase(std::unique(lpairs.begin(), lpairs.end()), lpairs.end());
+    c->n_pairs = (int64_t)lpairs.size();
+    c->n_pair_terms = (int64_t)pk_term.size();
+    std::vector<int32_t> rp_start(c->n_pairs + 1, 0), rp_list(pk_key.size()), rp_e;
+    {
+        std::vector<int32_t> pid(pk_key.size());
+        for (size_t q = 0; q < pk_key.size(); ++q) {
+            pid[q] = (int32_t)(std::lower_bound(lpairs.begin(), lpairs.end(), pk_key[q]) - lpairs.begin());
+            rp_start[pid[q] + 1]++;
+        }
+        for (int64_t q = 0; q < c->n_pairs; ++q) rp_start[q + 1] += rp_start[q];
+        std::vector<int32_t> fill(rp_start.begin(), rp_start.end() - 1);
+        for (size_t q = 0; q < pk_key.size(); ++q) rp_list[fill[pid[q]]++] = (int32_t)q;
+        for (auto& q : lpairs) { rp_e.push_back(q.first); rp_e.push_back(q.second); }
+    }
+    std::vector<int32_t> ri_start(L.n_img + 1, 0), ri_list(ik_img.size()), img_cam(L.n_img, -1);
+    {
+        for (int32_t e : ik_img) ri_start[e + 1]++;
+        for (int e = 0; e < L.n_img; ++e) ri_start[e + 1] += ri_start[e];
+        std::vector<int32_t> fill(ri_start.begin(), ri_start.end() - 1);
+        for (size_t q = 0; q < ik_img.size(); ++q) ri_list[fill[ik_img[q]]++] = (int32_t)q;
+        for (int64_t o = 0; o < c->n_obs; ++o) img_cam[img[o]] = cam[o];
+    }
+    std::vector<int32_t> rc_start(L.n_cam + 1, 0), rc_list(c->n_chunks);
+    {
+        for (int32_t k : ck_cam) rc_start[k + 1]++;
+        for (int k = 0; k < L.n_cam; ++k) rc_start[k + 1] += rc_start[k];
+        std::vector<int32_t> fill(rc_start.begin(), rc_start.end() - 1);
+        for (int64_t ch = 0; ch < c->n_chunks; ++ch) rc_list[fill[ck_cam[ch]]++] = (int32_t)ch;
+    }
+    A.n_pk = (int64_t)pk_key.size();
+    A.n_ik = (int64_t)ik_img.size();
+    std::vector<int32_t> abuf;
+    auto put = [&](const std::vector<int32_t>& v) {
+        const int64_t off = (int64_t)abuf.size();
+        abuf.insert(abuf.end(), v.begin(), v.end());
+        return off;
+    };
+    A.ck_cam = put(ck_cam);
+    A.ck_pk = put(ck_pk);
+    A.pk_t = put(pk_t);
+    A.pk_term = put(pk_term);
+    A.ck_ik = put(ck_ik);
+    A.ik_o = put(ik_o);
+    A.ik_obs = put(ik_obs);
+    A.rp_start = put(rp_start);
+    A.rp_e = put(rp_e);
+    A.rp_list = put(rp_list);
+    A.ri_start = put(ri_start);
+    A.ri_list = put(ri_list);
+    A.img_cam = put(img_cam);
+    A.rc_start = put(rc_start);
+    A.rc_list = put(rc_list);
     // the co-visible image pairs of ALL tie points (identical on every rank): the compact reduce
     // buffer of ranks > 1 and the block envelope of the reduced system
     std::vector<int32_t> gpairs;
@@ -439,10 +520,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     if ((rc = upload(&c->d_xy, xy)) || (rc = upload(&c->d_img, img)) || (rc = upload(&c->d_cam, cam)) ||
         (rc = upload(&c->d_pt, pt)) || (rc = upload(&c->d_ctl, ctl)) || (rc = upload(&c->d_lp_tie, lp_tie)) ||
         (rc = upload(&c->d_lp_start, lp_start)) || (rc = upload(&c->d_lp_cam, lp_cam)) ||
-        (rc = upload(&c->d_img_start, img_start)) || (rc = upload(&c->d_img_obs, img_obs)) ||
-        (rc = upload(&c->d_cam_lp, cam_lp)) || (rc = upload(&c->d_cam_ctl, cam_ctl)) ||
-        (rc = upload(&c->d_pair_e, pair_e)) || (rc = upload(&c->d_pair_start, pair_start)) ||
-        (rc = upload(&c->d_pair_ij, pair_ij)) || (rc = upload(&c->d_xfull, c->xfull0)) ||
+        (rc = upload(&c->d_acc, abuf)) || (rc = upload(&c->d_xfull, c->xfull0)) ||
         (rc = upload(&c->d_caminfo, caminfo)) || (rc = upload(&c->d_active, active)) ||
         (rc = upload(&c->d_counted, counted)) || (rc = upload(&c->d_obs_pho, pho)) ||
         (rc = upload(&c->d_chunk_obs, chunk_obs)) || (rc = upload(&c->d_chunk_pt, chunk_pt)) ||
@@ -457,12 +535,14 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     c->pt_comp = 12 + 6 * L.cw;
     const int npk = L.cw * (L.cw + 1) / 2 + L.cw;
     c->n_part = (int)std::max<int64_t>((L.u_full + 255) / 256, (c->n_obs + 255) / 256 * 3) + 8;
-    if ((rc = dalloc(&c->d_delta, L.u_full)) || (rc = dalloc(&c->d_img_tab, (size_t)L.n_img * IMG_TAB)) ||
+    if ((rc = dalloc(&c->d_delta, L.u_full)) || (rc = dalloc(&c->d_xlin, L.u_full)) || (rc = dalloc(&c->d_img_tab, (size_t)L.n_img * IMG_TAB)) ||
         (rc = dalloc(&c->d_cam_tab, (size_t)L.n_cam * c->cam_tab_stride)) ||
         (rc = dalloc(&c->d_G, (size_t)std::max(L.n_img, 1) * 42)) ||
         (rc = dalloc(&c->d_J, (size_t)c->ncomp * c->n_obs_pad)) || (rc = dalloc(&c->d_WT, (size_t)36 * c->n_obs_pad)) ||
         (rc = dalloc(&c->d_pt_tab, (size_t)c->pt_comp * c->n_lp_pad)) ||
-        (rc = dalloc(&c->d_slab, (size_t)std::max(L.n_cam, 1) * NSLAB * npk)) ||
+        (rc = dalloc(&c->d_ppart, (size_t)A.n_pk * 36)) ||
+        (rc = dalloc(&c->d_ipart, (size_t)A.n_ik * (27 + 6 * L.cw))) ||
+        (rc = dalloc(&c->d_cpart, (size_t)c->n_chunks * npk)) ||
         (rc = dalloc(&c->d_S, (size_t)(L.n_pad + NB) * L.ld)) || (rc = dalloc(&c->d_X, (size_t)L.n_pad)) ||
         (rc = dalloc(&c->d_dinv, (size_t)(L.n_pad / NB) * 8 * 256)) ||
         (rc = dalloc(&c->d_linv, (size_t)(L.n_pad / NB) * NB * NB)) ||
@@ -471,7 +551,8 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         destroy(c);
         return rc;
     }
-    if ((rc = chol_setup(*c))) { destroy(c); return rc; }
+    if ((rc = chol_setup(*c)) || (rc = acc_setup(*c))) { destroy(c); return rc; }
+    if (getenv("FBA_LR_PROFILE") && c->n_chunks > 0) FBA_HIP(hipMalloc((void**)&c->d_lrprof, sizeof(uint64_t) * 8 * c->n_chunks));
     FBA_HIP(hipMemset(c->d_delta, 0, sizeof(double) * L.u_full));
     FBA_HIP(hipMemset(c->d_scal, 0, sizeof(double) * 16));
     FBA_HIP(hipHostMalloc((void**)&c->h_pinned, sizeof(double) * 64));
@@ -502,11 +583,25 @@ static inline void mark(Ctx* c, int i) {
 static int accumulate(Ctx* c) {
     int rc;
     mark(c, 0);
-    if ((rc = launch_params(*c)) || (rc = launch_linearize(*c))) return rc;
+    if ((rc = launch_params(*c))) return rc;
+    FBA_HIP(hipMemcpyAsync(c->d_xlin, c->d_xfull, sizeof(double) * c->L.u_full, hipMemcpyDeviceToDevice, c->stream));
     mark(c, 1);
-    if ((rc = launch_point(*c))) return rc;
     mark(c, 2);
     if ((rc = launch_accumulate(*c))) return rc;
+    if (c->d_lrprof) {  // FBA_LR_PROFILE: per-phase averages of k_lin_reduce (us)
+        std::vector<uint64_t> tp(8 * c->n_chunks);
+        FBA_HIP(hipMemcpyAsync(tp.data(), c->d_lrprof, sizeof(uint64_t) * tp.size(), hipMemcpyDeviceToHost, c->stream));
+        FBA_HIP(hipStreamSynchronize(c->stream));
+        double ph[5] = {0, 0, 0, 0, 0};
+        uint64_t lo = UINT64_MAX, hi = 0;
+        for (int64_t ch = 0; ch < c->n_chunks; ++ch) {
+            for (int i = 0; i < 5; ++i) ph[i] += (double)(tp[8 * ch + i + 1] - tp[8 * ch + i]) * 0.01 / (double)c->n_chunks;
+            lo = std::min(lo, tp[8 * ch]);
+            hi = std::max(hi, tp[8 * ch + 5]);
+        }
+        fprintf(stderr, "[fba] k_lin_reduce per chunk (us): model %.2f points %.2f couplings %.2f stage+camera %.2f "
+                "items %.2f; span %.1f\n", ph[0], ph[1], ph[2], ph[3], ph[4], (double)(hi - lo) * 0.01);
+    }
     if (c->opt.world > 1 && (rc = launch_pack(*c, 0))) return rc;
     mark(c, 3);
     c->have_lin = true;
@@ -735,8 +830,11 @@ int fba_residuals(fba_ctx* ctx, double* v, double* rsd, double* stats) {
     Ctx* c = reinterpret_cast<Ctx*>(ctx);
     if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }
     if (!c->have_lin || !c->have_delta) { set_error("fba_residuals needs at least one iteration"); return FBA_ERR_ARG; }
-    int rc = launch_residuals(*c);
-    if (rc) return rc;
+    // v = A delta + w with A, w of the last linearisation (main.m:569): its Jacobian rows again, at
+    // the parameters it was taken at
+    int rc;
+    if ((rc = launch_params(*c, c->d_xlin)) || (rc = launch_linearize(*c, c->d_xlin)) || (rc = launch_residuals(*c)))
+        return rc;
     const int64_t n = c->n_obs;
     const int nblk = (int)((n + 255) / 256);
     std::vector<double> res(7 * (size_t)n), part(3 * (size_t)nblk);

@@ -17,7 +17,10 @@
 namespace fba {
 
 constexpr int NB = 128;       // Cholesky block size (rows/cols of one panel block, fba_chol.hip)
-constexpr int NSLAB = 512;    // slabs per camera in the two-stage camera-block reduction
+constexpr int CHUNK_OBS = 256;  // observations per k_lin_reduce / k_lin_point workgroup (chunk)
+constexpr int CHUNK_PTS = 64;   // tie points per chunk
+constexpr int CHUNK_TERMS = 2048;  // co-visibility terms per chunk staged in LDS (a single larger point
+                                   // is read from HBM instead)
 
 // per-image device table (k_params): eop[6], M[9], dM/domega[9], dM/dphi[9], dM/dkappa[9], pad
 constexpr int IMG_TAB = 48;
@@ -55,6 +58,27 @@ struct Sched {
     std::vector<int32_t> buf;     // host image of the lists (uploaded to Ctx::d_sched)
 };
 
+// Accumulation plan (fba_capi.cpp create, run by k_lin_reduce and the k_red_* kernels): offsets
+// into the int32 device buffer Ctx::d_acc.
+struct AccPlan {
+    int64_t ck_cam = 0;    // [n_chunks] camera of each chunk
+    int64_t ck_pk = 0;     // [n_chunks+1] pair-key range of each chunk
+    int64_t pk_t = 0;      // [n_pk+1] term range of each pair key
+    int64_t pk_term = 0;   // [n_terms] (i | j << 16): chunk-local observations in image e1 / e2
+    int64_t ck_ik = 0;     // [n_chunks+1] image-key range of each chunk
+    int64_t ik_o = 0;      // [n_ik+1] observation range of each image key
+    int64_t ik_obs = 0;    // chunk-local observations of each image key
+    int64_t rp_start = 0;  // [n_pairs+1] partial slots (pair keys) of each local pair, chunk order
+    int64_t rp_e = 0;      // [2 n_pairs] (e1, e2)
+    int64_t rp_list = 0;
+    int64_t ri_start = 0;  // [n_img+1] image keys of each image
+    int64_t ri_list = 0;
+    int64_t img_cam = 0;   // [n_img] camera of each image (-1: no local observation)
+    int64_t rc_start = 0;  // [n_cam+1] chunks of each camera
+    int64_t rc_list = 0;
+    int64_t n_pk = 0, n_ik = 0;
+};
+
 struct Ctx {
     fba_problem prob{};   // shallow copy (pointers valid only during fba_create)
     fba_settings set{};
@@ -87,16 +111,16 @@ struct Ctx {
     int32_t* d_lp_tie = nullptr; // [n_lp] global tie index of local point
     int32_t* d_lp_start = nullptr;   // [n_lp+1] obs range of each local point
     int32_t* d_lp_cam = nullptr;     // [n_lp] camera of each local point
-    int32_t* d_img_start = nullptr;  // [n_img+1] CSR of local obs per image
-    int32_t* d_img_obs = nullptr;
-    int32_t* d_cam_lp = nullptr;     // [n_cam+1] local point range per camera (points sorted by camera)
-    int32_t* d_cam_ctl = nullptr;    // [n_cam+1] control obs range per camera (within control section)
-    int64_t n_chunks = 0;            // k_lin_point workgroups: whole tie points, <= 256 observations
+    int64_t n_chunks = 0;            // k_lin_reduce workgroups: whole tie points of one camera
+    AccPlan acc;                     // accumulation plan (offsets into d_acc)
+    int32_t* d_acc = nullptr;
+    double* d_ppart = nullptr;       // [acc.n_pk][36] pair-block partials
+    double* d_ipart = nullptr;       // [acc.n_ik][27 + 6 cw] image partials: diagonal block, RHS, image-camera
+    uint64_t* d_lrprof = nullptr;    // FBA_LR_PROFILE: k_lin_reduce phase timestamps [n_chunks][8]
+    double* d_cpart = nullptr;       // [n_chunks][cw(cw+1)/2 + cw] camera-block partials
     int32_t* d_chunk_obs = nullptr;  // [n_chunks+1] observation range of each chunk
     int32_t* d_chunk_pt = nullptr;   // [n_chunks+1] local point range of each chunk
     int64_t n_pairs = 0, n_pair_terms = 0;
-    int32_t* d_pair_e = nullptr;     // [2*n_pairs] (e1,e2) with e1 > e2
-    int32_t* d_pair_start = nullptr; // [n_pairs+1]
     // multi-rank compact reduce buffer: the entries of S that any rank can write (global co-visible
     // image pairs, diagonal blocks, camera rows, RHS row), packed after fba_accumulate
     int64_t n_gpairs = 0, n_red = 0;
@@ -107,9 +131,9 @@ struct Ctx {
     int32_t* d_sched = nullptr;             // device image of the schedule lists (offsets in sched)
     int32_t* d_gpairs = nullptr;     // [2*n_gpairs] (e1,e2), e1 > e2, over ALL tie points
     double* d_red = nullptr;         // [n_red]
-    int32_t* d_pair_ij = nullptr;    // [2*n_pair_terms] (obs in e1, obs in e2)
 
     double* d_xfull = nullptr;   // [u_full]
+    double* d_xlin = nullptr;    // [u_full] the last linearisation point (residuals after the loop)
     double* d_delta = nullptr;   // [u_full] last de-scaled correction
     double* d_img_tab = nullptr; // [n_img*IMG_TAB]
     double* d_cam_tab = nullptr; // [n_cam*cam_tab_stride]
@@ -121,7 +145,6 @@ struct Ctx {
     double* d_pt_tab = nullptr;  // [n_lp_pad][pt_comp] Vinv(6) vb(3) b(3) Wc(3cw) Tc(3cw)
     int pt_comp = 0;
     int64_t n_lp_pad = 0;
-    double* d_slab = nullptr;    // camera reduction slabs
     double* d_S = nullptr;       // [(n_pad+NB)*ld] normal matrix (lower) + RHS rows
     double* d_X = nullptr;       // [n_pad] solution of the bordered solve
     double* d_dinv = nullptr;    // [(n_pad/NB)*8*256] inverses of the 16x16 diagonal blocks of L
@@ -165,12 +188,12 @@ void set_error(const std::string& msg);
 // kernel launchers (fba_kernels.hip / fba_chol.hip)
 std::vector<int32_t> camera_order(const fba_problem* p);  // internal image slot -> EXT row or -1 (fba_order.cpp)
 void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pairs);  // pairs: (e1, e2) slots, e1 > e2
-int launch_params(Ctx& c);
-int launch_linearize(Ctx& c);
-int launch_point(Ctx& c);
+int launch_params(Ctx& c, const double* x = nullptr);     // x: parameters (default d_xfull)
+int launch_linearize(Ctx& c, const double* x = nullptr);  // Jacobian rows to d_J (residuals, dense AwG)
 int launch_accumulate(Ctx& c);   // zero S, image, pair, camera blocks, unit diagonal for unused
 int launch_border(Ctx& c);       // alpha, G G^T border, RHS rows
-int chol_setup(Ctx& c);          // one-time kernel attributes, streams, events
+int chol_setup(Ctx& c);
+int acc_setup(Ctx& c);            // kernel attributes of the accumulation kernels          // one-time kernel attributes, streams, events
 int launch_pack(Ctx& c, int dir);  // multi-rank compact reduce buffer: 0 = S -> buffer, 1 = buffer -> S
 int launch_cholesky(Ctx& c);     // factor + forward solve of RHS rows
 int launch_backward(Ctx& c);     // border combine + backward solve -> delta_c

@@ -4,14 +4,14 @@
 //   k_params        per image: EOPs + rotation M and dM/d(omega,phi,kappa) (BuildAwG.m:163-165),
 //                   inner-constraint block G (BuildAwG.m:516-523); per camera: IOPs, rmax^(2j)
 //                   scales (BuildAwG.m:422-426)
-//   k_lin_point     one thread per image point: misclosure w (BuildAwG.m:505-512) and the 2 Jacobian
-//                   rows over [6 EOP | xp yp c K1..Knk P1 P2 | X Y Z] (BuildAwG.m:216-503) by the
-//                   chain rule of the forward model (BuildAwG.m:163-213); then, per chunk of whole
-//                   tie points in LDS, V = Jp'PJp, Vinv and the couplings W = Je'PJp, T = W Vinv
-//                   (Schur elimination of the tie points)
-//   k_image         one workgroup per image: reduced diagonal block, image-camera block, RHS rows
-//   k_pairs         one wave per co-visible image pair: off-diagonal reduced blocks
-//   k_cam_*         two-stage deterministic reduction of the camera block
+//   k_lin_reduce    per chunk of whole tie points (one camera): the misclosure w (BuildAwG.m:505-512)
+//                   and the 2 Jacobian rows over [6 EOP | xp yp c K1..Knk P1 P2 | X Y Z]
+//                   (BuildAwG.m:216-503) by the chain rule of the forward model (BuildAwG.m:163-213),
+//                   the tie-point elimination (V = Jp'PJp, its factor, couplings) and the chunk's
+//                   partial sums of every reduced block it touches, all in registers and LDS
+//   k_red_*         the partials of each reduced block added in chunk order: image-pair blocks,
+//                   image diagonal blocks + RHS + image-camera blocks, camera blocks
+//   k_lin_point     the same linearisation writing the Jacobian rows out (residuals, dense AwG)
 //   k_border        inner-constraint bordering M = S + G W G' (reference: NG = [N G; G' 0],
 //                   main.m:428-432), unit diagonal for fixed parameters, RHS rows
 //   k_backsub       tie-point corrections from the camera-side solution
@@ -235,7 +235,7 @@ __global__ __launch_bounds__(256) void k_lin_point(
     const int o0 = chunk_obs[c], o1 = chunk_obs[c + 1];
     const int p0 = chunk_pt[c], p1 = chunk_pt[c + 1];
     const int o = o0 + t;
-    const bool active = o < o1;
+    const bool active = t < CHUNK_OBS && o < o1;
     double jr[2][NJ];
     double w0 = 0.0, w1 = 0.0;
     int p = -1;
@@ -337,373 +337,393 @@ __global__ __launch_bounds__(256) void k_lin_point(
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_image: one workgroup per image; 32 observations at a time staged in LDS (J row, W/T, the
-// point's vb and Wc); thread q owns one output entry:
-//   q < 21            reduced diagonal block U_e (lower, a >= b)
-//   21 <= q < 27      reduced RHS r_e
-//   27 <= q < 27+6CW  image-camera block (camera row c, image column a)
-// Two thread groups split the staged observations; their sums are added in a fixed order.
-// The gathers are software-pipelined: the observation/point indices of chunk c+1 are fetched before
-// chunk c is published to LDS, and its rows are loaded into registers (all loads of a thread in
-// flight together) while chunk c is reduced.
+// k_lin_reduce: the Gauss-Newton linearisation and the point-reduced normal equations of one chunk
+// (<= 256 observations of <= 64 whole tie points of one camera, or control observations), from
+// registers and LDS only -- no Jacobian round trip through HBM, no gathers:
+//   (A) one thread per observation: forward model and Jacobian (obs_model, BuildAwG.m:163-503);
+//   (B) one thread per point: V = Jp'PJp, b = Jp'Pw, Wc = Jc'PJp, V^-1, vb = V^-1 b, Tc = Wc V^-1
+//       (vb, Tc to HBM for the back-substitution), and the factor R = L^-T of V = L L' (so
+//       V^-1 = R R'), rb = R'b, Uc = Wc R;
+//   (C) one thread per observation: W = Je'PJp, T = W V^-1 (to HBM, back-substitution), U = W R;
+//       the observation's P^1/2-scaled Jacobian rows and misclosures into LDS;
+//   (D) every (key, entry) of the chunk's partial sums (keys from the host plan, AccPlan):
+//         camera     Jc'PJc - Uc Uc',  Jc'Pw - Uc rb                         (summed over the chunk)
+//         image e    Je'PJe - U U' (lower), Je'Pw - U rb, Jc'PJe - Uc U'     (its observations)
+//         pair e1>e2 -sum U_i U_j'  over the chunk's points seen by both     (= -T_i W_j')
+//       each summed in a fixed order and stored as one partial; k_red_* add the partials of a
+//       block in chunk order, so the result is deterministic.
+// The Schur complement identities: W V^-1 W' = U U', W V^-1 b = U rb, Wc V^-1 W' = Uc U'.
 // ------------------------------------------------------------------------------------------------
 __constant__ int c_tri_a[21] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 4, 5, 5, 5, 5, 5, 5};
 __constant__ int c_tri_b[21] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4, 0, 1, 2, 3, 4, 5};
 
 template <int NK>
-__global__ __launch_bounds__(256) void k_image(const double* __restrict__ J, const double* __restrict__ WT,
-                                               const double* __restrict__ PT, const int32_t* __restrict__ pt,
-                                               const int32_t* __restrict__ cam, const int32_t* __restrict__ img_start,
-                                               const int32_t* __restrict__ img_obs, double* __restrict__ S, int64_t ld,
-                                               int64_t n_pad, int n_img, double px, double py) {
+struct LR {
+    static constexpr int CW = 5 + NK;
+    static constexpr int ES = 15 + 2 * CW;          // per-observation staging stride (doubles)
+    static constexpr int US = 19;                   // U row stride
+    static constexpr int PPS = 15 + 3 * CW;         // per-point: Vinv 6 | R 6 | rb 3 | Uc 3CW
+    static constexpr int NIMG = 27 + 6 * CW;        // image partial: 21 lower + 6 RHS + 6CW image-camera
+    static constexpr int NCAM = CW * (CW + 1) / 2 + CW;
+    // + ints: point of each observation, the chunk's plan (pair-key term offsets, terms, image-key
+    // observation offsets, observations)
+    static constexpr int NI = CHUNK_OBS + (CHUNK_TERMS + 1) + CHUNK_TERMS + (CHUNK_OBS + 1) + CHUNK_OBS;
+    static constexpr int CAM_SPLIT = 512 / NCAM;   // camera entries: observation sub-ranges in parallel
+    static constexpr size_t LDS = sizeof(double) * (CHUNK_OBS * ES + CHUNK_OBS * US + CHUNK_PTS * PPS + 512) +
+                                  sizeof(int) * NI;
+};
+
+constexpr int LR_THREADS = 512;  // observation phases use the first CHUNK_OBS threads, (D) all of them
+
+template <int NK>
+__global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
+    const double* __restrict__ xy, const int32_t* __restrict__ img, const int32_t* __restrict__ cam,
+    const int32_t* __restrict__ pt, const int32_t* __restrict__ lp_tie, const double* __restrict__ ctl,
+    const double* __restrict__ xfull, const double* __restrict__ img_tab, const double* __restrict__ cam_tab,
+    const int32_t* __restrict__ chunk_obs, const int32_t* __restrict__ chunk_pt, const int32_t* __restrict__ lp_start,
+    const int32_t* __restrict__ A, const AccPlan plan, double* __restrict__ WT, double* __restrict__ PT,
+    double* __restrict__ ppart, double* __restrict__ ipart, double* __restrict__ cpart, int64_t u_c, int type,
+    int cam_stride, unsigned eop_mask, unsigned cam_mask, double px, double py, uint64_t* __restrict__ tprof) {
     using LY = Lay<NK>;
-    constexpr int CW = LY::CW, NJ = LY::NJ, JS = LY::JS, PS = LY::PS;
-    constexpr int NP = 3 + 3 * CW;           // vb | Wc
-    constexpr int F = JS + 36 + NP;          // J row | W,T | vb | Wc
-    constexpr int CH = 32;
-    constexpr int NOUT = 27 + 6 * CW;
-    constexpr int NJ2 = JS / 2, NW2 = 18;
-    constexpr int RJ = (CH * NJ2 + 255) / 256, RW = (CH * NW2 + 255) / 256, RP = (CH * NP + 255) / 256;
-    static_assert(JS % 2 == 0, "J rows are read as double2");
-    __shared__ double st[CH][F + 1];
-    __shared__ double part[128];
-    __shared__ int so[2][CH], sp[2][CH];
-    const int e = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int g = tid >> 7, q = tid & 127;
-    const int i0 = img_start[e], i1 = img_start[e + 1];
-    if (i0 == i1) return;
-    int kind = 0, a = 0, b = 0;
-    if (q < 21) { kind = 0; a = c_tri_a[q]; b = c_tri_b[q]; }
-    else if (q < 27) { kind = 1; a = q - 21; }
-    else if (q < NOUT) { kind = 2; a = (q - 27) % 6; b = (q - 27) / 6; }
-    const double2* J2 = reinterpret_cast<const double2*>(J);
-    const double2* W2 = reinterpret_cast<const double2*>(WT);
-    double2 rj[RJ], rw[RW];
-    double rp[RP];
-    auto fetch_idx = [&](int base, int buf) {
-        if (tid < CH) {
-            const int o = (base + tid < i1) ? img_obs[base + tid] : 0;
-            so[buf][tid] = o;
-            sp[buf][tid] = (base + tid < i1) ? pt[o] : -1;
-        }
+    using R_ = LR<NK>;
+    // optional phase timestamps (FBA_LR_PROFILE): 100 MHz wall clock at the phase boundaries
+    auto stamp = [&](int i) {
+        if (tprof && threadIdx.x == 0) tprof[(int64_t)blockIdx.x * 8 + i] = wall_clock64();
     };
-    auto fetch_rows = [&](int buf, int n) {
-#pragma unroll
-        for (int r = 0; r < RJ; ++r) {
-            const int idx = tid + 256 * r, k = idx / NJ2, f = idx - k * NJ2;
-            if (idx < n * NJ2) rj[r] = J2[(int64_t)so[buf][k] * NJ2 + f];
-        }
-#pragma unroll
-        for (int r = 0; r < RW; ++r) {
-            const int idx = tid + 256 * r, k = idx / NW2, f = idx - k * NW2;
-            if (idx < n * NW2) rw[r] = W2[(int64_t)so[buf][k] * NW2 + f];
-        }
-#pragma unroll
-        for (int r = 0; r < RP; ++r) {
-            const int idx = tid + 256 * r, k = idx / NP, f = idx - k * NP;
-            if (idx < n * NP) {
-                const int p = sp[buf][k];
-                rp[r] = (p < 0) ? 0.0 : PT[(int64_t)p * PS + (f < 3 ? 6 + f : 12 + f - 3)];
-            }
-        }
-    };
-    auto publish = [&](int n) {
-#pragma unroll
-        for (int r = 0; r < RJ; ++r) {
-            const int idx = tid + 256 * r, k = idx / NJ2, f = idx - k * NJ2;
-            if (idx < n * NJ2) { st[k][2 * f] = rj[r].x; st[k][2 * f + 1] = rj[r].y; }
-        }
-#pragma unroll
-        for (int r = 0; r < RW; ++r) {
-            const int idx = tid + 256 * r, k = idx / NW2, f = idx - k * NW2;
-            if (idx < n * NW2) { st[k][JS + 2 * f] = rw[r].x; st[k][JS + 2 * f + 1] = rw[r].y; }
-        }
-#pragma unroll
-        for (int r = 0; r < RP; ++r) {
-            const int idx = tid + 256 * r, k = idx / NP, f = idx - k * NP;
-            if (idx < n * NP) st[k][JS + 36 + f] = rp[r];
-        }
-    };
-    fetch_idx(i0, 0);
-    __syncthreads();
-    fetch_rows(0, min(CH, i1 - i0));
-    double acc = 0.0;
-    int buf = 0;
-    for (int base = i0; base < i1; base += CH, buf ^= 1) {
-        const int n = min(CH, i1 - base);
-        const bool more = base + CH < i1;
-        if (more) fetch_idx(base + CH, buf ^ 1);
-        publish(n);
-        __syncthreads();
-        if (more) fetch_rows(buf ^ 1, min(CH, i1 - base - CH));
-        if (q < NOUT) {
-            for (int k = g; k < n; k += 2) {
-                const double* r = st[k];
-                const double ea0 = r[a], ea1 = r[NJ + a];
-                const bool tie = sp[buf][k] >= 0;
-                if (kind == 0) {
-                    acc += px * ea0 * r[b] + py * ea1 * r[NJ + b];
-                    if (tie) {
-                        const double* T = r + JS + 18 + 3 * a;
-                        const double* W = r + JS + 3 * b;
-                        acc -= T[0] * W[0] + T[1] * W[1] + T[2] * W[2];
-                    }
-                } else if (kind == 1) {
-                    acc += px * ea0 * r[2 * NJ] + py * ea1 * r[2 * NJ + 1];
-                    if (tie) {
-                        const double* W = r + JS + 3 * a;
-                        const double* vb = r + JS + 36;
-                        acc -= W[0] * vb[0] + W[1] * vb[1] + W[2] * vb[2];
-                    }
-                } else {
-                    acc += px * ea0 * r[6 + b] + py * ea1 * r[NJ + 6 + b];
-                    if (tie) {
-                        const double* T = r + JS + 18 + 3 * a;
-                        const double* Wc = r + JS + 39 + 3 * b;
-                        acc -= T[0] * Wc[0] + T[1] * Wc[1] + T[2] * Wc[2];
-                    }
-                }
-            }
-        }
-        __syncthreads();
-    }
-    if (g == 1) part[q] = acc;
-    __syncthreads();
-    if (g == 0 && q < NOUT) {
-        acc += part[q];
-        if (kind == 0) {
-            S[(int64_t)(6 * e + a) * ld + 6 * e + b] = acc;
-        } else if (kind == 1) {
-            S[n_pad * ld + 6 * e + a] = acc;
+    stamp(0);
+    constexpr int CW = LY::CW, NJ = LY::NJ, PS = LY::PS;
+    constexpr int ES = R_::ES, US = R_::US, PPS = R_::PPS, NIMG = R_::NIMG, NCAM = R_::NCAM;
+    constexpr int CAM_SPLIT = R_::CAM_SPLIT;
+    static_assert(LR_THREADS >= 512 && LR_THREADS >= CHUNK_OBS, "thread roles");
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* QE = lds;                                  // [CHUNK_OBS][ES]
+    double* Us = QE + CHUNK_OBS * ES;                  // [CHUNK_OBS][US]
+    double* PP = Us + CHUNK_OBS * US;                  // [CHUNK_PTS][PPS]
+    double* camp = PP + CHUNK_PTS * PPS;                     // [CAM_SPLIT][NCAM] camera sub-range sums
+    int* pl = reinterpret_cast<int*>(camp + 512);            // [CHUNK_OBS] chunk-local point or -1
+    int* s_pkt = pl + CHUNK_OBS;                             // [<= CHUNK_TERMS + 1] term offsets of the pair keys
+    int* s_term = s_pkt + CHUNK_TERMS + 1;                   // [<= CHUNK_TERMS]
+    int* s_iko = s_term + CHUNK_TERMS;                       // [<= CHUNK_OBS + 1] observation offsets of image keys
+    int* s_ikobs = s_iko + CHUNK_OBS + 1;                    // [<= CHUNK_OBS]
+    const int t = threadIdx.x;
+    const int c = blockIdx.x;
+    const int o0 = chunk_obs[c], o1 = chunk_obs[c + 1];
+    const int p0 = chunk_pt[c], p1 = chunk_pt[c + 1];
+    const int o = o0 + t;
+    const bool active = t < CHUNK_OBS && o < o1;
+    double jr[2][NJ];
+    double w0 = 0.0, w1 = 0.0;
+    int p = -1;
+    // (A)
+    if (active) {
+        const double x = xy[2 * (int64_t)o], y = xy[2 * (int64_t)o + 1];
+        const int e = img[o], k = cam[o];
+        p = pt[o];
+        double X, Y, Z;
+        if (p >= 0) {
+            const double* q = xfull + u_c + 3 * (int64_t)lp_tie[p];
+            X = q[0]; Y = q[1]; Z = q[2];
         } else {
-            const int k = cam[img_obs[i0]];
-            S[(int64_t)(6 * (int64_t)n_img + (int64_t)k * CW + b) * ld + 6 * e + a] = acc;
+            const double* q = ctl + 3 * (int64_t)(-1 - p);
+            X = q[0]; Y = q[1]; Z = q[2];
+        }
+        obs_model<NK>(x, y, img_tab + (int64_t)e * IMG_TAB, cam_tab + (int64_t)k * cam_stride, X, Y, Z, p >= 0, type,
+                      eop_mask, cam_mask, jr, w0, w1);
+        if (p >= 0) {
+            double* q = QE + t * ES;  // Jp (2x3) | w (2) | Jc (2xCW), raw
+#pragma unroll
+            for (int m = 0; m < 3; ++m) { q[m] = jr[0][6 + CW + m]; q[3 + m] = jr[1][6 + CW + m]; }
+            q[6] = w0;
+            q[7] = w1;
+#pragma unroll
+            for (int m = 0; m < CW; ++m) { q[8 + m] = jr[0][6 + m]; q[8 + CW + m] = jr[1][6 + m]; }
         }
     }
-}
-
-// ------------------------------------------------------------------------------------------------
-// k_pairs: off-diagonal image-image blocks S(e1,e2) = -sum W_i Vinv W_j^T = -sum T_i W_j^T over the tie
-// points the two images share; one wave per co-visible pair.  The (T_i, W_j) rows of 32 terms at a
-// time are gathered with 16-byte loads into LDS (9 per lane per chunk -- narrow per-entry loads made
-// this kernel bound by vector-memory instruction issue), the next chunk's rows and indices are in
-// flight while the current chunk is reduced; lanes 0..35 own the 6x6 entries, 4 partial sums each.
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_pairs(const double* __restrict__ WT, const int32_t* __restrict__ pair_e,
-                                              const int32_t* __restrict__ pair_start, const int32_t* __restrict__ pair_ij,
-                                              double* __restrict__ S, int64_t ld, int64_t n_pairs) {
-    // XCD-aware: workgroups are dealt round-robin over the 8 XCDs, so block b works on pair
-    // (b % 8) * per + b / 8 -- each XCD walks a contiguous run of the (e1, e2)-sorted pair list and
-    // the W/T rows of an image's observations are re-read from that XCD's L2
-    const int64_t per = (n_pairs + 7) / 8;
-    const int64_t pr = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
-    if (pr >= n_pairs) return;
-    constexpr int CH = 32, RS = 18;  // terms per chunk, doubles per staged row
-    __shared__ __attribute__((aligned(16))) double rows[CH][2][RS];
-    __shared__ int2 idx[2][CH];
-    const int q = threadIdx.x;
-    const int a = q / 6, b = q % 6;
-    const int e1 = pair_e[2 * pr], e2 = pair_e[2 * pr + 1];
-    const int t0 = pair_start[pr], t1 = pair_start[pr + 1];
-    const int nch = (t1 - t0 + CH - 1) / CH;
-    const int2* ij2 = reinterpret_cast<const int2*>(pair_ij);
-    const double2* WT2 = reinterpret_cast<const double2*>(WT);
-    // item it (< 2*9*CH): term it / 18, row (it / 9) & 1 (0: T_i = WT[i][18..36), 1: W_j = WT[j][0..18)),
-    // 16-byte part it % 9
-    constexpr int NR = (2 * 9 * CH + 63) / 64;  // 9 loads per lane
-    double2 rv[NR];
-    int2 iv = make_int2(0, 0);
-    auto fetch_rows = [&](int c, int buf) {
-        const int n = min(CH, t1 - t0 - c * CH);
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            const int it = q + 64 * r, k = it / 18, row = (it / 9) & 1, part = it % 9;
-            if (k < n) {
-                const int2 t = idx[buf][k];
-                rv[r] = WT2[(int64_t)(row ? t.y : t.x) * 18 + (row ? 0 : 9) + part];
-            }
-        }
-    };
-    auto fetch_idx = [&](int c) {
-        if (q < CH && t0 + c * CH + q < t1) iv = ij2[t0 + c * CH + q];
-    };
-    fetch_idx(0);
-    if (q < CH) idx[0][q] = iv;
+    if (t < CHUNK_OBS) pl[t] = (active && p >= 0) ? p - p0 : -1;
     __syncthreads();
-    if (nch > 0) fetch_rows(0, 0);
-    if (nch > 1) fetch_idx(1);
-    double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
-    for (int c = 0; c < nch; ++c) {
-        const int n = min(CH, t1 - t0 - c * CH);
+    stamp(1);
+    // (B)
+    if (t < p1 - p0) {
+        const int lp = p0 + t;
+        const int a0 = lp_start[lp] - o0, a1 = lp_start[lp + 1] - o0;
+        double V00 = 0, V01 = 0, V02 = 0, V11 = 0, V12 = 0, V22 = 0, b0 = 0, b1 = 0, b2 = 0;
+        double Wc[CW][3];
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            const int it = q + 64 * r, k = it / 18, row = (it / 9) & 1, part = it % 9;
-            if (k < n) *reinterpret_cast<double2*>(&rows[k][row][2 * part]) = rv[r];
-        }
-        if (c + 1 < nch && q < CH) idx[(c + 1) & 1][q] = iv;
-        __syncthreads();
-        if (c + 1 < nch) fetch_rows(c + 1, (c + 1) & 1);
-        if (c + 2 < nch) fetch_idx(c + 2);
-        if (q < 36) {
-            int k = 0;
-            for (; k + 4 <= n; k += 4) {
-                const double* T0 = rows[k][0] + 3 * a; const double* W0 = rows[k][1] + 3 * b;
-                const double* T1 = rows[k + 1][0] + 3 * a; const double* W1 = rows[k + 1][1] + 3 * b;
-                const double* T2 = rows[k + 2][0] + 3 * a; const double* W2 = rows[k + 2][1] + 3 * b;
-                const double* T3 = rows[k + 3][0] + 3 * a; const double* W3 = rows[k + 3][1] + 3 * b;
-                acc0 -= T0[0] * W0[0] + T0[1] * W0[1] + T0[2] * W0[2];
-                acc1 -= T1[0] * W1[0] + T1[1] * W1[1] + T1[2] * W1[2];
-                acc2 -= T2[0] * W2[0] + T2[1] * W2[1] + T2[2] * W2[2];
-                acc3 -= T3[0] * W3[0] + T3[1] * W3[1] + T3[2] * W3[2];
-            }
-            for (; k < n; ++k) {
-                const double* T = rows[k][0] + 3 * a;
-                const double* W = rows[k][1] + 3 * b;
-                acc0 -= T[0] * W[0] + T[1] * W[1] + T[2] * W[2];
-            }
-        }
-        __syncthreads();
-    }
-    if (q < 36) S[(int64_t)(6 * e1 + a) * ld + 6 * e2 + b] = (acc0 + acc1) + (acc2 + acc3);
-}
-
-// ------------------------------------------------------------------------------------------------
-// camera block: stage 1 (NSLAB x n_cam workgroups) -> slabs, stage 2 -> S.  Each slab covers a
-// contiguous range of the camera's tie points (their observations are contiguous) and of its
-// control observations; observations and point rows are staged through LDS 32 at a time.
-// entry q < CW(CW+1)/2: lower (c1 >= c2);  q >= that: RHS entry c
-// ------------------------------------------------------------------------------------------------
-template <int NK>
-__global__ __launch_bounds__(128) void k_cam_stage1(const double* __restrict__ J, const double* __restrict__ PT,
-                                                    const int32_t* __restrict__ lp_start,
-                                                    const int32_t* __restrict__ cam_lp, const int32_t* __restrict__ cam_ctl,
-                                                    double* __restrict__ slab, int64_t n_obs_tie, double px, double py) {
-    using LY = Lay<NK>;
-    constexpr int CW = LY::CW, NJ = LY::NJ, JS = LY::JS, PS = LY::PS;
-    constexpr int NPK = CW * (CW + 1) / 2;
-    constexpr int CH = 32;
-    constexpr int FP = 3 + 6 * CW;  // vb, Wc, Tc of a point
-    __shared__ double so[CH][2 * CW + 3];
-    __shared__ double sp[CH][FP + 1];
-    const int s = blockIdx.x, k = blockIdx.y, q = threadIdx.x;
-    int c1 = 0, c2 = -1;
-    if (q < NPK) {
-        int rem = q;
-        while (rem > c1) { rem -= c1 + 1; ++c1; }
-        c2 = rem;
-    } else {
-        c1 = q - NPK;
-    }
-    const bool act = q < NPK + CW;
-    double acc = 0.0;
-    const int64_t p0 = cam_lp[k], p1 = cam_lp[k + 1];
-    const int64_t np = p1 - p0;
-    const int64_t a0 = p0 + np * s / NSLAB, a1 = p0 + np * (s + 1) / NSLAB;
-    const int64_t q0 = cam_ctl[k], q1 = cam_ctl[k + 1];
-    const int64_t nq = q1 - q0;
-    const int64_t b0 = q0 + nq * s / NSLAB, b1 = q0 + nq * (s + 1) / NSLAB;
-    // direct terms over the observations: tie observations of points [a0,a1), then control ones.
-    // Chunks of 32 observations; the rows of chunk c+1 are loaded into registers while chunk c is
-    // reduced from LDS.
-    const int64_t oa0 = (a0 < a1) ? lp_start[a0] : 0, oa1 = (a0 < a1) ? lp_start[a1] : 0;
-    const int64_t ob0 = n_obs_tie + b0, ob1 = n_obs_tie + b1;
-    const int nc0 = (int)((oa1 - oa0 + CH - 1) / CH), nc1 = (int)((ob1 - ob0 + CH - 1) / CH);
-    constexpr int FO = 2 * CW + 2;
-    constexpr int RO = (CH * FO + 127) / 128, RPT = (CH * FP + 127) / 128;
-    auto chunk = [&](int c, int64_t& base) -> int {
-        if (c < nc0) { base = oa0 + (int64_t)c * CH; return (int)min((int64_t)CH, oa1 - base); }
-        base = ob0 + (int64_t)(c - nc0) * CH;
-        return (int)min((int64_t)CH, ob1 - base);
-    };
-    double ro[RO];
-    auto fetch_o = [&](int c) {
-        int64_t base;
-        const int n = chunk(c, base);
+        for (int q = 0; q < CW; ++q) Wc[q][0] = Wc[q][1] = Wc[q][2] = 0.0;
+        for (int i = a0; i < a1; ++i) {
+            const double* r = QE + i * ES;
 #pragma unroll
-        for (int r = 0; r < RO; ++r) {
-            const int idx = q + 128 * r, kk = idx / FO, f = idx - kk * FO;
-            if (idx < n * FO) {
-                const double* row = J + (base + kk) * JS;
-                ro[r] = (f < CW) ? row[6 + f] : (f < 2 * CW ? row[NJ + 6 + f - CW] : row[2 * NJ + f - 2 * CW]);
-            }
-        }
-        return n;
-    };
-    const int nco = nc0 + nc1;
-    int n_cur = nco > 0 ? fetch_o(0) : 0;
-    for (int c = 0; c < nco; ++c) {
-        const int n = n_cur;
+            for (int row = 0; row < 2; ++row) {
+                const double pr = row ? py : px;
+                const double j0 = r[3 * row], j1 = r[3 * row + 1], j2 = r[3 * row + 2], wv = r[6 + row];
+                const double q0 = pr * j0, q1 = pr * j1, q2 = pr * j2;
+                V00 += q0 * j0; V01 += q0 * j1; V02 += q0 * j2;
+                V11 += q1 * j1; V12 += q1 * j2; V22 += q2 * j2;
+                b0 += q0 * wv; b1 += q1 * wv; b2 += q2 * wv;
 #pragma unroll
-        for (int r = 0; r < RO; ++r) {
-            const int idx = q + 128 * r, kk = idx / FO, f = idx - kk * FO;
-            if (idx < n * FO) so[kk][f] = ro[r];
-        }
-        __syncthreads();
-        if (c + 1 < nco) n_cur = fetch_o(c + 1);
-        if (act)
-            for (int kk = 0; kk < n; ++kk) {
-                const double* r = so[kk];
-                const double s0 = (c2 >= 0) ? r[c2] : r[2 * CW];
-                const double s1 = (c2 >= 0) ? r[CW + c2] : r[2 * CW + 1];
-                acc += px * r[c1] * s0 + py * r[CW + c1] * s1;
-            }
-        __syncthreads();
-    }
-    // Schur terms of the points [a0, a1), pipelined the same way
-    double rpt[RPT];
-    auto fetch_p = [&](int64_t base) {
-        const int n = (int)min((int64_t)CH, a1 - base);
-#pragma unroll
-        for (int r = 0; r < RPT; ++r) {
-            const int idx = q + 128 * r, kk = idx / FP, f = idx - kk * FP;
-            if (idx < n * FP) rpt[r] = PT[(base + kk) * PS + 6 + (f < 3 ? f : f + 3)];
-        }
-        return n;
-    };
-    n_cur = a0 < a1 ? fetch_p(a0) : 0;
-    for (int64_t base = a0; base < a1; base += CH) {
-        const int n = n_cur;
-#pragma unroll
-        for (int r = 0; r < RPT; ++r) {
-            const int idx = q + 128 * r, kk = idx / FP, f = idx - kk * FP;
-            if (idx < n * FP) sp[kk][f] = rpt[r];
-        }
-        __syncthreads();
-        if (base + CH < a1) n_cur = fetch_p(base + CH);
-        if (act)
-            for (int kk = 0; kk < n; ++kk) {
-                const double* r = sp[kk];  // vb 0..2, Wc 3.., Tc 3+3CW..
-                if (c2 >= 0) {
-                    const double* T = r + 3 + 3 * CW + 3 * c1;
-                    const double* W = r + 3 + 3 * c2;
-                    acc -= T[0] * W[0] + T[1] * W[1] + T[2] * W[2];
-                } else {
-                    const double* W = r + 3 + 3 * c1;
-                    acc -= W[0] * r[0] + W[1] * r[1] + W[2] * r[2];
+                for (int q = 0; q < CW; ++q) {
+                    const double jc = r[8 + row * CW + q];
+                    Wc[q][0] += jc * q0; Wc[q][1] += jc * q1; Wc[q][2] += jc * q2;
                 }
             }
-        __syncthreads();
+        }
+        // symmetric 3x3 inverse (adjugate)
+        const double c00 = V11 * V22 - V12 * V12, c01 = V02 * V12 - V01 * V22, c02 = V01 * V12 - V02 * V11;
+        const double id = 1.0 / (V00 * c00 + V01 * c01 + V02 * c02);
+        const double I00 = c00 * id, I01 = c01 * id, I02 = c02 * id;
+        const double I11 = (V00 * V22 - V02 * V02) * id, I12 = (V01 * V02 - V00 * V12) * id,
+                     I22 = (V00 * V11 - V01 * V01) * id;
+        double* P = PT + (int64_t)lp * PS;
+        P[6] = I00 * b0 + I01 * b1 + I02 * b2;
+        P[7] = I01 * b0 + I11 * b1 + I12 * b2;
+        P[8] = I02 * b0 + I12 * b1 + I22 * b2;
+#pragma unroll
+        for (int q = 0; q < CW; ++q) {
+            P[12 + 3 * CW + 3 * q] = Wc[q][0] * I00 + Wc[q][1] * I01 + Wc[q][2] * I02;
+            P[13 + 3 * CW + 3 * q] = Wc[q][0] * I01 + Wc[q][1] * I11 + Wc[q][2] * I12;
+            P[14 + 3 * CW + 3 * q] = Wc[q][0] * I02 + Wc[q][1] * I12 + Wc[q][2] * I22;
+        }
+        // V = L L', R = L^-T (upper): r00 = m00, r01 = m10, r02 = m20, r11 = m11, r12 = m21, r22 = m22
+        const double l00 = sqrt(V00), l10 = V01 / l00, l20 = V02 / l00;
+        const double l11 = sqrt(V11 - l10 * l10), l21 = (V12 - l20 * l10) / l11;
+        const double l22 = sqrt(V22 - l20 * l20 - l21 * l21);
+        const double m00 = 1.0 / l00, m11 = 1.0 / l11, m22 = 1.0 / l22;
+        const double m10 = -l10 * m00 * m11, m21 = -l21 * m11 * m22, m20 = -(l20 * m00 + l21 * m10) * m22;
+        double* pp = PP + t * PPS;
+        pp[0] = I00; pp[1] = I01; pp[2] = I02; pp[3] = I11; pp[4] = I12; pp[5] = I22;
+        pp[6] = m00; pp[7] = m10; pp[8] = m20; pp[9] = m11; pp[10] = m21; pp[11] = m22;
+        pp[12] = m00 * b0;
+        pp[13] = m10 * b0 + m11 * b1;
+        pp[14] = m20 * b0 + m21 * b1 + m22 * b2;
+#pragma unroll
+        for (int q = 0; q < CW; ++q) {
+            pp[15 + 3 * q] = Wc[q][0] * m00;
+            pp[16 + 3 * q] = Wc[q][0] * m10 + Wc[q][1] * m11;
+            pp[17 + 3 * q] = Wc[q][0] * m20 + Wc[q][1] * m21 + Wc[q][2] * m22;
+        }
     }
-    if (act) slab[((int64_t)k * NSLAB + s) * (NPK + CW) + q] = acc;
+    __syncthreads();
+    stamp(2);
+    // (C)
+    if (active) {
+        double* u = Us + t * US;
+        if (p >= 0) {
+            const double* pp = PP + (p - p0) * PPS;
+            const double I00 = pp[0], I01 = pp[1], I02 = pp[2], I11 = pp[3], I12 = pp[4], I22 = pp[5];
+            const double r00 = pp[6], r01 = pp[7], r02 = pp[8], r11 = pp[9], r12 = pp[10], r22 = pp[11];
+            double* To = WT + (int64_t)o * 36 + 18;
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+                const double e0 = px * jr[0][a], e1 = py * jr[1][a];
+                const double v0 = e0 * jr[0][6 + CW + 0] + e1 * jr[1][6 + CW + 0];
+                const double v1 = e0 * jr[0][6 + CW + 1] + e1 * jr[1][6 + CW + 1];
+                const double v2 = e0 * jr[0][6 + CW + 2] + e1 * jr[1][6 + CW + 2];
+                To[3 * a] = v0 * I00 + v1 * I01 + v2 * I02;
+                To[3 * a + 1] = v0 * I01 + v1 * I11 + v2 * I12;
+                To[3 * a + 2] = v0 * I02 + v1 * I12 + v2 * I22;
+                u[3 * a] = v0 * r00;
+                u[3 * a + 1] = v0 * r01 + v1 * r11;
+                u[3 * a + 2] = v0 * r02 + v1 * r12 + v2 * r22;
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < 18; ++m) u[m] = 0.0;
+        }
+        const double sx = sqrt(px), sy = sqrt(py);
+        double* E = QE + t * ES;  // own row: the point phase has finished reading it
+#pragma unroll
+        for (int a = 0; a < 6; ++a) { E[a] = sx * jr[0][a]; E[6 + a] = sy * jr[1][a]; }
+        E[12] = sx * w0;
+        E[13] = sy * w1;
+#pragma unroll
+        for (int q = 0; q < CW; ++q) { E[14 + q] = sx * jr[0][6 + q]; E[14 + CW + q] = sy * jr[1][6 + q]; }
+    }
+    __syncthreads();
+    stamp(3);
+    // (D) camera entries first (the longest items), then image keys, then pair keys.  The chunk's
+    // plan lists are staged in LDS first (every inner loop then runs out of LDS); the terms of a
+    // chunk holding one point with more than CHUNK_TERMS of them stay in HBM.
+    const int kp0 = A[plan.ck_pk + c], kp1 = A[plan.ck_pk + c + 1];
+    const int ki0 = A[plan.ck_ik + c], ki1 = A[plan.ck_ik + c + 1];
+    const int tb0 = A[plan.pk_t + kp0], ntm = A[plan.pk_t + kp1] - tb0;
+    const int ob0 = A[plan.ik_o + ki0], nio = A[plan.ik_o + ki1] - ob0;
+    const bool stage_terms = ntm <= CHUNK_TERMS;
+    for (int i = t; i <= kp1 - kp0 && stage_terms; i += LR_THREADS) s_pkt[i] = A[plan.pk_t + kp0 + i] - tb0;
+    for (int i = t; i < ntm && stage_terms; i += LR_THREADS) s_term[i] = A[plan.pk_term + tb0 + i];
+    for (int i = t; i <= ki1 - ki0; i += LR_THREADS) s_iko[i] = A[plan.ik_o + ki0 + i] - ob0;
+    for (int i = t; i < nio; i += LR_THREADS) s_ikobs[i] = A[plan.ik_obs + ob0 + i];
+    const int nob = o1 - o0, np = p1 - p0;
+    // camera entries: CAM_SPLIT observation sub-ranges in parallel
+    if (t < CAM_SPLIT * NCAM) {
+        constexpr int NPK = CW * (CW + 1) / 2;
+        const int it = t % NCAM, part = t / NCAM;
+        int c1 = 0, c2 = -1;
+        if (it < NPK) {
+            int rem = it;
+            while (rem > c1) { rem -= c1 + 1; ++c1; }
+            c2 = rem;
+        } else {
+            c1 = it - NPK;
+        }
+        const int l0 = nob * part / CAM_SPLIT, l1 = nob * (part + 1) / CAM_SPLIT;
+        double s = 0.0;
+        for (int l = l0; l < l1; ++l) {
+            const double* r = QE + l * ES;
+            const double s0 = (c2 >= 0) ? r[14 + c2] : r[12];
+            const double s1 = (c2 >= 0) ? r[14 + CW + c2] : r[13];
+            s += r[14 + c1] * s0 + r[14 + CW + c1] * s1;
+        }
+        if (part == CAM_SPLIT - 1)  // the points' Schur terms with the last sub-range
+            for (int q = 0; q < np; ++q) {
+                const double* pp = PP + q * PPS;
+                const double* u1 = pp + 15 + 3 * c1;
+                const double* u2 = (c2 >= 0) ? pp + 15 + 3 * c2 : pp + 12;
+                s -= u1[0] * u2[0] + u1[1] * u2[1] + u1[2] * u2[2];
+            }
+        camp[part * NCAM + it] = s;
+    }
+    __syncthreads();
+    if (t < NCAM) {
+        double s = 0.0;
+        for (int part = 0; part < CAM_SPLIT; ++part) s += camp[part * NCAM + t];
+        cpart[(int64_t)c * NCAM + t] = s;
+    }
+    stamp(4);
+    const int* pkt = stage_terms ? s_pkt : A + plan.pk_t + kp0;
+    const int* term = stage_terms ? s_term : A + plan.pk_term + tb0;
+    const int toff = stage_terms ? 0 : tb0;
+    // one thread per (key, row a): image keys first, then pair keys; each thread keeps its row's
+    // outputs in registers (independent accumulators), the rows it reads are LDS broadcasts
+    const int n2 = 6 * (ki1 - ki0), n3 = n2 + 6 * (kp1 - kp0);
+    for (int it = t; it < n3; it += LR_THREADS) {
+        if (it < n2) {
+            const int K = ki0 + it / 6, a = it % 6;
+            double d[6], ic[CW], r = 0.0;
+#pragma unroll
+            for (int b = 0; b < 6; ++b) d[b] = 0.0;
+#pragma unroll
+            for (int q = 0; q < CW; ++q) ic[q] = 0.0;
+            for (int x = s_iko[K - ki0]; x < s_iko[K - ki0 + 1]; ++x) {
+                const int l = s_ikobs[x];
+                const double* E = QE + l * ES;
+                const double* u = Us + l * US;
+                const double ea = E[a], fa = E[6 + a];
+                const double u0 = u[3 * a], u1 = u[3 * a + 1], u2 = u[3 * a + 2];
+#pragma unroll
+                for (int b = 0; b < 6; ++b)
+                    d[b] += ea * E[b] + fa * E[6 + b] - (u0 * u[3 * b] + u1 * u[3 * b + 1] + u2 * u[3 * b + 2]);
+                r += ea * E[12] + fa * E[13];
+#pragma unroll
+                for (int q = 0; q < CW; ++q) ic[q] += E[14 + q] * ea + E[14 + CW + q] * fa;
+                const int pq = pl[l];
+                if (pq >= 0) {
+                    const double* pp = PP + pq * PPS;
+                    r -= u0 * pp[12] + u1 * pp[13] + u2 * pp[14];
+#pragma unroll
+                    for (int q = 0; q < CW; ++q)
+                        ic[q] -= u0 * pp[15 + 3 * q] + u1 * pp[16 + 3 * q] + u2 * pp[17 + 3 * q];
+                }
+            }
+            double* out = ipart + (int64_t)K * NIMG;
+            const int tri0 = a * (a + 1) / 2;  // lower entries (a, b <= a) at tri0 + b
+#pragma unroll
+            for (int b = 0; b < 6; ++b)
+                if (b <= a) out[tri0 + b] = d[b];
+            out[21 + a] = r;
+#pragma unroll
+            for (int q = 0; q < CW; ++q) out[27 + 6 * q + a] = ic[q];
+        } else {
+            const int K = kp0 + (it - n2) / 6, a = (it - n2) % 6;
+            double acc[6];
+#pragma unroll
+            for (int b = 0; b < 6; ++b) acc[b] = 0.0;
+            for (int q = pkt[K - kp0] - toff; q < pkt[K - kp0 + 1] - toff; ++q) {
+                const int tm = term[q];
+                const double* ui = Us + (tm & 0xffff) * US + 3 * a;
+                const double* uj = Us + (tm >> 16) * US;
+                const double i0 = ui[0], i1 = ui[1], i2 = ui[2];
+#pragma unroll
+                for (int b = 0; b < 6; ++b) acc[b] += i0 * uj[3 * b] + i1 * uj[3 * b + 1] + i2 * uj[3 * b + 2];
+            }
+            double* out = ppart + (int64_t)K * 36 + 6 * a;
+#pragma unroll
+            for (int b = 0; b < 6; ++b) out[b] = -acc[b];
+        }
+    }
+    __syncthreads();
+    stamp(5);
 }
 
+// k_red_pairs: S(e1, e2) = the sum of the pair's partials in chunk order (one wave per pair)
+__global__ __launch_bounds__(256) void k_red_pairs(const double* __restrict__ ppart, const int32_t* __restrict__ A,
+                                                   const AccPlan plan, double* __restrict__ S, int64_t ld,
+                                                   int64_t n_pairs) {
+    const int64_t pr = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (pr >= n_pairs || lane >= 36) return;
+    double s = 0.0;
+    for (int q = A[plan.rp_start + pr]; q < A[plan.rp_start + pr + 1]; ++q)
+        s += ppart[(int64_t)A[plan.rp_list + q] * 36 + lane];
+    const int64_t e1 = A[plan.rp_e + 2 * pr], e2 = A[plan.rp_e + 2 * pr + 1];
+    S[(6 * e1 + lane / 6) * ld + 6 * e2 + lane % 6] = s;
+}
+
+// k_red_images: the diagonal block, RHS and image-camera block of image e from its partials
 template <int NK>
-__global__ void k_cam_stage2(const double* __restrict__ slab, double* __restrict__ S, int64_t ld, int64_t n_pad,
-                             int n_img) {
-    constexpr int CW = 5 + NK;
-    constexpr int NPK = CW * (CW + 1) / 2;
-    const int k = blockIdx.x, q = threadIdx.x;
-    if (q >= NPK + CW) return;
-    double acc = 0.0;
-    for (int s = 0; s < NSLAB; ++s) acc += slab[((int64_t)k * NSLAB + s) * (NPK + CW) + q];
+__global__ __launch_bounds__(128) void k_red_images(const double* __restrict__ ipart, const int32_t* __restrict__ A,
+                                                    const AccPlan plan, double* __restrict__ S, int64_t ld,
+                                                    int64_t n_pad, int n_img) {
+    constexpr int CW = 5 + NK, NIMG = LR<NK>::NIMG;
+    const int e = blockIdx.x, q = threadIdx.x;
+    const int r0 = A[plan.ri_start + e], r1 = A[plan.ri_start + e + 1];
+    if (r0 == r1 || q >= NIMG) return;
+    double s = 0.0;
+    for (int x = r0; x < r1; ++x) s += ipart[(int64_t)A[plan.ri_list + x] * NIMG + q];
+    if (q < 21) {
+        S[(6 * (int64_t)e + c_tri_a[q]) * ld + 6 * e + c_tri_b[q]] = s;
+    } else if (q < 27) {
+        S[n_pad * ld + 6 * e + (q - 21)] = s;
+    } else {
+        const int k = A[plan.img_cam + e], a = (q - 27) % 6, b = (q - 27) / 6;
+        S[(6 * (int64_t)n_img + (int64_t)k * CW + b) * ld + 6 * e + a] = s;
+    }
+}
+
+// k_red_cam: camera block (lower) and camera RHS from the chunk partials of the camera; 4 groups
+// of 128 threads each add a contiguous quarter of the camera's chunks (4 loads in flight), then the
+// four sums in order
+template <int NK>
+__global__ __launch_bounds__(512) void k_red_cam(const double* __restrict__ cpart, const int32_t* __restrict__ A,
+                                                 const AccPlan plan, double* __restrict__ S, int64_t ld, int64_t n_pad,
+                                                 int n_img) {
+    constexpr int CW = 5 + NK, NCAM = LR<NK>::NCAM, NPK = CW * (CW + 1) / 2;
+    static_assert(NCAM <= 128, "one thread per camera entry");
+    __shared__ double part[4][128];
+    const int k = blockIdx.x, w = threadIdx.x >> 7, q = threadIdx.x & 127;
+    const int x0 = A[plan.rc_start + k], x1 = A[plan.rc_start + k + 1], n = x1 - x0;
+    const int y0 = x0 + n * w / 4, y1 = x0 + n * (w + 1) / 4;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    if (q < NCAM) {
+        int x = y0;
+        for (; x + 4 <= y1; x += 4) {
+            s0 += cpart[(int64_t)A[plan.rc_list + x] * NCAM + q];
+            s1 += cpart[(int64_t)A[plan.rc_list + x + 1] * NCAM + q];
+            s2 += cpart[(int64_t)A[plan.rc_list + x + 2] * NCAM + q];
+            s3 += cpart[(int64_t)A[plan.rc_list + x + 3] * NCAM + q];
+        }
+        for (; x < y1; ++x) s0 += cpart[(int64_t)A[plan.rc_list + x] * NCAM + q];
+    }
+    part[w][q] = (s0 + s1) + (s2 + s3);
+    __syncthreads();
+    if (threadIdx.x >= NCAM) return;
+    const double s = (part[0][q] + part[1][q]) + (part[2][q] + part[3][q]);
     const int64_t base = 6 * (int64_t)n_img + (int64_t)k * CW;
     if (q < NPK) {
         int c1 = 0, rem = q;
         while (rem > c1) { rem -= c1 + 1; ++c1; }
-        S[(base + c1) * ld + base + rem] = acc;
+        S[(base + c1) * ld + base + rem] = s;
     } else {
-        S[n_pad * ld + base + (q - NPK)] = acc;
+        S[n_pad * ld + base + (q - NPK)] = s;
     }
 }
 
@@ -1005,9 +1025,9 @@ static inline unsigned cam_mask(const fba_settings& s, int nk) {
 static inline double px_of(const Ctx& c) { return 1.0 / (c.set.meas_std_x * c.set.meas_std_x); }
 static inline double py_of(const Ctx& c) { return 1.0 / (c.set.meas_std_y * c.set.meas_std_y); }
 
-int launch_params(Ctx& c) {
+int launch_params(Ctx& c, const double* x) {
     const int n = c.L.n_img + c.L.n_cam;
-    k_params<<<(n + 63) / 64, 64, 0, c.stream>>>(c.d_xfull, c.d_caminfo, c.d_img_tab, c.d_cam_tab, c.d_G, c.d_active,
+    k_params<<<(n + 63) / 64, 64, 0, c.stream>>>(x ? x : c.d_xfull, c.d_caminfo, c.d_img_tab, c.d_cam_tab, c.d_G, c.d_active,
                                                    c.L.n_img, c.L.n_cam, c.L.nk, c.L.cw, c.cam_tab_stride,
                                                    c.set.inner_constraints);
     FBA_HIP(hipGetLastError());
@@ -1015,12 +1035,12 @@ int launch_params(Ctx& c) {
 }
 
 // linearisation fused with the tie-point reduction (the dense debug path uses the same kernel)
-int launch_linearize(Ctx& c) {
+int launch_linearize(Ctx& c, const double* x) {
     if (c.n_chunks == 0) return FBA_OK;
     const unsigned em = eop_mask(c.set), cm = cam_mask(c.set, c.L.nk);
 #define LIN(NKV)                                                                                               \
     k_lin_point<NKV><<<(unsigned)c.n_chunks, 256, 0, c.stream>>>(                                              \
-        c.d_xy, c.d_img, c.d_cam, c.d_pt, c.d_lp_tie, c.d_ctl, c.d_xfull, c.d_img_tab, c.d_cam_tab,             \
+        c.d_xy, c.d_img, c.d_cam, c.d_pt, c.d_lp_tie, c.d_ctl, x ? x : c.d_xfull, c.d_img_tab, c.d_cam_tab,     \
         c.d_chunk_obs, c.d_chunk_pt, c.d_lp_start, c.d_J, c.d_WT, c.d_pt_tab, c.L.u_c, c.set.type,              \
         c.cam_tab_stride, em, cm, px_of(c), py_of(c))
     FBA_NK_DISPATCH(c.L.nk, LIN);
@@ -1029,34 +1049,34 @@ int launch_linearize(Ctx& c) {
     return FBA_OK;
 }
 
-int launch_point(Ctx& c) {
-    (void)c;  // fused into k_lin_point
-    return FBA_OK;
-}
-
 int launch_accumulate(Ctx& c) {
     const Layout& L = c.L;
     FBA_HIP(hipMemsetAsync(c.d_S, 0, sizeof(double) * (size_t)(L.n_pad + NB) * L.ld, c.stream));
+    if (c.n_chunks == 0) return FBA_OK;
+    const unsigned em = eop_mask(c.set), cm = cam_mask(c.set, c.L.nk);
     const double px = px_of(c), py = py_of(c);
-#define IMG(NKV)                                                                                          \
-    k_image<NKV><<<L.n_img, 256, 0, c.stream>>>(c.d_J, c.d_WT, c.d_pt_tab, c.d_pt, c.d_cam, c.d_img_start, \
-                                                c.d_img_obs, c.d_S, L.ld, L.n_pad, L.n_img, px, py)
-    FBA_NK_DISPATCH(L.nk, IMG);
-#undef IMG
+#define ACC(NKV)                                                                                                  \
+    k_lin_reduce<NKV><<<(unsigned)c.n_chunks, LR_THREADS, LR<NKV>::LDS, c.stream>>>(                              \
+        c.d_xy, c.d_img, c.d_cam, c.d_pt, c.d_lp_tie, c.d_ctl, c.d_xfull, c.d_img_tab, c.d_cam_tab,                \
+        c.d_chunk_obs, c.d_chunk_pt, c.d_lp_start, c.d_acc, c.acc, c.d_WT, c.d_pt_tab, c.d_ppart, c.d_ipart,       \
+        c.d_cpart, c.L.u_c, c.set.type, c.cam_tab_stride, em, cm, px, py, c.d_lrprof);                            \
+    if (c.n_pairs > 0)                                                                                            \
+        k_red_pairs<<<(unsigned)((c.n_pairs + 3) / 4), 256, 0, c.stream>>>(c.d_ppart, c.d_acc, c.acc, c.d_S, L.ld, \
+                                                                         c.n_pairs);                              \
+    k_red_images<NKV><<<(unsigned)L.n_img, 128, 0, c.stream>>>(c.d_ipart, c.d_acc, c.acc, c.d_S, L.ld, L.n_pad,   \
+                                                               L.n_img);                                          \
+    k_red_cam<NKV><<<(unsigned)L.n_cam, 512, 0, c.stream>>>(c.d_cpart, c.d_acc, c.acc, c.d_S, L.ld, L.n_pad, L.n_img)
+    FBA_NK_DISPATCH(L.nk, ACC);
+#undef ACC
     FBA_HIP(hipGetLastError());
-    if (c.n_pairs > 0) {
-        k_pairs<<<(unsigned)(8 * ((c.n_pairs + 7) / 8)), 64, 0, c.stream>>>(c.d_WT, c.d_pair_e, c.d_pair_start,
-                                                                       c.d_pair_ij, c.d_S, L.ld, c.n_pairs);
-        FBA_HIP(hipGetLastError());
-    }
-    dim3 g1(NSLAB, L.n_cam);
-#define CAM(NKV)                                                                                               \
-    k_cam_stage1<NKV><<<g1, 128, 0, c.stream>>>(c.d_J, c.d_pt_tab, c.d_lp_start, c.d_cam_lp, c.d_cam_ctl,     \
-                                                c.d_slab, c.n_obs_tie, px, py);                               \
-    k_cam_stage2<NKV><<<L.n_cam, 128, 0, c.stream>>>(c.d_slab, c.d_S, L.ld, L.n_pad, L.n_img)
-    FBA_NK_DISPATCH(L.nk, CAM);
-#undef CAM
-    FBA_HIP(hipGetLastError());
+    return FBA_OK;
+}
+
+int acc_setup(Ctx& c) {
+#define SET(NKV) \
+    FBA_HIP(hipFuncSetAttribute((const void*)k_lin_reduce<NKV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LR<NKV>::LDS))
+    FBA_NK_DISPATCH(c.L.nk, SET);
+#undef SET
     return FBA_OK;
 }
 
