@@ -166,7 +166,7 @@ static void partition(const fba_problem* p, int world, std::vector<int32_t>& tie
 static void destroy(Ctx* c) {
     if (!c) return;
     void* ptrs[] = {c->d_chunk_obs, c->d_chunk_pt, c->d_xy, c->d_img, c->d_cam, c->d_pt, c->d_ctl, c->d_lp_tie, c->d_lp_start, c->d_lp_cam,
-                    c->d_acc, c->d_ppart, c->d_ipart, c->d_cpart, c->d_lrprof, c->d_gpairs, c->d_red, c->d_xfull, c->d_xlin, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
+                    c->d_acc, c->d_ppart, c->d_ipart, c->d_cpart, c->d_cseg, c->d_bscr, c->d_lrprof, c->d_gpairs, c->d_red, c->d_xfull, c->d_xlin, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
                     c->d_pt_tab, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
                     c->d_active, c->d_counted, c->d_obs_pho, c->d_sched};
     for (void* q : ptrs)
@@ -176,6 +176,7 @@ static void destroy(Ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (auto e : c->probe_ev)
         if (e) (void)hipEventDestroy(e);
+
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -538,11 +539,13 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     if ((rc = dalloc(&c->d_delta, L.u_full)) || (rc = dalloc(&c->d_xlin, L.u_full)) || (rc = dalloc(&c->d_img_tab, (size_t)L.n_img * IMG_TAB)) ||
         (rc = dalloc(&c->d_cam_tab, (size_t)L.n_cam * c->cam_tab_stride)) ||
         (rc = dalloc(&c->d_G, (size_t)std::max(L.n_img, 1) * 42)) ||
-        (rc = dalloc(&c->d_J, (size_t)c->ncomp * c->n_obs_pad)) || (rc = dalloc(&c->d_WT, (size_t)36 * c->n_obs_pad)) ||
+        (rc = dalloc(&c->d_J, (size_t)c->ncomp * c->n_obs_pad)) || (rc = dalloc(&c->d_WT, (size_t)18 * c->n_obs_pad)) ||
         (rc = dalloc(&c->d_pt_tab, (size_t)c->pt_comp * c->n_lp_pad)) ||
         (rc = dalloc(&c->d_ppart, (size_t)A.n_pk * 36)) ||
         (rc = dalloc(&c->d_ipart, (size_t)A.n_ik * (27 + 6 * L.cw))) ||
         (rc = dalloc(&c->d_cpart, (size_t)c->n_chunks * npk)) ||
+        (rc = dalloc(&c->d_cseg, (size_t)std::max(L.n_cam, 1) * 64 * npk)) ||
+        (rc = dalloc(&c->d_bscr, (size_t)(32 * 14 + (L.n_pad / NB) * 120))) ||
         (rc = dalloc(&c->d_S, (size_t)(L.n_pad + NB) * L.ld)) || (rc = dalloc(&c->d_X, (size_t)L.n_pad)) ||
         (rc = dalloc(&c->d_dinv, (size_t)(L.n_pad / NB) * 8 * 256)) ||
         (rc = dalloc(&c->d_linv, (size_t)(L.n_pad / NB) * NB * NB)) ||
@@ -554,6 +557,9 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     if ((rc = chol_setup(*c)) || (rc = acc_setup(*c))) { destroy(c); return rc; }
     if (getenv("FBA_LR_PROFILE") && c->n_chunks > 0) FBA_HIP(hipMalloc((void**)&c->d_lrprof, sizeof(uint64_t) * 8 * c->n_chunks));
     FBA_HIP(hipMemset(c->d_delta, 0, sizeof(double) * L.u_full));
+    // outside the factor's block pattern S stays zero; the pattern itself is zeroed per accumulation
+    FBA_HIP(hipMemsetAsync(c->d_S, 0, sizeof(double) * (size_t)(L.n_pad + NB) * L.ld, c->stream));
+    FBA_HIP(hipStreamSynchronize(c->stream));
     FBA_HIP(hipMemset(c->d_scal, 0, sizeof(double) * 16));
     FBA_HIP(hipHostMalloc((void**)&c->h_pinned, sizeof(double) * 64));
     for (auto& e : c->ev) FBA_HIP(hipEventCreate(&e));

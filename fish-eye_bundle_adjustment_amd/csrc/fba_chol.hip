@@ -170,8 +170,14 @@ __device__ __forceinline__ bool leaf_factor(double (&a)[IB], double (&x)[IB], in
 constexpr int POTRF_NT = (CB / IB) * (CB / IB + 1) / 2;  // 36 lower tiles
 constexpr size_t POTRF_LDS = sizeof(double) * (POTRF_NT + 1) * IB * 17;
 
+// TS: shader-clock stamps of wave 0's critical path into ts[] (calibration builds only,
+// scripts/ubench/chol_ubench.hip)
+template <bool TS>
 __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ cols,
-                                                  double* __restrict__ dinv, double* __restrict__ scal) {
+                                                  double* __restrict__ dinv, double* __restrict__ scal,
+                                                  unsigned long long* __restrict__ ts) {
+#define POTRF_TS(i) do { if (TS && threadIdx.x == 0 && blockIdx.x == 0) ts[i] = __builtin_amdgcn_s_memtime(); } while (0)
+    POTRF_TS(0);
     const int64_t k0 = (int64_t)cols[blockIdx.x] * CB;  // one diagonal block per workgroup (one level)
     extern __shared__ __attribute__((aligned(16))) double smem[];
     // lower-triangle tiles only (80 KB, so the kernel fits beside a bulk-update workgroup on a CU):
@@ -227,7 +233,9 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
             }
         }
         if (wave == 0) {
+            POTRF_TS(1);
             ok = leaf_factor(a, x, lr);
+            POTRF_TS(2);
             if (lane < IB) {
 #pragma unroll
                 for (int c = 0; c < IB; ++c) {
@@ -249,6 +257,7 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
     for (int s = 0; s < CB / IB; ++s) {
         const int c0 = s * IB;
         __syncthreads();  // B1: L_ss, D_s in LDS; column s updated
+        POTRF_TS(3 + 4 * s);
         if (s == CB / IB - 1) break;
         // panel solve X_t = A_ts D_s^T: wave 0 tile s+1, waves 1..3 tiles s+2..7
         {
@@ -265,6 +274,7 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
             }
         }
         __syncthreads();  // B2: panel column s solved
+        POTRF_TS(4 + 4 * s);
         if (wave == 0) {
             // next diagonal tile, then its leaf factor
             const int R = c0 + IB;
@@ -281,7 +291,9 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
             double a[IB], x[IB];
 #pragma unroll
             for (int c = 0; c < IB; ++c) a[c] = AT((R + lr), R + c);
+            POTRF_TS(5 + 4 * s);
             ok &= leaf_factor(a, x, lr);
+            POTRF_TS(6 + 4 * s);
             if (lane < IB) {
 #pragma unroll
                 for (int c = 0; c < IB; ++c) {
@@ -326,7 +338,9 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
     }
     if (!ok && lane == 0 && scal[1] == 0.0) scal[1] = (double)(k0 + 1);
     store_col(CB / IB - 1, tid, 256);
+    POTRF_TS(40);
 #undef AT
+#undef POTRF_TS
 }
 
 
@@ -527,84 +541,96 @@ __global__ __launch_bounds__(256) void k_syrk_multi(double* __restrict__ S, int6
 // ------------------------------------------------------------------------------------------------
 // border combine (inner constraints): RHS rows n_pad + 0 (y) and n_pad + 1..7 (Z), length n
 // ------------------------------------------------------------------------------------------------
-// Gram matrix of the 15 forward-solved RHS rows [y | A (7) | B (7)] (row a per workgroup, fixed-order
-// reductions), into scal[32 + 15a + b]
+// k_border_gram: the Gram matrix of the 15 forward-solved RHS rows [y | A (7) | B (7)], one 128-column
+// segment per workgroup (staged in LDS): the 120 entries (a <= b) of the segment into gpart[seg][120]
 __global__ __launch_bounds__(256) void k_border_gram(const double* __restrict__ S, int64_t ld, int64_t n_pad,
-                                                     double* __restrict__ scal) {
-    __shared__ double red[4][15];
-    const int a = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const double* ra = S + (n_pad + a) * ld;
-    double acc[15];
-#pragma unroll
-    for (int b = 0; b < 15; ++b) acc[b] = 0.0;
-    for (int64_t i = tid; i < n_pad; i += 256) {
-        const double v = ra[i];
-#pragma unroll
-        for (int b = 0; b < 15; ++b) acc[b] += v * S[(n_pad + b) * ld + i];
-    }
-#pragma unroll
-    for (int b = 0; b < 15; ++b) {
-        double v = acc[b];
-#pragma unroll
-        for (int w = 32; w > 0; w >>= 1) v += __shfl_xor(v, w, 64);
-        acc[b] = v;
-    }
-    if (lane == 0)
-#pragma unroll
-        for (int b = 0; b < 15; ++b) red[wave][b] = acc[b];
+                                                     double* __restrict__ gpart) {
+    __shared__ double R[15][CB + 1];
+    __shared__ double half[2][120];
+    const int tid = threadIdx.x, seg = blockIdx.x;
+    const int64_t c0 = (int64_t)seg * CB;
+    for (int i = tid; i < 15 * CB; i += 256) R[i / CB][i % CB] = S[(n_pad + i / CB) * ld + c0 + i % CB];
     __syncthreads();
-    if (tid < 15) scal[32 + 15 * a + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+    const int e = tid % 120, h = tid / 120;  // threads 0..239: entry e, half h of the 128 columns
+    if (h < 2) {
+        int a = 0, rem = e;
+        while (rem >= 15 - a) { rem -= 15 - a; ++a; }
+        const int b = a + rem;
+        double v = 0.0;
+        for (int k = 64 * h; k < 64 * h + 64; ++k) v += R[a][k] * R[b][k];
+        half[h][e] = v;
+    }
+    __syncthreads();
+    if (tid < 120) gpart[(int64_t)seg * 120 + tid] = half[0][tid] + half[1][tid];
 }
 
-// Solve [[A'A - I, A'B], [B'A, B'B]] [z; k] = -[A'y; B'y] (14x14, partial pivoting, in LDS with
-// the workgroup's threads) and form u = y + A z + B k in the RHS row (derivation in fba_kernels.hip,
-// border section)
+// k_border_combine: every workgroup adds the Gram segments (fixed order), solves
+// [[A'A - I, A'B], [B'A, B'B]] [z; k] = -[A'y; B'y] (14x14, partial pivoting, wave 0 alone) and forms
+// u = y + A z + B k on its 256 entries of the RHS row (derivation in fba_kernels.hip, border section)
 __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, int64_t ld, int64_t n_pad,
-                                                        const double* __restrict__ scal) {
+                                                        const double* __restrict__ gpart, int nseg) {
+    __shared__ double g[15][15];
     __shared__ double H[14][16];
-    __shared__ double f[14];
     __shared__ double coef[14];
-    __shared__ int piv;
     const int tid = threadIdx.x;
-    const double* g = scal + 32;  // g[15a + b], index 0 = y, 1..7 = A, 8..14 = B
-    if (tid < 14 * 15) {
-        const int r = tid / 15, q = tid % 15;
-        H[r][q] = (q < 14) ? g[15 * (1 + r) + (1 + q)] - ((r == q && r < 7) ? 1.0 : 0.0) : -g[15 * (1 + r)];
+    if (tid < 120) {
+        int a = 0, rem = tid;
+        while (rem >= 15 - a) { rem -= 15 - a; ++a; }
+        const int b = a + rem;
+        double v0 = 0.0, v1 = 0.0;
+        int q = 0;
+        for (; q + 2 <= nseg; q += 2) {
+            v0 += gpart[(int64_t)q * 120 + tid];
+            v1 += gpart[(int64_t)(q + 1) * 120 + tid];
+        }
+        if (q < nseg) v0 += gpart[(int64_t)q * 120 + tid];
+        g[a][b] = g[b][a] = v0 + v1;
     }
     __syncthreads();
-    for (int col = 0; col < 14; ++col) {
+    if (tid < 64) {
+        // wave 0: lanes 0..13 own the rows of H; LDS traffic ordered by lgkmcnt waits in one wave
+#define WSYNC() do { __builtin_amdgcn_s_waitcnt(0xC07F); __builtin_amdgcn_wave_barrier(); } while (0)
+        for (int i = tid; i < 14 * 15; i += 64) {
+            const int r = i / 15, q = i % 15;
+            H[r][q] = (q < 14) ? g[1 + r][1 + q] - ((r == q && r < 7) ? 1.0 : 0.0) : -g[1 + r][0];
+        }
+        WSYNC();
+        for (int col = 0; col < 14; ++col) {
+            // pivot: the first row of maximal |H[r][col]|, r >= col (wave reduction, ties to the lower row)
+            double v = (tid >= col && tid < 14) ? fabs(H[tid][col]) : -1.0;
+            int p = tid;
+#pragma unroll
+            for (int w = 1; w < 16; w <<= 1) {
+                const double ov = __shfl_xor(v, w, 64);
+                const int op = __shfl_xor(p, w, 64);
+                if (ov > v || (ov == v && op < p)) { v = ov; p = op; }
+            }
+            p = __shfl(p, 0, 64);
+            if (p != col && tid < 15) {
+                const double t = H[col][tid];
+                H[col][tid] = H[p][tid];
+                H[p][tid] = t;
+            }
+            WSYNC();
+            const double f = (tid > col && tid < 14) ? H[tid][col] / H[col][col] : 0.0;
+            WSYNC();
+            if (tid > col && tid < 14)
+                for (int q = col; q < 15; ++q) H[tid][q] -= f * H[col][q];
+            WSYNC();
+        }
         if (tid == 0) {
-            int p = col;
-            for (int r = col + 1; r < 14; ++r)
-                if (fabs(H[r][col]) > fabs(H[p][col])) p = r;
-            piv = p;
+            for (int r = 13; r >= 0; --r) {
+                double v = H[r][14];
+                for (int q = r + 1; q < 14; ++q) v -= H[r][q] * coef[q];
+                coef[r] = v / H[r][r];
+            }
         }
-        __syncthreads();
-        const int p = piv;
-        if (p != col && tid < 15) {
-            const double t = H[col][tid];
-            H[col][tid] = H[p][tid];
-            H[p][tid] = t;
-        }
-        __syncthreads();
-        if (tid > col && tid < 14) f[tid] = H[tid][col] / H[col][col];
-        __syncthreads();
-        if (tid < 14 * 15) {
-            const int r = tid / 15, q = tid % 15;
-            if (r > col && q >= col) H[r][q] -= f[r] * H[col][q];
-        }
-        __syncthreads();
-    }
-    if (tid == 0) {
-        for (int r = 13; r >= 0; --r) {
-            double v = H[r][14];
-            for (int q = r + 1; q < 14; ++q) v -= H[r][q] * coef[q];
-            coef[r] = v / H[r][r];
-        }
+#undef WSYNC
     }
     __syncthreads();
-    double* yw = S + n_pad * ld;
-    for (int64_t i = tid; i < n_pad; i += 256) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + tid;
+    if (i < n_pad) {
+        double* yw = S + n_pad * ld;
         double v = yw[i];
 #pragma unroll
         for (int m = 0; m < 14; ++m) v += S[(n_pad + 1 + m) * ld + i] * coef[m];
@@ -612,17 +638,19 @@ __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, 
     }
 }
 
+constexpr size_t TRTRI_LDS = sizeof(double) * (CB * LDA + 4 * IB * 17);
+
 // ------------------------------------------------------------------------------------------------
-// k_trtri128: inverse of every 128x128 diagonal block of L (one workgroup per block, all blocks in
-// parallel after the factorisation): block forward substitution on the 8x8 grid of 16x16 tiles,
+// k_trtri128: inverse of the 128x128 diagonal blocks (the listed columns, or all; one workgroup per
+// block, after the factorisation): block forward substitution on the 8x8 grid of 16x16 tiles,
 // X_ii = D_i, X_ij = -D_i sum_{k=j}^{i-1} L_ik X_kj, on v_mfma_f64_16x16x4_f64.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_trtri128(const double* __restrict__ S, int64_t ld,
+__global__ __launch_bounds__(256) void k_trtri128(const double* __restrict__ S, int64_t ld, const int32_t* __restrict__ cols,
                                                   const double* __restrict__ dinv, double* __restrict__ linv) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* X = smem;                   // [128][LDA]
     double* Y = smem + CB * LDA;        // [4 waves][16][17]
-    const int kb = blockIdx.x;
+    const int kb = cols ? cols[blockIdx.x] : (int)blockIdx.x;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int lr = lane & 15, lk = lane >> 4;
     const double* L = S + (int64_t)kb * CB * ld + (int64_t)kb * CB;
@@ -748,7 +776,8 @@ int launch_cholesky(Ctx& c) {
     const Sched& s = c.sched;
     for (int w = 0; w < s.n_waves; ++w) {
         const Sched::Wave& W = s.w[w];
-        k_potrf128<<<(unsigned)W.ncol, 256, POTRF_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.cols, c.d_dinv, c.d_scal);
+        k_potrf128<false><<<(unsigned)W.ncol, 256, POTRF_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.cols, c.d_dinv, c.d_scal,
+                                                                          nullptr);
         k_trsm128<<<(unsigned)(2 * W.ntrsm), 256, TRSM_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.trsm, c.d_dinv);
         if (W.ntile == 0) continue;
         const bool pr = c.probe && c.probe_n < (int)c.probe_ev.size() / 2;
@@ -766,13 +795,14 @@ int launch_cholesky(Ctx& c) {
 }
 
 int launch_backward(Ctx& c) {
-    const int64_t ld = c.L.ld, nb = c.L.n_pad / CB;
-    const size_t lds_trtri = sizeof(double) * (CB * LDA + 4 * IB * 17);
+    const int64_t ld = c.L.ld;
     if (c.set.inner_constraints) {
-        k_border_gram<<<15, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_scal);
-        k_border_combine<<<1, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_scal);
+        const int nseg = (int)(c.L.n_pad / CB);
+        k_border_gram<<<(unsigned)nseg, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_bscr + 32 * 14);
+        k_border_combine<<<(unsigned)((c.L.n_pad + 255) / 256), 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad,
+                                                                                   c.d_bscr + 32 * 14, nseg);
     }
-    k_trtri128<<<(unsigned)nb, 256, lds_trtri, c.stream>>>(c.d_S, ld, c.d_dinv, c.d_linv);
+    k_trtri128<<<(unsigned)(c.L.n_pad / CB), 256, TRTRI_LDS, c.stream>>>(c.d_S, ld, nullptr, c.d_dinv, c.d_linv);
     const Sched& s = c.sched;
     for (int w = s.n_waves - 1; w >= 0; --w) {
         const Sched::BWave& B = s.b[w];
@@ -786,10 +816,10 @@ int launch_backward(Ctx& c) {
 }
 
 int chol_setup(Ctx& c) {
-    FBA_HIP(hipFuncSetAttribute((const void*)k_potrf128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)POTRF_LDS));
+    FBA_HIP(hipFuncSetAttribute((const void*)k_potrf128<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)POTRF_LDS));
     FBA_HIP(hipFuncSetAttribute((const void*)k_trsm128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRSM_LDS));
-    const size_t lds_trtri = sizeof(double) * (CB * LDA + 4 * IB * 17);
-    FBA_HIP(hipFuncSetAttribute((const void*)k_trtri128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_trtri));
+    FBA_HIP(hipFuncSetAttribute((const void*)k_trtri128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRTRI_LDS));
+
     c.probe_ev.assign(2 * std::max(c.sched.n_waves, 1), nullptr);
     for (auto& e : c.probe_ev) FBA_HIP(hipEventCreate(&e));
     return FBA_OK;

@@ -53,6 +53,8 @@ struct Sched {
     };
     int n_waves = 0;
     int64_t n_tiles = 0;
+    int64_t zero = 0;             // (block row, block column) of every block of the factor's pattern
+    int nzero = 0;                // (diagonal, panel and RHS blocks): zeroed before each accumulation
     std::vector<Wave> w;          // factorisation, level 0 up
     std::vector<BWave> b;         // backward solve, indexed by level (run top down)
     std::vector<int32_t> buf;     // host image of the lists (uploaded to Ctx::d_sched)
@@ -141,7 +143,9 @@ struct Ctx {
     double* d_G = nullptr;       // [n_img*42] inner-constraint blocks (6x7 per image, row-major)
     double* d_J = nullptr;       // [n_obs_pad][ncomp] per-obs Jacobian rows + misclosure (obs-major)
     int ncomp = 0;
-    double* d_WT = nullptr;      // [n_obs_pad][36] per-obs W (18) and T = W V^-1 (18)
+    double* d_cseg = nullptr;    // [n_cam][64][NCAM] camera segment sums (k_red_cam_seg)
+    double* d_bscr = nullptr;    // border scratch: [32][14] weight segment sums | [n_pad/NB][120] Gram segments
+    double* d_WT = nullptr;      // [n_obs_pad][18] per-obs T = W V^-1 (back-substitution)
     double* d_pt_tab = nullptr;  // [n_lp_pad][pt_comp] Vinv(6) vb(3) b(3) Wc(3cw) Tc(3cw)
     int pt_comp = 0;
     int64_t n_lp_pad = 0;

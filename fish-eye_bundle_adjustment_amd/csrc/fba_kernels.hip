@@ -97,7 +97,7 @@ __global__ void k_params(const double* __restrict__ xfull, const double* __restr
 // ------------------------------------------------------------------------------------------------
 // Device layouts (observation-major so a thread / wave touches contiguous bytes):
 //   J   [o][JS], JS = 2*NJ + 2: Jacobian row x (NJ columns: 6 EOP | CW camera | 3 XYZ), row y, w
-//   WT  [o][36]: W[a][m] = (Je' P Jp)[a][m] at 3a+m, T = W Vinv at 18+3a+m
+//   WT  [o][18]: T = W Vinv at 3a+m, W = Je' P Jp (the back-substitution's only per-observation input)
 //   PT  [p][PS], PS = 12 + 6*CW: Vinv (00 01 02 11 12 22), vb = Vinv b, b, Wc[c][m], Tc = Wc Vinv
 // ------------------------------------------------------------------------------------------------
 template <int NK>
@@ -321,17 +321,16 @@ __global__ __launch_bounds__(256) void k_lin_point(
     if (active && p >= 0) {
         const double* vi = vinv[p - p0];
         const double I00 = vi[0], I01 = vi[1], I02 = vi[2], I11 = vi[3], I12 = vi[4], I22 = vi[5];
-        double* Wo = WT + (int64_t)o * 36;
+        double* To = WT + (int64_t)o * 18;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             const double e0 = px * jr[0][a], e1 = py * jr[1][a];
             const double v0 = e0 * jr[0][6 + CW + 0] + e1 * jr[1][6 + CW + 0];
             const double v1 = e0 * jr[0][6 + CW + 1] + e1 * jr[1][6 + CW + 1];
             const double v2 = e0 * jr[0][6 + CW + 2] + e1 * jr[1][6 + CW + 2];
-            Wo[3 * a] = v0; Wo[3 * a + 1] = v1; Wo[3 * a + 2] = v2;
-            Wo[18 + 3 * a] = v0 * I00 + v1 * I01 + v2 * I02;
-            Wo[19 + 3 * a] = v0 * I01 + v1 * I11 + v2 * I12;
-            Wo[20 + 3 * a] = v0 * I02 + v1 * I12 + v2 * I22;
+            To[3 * a] = v0 * I00 + v1 * I01 + v2 * I02;
+            To[3 * a + 1] = v0 * I01 + v1 * I11 + v2 * I12;
+            To[3 * a + 2] = v0 * I02 + v1 * I12 + v2 * I22;
         }
     }
 }
@@ -511,7 +510,7 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
             const double* pp = PP + (p - p0) * PPS;
             const double I00 = pp[0], I01 = pp[1], I02 = pp[2], I11 = pp[3], I12 = pp[4], I22 = pp[5];
             const double r00 = pp[6], r01 = pp[7], r02 = pp[8], r11 = pp[9], r12 = pp[10], r22 = pp[11];
-            double* To = WT + (int64_t)o * 36 + 18;
+            double* To = WT + (int64_t)o * 18;
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
                 const double e0 = px * jr[0][a], e1 = py * jr[1][a];
@@ -689,34 +688,48 @@ __global__ __launch_bounds__(128) void k_red_images(const double* __restrict__ i
     }
 }
 
-// k_red_cam: camera block (lower) and camera RHS from the chunk partials of the camera; 4 groups
-// of 128 threads each add a contiguous quarter of the camera's chunks (4 loads in flight), then the
-// four sums in order
+// camera block (lower) and camera RHS from the chunk partials of the camera, in two fixed-order
+// stages: k_red_cam_seg sums CAM_SEG contiguous segments of the camera's chunk list in parallel
+// (one workgroup each, 4 loads in flight per thread), k_red_cam adds the segment sums in order
+constexpr int CAM_SEG = 64;
+
 template <int NK>
-__global__ __launch_bounds__(512) void k_red_cam(const double* __restrict__ cpart, const int32_t* __restrict__ A,
-                                                 const AccPlan plan, double* __restrict__ S, int64_t ld, int64_t n_pad,
-                                                 int n_img) {
-    constexpr int CW = 5 + NK, NCAM = LR<NK>::NCAM, NPK = CW * (CW + 1) / 2;
+__global__ __launch_bounds__(128) void k_red_cam_seg(const double* __restrict__ cpart, const int32_t* __restrict__ A,
+                                                     const AccPlan plan, double* __restrict__ cseg) {
+    constexpr int NCAM = LR<NK>::NCAM;
     static_assert(NCAM <= 128, "one thread per camera entry");
-    __shared__ double part[4][128];
-    const int k = blockIdx.x, w = threadIdx.x >> 7, q = threadIdx.x & 127;
-    const int x0 = A[plan.rc_start + k], x1 = A[plan.rc_start + k + 1], n = x1 - x0;
-    const int y0 = x0 + n * w / 4, y1 = x0 + n * (w + 1) / 4;
+    const int k = blockIdx.x / CAM_SEG, g = blockIdx.x % CAM_SEG, q = threadIdx.x;
+    if (q >= NCAM) return;
+    const int x0 = A[plan.rc_start + k], n = A[plan.rc_start + k + 1] - x0;
+    const int y0 = x0 + (int)((int64_t)n * g / CAM_SEG), y1 = x0 + (int)((int64_t)n * (g + 1) / CAM_SEG);
     double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    if (q < NCAM) {
-        int x = y0;
-        for (; x + 4 <= y1; x += 4) {
-            s0 += cpart[(int64_t)A[plan.rc_list + x] * NCAM + q];
-            s1 += cpart[(int64_t)A[plan.rc_list + x + 1] * NCAM + q];
-            s2 += cpart[(int64_t)A[plan.rc_list + x + 2] * NCAM + q];
-            s3 += cpart[(int64_t)A[plan.rc_list + x + 3] * NCAM + q];
-        }
-        for (; x < y1; ++x) s0 += cpart[(int64_t)A[plan.rc_list + x] * NCAM + q];
+    int x = y0;
+    for (; x + 4 <= y1; x += 4) {
+        s0 += cpart[(int64_t)A[plan.rc_list + x] * NCAM + q];
+        s1 += cpart[(int64_t)A[plan.rc_list + x + 1] * NCAM + q];
+        s2 += cpart[(int64_t)A[plan.rc_list + x + 2] * NCAM + q];
+        s3 += cpart[(int64_t)A[plan.rc_list + x + 3] * NCAM + q];
     }
-    part[w][q] = (s0 + s1) + (s2 + s3);
-    __syncthreads();
-    if (threadIdx.x >= NCAM) return;
-    const double s = (part[0][q] + part[1][q]) + (part[2][q] + part[3][q]);
+    for (; x < y1; ++x) s0 += cpart[(int64_t)A[plan.rc_list + x] * NCAM + q];
+    cseg[((int64_t)k * CAM_SEG + g) * NCAM + q] = (s0 + s1) + (s2 + s3);
+}
+
+template <int NK>
+__global__ __launch_bounds__(128) void k_red_cam(const double* __restrict__ cseg, double* __restrict__ S, int64_t ld,
+                                                 int64_t n_pad, int n_img) {
+    constexpr int CW = 5 + NK, NCAM = LR<NK>::NCAM, NPK = CW * (CW + 1) / 2;
+    const int k = blockIdx.x, q = threadIdx.x;
+    if (q >= NCAM) return;
+    const double* p = cseg + (int64_t)k * CAM_SEG * NCAM + q;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+#pragma unroll 4
+    for (int g = 0; g < CAM_SEG; g += 4) {
+        s0 += p[g * NCAM];
+        s1 += p[(g + 1) * NCAM];
+        s2 += p[(g + 2) * NCAM];
+        s3 += p[(g + 3) * NCAM];
+    }
+    const double s = (s0 + s1) + (s2 + s3);
     const int64_t base = 6 * (int64_t)n_img + (int64_t)k * CW;
     if (q < NPK) {
         int c1 = 0, rem = q;
@@ -735,16 +748,22 @@ __global__ __launch_bounds__(512) void k_red_cam(const double* __restrict__ cpar
 //   r | A = G_l W_l^1/2 | B = G D   (D = the same equilibration over all images; B'x = 0 <=> G'x = 0)
 // in k_border_combine.  scal: [1] Cholesky failure flag, [2] sumabs, [8..14] W_l, [16..22] D^2.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_border_weights(const double* __restrict__ S, const double* __restrict__ G,
-                                                         double* __restrict__ scal, int64_t ld, int n_img, int n_loc,
-                                                         int ic) {
-    __shared__ double red[16][14];
+// k_border_weights: BW_SEG workgroups, each the 14 weight sums over a contiguous range of the 6 n_img
+// EOP rows -> part[seg][14]; the consumers (k_border, k_finish_rhs) add the segments in order
+constexpr int BW_SEG = 32;
+
+__global__ __launch_bounds__(256) void k_border_weights(const double* __restrict__ S, const double* __restrict__ G,
+                                                        double* __restrict__ scal, double* __restrict__ part, int64_t ld,
+                                                        int n_img, int n_loc, int ic) {
+    __shared__ double red[4][14];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int64_t n = 6 * (int64_t)n_img;
+    const int64_t i0 = n * blockIdx.x / BW_SEG, i1 = n * (blockIdx.x + 1) / BW_SEG;
     double a[14];
 #pragma unroll
     for (int m = 0; m < 14; ++m) a[m] = 0.0;
     if (ic) {
-        for (int64_t i = tid; i < 6 * (int64_t)n_img; i += 1024) {
+        for (int64_t i = i0 + tid; i < i1; i += 256) {
             const double sii = S[i * ld + i];
             const double* g = G + (i / 6) * 42 + (i % 6) * 7;
             const bool ok = sii > 0.0, loc = i < 6 * (int64_t)n_loc;
@@ -765,19 +784,26 @@ __global__ __launch_bounds__(1024) void k_border_weights(const double* __restric
         if (lane == 0) red[wave][m] = v;
     }
     __syncthreads();
-    if (tid < 14) {
+    if (tid < 14) part[blockIdx.x * 14 + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+    if (blockIdx.x == 0 && tid == 0) scal[1] = 0.0;  // Cholesky failure flag
+}
+
+// the 14 weights (W_l: 0..6, D^2: 7..13) from the segment sums, into LDS w[14]; every thread calls it
+__device__ __forceinline__ void border_weights_lds(const double* __restrict__ part, double* w) {
+    const int t = threadIdx.x;
+    if (t < 14) {
         double v = 0.0;
-        for (int w = 0; w < 16; ++w) v += red[w][tid];
-        const int m = tid % 7;
-        if (tid < 7) scal[8 + m] = v > 0.0 ? 1.0 / v : 1.0;
-        else scal[16 + m] = v > 0.0 ? 1.0 / v : 1.0;
+        for (int g = 0; g < BW_SEG; ++g) v += part[g * 14 + t];
+        w[t] = v > 0.0 ? 1.0 / v : 1.0;
     }
-    if (tid == 0) scal[1] = 0.0;  // Cholesky failure flag
+    __syncthreads();
 }
 
 // M += G_l W_l G_l' on the 6 n_loc x 6 n_loc block (lower part)
-__global__ void k_border(double* __restrict__ S, const double* __restrict__ G, const double* __restrict__ scal,
-                         int64_t ld, int n_loc) {
+__global__ __launch_bounds__(256) void k_border(double* __restrict__ S, const double* __restrict__ G,
+                                                const double* __restrict__ part, int64_t ld, int n_loc) {
+    __shared__ double w[14];
+    border_weights_lds(part, w);
     const int64_t n = 6 * (int64_t)n_loc;
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n * n; q += (int64_t)gridDim.x * blockDim.x) {
         const int64_t i = q / n, j = q % n;
@@ -785,15 +811,19 @@ __global__ void k_border(double* __restrict__ S, const double* __restrict__ G, c
         const double* gi = G + (i / 6) * 42 + (i % 6) * 7;
         const double* gj = G + (j / 6) * 42 + (j % 6) * 7;
         double acc = 0.0;
-        for (int m = 0; m < 7; ++m) acc += gi[m] * scal[8 + m] * gj[m];
+        for (int m = 0; m < 7; ++m) acc += gi[m] * w[m] * gj[m];
         S[i * ld + j] += acc;
     }
 }
 
-__global__ void k_finish_rhs(double* __restrict__ S, const double* __restrict__ G, const double* __restrict__ scal,
-                             const uint8_t* __restrict__ active, int64_t ld, int64_t n_pad, int64_t u_c, int n_img,
-                             int n_loc, int ic) {
+__global__ __launch_bounds__(256) void k_finish_rhs(double* __restrict__ S, const double* __restrict__ G,
+                                                    double* __restrict__ scal, const double* __restrict__ part,
+                                                    const uint8_t* __restrict__ active, int64_t ld, int64_t n_pad,
+                                                    int64_t u_c, int n_img, int n_loc, int ic) {
+    __shared__ double w[14];
+    if (ic) border_weights_lds(part, w);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (ic && blockIdx.x == 0 && threadIdx.x < 14) scal[8 + (threadIdx.x / 7) * 8 + threadIdx.x % 7] = w[threadIdx.x];
     if (i >= n_pad) return;
     if (i >= u_c || !active[i]) {
         // fixed parameter or padding: decoupled unit row, zero RHS
@@ -803,8 +833,8 @@ __global__ void k_finish_rhs(double* __restrict__ S, const double* __restrict__ 
     if (ic) {
         const double* g = G + (i / 6) * 42 + (i % 6) * 7;
         for (int m = 0; m < 7; ++m) {
-            S[(n_pad + 1 + m) * ld + i] = (i < 6 * (int64_t)n_loc) ? sqrt(scal[8 + m]) * g[m] : 0.0;   // A
-            S[(n_pad + 8 + m) * ld + i] = (i < 6 * (int64_t)n_img) ? sqrt(scal[16 + m]) * g[m] : 0.0;  // B
+            S[(n_pad + 1 + m) * ld + i] = (i < 6 * (int64_t)n_loc) ? sqrt(w[m]) * g[m] : 0.0;      // A
+            S[(n_pad + 8 + m) * ld + i] = (i < 6 * (int64_t)n_img) ? sqrt(w[7 + m]) * g[m] : 0.0;  // B
         }
     }
 }
@@ -826,7 +856,7 @@ __global__ void k_backsub(const double* __restrict__ WT, const double* __restric
     double d0 = P[6], d1 = P[7], d2 = P[8];
     for (int o = lp_start[p]; o < lp_start[p + 1]; ++o) {
         const double* de = delta + 6 * (int64_t)img[o];
-        const double* T = WT + (int64_t)o * 36 + 18;
+        const double* T = WT + (int64_t)o * 18;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             d0 += T[3 * a] * de[a]; d1 += T[3 * a + 1] * de[a]; d2 += T[3 * a + 2] * de[a];
@@ -1049,9 +1079,22 @@ int launch_linearize(Ctx& c, const double* x) {
     return FBA_OK;
 }
 
+// zero the blocks of the factor's pattern (Sched::zero); 8 workgroups of 16 rows per 128x128 block
+__global__ __launch_bounds__(256) void k_zero_blocks(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ blk) {
+    const int b = blockIdx.x >> 3;
+    const int64_t r0 = (int64_t)blk[2 * b] * NB + (blockIdx.x & 7) * 16, c0 = (int64_t)blk[2 * b + 1] * NB;
+    const double2 z = {0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int i = threadIdx.x + 256 * q, r = i >> 6, c = (i & 63) * 2;
+        *reinterpret_cast<double2*>(S + (r0 + r) * ld + c0 + c) = z;
+    }
+}
+
 int launch_accumulate(Ctx& c) {
     const Layout& L = c.L;
-    FBA_HIP(hipMemsetAsync(c.d_S, 0, sizeof(double) * (size_t)(L.n_pad + NB) * L.ld, c.stream));
+    if (c.sched.nzero > 0)
+        k_zero_blocks<<<(unsigned)(8 * c.sched.nzero), 256, 0, c.stream>>>(c.d_S, L.ld, c.d_sched + c.sched.zero);
     if (c.n_chunks == 0) return FBA_OK;
     const unsigned em = eop_mask(c.set), cm = cam_mask(c.set, c.L.nk);
     const double px = px_of(c), py = py_of(c);
@@ -1065,7 +1108,8 @@ int launch_accumulate(Ctx& c) {
                                                                          c.n_pairs);                              \
     k_red_images<NKV><<<(unsigned)L.n_img, 128, 0, c.stream>>>(c.d_ipart, c.d_acc, c.acc, c.d_S, L.ld, L.n_pad,   \
                                                                L.n_img);                                          \
-    k_red_cam<NKV><<<(unsigned)L.n_cam, 512, 0, c.stream>>>(c.d_cpart, c.d_acc, c.acc, c.d_S, L.ld, L.n_pad, L.n_img)
+    k_red_cam_seg<NKV><<<(unsigned)(L.n_cam * CAM_SEG), 128, 0, c.stream>>>(c.d_cpart, c.d_acc, c.acc, c.d_cseg);  \
+    k_red_cam<NKV><<<(unsigned)L.n_cam, 128, 0, c.stream>>>(c.d_cseg, c.d_S, L.ld, L.n_pad, L.n_img)
     FBA_NK_DISPATCH(L.nk, ACC);
 #undef ACC
     FBA_HIP(hipGetLastError());
@@ -1083,14 +1127,14 @@ int acc_setup(Ctx& c) {
 int launch_border(Ctx& c) {
     const Layout& L = c.L;
     const int ic = c.set.inner_constraints;
-    k_border_weights<<<1, 1024, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, L.ld, L.n_img, c.n_loc, ic);
+    k_border_weights<<<BW_SEG, 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, c.d_bscr, L.ld, L.n_img, c.n_loc, ic);
     FBA_HIP(hipGetLastError());
     if (ic && c.n_loc > 0) {
         const int64_t n = 6 * (int64_t)c.n_loc;
-        k_border<<<(unsigned)((n * n + 255) / 256), 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, L.ld, c.n_loc);
+        k_border<<<(unsigned)((n * n + 255) / 256), 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_bscr, L.ld, c.n_loc);
         FBA_HIP(hipGetLastError());
     }
-    k_finish_rhs<<<(unsigned)((L.n_pad + 255) / 256), 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, c.d_active,
+    k_finish_rhs<<<(unsigned)((L.n_pad + 255) / 256), 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, c.d_bscr, c.d_active,
                                                                            L.ld, L.n_pad, L.u_c, L.n_img, c.n_loc, ic);
     FBA_HIP(hipGetLastError());
     return FBA_OK;

@@ -419,6 +419,14 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
         B.src = at();
         for (auto& t : tg) buf.insert(buf.end(), t.second.begin(), t.second.end());
     }
+    // the blocks the factorisation touches (everything else in S stays zero from fba_create on)
+    s.zero = at();
+    for (int64_t k = 0; k < nb; ++k) {
+        buf.push_back((int32_t)k);
+        buf.push_back((int32_t)k);
+        for (int32_t r : R[k]) { buf.push_back(r); buf.push_back((int32_t)k); }
+    }
+    s.nzero = (int)((at() - s.zero) / 2);
     s.n_tiles = ntile_total;
     s.buf = std::move(buf);
     if (c.opt.verbose)

@@ -1,0 +1,119 @@
+// Calibration micro-benchmark of the Cholesky kernels (not part of the product):
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 chol_ubench.hip -o chol_ubench
+// k_potrf128 alone on one 128x128 SPD block (timed, checked against a host Cholesky) and its
+// shader-clock breakdown (k_potrf128<true>: stamps of wave 0's critical path); k_trsm128 on a tall
+// panel; k_syrk_multi with one target / one source (the latency floor of a trailing-update launch).
+#include "../../fish-eye_bundle_adjustment_amd/csrc/fba_chol.hip"
+
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+namespace fba { void set_error(const std::string&) {} }
+using namespace fba;
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
+
+template <class F>
+static float time_us(F&& f, int reps) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    f();
+    (void)hipDeviceSynchronize();
+    float best = 1e30f;
+    for (int r = 0; r < reps; ++r) {
+        (void)hipEventRecord(a);
+        f();
+        (void)hipEventRecord(b);
+        (void)hipEventSynchronize(b);
+        float ms;
+        (void)hipEventElapsedTime(&ms, a, b);
+        best = std::min(best, ms);
+    }
+    return 1e3f * best;
+}
+
+int main() {
+    const int n = 128;
+    const int64_t ld = 8192;
+    const int64_t rows = 7808 + 128;  // 61 block rows + RHS block row
+    std::vector<double> M((size_t)rows * ld, 0.0);
+    unsigned s = 12345;
+    auto rnd = [&]() { s = s * 1664525u + 1013904223u; return (s >> 8) * (1.0 / 16777216.0) - 0.5; };
+    std::vector<double> B((size_t)n * n);
+    for (auto& b : B) b = rnd();
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            double v = 0;
+            for (int k = 0; k < n; ++k) v += B[i * n + k] * B[j * n + k];
+            M[i * ld + j] = v + (i == j ? n : 0);
+        }
+    for (int64_t i = n; i < rows; ++i)
+        for (int j = 0; j < n; ++j) M[i * ld + j] = rnd();
+    double *dS, *dinv, *scal;
+    unsigned long long* dts;
+    int32_t* dl;
+    CK(hipMalloc(&dS, M.size() * 8));
+    CK(hipMalloc(&dinv, 64 * 256 * 8));
+    CK(hipMalloc(&scal, 64 * 8));
+    CK(hipMalloc(&dts, 64 * 8));
+    CK(hipMalloc(&dl, 4096 * 4));
+    CK(hipMemset(scal, 0, 64 * 8));
+    std::vector<int32_t> lists(4096, 0);
+    // [0] = potrf column 0; [2..] = trsm tasks (0, r), r = 1..61; [200] = syrk tile (1,1), src_start {0,1}, src {0}
+    for (int r = 1; r <= 61; ++r) { lists[2 * r] = 0; lists[2 * r + 1] = r; }
+    lists[200] = 1; lists[201] = 1; lists[202] = 0; lists[203] = 1; lists[204] = 0;
+    CK(hipMemcpy(dl, lists.data(), lists.size() * 4, hipMemcpyHostToDevice));
+    CK(hipFuncSetAttribute((const void*)k_potrf128<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)POTRF_LDS));
+    CK(hipFuncSetAttribute((const void*)k_potrf128<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)POTRF_LDS));
+    CK(hipFuncSetAttribute((const void*)k_trsm128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRSM_LDS));
+    auto reset = [&]() { return hipMemcpy(dS, M.data(), M.size() * 8, hipMemcpyHostToDevice); };
+    CK(reset());
+    const float tp = time_us([&] { k_potrf128<false><<<1, 256, POTRF_LDS>>>(dS, ld, dl, dinv, scal, nullptr); }, 20);
+    // check: L from the last run (factoring the original block every time: reset, run once)
+    CK(reset());
+    k_potrf128<false><<<1, 256, POTRF_LDS>>>(dS, ld, dl, dinv, scal, nullptr);
+    CK(hipDeviceSynchronize());
+    std::vector<double> L((size_t)n * ld);
+    CK(hipMemcpy(L.data(), dS, L.size() * 8, hipMemcpyDeviceToHost));
+    double err = 0.0, nrm = 0.0;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j <= i; ++j) {
+            double v = 0;
+            for (int k = 0; k <= j; ++k) v += L[i * ld + k] * L[j * ld + k];
+            err = std::max(err, std::fabs(v - M[i * ld + j]));
+            nrm = std::max(nrm, std::fabs(M[i * ld + j]));
+        }
+    printf("k_potrf128           %8.2f us  |LL'-A|/|A| %.2e\n", tp, err / nrm);
+    CK(reset());
+    k_potrf128<true><<<1, 256, POTRF_LDS>>>(dS, ld, dl, dinv, scal, dts);
+    CK(hipDeviceSynchronize());
+    CK(reset());
+    const float tq = time_us([&] { k_potrf128<true><<<1, 256, POTRF_LDS>>>(dS, ld, dl, dinv, scal, dts); }, 1);
+    unsigned long long q[64];
+    CK(hipMemcpy(q, dts, sizeof q, hipMemcpyDeviceToHost));
+    printf("k_potrf128<TS>       %8.2f us, %llu clocks = %.2f GHz\n", tq, q[40] - q[0], (q[40] - q[0]) / (1e3 * tq));
+    printf("  start->leaf0 %llu  leaf0 %llu  ->B1 %llu\n", q[1] - q[0], q[2] - q[1], q[3] - q[2]);
+    unsigned long long tl = q[2] - q[1], tpan = 0, tdiag = 0, tend = 0;
+    for (int t = 0; t < 7; ++t) {
+        const unsigned long long pan = q[4 + 4 * t] - q[3 + 4 * t], dg = q[5 + 4 * t] - q[4 + 4 * t],
+                                 lf = q[6 + 4 * t] - q[5 + 4 * t], e = q[7 + 4 * t] - q[6 + 4 * t];
+        tpan += pan; tdiag += dg; tl += lf; tend += e;
+        printf("  s%d: B1->B2 %5llu  B2->leaf %5llu  leaf %5llu  leaf->B1 %5llu\n", t, pan, dg, lf, e);
+    }
+    printf("  totals: leaves %llu  panel(B1->B2) %llu  diag-update %llu  leaf->B1 %llu  final store %llu\n", tl, tpan,
+           tdiag, tend, q[40] - q[31]);
+    // trsm: 61 panel blocks below the factored block (two workgroups each)
+    CK(reset());
+    k_potrf128<false><<<1, 256, POTRF_LDS>>>(dS, ld, dl, dinv, scal, nullptr);
+    for (int nt : {1, 8, 61}) {
+        const float tt = time_us([&] { k_trsm128<<<(unsigned)(2 * nt), 256, TRSM_LDS>>>(dS, ld, dl + 2, dinv); }, 10);
+        printf("k_trsm128 %2d tasks   %8.2f us\n", nt, tt);
+    }
+    const float ts1 = time_us([&] { k_syrk_multi<<<4, 256>>>(dS, ld, dl + 200, dl + 202, dl + 204); }, 10);
+    printf("k_syrk_multi 1 tile   %8.2f us (K = 128)\n", ts1);
+    const float te = time_us([&] { k_neg_copy<<<1, 64>>>(dinv, dinv + 64, 1); }, 20);
+    printf("empty-ish launch      %8.2f us\n", te);
+    return 0;
+}

@@ -120,6 +120,9 @@ int main(int argc, char** argv) {
                (long)s.n_tiles);
         for (int v : per) printf(" %d", v);
         printf("\n");
+        for (int w = 0; w < s.n_waves; ++w)  // per level: columns, panel tasks, update targets, GFLOP
+            printf("level %2d: cols %3d trsm %4d tiles %5d gflop %.3f\n", w, s.w[w].ncol, s.w[w].ntrsm, s.w[w].ntile,
+                   s.w[w].flops * 1e-9);
         return 0;
     }
     const int64_t n = L.n_pad, nb = n / NB, nr = n + NB;  // rows: matrix + RHS block row
