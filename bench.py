@@ -121,18 +121,24 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    ctx.set_timing(True)
-    phases = np.zeros(8)
     barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     dsum = []
     for _ in range(args.steps):
         dsum.append(step())
-        phases += ctx.timings()
     torch.cuda.synchronize(dev)
     barrier()
     dt = time.perf_counter() - t0
+
+    # per-phase breakdown, outside the timed region: the same steps with HIP events between the phases
+    # (eager launches: the timed loop above replays the captured iteration graphs)
+    ctx.set_timing(True)
+    phases = np.zeros(8)
+    n_phase = max(1, min(args.steps, 3))
+    for _ in range(n_phase):
+        step()
+        phases += ctx.timings()
     ctx.set_timing(False)
     if world > 1:
         import torch.distributed as dist
@@ -142,7 +148,7 @@ def main():
 
     names = ["linearize", "point", "accumulate", "border", "cholesky", "backward", "update", "total"]
     ms = {n: float(v) for n, v in zip(names, phases)}
-    t, chol_flops, lin_bytes = phase_roofline(ds, ms, args.steps)
+    t, chol_flops, lin_bytes = phase_roofline(ds, ms, n_phase)
 
     # roofline of the dominant kernel, outside the timed region: one more step with HIP events
     # around every launch of the Cholesky trailing update (k_syrk_multi, one per elimination-tree

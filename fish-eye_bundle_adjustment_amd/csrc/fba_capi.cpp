@@ -167,7 +167,7 @@ static void destroy(Ctx* c) {
     if (!c) return;
     void* ptrs[] = {c->d_chunk_obs, c->d_chunk_pt, c->d_xy, c->d_img, c->d_cam, c->d_pt, c->d_ctl, c->d_lp_tie, c->d_lp_start, c->d_lp_cam,
                     c->d_acc, c->d_ppart, c->d_ipart, c->d_cpart, c->d_cseg, c->d_bscr, c->d_lrprof, c->d_gpairs, c->d_red, c->d_xfull, c->d_xlin, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
-                    c->d_pt_tab, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
+                    c->d_pt_tab, c->d_P, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
                     c->d_active, c->d_counted, c->d_obs_pho, c->d_sched};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
@@ -176,6 +176,8 @@ static void destroy(Ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (auto e : c->probe_ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto g : c->graph)
+        if (g) (void)hipGraphExecDestroy(g);
 
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -545,8 +547,9 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         (rc = dalloc(&c->d_ipart, (size_t)A.n_ik * (27 + 6 * L.cw))) ||
         (rc = dalloc(&c->d_cpart, (size_t)c->n_chunks * npk)) ||
         (rc = dalloc(&c->d_cseg, (size_t)std::max(L.n_cam, 1) * 64 * npk)) ||
-        (rc = dalloc(&c->d_bscr, (size_t)(32 * 14 + (L.n_pad / NB) * 120))) ||
-        (rc = dalloc(&c->d_S, (size_t)(L.n_pad + NB) * L.ld)) || (rc = dalloc(&c->d_X, (size_t)L.n_pad)) ||
+        (rc = dalloc(&c->d_bscr, (size_t)(32 * 14 + 16 * 120))) ||  // k_border_weights / k_border_gram segments
+        (rc = dalloc(&c->d_S, (size_t)(L.n_pad + NB) * L.ld)) ||
+        (rc = dalloc(&c->d_P, (size_t)std::max(c->sched.n_scratch, 1) * 4096)) || (rc = dalloc(&c->d_X, (size_t)L.n_pad)) ||
         (rc = dalloc(&c->d_dinv, (size_t)(L.n_pad / NB) * 8 * 256)) ||
         (rc = dalloc(&c->d_linv, (size_t)(L.n_pad / NB) * NB * NB)) ||
         (rc = dalloc(&c->d_scal, 32 + 256)) || (rc = dalloc(&c->d_part, (size_t)c->n_part)) ||
@@ -586,7 +589,40 @@ static inline void mark(Ctx* c, int i) {
     if (c->timing) (void)hipEventRecord(c->ev[i], c->stream);
 }
 
-static int accumulate(Ctx* c) {
+static bool graph_eligible(const Ctx* c) {
+    static const bool off = getenv("FBA_NO_GRAPH") && atoi(getenv("FBA_NO_GRAPH")) != 0;
+    return !off && c->graphs_ok && c->own_stream && !c->timing && !c->probe && !c->d_lrprof;
+}
+
+// run body() on the context's stream, through a graph captured from its first run when eligible
+template <class F>
+static int run_graph(Ctx* c, int which, F&& body) {
+    if (!graph_eligible(c)) return body();
+    if (!c->graph[which]) {
+        FBA_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        const int rc = body();
+        hipGraph_t g = nullptr;
+        const hipError_t e = hipStreamEndCapture(c->stream, &g);
+        if (rc != FBA_OK || e != hipSuccess || !g) {
+            if (g) (void)hipGraphDestroy(g);
+            (void)hipGetLastError();  // do not leave the capture's error to the next call's checks
+            if (rc != FBA_OK) return rc;
+            c->graphs_ok = false;  // capture unsupported here: run eagerly from now on
+            return body();
+        }
+        const hipError_t ei = hipGraphInstantiate(&c->graph[which], g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (ei != hipSuccess) {
+            c->graph[which] = nullptr;
+            c->graphs_ok = false;
+            return body();
+        }
+    }
+    FBA_HIP(hipGraphLaunch(c->graph[which], c->stream));
+    return FBA_OK;
+}
+
+static int accumulate_body(Ctx* c) {
     int rc;
     mark(c, 0);
     if ((rc = launch_params(*c))) return rc;
@@ -610,25 +646,37 @@ static int accumulate(Ctx* c) {
     }
     if (c->opt.world > 1 && (rc = launch_pack(*c, 0))) return rc;
     mark(c, 3);
-    c->have_lin = true;
     return FBA_OK;
 }
 
-static int solve_update(Ctx* c, double* dsum) {
+static int accumulate(Ctx* c) {
+    const int rc = run_graph(c, 0, [&] { return accumulate_body(c); });
+    if (rc == FBA_OK) c->have_lin = true;
+    return rc;
+}
+
+static int solve_body(Ctx* c) {
     int rc;
     const Layout& L = c->L;
-    if (!c->have_lin) { set_error("fba_solve_update before fba_accumulate"); return FBA_ERR_ARG; }
     if (c->opt.world > 1 && (rc = launch_pack(*c, 1))) return rc;
     if ((rc = launch_border(*c))) return rc;
     mark(c, 4);
     if ((rc = launch_cholesky(*c))) return rc;
     mark(c, 5);
-    FBA_HIP(hipMemsetAsync(c->d_delta + L.u_c, 0, sizeof(double) * (L.u_full - L.u_c), c->stream));
+    if (L.u_full > L.u_c)  // (a zero-byte memset is not a valid graph node)
+        FBA_HIP(hipMemsetAsync(c->d_delta + L.u_c, 0, sizeof(double) * (L.u_full - L.u_c), c->stream));
     if ((rc = launch_backward(*c))) return rc;
     mark(c, 6);
     if ((rc = launch_backsub_update(*c))) return rc;
     mark(c, 7);
     FBA_HIP(hipMemcpyAsync(c->h_pinned, c->d_scal, sizeof(double) * 4, hipMemcpyDeviceToHost, c->stream));
+    return FBA_OK;
+}
+
+static int solve_update(Ctx* c, double* dsum) {
+    int rc;
+    if (!c->have_lin) { set_error("fba_solve_update before fba_accumulate"); return FBA_ERR_ARG; }
+    if ((rc = run_graph(c, 1, [&] { return solve_body(c); }))) return rc;
     FBA_HIP(hipStreamSynchronize(c->stream));
     if (c->timing) {
         float ms;

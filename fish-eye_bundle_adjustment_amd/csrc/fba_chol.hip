@@ -16,8 +16,9 @@
 //                   v_mfma_f64_16x16x4_f64); writes L_kk and the eight 16x16 inverses D_s = L_ss^-1
 //     k_trsm128     the panel blocks of those columns, X = A L_kk^-T by blocked substitution
 //                   X_s = (A_s - sum_{t<s} X_t L_st^T) D_s^T: all MFMA, 16 rows per wave
-//     k_syrk_multi  the trailing updates of the level, C -= sum_k X_ik X_jk^T, 64x64 tiles, K = 128
-//                   per source column staged through LDS in 32-deep slices
+//     k_syrk_multi  the trailing updates of the level, C -= sum_k X_ik X_jk^T, 64x64 quarters, K = 128
+//                   per source column staged through LDS in 32-deep slices; targets with many sources
+//                   split into groups (scratch quarters, k_syrk_combine adds them in order)
 //   forward solve   the right-hand sides [r | A | B] (B = G D, D an equilibration over all images)
 //                   are stored as extra ROWS below M (one extra block row, in every panel), so the
 //                   panel solves compute Y' = (L^-1 [r A B])' as a by-product
@@ -345,7 +346,8 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
 
 
 // ------------------------------------------------------------------------------------------------
-// k_trsm128: one (column k, block row r) task per 2 workgroups, r in the panel rows of column k:
+// k_trsm128: one workgroup per 64-row half of a panel block (column k, block row r), r in the panel rows of
+// column k:
 //   X = A L^-T by blocked substitution, X_s = (A_s - sum_{t<s} X_t L_st^T) D_s^T.
 // 256 threads = 4 waves x 16 rows.  L_kk was just written by another CU, so its reads are far-cache
 // latency bound: the whole workgroup stages the 28 off-diagonal 16x16 tiles of L_kk and the eight
@@ -364,9 +366,10 @@ __global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t
     double* Dt = Lt + TRSM_NT * IB * 17;    // [8][IB][17]    D_s
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int lr = lane & 15, lk = lane >> 4;
-    // task (column k, block row r): 2 workgroups of 64 rows each
-    const int64_t k0 = (int64_t)tasks[2 * (blockIdx.x >> 1)] * CB;
-    const int64_t rbase = (int64_t)tasks[2 * (blockIdx.x >> 1) + 1] * CB + (blockIdx.x & 1) * 64 + wave * IB;
+    // record (column k, 2 r + h): rows 64 h .. 64 h + 63 of panel block (r, k)
+    const int64_t k0 = (int64_t)tasks[2 * blockIdx.x] * CB;
+    const int rh = tasks[2 * blockIdx.x + 1];
+    const int64_t rbase = (int64_t)(rh >> 1) * CB + (rh & 1) * 64 + wave * IB;
     double* Xw = X + wave * IB * LDA;
     double* Tw = T + wave * IB * 17;
     const double* L = S + k0 * ld + k0;
@@ -457,37 +460,39 @@ __global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_syrk_multi: the trailing updates of one level, C(i,j) -= sum_k X_ik X_jk^T over the level's
-// columns k whose panel holds both block rows i and j (ascending k, in one workgroup: the result does
-// not depend on the schedule).  64x64 output quarters (4 workgroups per 128x128 target, the
-// strictly upper quarter of a diagonal target skipped), K = 128 per source column staged through LDS
-// in 32-deep slices, the next slice prefetched into registers while the MFMAs of the current one run.
+// k_syrk_multi: the trailing updates of one level, one 64x64 output quarter per workgroup (task record,
+// Sched): C(i,j) -= sum_k X_ik X_jk^T over the task's source columns k (ascending), or, for a split
+// target, the partial sum of a group of sources into a scratch quarter (k_syrk_combine adds the groups
+// in order): the result does not depend on the schedule.  K = 128 per source column staged through
+// LDS in 32-deep slices, the next slice prefetched into registers while the MFMAs of the current one
+// run.
 // ------------------------------------------------------------------------------------------------
 constexpr int KS = 32;
 constexpr int LDK = 34;   // LDS stride of a 32-deep slice: bank = (4r + 2k) mod 64, conflict-free
 
-__global__ __launch_bounds__(256) void k_syrk_multi(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ tiles,
-                                                    const int32_t* __restrict__ src_start,
-                                                    const int32_t* __restrict__ src) {
+__global__ __launch_bounds__(256) void k_syrk_multi(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ tasks,
+                                                    const int32_t* __restrict__ src, double* __restrict__ P) {
     __shared__ __attribute__((aligned(16))) double As[64][LDK];
     __shared__ __attribute__((aligned(16))) double Bs[64][LDK];
-    const int t = blockIdx.x >> 2, qr = (blockIdx.x >> 1) & 1, qc = blockIdx.x & 1;
-    const int64_t bi = tiles[2 * t], bj = tiles[2 * t + 1];
-    if (bi == bj && qr == 0 && qc == 1) return;
-    const int s0 = src_start[t], nsl = 4 * (src_start[t + 1] - s0);
+    const int32_t* tk = tasks + Sched::SYRK_REC * blockIdx.x;
+    const int64_t bi = tk[0], bj = tk[1];
+    const int qr = tk[2] >> 1, qc = tk[2] & 1, s0 = tk[3], slot = tk[5];
+    const int nsl = 4 * (tk[4] - s0);
     const int32_t* ks_src = src + s0;
     const int64_t r0 = bi * CB + qr * 64, c0 = bj * CB + qc * 64;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int lr = lane & 15, lk = lane >> 4;
     const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
-    double* Cp = S + (r0 + wr + lk) * ld + c0 + wc + lr;
+    // output: the C quarter in place, or scratch quarter `slot` (row-major 64x64, starts from zero)
+    double* Cp = slot < 0 ? S + (r0 + wr + lk) * ld + c0 + wc + lr : P + (int64_t)slot * 4096 + (wr + lk) * 64 + wc + lr;
+    const int64_t ldc = slot < 0 ? ld : 64;
     dbl4 acc[2][2];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc[a][b][r] = Cp[(a * 16 + 4 * r) * ld + b * 16];
+            for (int r = 0; r < 4; ++r) acc[a][b][r] = slot < 0 ? Cp[(a * 16 + 4 * r) * ldc + b * 16] : 0.0;
     const int rr = tid >> 2, cc = (tid & 3) * 8;
     const double* ga = S + (r0 + rr) * ld + cc;
     const double* gb = S + (c0 + rr) * ld + cc;
@@ -535,31 +540,73 @@ __global__ __launch_bounds__(256) void k_syrk_multi(double* __restrict__ S, int6
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) Cp[(a * 16 + 4 * r) * ld + b * 16] = acc[a][b][r];
+            for (int r = 0; r < 4; ++r) Cp[(a * 16 + 4 * r) * ldc + b * 16] = acc[a][b][r];
+}
+
+// k_syrk_combine: C quarter += the scratch quarters of a split target in slot order (each holds the
+// negated partial sum of its source group)
+__global__ __launch_bounds__(256) void k_syrk_combine(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ comb,
+                                                      const double* __restrict__ P) {
+    const int32_t* cb = comb + Sched::COMB_REC * blockIdx.x;
+    const int64_t r0 = (int64_t)cb[0] * CB + (cb[2] >> 1) * 64, c0 = (int64_t)cb[1] * CB + (cb[2] & 1) * 64;
+    const int first = cb[3], n = cb[4];
+    double2 v[8];
+    double2* cp[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {  // thread -> 8 double2 of the quarter, all loads of a round in flight
+        const int e = 2 * (threadIdx.x + 256 * q), r = e >> 6, cl = e & 63;
+        cp[q] = reinterpret_cast<double2*>(S + (r0 + r) * ld + c0 + cl);
+        v[q] = *cp[q];
+    }
+    for (int g = 0; g < n; ++g) {
+        const double* pg = P + (int64_t)(first + g) * 4096;
+        double2 p[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) p[q] = *reinterpret_cast<const double2*>(pg + 2 * (threadIdx.x + 256 * q));
+#pragma unroll
+        for (int q = 0; q < 8; ++q) { v[q].x += p[q].x; v[q].y += p[q].y; }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) *cp[q] = v[q];
 }
 
 // ------------------------------------------------------------------------------------------------
 // border combine (inner constraints): RHS rows n_pad + 0 (y) and n_pad + 1..7 (Z), length n
 // ------------------------------------------------------------------------------------------------
-// k_border_gram: the Gram matrix of the 15 forward-solved RHS rows [y | A (7) | B (7)], one 128-column
-// segment per workgroup (staged in LDS): the 120 entries (a <= b) of the segment into gpart[seg][120]
+// k_border_gram: the Gram matrix of the 15 forward-solved RHS rows [y | A (7) | B (7)]: GRAM_SEG
+// workgroups, each a contiguous range of 128-column tiles staged through LDS, the 120 entries (a <= b)
+// of its range into gpart[seg][120]
+constexpr int GRAM_SEG = 16;
+
 __global__ __launch_bounds__(256) void k_border_gram(const double* __restrict__ S, int64_t ld, int64_t n_pad,
                                                      double* __restrict__ gpart) {
     __shared__ double R[15][CB + 1];
     __shared__ double half[2][120];
     const int tid = threadIdx.x, seg = blockIdx.x;
-    const int64_t c0 = (int64_t)seg * CB;
-    for (int i = tid; i < 15 * CB; i += 256) R[i / CB][i % CB] = S[(n_pad + i / CB) * ld + c0 + i % CB];
-    __syncthreads();
+    const int64_t nt = n_pad / CB, t0 = nt * seg / GRAM_SEG, t1 = nt * (seg + 1) / GRAM_SEG;
     const int e = tid % 120, h = tid / 120;  // threads 0..239: entry e, half h of the 128 columns
-    if (h < 2) {
-        int a = 0, rem = e;
-        while (rem >= 15 - a) { rem -= 15 - a; ++a; }
-        const int b = a + rem;
-        double v = 0.0;
-        for (int k = 64 * h; k < 64 * h + 64; ++k) v += R[a][k] * R[b][k];
-        half[h][e] = v;
+    int a = 0, rem = e;
+    while (rem >= 15 - a) { rem -= 15 - a; ++a; }
+    const int b = a + rem;
+    double v = 0.0;
+    for (int64_t t = t0; t < t1; ++t) {
+        __syncthreads();
+        double x[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int i = tid + 256 * q;
+            x[q] = i < 15 * CB ? S[(n_pad + i / CB) * ld + t * CB + i % CB] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int i = tid + 256 * q;
+            if (i < 15 * CB) R[i / CB][i % CB] = x[q];
+        }
+        __syncthreads();
+        if (h < 2)
+            for (int k = 64 * h; k < 64 * h + 64; ++k) v += R[a][k] * R[b][k];
     }
+    if (h < 2) half[h][e] = v;
     __syncthreads();
     if (tid < 120) gpart[(int64_t)seg * 120 + tid] = half[0][tid] + half[1][tid];
 }
@@ -568,7 +615,7 @@ __global__ __launch_bounds__(256) void k_border_gram(const double* __restrict__ 
 // [[A'A - I, A'B], [B'A, B'B]] [z; k] = -[A'y; B'y] (14x14, partial pivoting, wave 0 alone) and forms
 // u = y + A z + B k on its 256 entries of the RHS row (derivation in fba_kernels.hip, border section)
 __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, int64_t ld, int64_t n_pad,
-                                                        const double* __restrict__ gpart, int nseg) {
+                                                        const double* __restrict__ gpart) {
     __shared__ double g[15][15];
     __shared__ double H[14][16];
     __shared__ double coef[14];
@@ -577,14 +624,13 @@ __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, 
         int a = 0, rem = tid;
         while (rem >= 15 - a) { rem -= 15 - a; ++a; }
         const int b = a + rem;
-        double v0 = 0.0, v1 = 0.0;
-        int q = 0;
-        for (; q + 2 <= nseg; q += 2) {
-            v0 += gpart[(int64_t)q * 120 + tid];
-            v1 += gpart[(int64_t)(q + 1) * 120 + tid];
-        }
-        if (q < nseg) v0 += gpart[(int64_t)q * 120 + tid];
-        g[a][b] = g[b][a] = v0 + v1;
+        double x[GRAM_SEG];
+#pragma unroll
+        for (int q = 0; q < GRAM_SEG; ++q) x[q] = gpart[q * 120 + tid];
+        double v = 0.0;
+#pragma unroll
+        for (int q = 0; q < GRAM_SEG; ++q) v += x[q];
+        g[a][b] = g[b][a] = v;
     }
     __syncthreads();
     if (tid < 64) {
@@ -778,17 +824,18 @@ int launch_cholesky(Ctx& c) {
         const Sched::Wave& W = s.w[w];
         k_potrf128<false><<<(unsigned)W.ncol, 256, POTRF_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.cols, c.d_dinv, c.d_scal,
                                                                           nullptr);
-        k_trsm128<<<(unsigned)(2 * W.ntrsm), 256, TRSM_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.trsm, c.d_dinv);
-        if (W.ntile == 0) continue;
+        k_trsm128<<<(unsigned)W.ntrsm, 256, TRSM_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.trsm, c.d_dinv);
+        if (W.ntask == 0) continue;
         const bool pr = c.probe && c.probe_n < (int)c.probe_ev.size() / 2;
         if (pr) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
-        k_syrk_multi<<<(unsigned)(4 * W.ntile), 256, 0, c.stream>>>(c.d_S, ld, c.d_sched + W.tiles,
-                                                                     c.d_sched + W.src_start, c.d_sched + W.src);
+        k_syrk_multi<<<(unsigned)W.ntask, 256, 0, c.stream>>>(c.d_S, ld, c.d_sched + W.tasks, c.d_sched + W.src, c.d_P);
         if (pr) {
             FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], c.stream));
             c.probe_flops += W.flops;
             ++c.probe_n;
         }
+        if (W.ncomb > 0)
+            k_syrk_combine<<<(unsigned)W.ncomb, 256, 0, c.stream>>>(c.d_S, ld, c.d_sched + W.comb, c.d_P);
     }
     FBA_HIP(hipGetLastError());
     return FBA_OK;
@@ -797,10 +844,9 @@ int launch_cholesky(Ctx& c) {
 int launch_backward(Ctx& c) {
     const int64_t ld = c.L.ld;
     if (c.set.inner_constraints) {
-        const int nseg = (int)(c.L.n_pad / CB);
-        k_border_gram<<<(unsigned)nseg, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_bscr + 32 * 14);
+        k_border_gram<<<GRAM_SEG, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_bscr + 32 * 14);
         k_border_combine<<<(unsigned)((c.L.n_pad + 255) / 256), 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad,
-                                                                                   c.d_bscr + 32 * 14, nseg);
+                                                                                   c.d_bscr + 32 * 14);
     }
     k_trtri128<<<(unsigned)(c.L.n_pad / CB), 256, TRTRI_LDS, c.stream>>>(c.d_S, ld, nullptr, c.d_dinv, c.d_linv);
     const Sched& s = c.sched;

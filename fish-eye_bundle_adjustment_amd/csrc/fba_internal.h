@@ -41,10 +41,16 @@ struct Layout {
 
 // Block schedule of the reduced-system Cholesky (fba_order.cpp): one batched step per level of the
 // elimination tree.  All offsets index the int32 device buffer Ctx::d_sched.
+//   trsm records  (k, 2 r + h): panel block (r, k), row half h (halves of padding rows are skipped)
+//   task records  SYRK_REC ints: (i, j, quarter 2 qr + qc, s0, s1, slot): C(i,j) quarter -= sum of
+//                 X_ik X_jk' over the sources src[s0..s1) (ascending); slot >= 0: the sum goes to the
+//                 scratch quarter `slot` instead (split targets), combined by a COMB_REC record
+//                 (i, j, quarter, first slot, slots): C -= P_first - ... in slot order
 struct Sched {
+    static constexpr int SYRK_REC = 6, COMB_REC = 5;
     struct Wave {
-        int64_t cols = 0, trsm = 0, tiles = 0, src_start = 0, src = 0;  // offsets
-        int ncol = 0, ntrsm = 0, ntile = 0;
+        int64_t cols = 0, trsm = 0, tasks = 0, src = 0, comb = 0;  // offsets
+        int ncol = 0, ntrsm = 0, ntask = 0, ncomb = 0;
         double flops = 0.0;       // trailing-update flops of the level (kernel probe)
     };
     struct BWave {
@@ -55,6 +61,7 @@ struct Sched {
     int64_t n_tiles = 0;
     int64_t zero = 0;             // (block row, block column) of every block of the factor's pattern
     int nzero = 0;                // (diagonal, panel and RHS blocks): zeroed before each accumulation
+    int n_scratch = 0;            // 64x64 scratch quarters of the split targets (max over levels)
     std::vector<Wave> w;          // factorisation, level 0 up
     std::vector<BWave> b;         // backward solve, indexed by level (run top down)
     std::vector<int32_t> buf;     // host image of the lists (uploaded to Ctx::d_sched)
@@ -88,6 +95,10 @@ struct Ctx {
     Layout L;
     hipStream_t stream = nullptr;
     bool own_stream = false;
+    // the two halves of an iteration captured once as HIP graphs (own stream, no timing / probe /
+    // profile events; FBA_NO_GRAPH=1 disables): [0] linearise + accumulate, [1] solve + update
+    hipGraphExec_t graph[2] = {nullptr, nullptr};
+    bool graphs_ok = true;
     int device = 0;
 
     // host copies of the problem (kept for residual output, xhat mapping)
@@ -144,11 +155,12 @@ struct Ctx {
     double* d_J = nullptr;       // [n_obs_pad][ncomp] per-obs Jacobian rows + misclosure (obs-major)
     int ncomp = 0;
     double* d_cseg = nullptr;    // [n_cam][64][NCAM] camera segment sums (k_red_cam_seg)
-    double* d_bscr = nullptr;    // border scratch: [32][14] weight segment sums | [n_pad/NB][120] Gram segments
+    double* d_bscr = nullptr;    // border scratch: [32][14] weight segment sums | [16][120] Gram segments
     double* d_WT = nullptr;      // [n_obs_pad][18] per-obs T = W V^-1 (back-substitution)
     double* d_pt_tab = nullptr;  // [n_lp_pad][pt_comp] Vinv(6) vb(3) b(3) Wc(3cw) Tc(3cw)
     int pt_comp = 0;
     int64_t n_lp_pad = 0;
+    double* d_P = nullptr;       // [Sched::n_scratch][64*64] partial sums of split update targets
     double* d_S = nullptr;       // [(n_pad+NB)*ld] normal matrix (lower) + RHS rows
     double* d_X = nullptr;       // [n_pad] solution of the bordered solve
     double* d_dinv = nullptr;    // [(n_pad/NB)*8*256] inverses of the 16x16 diagonal blocks of L

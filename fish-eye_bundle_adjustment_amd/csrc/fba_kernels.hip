@@ -792,8 +792,12 @@ __global__ __launch_bounds__(256) void k_border_weights(const double* __restrict
 __device__ __forceinline__ void border_weights_lds(const double* __restrict__ part, double* w) {
     const int t = threadIdx.x;
     if (t < 14) {
+        double x[BW_SEG];
+#pragma unroll
+        for (int g = 0; g < BW_SEG; ++g) x[g] = part[g * 14 + t];
         double v = 0.0;
-        for (int g = 0; g < BW_SEG; ++g) v += part[g * 14 + t];
+#pragma unroll
+        for (int g = 0; g < BW_SEG; ++g) v += x[g];
         w[t] = v > 0.0 ? 1.0 / v : 1.0;
     }
     __syncthreads();

@@ -353,6 +353,12 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
     s.n_waves = nw;
     std::vector<std::vector<int32_t>> wave(nw);
     for (int64_t k = 0; k < nb; ++k) wave[level[k]].push_back((int32_t)k);
+    // rows of block row i that carry unknowns (the rest is padding: zero rows that stay zero, so the
+    // second 64-row half of a block row with <= 64 of them is skipped by the panel solves and updates)
+    auto real_rows = [&](int64_t i) -> int64_t {
+        if (i == nb) return L.nrhs;
+        return std::max<int64_t>(0, std::min<int64_t>(NB, L.u_c - i * NB));
+    };
     std::vector<int32_t> buf;  // device image
     auto at = [&]() { return (int64_t)buf.size(); };
     s.w.resize(nw);
@@ -364,7 +370,9 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
         buf.insert(buf.end(), wave[w].begin(), wave[w].end());
         W.trsm = at();
         for (int32_t k : wave[w])
-            for (int32_t r : R[k]) { buf.push_back(k); buf.push_back(r); }
+            for (int32_t r : R[k])
+                for (int h = 0; h < 2; ++h)
+                    if (h == 0 || real_rows(r) > NB / 2) { buf.push_back(k); buf.push_back(2 * r + h); }
         W.ntrsm = (int)((at() - W.trsm) / 2);
         // trailing-update targets (i, j), j < nb, with their source columns in ascending order
         std::map<std::pair<int32_t, int32_t>, std::vector<int32_t>> tg;
@@ -373,27 +381,51 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
                 if (R[k][b] == nb) continue;
                 for (size_t a = b; a < R[k].size(); ++a) tg[{R[k][a], R[k][b]}].push_back(k);
             }
-        std::vector<std::pair<std::pair<int32_t, int32_t>, std::vector<int32_t>>> tl(tg.begin(), tg.end());
-        // longest (most sources) first, then by block column: the long workgroups start early
-        std::stable_sort(tl.begin(), tl.end(), [](const auto& a, const auto& b) {
-            if (a.second.size() != b.second.size()) return a.second.size() > b.second.size();
-            return a.first.second != b.first.second ? a.first.second < b.first.second : a.first.first < b.first.first;
-        });
-        W.ntile = (int)tl.size();
-        W.tiles = at();
-        for (auto& t : tl) { buf.push_back(t.first.first); buf.push_back(t.first.second); }
-        W.src_start = at();
-        int32_t acc = 0;
-        for (auto& t : tl) { buf.push_back(acc); acc += (int32_t)t.second.size(); }
-        buf.push_back(acc);
-        W.src = at();
+        // quarter tasks; a target with more than SPLIT sources is split into groups of <= SPLIT
+        // consecutive sources summed into scratch quarters and combined in group order afterwards,
+        // so no workgroup runs more than SPLIT * 128 deep (the long poles of a level)
+        constexpr int SPLIT = 2;
+        struct Task { int32_t i, j, q, s0, s1, slot; };
+        std::vector<Task> tasks;
+        std::vector<int32_t> src, comb;
+        int slots = 0, ncomb = 0;
         W.flops = 0.0;
-        for (auto& t : tl) {
-            buf.insert(buf.end(), t.second.begin(), t.second.end());
-            const int quarters = t.first.first == t.first.second ? 3 : 4;
-            W.flops += (double)t.second.size() * quarters * 2.0 * 64 * 64 * NB;
+        for (auto& t : tg) {
+            const int32_t i = t.first.first, j = t.first.second;
+            const int32_t s0 = (int32_t)src.size();
+            src.insert(src.end(), t.second.begin(), t.second.end());
+            const int32_t ns = (int32_t)t.second.size();
+            const bool split = ns > SPLIT;
+            for (int q = 0; q < 4; ++q) {
+                const int qr = q >> 1, qc = q & 1;
+                if (i == j && qr == 0 && qc == 1) continue;  // strictly upper quarter of a diagonal block
+                if ((qr == 1 && real_rows(i) <= NB / 2) || (qc == 1 && real_rows(j) <= NB / 2)) continue;
+                if (!split) {
+                    tasks.push_back({i, j, q, s0, s0 + ns, -1});
+                } else {
+                    const int first = slots;
+                    for (int32_t g = 0; g < ns; g += SPLIT) tasks.push_back({i, j, q, s0 + g, s0 + std::min(ns, g + SPLIT), slots++});
+                    comb.insert(comb.end(), {i, j, q, first, slots - first});
+                    ++ncomb;
+                }
+                W.flops += (double)ns * 2.0 * 64 * 64 * NB;
+            }
         }
-        ntile_total += W.ntile;
+        // longest (most sources) first, then by block column: the long workgroups start early
+        std::stable_sort(tasks.begin(), tasks.end(), [](const Task& a, const Task& b) {
+            if (a.s1 - a.s0 != b.s1 - b.s0) return a.s1 - a.s0 > b.s1 - b.s0;
+            return a.j != b.j ? a.j < b.j : a.i < b.i;
+        });
+        W.src = at();
+        buf.insert(buf.end(), src.begin(), src.end());
+        W.tasks = at();
+        W.ntask = (int)tasks.size();
+        for (auto& t : tasks) buf.insert(buf.end(), {t.i, t.j, t.q, t.s0, t.s1, t.slot});
+        W.comb = at();
+        W.ncomb = ncomb;
+        buf.insert(buf.end(), comb.begin(), comb.end());
+        s.n_scratch = std::max(s.n_scratch, slots);
+        ntile_total += (int64_t)tg.size();
     }
     // backward solve L' x = y by levels, top down: the columns of level w get x = Linv' y; every
     // column j whose panel holds one of them gets y_j -= sum_i L(i,j)' x_i (i ascending)

@@ -61,9 +61,12 @@ int main() {
     CK(hipMalloc(&dl, 4096 * 4));
     CK(hipMemset(scal, 0, 64 * 8));
     std::vector<int32_t> lists(4096, 0);
-    // [0] = potrf column 0; [2..] = trsm tasks (0, r), r = 1..61; [200] = syrk tile (1,1), src_start {0,1}, src {0}
-    for (int r = 1; r <= 61; ++r) { lists[2 * r] = 0; lists[2 * r + 1] = r; }
-    lists[200] = 1; lists[201] = 1; lists[202] = 0; lists[203] = 1; lists[204] = 0;
+    // [0] = potrf column 0; [2..] = trsm records (0, 2 r + h), r = 1..61; [400] = syrk task
+    // (1, 0, quarter 0, sources [0, 1), in place), [410] = source list {0}
+    for (int q = 0; q < 122; ++q) { lists[2 + 2 * q] = 0; lists[3 + 2 * q] = 2 * (1 + q / 2) + (q & 1); }
+    const int32_t task[6] = {1, 0, 0, 0, 1, -1};
+    for (int q = 0; q < 6; ++q) lists[400 + q] = task[q];
+    lists[410] = 0;
     CK(hipMemcpy(dl, lists.data(), lists.size() * 4, hipMemcpyHostToDevice));
     CK(hipFuncSetAttribute((const void*)k_potrf128<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)POTRF_LDS));
     CK(hipFuncSetAttribute((const void*)k_potrf128<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)POTRF_LDS));
@@ -109,10 +112,10 @@ int main() {
     k_potrf128<false><<<1, 256, POTRF_LDS>>>(dS, ld, dl, dinv, scal, nullptr);
     for (int nt : {1, 8, 61}) {
         const float tt = time_us([&] { k_trsm128<<<(unsigned)(2 * nt), 256, TRSM_LDS>>>(dS, ld, dl + 2, dinv); }, 10);
-        printf("k_trsm128 %2d tasks   %8.2f us\n", nt, tt);
+        printf("k_trsm128 %2d blocks  %8.2f us\n", nt, tt);
     }
-    const float ts1 = time_us([&] { k_syrk_multi<<<4, 256>>>(dS, ld, dl + 200, dl + 202, dl + 204); }, 10);
-    printf("k_syrk_multi 1 tile   %8.2f us (K = 128)\n", ts1);
+    const float ts1 = time_us([&] { k_syrk_multi<<<1, 256>>>(dS, ld, dl + 400, dl + 410, nullptr); }, 10);
+    printf("k_syrk_multi 1 quarter %7.2f us (K = 128)\n", ts1);
     const float te = time_us([&] { k_neg_copy<<<1, 64>>>(dinv, dinv + 64, 1); }, 20);
     printf("empty-ish launch      %8.2f us\n", te);
     return 0;

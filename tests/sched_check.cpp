@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <random>
+#include <map>
 #include <set>
 
 #include "../fish-eye_bundle_adjustment_amd/csrc/fba_internal.h"
@@ -93,6 +94,7 @@ int main(int argc, char** argv) {
     L.u_c = 6 * (int64_t)L.n_img + L.cw;
     L.n_pad = (L.u_c + NB - 1) / NB * NB;
     L.ld = L.n_pad;
+    L.nrhs = 15;
     c.n_loc = std::min(L.n_img, NB / 6);
     c.opt.verbose = 0;
     std::vector<int32_t> slot(n_img);
@@ -120,9 +122,21 @@ int main(int argc, char** argv) {
                (long)s.n_tiles);
         for (int v : per) printf(" %d", v);
         printf("\n");
-        for (int w = 0; w < s.n_waves; ++w)  // per level: columns, panel tasks, update targets, GFLOP
-            printf("level %2d: cols %3d trsm %4d tiles %5d gflop %.3f\n", w, s.w[w].ncol, s.w[w].ntrsm, s.w[w].ntile,
-                   s.w[w].flops * 1e-9);
+        for (int w = 0; w < s.n_waves; ++w) {  // per level: columns, panel halves, quarter tasks, GFLOP
+            const int32_t* tk = s.buf.data() + s.w[w].tasks;
+            int mx = 0;
+            std::map<int, int> hist;
+            for (int t = 0; t < s.w[w].ntask; ++t) {
+                const int ns = tk[Sched::SYRK_REC * t + 4] - tk[Sched::SYRK_REC * t + 3];
+                mx = std::max(mx, ns);
+                hist[ns]++;
+            }
+            printf("level %2d: cols %3d trsm %4d tasks %5d comb %3d gflop %.3f max-src %d  src-hist:", w, s.w[w].ncol,
+                   s.w[w].ntrsm, s.w[w].ntask, s.w[w].ncomb, s.w[w].flops * 1e-9, mx);
+            for (auto& h : hist) printf(" %d:%d", h.first, h.second);
+            printf("\n");
+        }
+        printf("scratch quarters %d\n", s.n_scratch);
         return 0;
     }
     const int64_t n = L.n_pad, nb = n / NB, nr = n + NB;  // rows: matrix + RHS block row
@@ -163,7 +177,9 @@ int main(int argc, char** argv) {
     std::vector<int> done(nb, 0);
     for (int w = 0; w < s.n_waves; ++w) {
         const Sched::Wave& W = s.w[w];
-        if (W.cols + W.ncol > nbuf || W.trsm + 2 * W.ntrsm > nbuf || W.tiles + 2 * W.ntile > nbuf) return fail("list bounds");
+        if (W.cols + W.ncol > nbuf || W.trsm + 2 * W.ntrsm > nbuf || W.tasks + Sched::SYRK_REC * W.ntask > nbuf ||
+            W.comb + Sched::COMB_REC * W.ncomb > nbuf)
+            return fail("list bounds");
         for (int q = 0; q < W.ncol; ++q) {  // potrf
             const int64_t k = B[W.cols + q];
             if (k < 0 || k >= nb || done[k]) return fail("potrf column");
@@ -182,37 +198,54 @@ int main(int argc, char** argv) {
                 }
             }
         }
-        for (int q = 0; q < W.ntrsm; ++q) {  // X = A L^-T
-            const int64_t k = B[W.trsm + 2 * q], r = B[W.trsm + 2 * q + 1];
+        for (int q = 0; q < W.ntrsm; ++q) {  // X = A L^-T on one 64-row half
+            const int64_t k = B[W.trsm + 2 * q], r = B[W.trsm + 2 * q + 1] >> 1, h = B[W.trsm + 2 * q + 1] & 1;
             if (k < 0 || k >= nb || !done[k] || r <= k || r > nb) return fail("trsm task");
             const double* Lk = Bk(k, k);
             double* X = Bk(r, k);
-            for (int i = 0; i < NB; ++i)
+            for (int i = 64 * h; i < 64 * h + 64; ++i)
                 for (int j = 0; j < NB; ++j) {
                     double v = X[(size_t)i * n + j];
                     for (int t = 0; t < j; ++t) v -= X[(size_t)i * n + t] * Lk[(size_t)j * n + t];
                     X[(size_t)i * n + j] = v / Lk[(size_t)j * n + j];
                 }
         }
-        for (int q = 0; q < W.ntile; ++q) {  // C(i,j) -= sum_k X_ik X_jk'
-            const int64_t i = B[W.tiles + 2 * q], j = B[W.tiles + 2 * q + 1];
+        std::vector<double> P((size_t)std::max(s.n_scratch, 1) * 4096, 0.0);
+        std::vector<int> slot_used(std::max(s.n_scratch, 1), 0);
+        for (int q = 0; q < W.ntask; ++q) {  // C quarter -= sum_k X_ik X_jk', or the group's partial
+            const int32_t* tk = B + W.tasks + Sched::SYRK_REC * q;
+            const int64_t i = tk[0], j = tk[1];
+            const int qr = tk[2] >> 1, qc = tk[2] & 1, slot = tk[5];
             if (j < 0 || j >= nb || i < j || i > nb || done[j]) return fail("update target");
-            const int32_t s0 = B[W.src_start + q], s1 = B[W.src_start + q + 1];
+            if (i == j && qr == 0 && qc == 1) return fail("upper quarter of a diagonal block");
+            if (slot >= s.n_scratch || (slot >= 0 && slot_used[slot]++)) return fail("scratch slot");
             int64_t prev = -1;
-            for (int32_t u = s0; u < s1; ++u) {
+            for (int32_t u = tk[3]; u < tk[4]; ++u) {
                 const int64_t k = B[W.src + u];
                 if (k <= prev || !done[k]) return fail("update sources");
                 prev = k;
                 const double* Xi = Bk(i, k);
                 const double* Xj = Bk(j, k);
                 double* C = Bk(i, j);
-                for (int a = 0; a < NB; ++a)
-                    for (int b = 0; b < NB; ++b) {
+                for (int a = 64 * qr; a < 64 * qr + 64; ++a)
+                    for (int b = 64 * qc; b < 64 * qc + 64; ++b) {
                         if (i == j && b > a) continue;
                         double v = 0.0;
                         for (int t = 0; t < NB; ++t) v += Xi[(size_t)a * n + t] * Xj[(size_t)b * n + t];
-                        C[(size_t)a * n + b] -= v;
+                        if (slot < 0) C[(size_t)a * n + b] -= v;
+                        else P[(size_t)slot * 4096 + (a - 64 * qr) * 64 + (b - 64 * qc)] -= v;
                     }
+            }
+        }
+        for (int q = 0; q < W.ncomb; ++q) {  // split targets: C += the group partials in slot order
+            const int32_t* cb = B + W.comb + Sched::COMB_REC * q;
+            double* C = Bk(cb[0], cb[1]);
+            const int qr = cb[2] >> 1, qc = cb[2] & 1;
+            for (int g = 0; g < cb[4]; ++g) {
+                if (cb[3] + g >= s.n_scratch || slot_used[cb[3] + g] != 1) return fail("combine slot");
+                for (int a = 0; a < 64; ++a)
+                    for (int b = 0; b < 64; ++b)
+                        C[(size_t)(64 * qr + a) * n + 64 * qc + b] += P[(size_t)(cb[3] + g) * 4096 + a * 64 + b];
             }
         }
     }
@@ -291,6 +324,8 @@ int main(int argc, char** argv) {
         printf("FAIL factor err %.3e solve err %.3e\n", rel, xrel);
         return 1;
     }
-    printf("ok levels=%d blocks=%ld slots=%d err=%.3e xerr=%.3e\n", s.n_waves, (long)nb, L.n_img, rel, xrel);
+    int ncomb = 0;
+    for (int w = 0; w < s.n_waves; ++w) ncomb += s.w[w].ncomb;
+    printf("ok levels=%d blocks=%ld slots=%d split=%d err=%.3e xerr=%.3e\n", s.n_waves, (long)nb, L.n_img, ncomb, rel, xrel);
     return 0;
 }

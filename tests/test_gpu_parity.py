@@ -111,6 +111,21 @@ def test_step_is_deterministic(fba, cam0_folders):
     assert np.array_equal(out[0][1], out[1][1])
 
 
+def test_graph_replay_matches_eager_launches(fba, cam0_folders):
+    """The captured iteration graphs (default) and eager launches (timing events on) give bit-identical
+    iterates: same kernels, same order, fixed-order reductions."""
+    ds = fba.load_folder(cam0_folders["stage3_fisheye"])
+    out = []
+    for eager in (False, True):
+        ctx = _ctx(fba, ds)
+        ctx.set_timing(eager)
+        d = [ctx.step() for _ in range(3)]
+        out.append((d, ctx.get_xhat()))
+        ctx.close()
+    assert out[0][0] == out[1][0]
+    assert np.array_equal(out[0][1], out[1][1])
+
+
 class _Hip:
     def __init__(self):
         self.lib = ctypes.CDLL("libamdhip64.so")

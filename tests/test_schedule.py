@@ -35,5 +35,7 @@ def test_level_schedule_matches_dense_cholesky(checker, n_img, seed, leaf):
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
     fields = dict(f.split("=") for f in r.stdout.split()[1:])
     assert int(fields["levels"]) <= int(fields["blocks"])
+    if (n_img, seed, leaf) == (300, 2, None):  # targets with > 2 source columns: split and combined
+        assert int(fields["split"]) > 0
     if leaf == 60:  # a dissected scene: independent subtrees share levels
         assert int(fields["levels"]) < int(fields["blocks"])
