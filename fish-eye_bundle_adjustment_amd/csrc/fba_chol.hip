@@ -160,7 +160,7 @@ __device__ __forceinline__ bool leaf_factor(double (&a)[IB], double (&x)[IB], in
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_potrf128: factor the 128x128 diagonal block at (k0, k0); 256 threads.
+// k_potrf128: factor the 128x128 diagonal block at (k0, k0); 512 threads.
 // Eight 16-column leaves.  A leaf is factored in registers by wave 0 (lane i = row i) with
 // row_newbcast DPP broadcasts: every broadcast L[l][j] feeds both the rank-1 update of the
 // leaf and the forward substitution of its inverse D_s = L_ss^-1 (lane c = column c), so the leaf
@@ -169,12 +169,14 @@ __device__ __forceinline__ bool leaf_factor(double (&a)[IB], double (&x)[IB], in
 // ------------------------------------------------------------------------------------------------
 
 constexpr int POTRF_NT = (CB / IB) * (CB / IB + 1) / 2;  // 36 lower tiles
-constexpr size_t POTRF_LDS = sizeof(double) * (POTRF_NT + 1) * IB * 17;
+constexpr int POTRF_THREADS = 512;                          // wave 0: the leaf chain; waves 1-7: the bulk
+constexpr int POTRF_NW = POTRF_THREADS / 64;
+constexpr size_t POTRF_LDS = sizeof(double) * (POTRF_NT + CB / IB) * IB * 17;  // + the eight D_s
 
 // TS: shader-clock stamps of wave 0's critical path into ts[] (calibration builds only,
 // scripts/ubench/chol_ubench.hip)
 template <bool TS>
-__global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ cols,
+__global__ __launch_bounds__(POTRF_THREADS) void k_potrf128(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ cols,
                                                   double* __restrict__ dinv, double* __restrict__ scal,
                                                   unsigned long long* __restrict__ ts) {
 #define POTRF_TS(i) do { if (TS && threadIdx.x == 0 && blockIdx.x == 0) ts[i] = __builtin_amdgcn_s_memtime(); } while (0)
@@ -184,7 +186,8 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
     // lower-triangle tiles only (80 KB, so the kernel fits beside a bulk-update workgroup on a CU):
     // element (r, c), r/16 >= c/16, at tile (r/16)(r/16+1)/2 + c/16, row r%16 (stride 17), col c%16
 #define AT(r, c) smem[(((r) >> 4) * (((r) >> 4) + 1) / 2 + ((c) >> 4)) * (IB * 17) + ((r) & 15) * 17 + ((c) & 15)]
-    double* Dl = smem + POTRF_NT * IB * 17;  // [16][17] current inverse D_s
+    double* Dall = smem + POTRF_NT * IB * 17;  // [8][16][17] the leaf inverses D_s (to dinv at the end)
+    double* Dl = Dall;                          // the current one
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int lr = lane & 15, lk = lane >> 4;
     const int64_t dbase = (k0 / CB) * (CB / IB) * (IB * IB);
@@ -219,12 +222,12 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
                 a[2 * h + 1] = v.y;
             }
         }
-        constexpr int NQ = ((POTRF_NT - 1) * 128 + 255) / 256;  // 18
+        constexpr int NQ = ((POTRF_NT - 1) * 128 + POTRF_THREADS - 1) / POTRF_THREADS;
         double2 v[NQ];
         int off[NQ];
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            const int i = tid + 256 * q, p = 1 + (i >> 7), n = (i >> 3) & 15, m = (i & 7) * 2;
+            const int i = tid + POTRF_THREADS * q, p = 1 + (i >> 7), n = (i >> 3) & 15, m = (i & 7) * 2;
             int ti = 0, pp = p;
             while (pp > ti) { pp -= ti + 1; ++ti; }
             off[q] = -1;
@@ -243,7 +246,6 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
                     if (c <= lane) AT(lane, c) = a[c];
                     const double d = (c >= lane) ? x[c] : 0.0;  // (L^-1)[c][lane]
                     Dl[c * 17 + lane] = d;
-                    dinv[dbase + c * IB + lane] = d;
                 }
             }
         }
@@ -259,11 +261,12 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
         const int c0 = s * IB;
         __syncthreads();  // B1: L_ss, D_s in LDS; column s updated
         POTRF_TS(3 + 4 * s);
+        Dl = Dall + s * IB * 17;
         if (s == CB / IB - 1) break;
-        // panel solve X_t = A_ts D_s^T: wave 0 tile s+1, waves 1..3 tiles s+2..7
+        // panel solve X_t = A_ts D_s^T: wave 0 tile s+1, waves 1..7 tiles s+2..7
         {
             const int t0 = (wave == 0) ? s + 1 : s + 1 + wave;
-            const int step = (wave == 0) ? CB : 3;
+            const int step = (wave == 0) ? CB : POTRF_NW - 1;
             for (int t = t0; t < CB / IB; t += step) {
                 const int r0 = t * IB;
                 dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
@@ -300,20 +303,21 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
                 for (int c = 0; c < IB; ++c) {
                     if (c <= lane) AT((R + lane), R + c) = a[c];
                     const double v = (c >= lane) ? x[c] : 0.0;  // (L^-1)[c][lane]
-                    Dl[c * 17 + lane] = v;  // safe: every wave finished reading D_s before B2
-                    dinv[dbase + (s + 1) * IB * IB + c * IB + lane] = v;
+                    Dall[(s + 1) * IB * 17 + c * 17 + lane] = v;
                 }
             }
         } else {
-            // waves 1-3: the rest of the trailing update, by tile rows s+2 .. 7 dealt in snake order
-            // (largest first) for balance; the tiles of a row go in pairs sharing the A operand,
-            // two independent MFMA chains
+            // bulk waves: the rest of the trailing update, tile rows s+2 .. 7 from the bottom (largest
+            // first); the tiles of a row go in pairs sharing the A operand (two independent MFMA
+            // chains), the pairs dealt round-robin over the waves
             const int nrows = CB / IB - 2 - s;
+            int unit = 0;
             for (int i = 0; i < nrows; ++i) {
-                const int w = ((i / 3) & 1) ? 3 - (i % 3) : 1 + (i % 3);
-                if (w != wave) continue;
                 const int R = (CB / IB - 1 - i) * IB;
-                for (int C = c0 + IB; C <= R; C += 2 * IB) {
+                for (int C = c0 + IB; C <= R; C += 2 * IB, ++unit) {
+                    // waves 1-3, 5-7: wave 4 shares wave 0's SIMD and stays out of the leaf's way
+                    const int u6 = unit % 6;
+                    if (u6 + (u6 >= 3 ? 2 : 1) != wave) continue;
                     const bool two = C + IB <= R;
                     dbl4 acc1, acc2 = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -334,11 +338,13 @@ __global__ __launch_bounds__(256) void k_potrf128(double* __restrict__ S, int64_
                         for (int r = 0; r < 4; ++r) AT((R + lk + 4 * r), C + IB + lr) = acc2[r];
                 }
             }
-            store_col(s, tid - 64, 192);  // block column s is final: write it out behind the update
+            store_col(s, tid - 64, POTRF_THREADS - 64);  // block column s is final: written behind the update
         }
     }
     if (!ok && lane == 0 && scal[1] == 0.0) scal[1] = (double)(k0 + 1);
-    store_col(CB / IB - 1, tid, 256);
+    store_col(CB / IB - 1, tid, POTRF_THREADS);
+    for (int i = tid; i < (CB / IB) * IB * IB; i += POTRF_THREADS)  // the leaf inverses, row-major 16x16 each
+        dinv[dbase + i] = Dall[(i >> 8) * IB * 17 + ((i >> 4) & 15) * 17 + (i & 15)];
     POTRF_TS(40);
 #undef AT
 #undef POTRF_TS
@@ -822,7 +828,7 @@ int launch_cholesky(Ctx& c) {
     const Sched& s = c.sched;
     for (int w = 0; w < s.n_waves; ++w) {
         const Sched::Wave& W = s.w[w];
-        k_potrf128<false><<<(unsigned)W.ncol, 256, POTRF_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.cols, c.d_dinv, c.d_scal,
+        k_potrf128<false><<<(unsigned)W.ncol, POTRF_THREADS, POTRF_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.cols, c.d_dinv, c.d_scal,
                                                                           nullptr);
         k_trsm128<<<(unsigned)W.ntrsm, 256, TRSM_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.trsm, c.d_dinv);
         if (W.ntask == 0) continue;

@@ -73,10 +73,10 @@ int main() {
     CK(hipFuncSetAttribute((const void*)k_trsm128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRSM_LDS));
     auto reset = [&]() { return hipMemcpy(dS, M.data(), M.size() * 8, hipMemcpyHostToDevice); };
     CK(reset());
-    const float tp = time_us([&] { k_potrf128<false><<<1, 256, POTRF_LDS>>>(dS, ld, dl, dinv, scal, nullptr); }, 20);
+    const float tp = time_us([&] { k_potrf128<false><<<1, POTRF_THREADS, POTRF_LDS>>>(dS, ld, dl, dinv, scal, nullptr); }, 20);
     // check: L from the last run (factoring the original block every time: reset, run once)
     CK(reset());
-    k_potrf128<false><<<1, 256, POTRF_LDS>>>(dS, ld, dl, dinv, scal, nullptr);
+    k_potrf128<false><<<1, POTRF_THREADS, POTRF_LDS>>>(dS, ld, dl, dinv, scal, nullptr);
     CK(hipDeviceSynchronize());
     std::vector<double> L((size_t)n * ld);
     CK(hipMemcpy(L.data(), dS, L.size() * 8, hipMemcpyDeviceToHost));
@@ -90,10 +90,10 @@ int main() {
         }
     printf("k_potrf128           %8.2f us  |LL'-A|/|A| %.2e\n", tp, err / nrm);
     CK(reset());
-    k_potrf128<true><<<1, 256, POTRF_LDS>>>(dS, ld, dl, dinv, scal, dts);
+    k_potrf128<true><<<1, POTRF_THREADS, POTRF_LDS>>>(dS, ld, dl, dinv, scal, dts);
     CK(hipDeviceSynchronize());
     CK(reset());
-    const float tq = time_us([&] { k_potrf128<true><<<1, 256, POTRF_LDS>>>(dS, ld, dl, dinv, scal, dts); }, 1);
+    const float tq = time_us([&] { k_potrf128<true><<<1, POTRF_THREADS, POTRF_LDS>>>(dS, ld, dl, dinv, scal, dts); }, 1);
     unsigned long long q[64];
     CK(hipMemcpy(q, dts, sizeof q, hipMemcpyDeviceToHost));
     printf("k_potrf128<TS>       %8.2f us, %llu clocks = %.2f GHz\n", tq, q[40] - q[0], (q[40] - q[0]) / (1e3 * tq));
@@ -109,7 +109,7 @@ int main() {
            tdiag, tend, q[40] - q[31]);
     // trsm: 61 panel blocks below the factored block (two workgroups each)
     CK(reset());
-    k_potrf128<false><<<1, 256, POTRF_LDS>>>(dS, ld, dl, dinv, scal, nullptr);
+    k_potrf128<false><<<1, POTRF_THREADS, POTRF_LDS>>>(dS, ld, dl, dinv, scal, nullptr);
     for (int nt : {1, 8, 61}) {
         const float tt = time_us([&] { k_trsm128<<<(unsigned)(2 * nt), 256, TRSM_LDS>>>(dS, ld, dl + 2, dinv); }, 10);
         printf("k_trsm128 %2d blocks  %8.2f us\n", nt, tt);
