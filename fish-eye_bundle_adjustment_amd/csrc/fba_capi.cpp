@@ -394,14 +394,19 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         std::stable_sort(tk.begin(), tk.end(), [](const auto& x, const auto& y) {
             return std::get<0>(x) != std::get<0>(y) ? std::get<0>(x) < std::get<0>(y) : std::get<1>(x) < std::get<1>(y);
         });
-        for (size_t q = 0; q < tk.size(); ++q) {
-            if (q == 0 || std::get<0>(tk[q]) != std::get<0>(tk[q - 1]) || std::get<1>(tk[q]) != std::get<1>(tk[q - 1])) {
-                if (q > 0) pk_t.push_back((int32_t)pk_term.size());
-                pk_key.emplace_back(std::get<0>(tk[q]), std::get<1>(tk[q]));
-            }
-            pk_term.push_back(std::get<2>(tk[q]));
+        // the chunk's pair keys, most terms first: the threads of a wave then run similar trip counts
+        std::vector<std::pair<size_t, size_t>> kr;  // [begin, end) in tk
+        for (size_t q = 0; q < tk.size(); ++q)
+            if (q == 0 || std::get<0>(tk[q]) != std::get<0>(tk[q - 1]) || std::get<1>(tk[q]) != std::get<1>(tk[q - 1]))
+                kr.emplace_back(q, q + 1);
+            else
+                kr.back().second = q + 1;
+        std::stable_sort(kr.begin(), kr.end(), [](const auto& x, const auto& y) { return x.second - x.first > y.second - y.first; });
+        for (auto& r : kr) {
+            pk_key.emplace_back(std::get<0>(tk[r.first]), std::get<1>(tk[r.first]));
+            for (size_t q = r.first; q < r.second; ++q) pk_term.push_back(std::get<2>(tk[q]));
+            pk_t.push_back((int32_t)pk_term.size());
         }
-        if (!tk.empty()) pk_t.push_back((int32_t)pk_term.size());
         ck_pk.push_back((int32_t)pk_key.size());
         std::vector<std::pair<int32_t, int32_t>> io;  // (image, local obs)
         for (int o = o0; o < o1; ++o) io.emplace_back(img[o], o - o0);
@@ -567,9 +572,10 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     FBA_HIP(hipHostMalloc((void**)&c->h_pinned, sizeof(double) * 64));
     for (auto& e : c->ev) FBA_HIP(hipEventCreate(&e));
     if (opt.verbose)
-        fprintf(stderr, "[fba] rank %d/%d: n_obs %ld (tie %ld), points %ld, pairs %ld (%ld terms), u_c %ld, n_pad %ld\n",
+        fprintf(stderr, "[fba] rank %d/%d: n_obs %ld (tie %ld), points %ld, pairs %ld (%ld terms), u_c %ld, n_pad %ld; "
+                "chunks %ld, pair keys %ld, image keys %ld\n",
                 opt.rank, opt.world, (long)c->n_obs, (long)c->n_obs_tie, (long)c->n_lp, (long)c->n_pairs,
-                (long)c->n_pair_terms, (long)L.u_c, (long)L.n_pad);
+                (long)c->n_pair_terms, (long)L.u_c, (long)L.n_pad, (long)c->n_chunks, (long)c->acc.n_pk, (long)c->acc.n_ik);
     *out = c;
     return FBA_OK;
 }

@@ -382,7 +382,7 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     const int32_t* __restrict__ chunk_obs, const int32_t* __restrict__ chunk_pt, const int32_t* __restrict__ lp_start,
     const int32_t* __restrict__ A, const AccPlan plan, double* __restrict__ WT, double* __restrict__ PT,
     double* __restrict__ ppart, double* __restrict__ ipart, double* __restrict__ cpart, int64_t u_c, int type,
-    int cam_stride, unsigned eop_mask, unsigned cam_mask, double px, double py, uint64_t* __restrict__ tprof) {
+    int cam_stride, unsigned eop_mask, unsigned cam_mask, double px, double py, uint64_t* __restrict__ tprof, int dbg) {
     using LY = Lay<NK>;
     using R_ = LR<NK>;
     // optional phase timestamps (FBA_LR_PROFILE): 100 MHz wall clock at the phase boundaries
@@ -588,66 +588,121 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
         cpart[(int64_t)c * NCAM + t] = s;
     }
     stamp(4);
-    const int* pkt = stage_terms ? s_pkt : A + plan.pk_t + kp0;
-    const int* term = stage_terms ? s_term : A + plan.pk_term + tb0;
-    const int toff = stage_terms ? 0 : tb0;
-    // one thread per (key, row a): image keys first, then pair keys; each thread keeps its row's
-    // outputs in registers (independent accumulators), the rows it reads are LDS broadcasts
-    const int n2 = 6 * (ki1 - ki0), n3 = n2 + 6 * (kp1 - kp0);
-    for (int it = t; it < n3; it += LR_THREADS) {
-        if (it < n2) {
-            const int K = ki0 + it / 6, a = it % 6;
-            double d[6], ic[CW], r = 0.0;
+    // image keys: one 8-lane group per (key, part) -- part 0 the lower diagonal block and RHS (27
+    // values), parts 1 and 2 the two halves of the image-camera block -- each lane accumulating
+    // every 8th observation of the key from its own LDS rows (no broadcast reads), then a fixed
+    // xor-butterfly over the 8 lanes; part-major unit order keeps the rows of a wave on one path
+    constexpr int HALF = (CW + 1) / 2;
+    constexpr int IV = 27 > 6 * HALF ? 27 : 6 * HALF;  // values per unit
+    {
+        const int nk = ki1 - ki0, nu = 3 * nk, g8 = t & 7;
+        for (int ub = t >> 3; ub < nu && !(dbg & 1); ub += LR_THREADS / 8) {
+            const int part = ub / nk, K = ki0 + ub % nk;
+            const int x0 = s_iko[K - ki0], x1 = s_iko[K - ki0 + 1];
+            double v[IV];
 #pragma unroll
-            for (int b = 0; b < 6; ++b) d[b] = 0.0;
-#pragma unroll
-            for (int q = 0; q < CW; ++q) ic[q] = 0.0;
-            for (int x = s_iko[K - ki0]; x < s_iko[K - ki0 + 1]; ++x) {
+            for (int q = 0; q < IV; ++q) v[q] = 0.0;
+            for (int x = x0 + g8; x < x1; x += 8) {
                 const int l = s_ikobs[x];
                 const double* E = QE + l * ES;
                 const double* u = Us + l * US;
-                const double ea = E[a], fa = E[6 + a];
-                const double u0 = u[3 * a], u1 = u[3 * a + 1], u2 = u[3 * a + 2];
-#pragma unroll
-                for (int b = 0; b < 6; ++b)
-                    d[b] += ea * E[b] + fa * E[6 + b] - (u0 * u[3 * b] + u1 * u[3 * b + 1] + u2 * u[3 * b + 2]);
-                r += ea * E[12] + fa * E[13];
-#pragma unroll
-                for (int q = 0; q < CW; ++q) ic[q] += E[14 + q] * ea + E[14 + CW + q] * fa;
                 const int pq = pl[l];
-                if (pq >= 0) {
-                    const double* pp = PP + pq * PPS;
-                    r -= u0 * pp[12] + u1 * pp[13] + u2 * pp[14];
+                double uu[18];
 #pragma unroll
-                    for (int q = 0; q < CW; ++q)
-                        ic[q] -= u0 * pp[15 + 3 * q] + u1 * pp[16 + 3 * q] + u2 * pp[17 + 3 * q];
+                for (int q = 0; q < 18; ++q) uu[q] = u[q];
+                if (part == 0) {
+                    double e[14];
+#pragma unroll
+                    for (int q = 0; q < 14; ++q) e[q] = E[q];
+#pragma unroll
+                    for (int aa = 0; aa < 6; ++aa)
+#pragma unroll
+                        for (int bb = 0; bb <= aa; ++bb)
+                            v[aa * (aa + 1) / 2 + bb] += e[aa] * e[bb] + e[6 + aa] * e[6 + bb] -
+                                                         (uu[3 * aa] * uu[3 * bb] + uu[3 * aa + 1] * uu[3 * bb + 1] +
+                                                          uu[3 * aa + 2] * uu[3 * bb + 2]);
+                    double rb0 = 0.0, rb1 = 0.0, rb2 = 0.0;
+                    if (pq >= 0) { const double* pp = PP + pq * PPS; rb0 = pp[12]; rb1 = pp[13]; rb2 = pp[14]; }
+#pragma unroll
+                    for (int aa = 0; aa < 6; ++aa)
+                        v[21 + aa] += e[aa] * e[12] + e[6 + aa] * e[13] - (uu[3 * aa] * rb0 + uu[3 * aa + 1] * rb1 + uu[3 * aa + 2] * rb2);
+                } else {
+                    const int q0 = (part - 1) * HALF;
+                    double e[12];
+#pragma unroll
+                    for (int q = 0; q < 12; ++q) e[q] = E[q];
+#pragma unroll
+                    for (int q = 0; q < HALF; ++q) {
+                        if (q0 + q >= CW) continue;
+                        const double fx = E[14 + q0 + q], fy = E[14 + CW + q0 + q];
+                        double c0 = 0.0, c1 = 0.0, c2 = 0.0;
+                        if (pq >= 0) {
+                            const double* pp = PP + pq * PPS + 15 + 3 * (q0 + q);
+                            c0 = pp[0]; c1 = pp[1]; c2 = pp[2];
+                        }
+#pragma unroll
+                        for (int aa = 0; aa < 6; ++aa)
+                            v[6 * q + aa] += fx * e[aa] + fy * e[6 + aa] - (uu[3 * aa] * c0 + uu[3 * aa + 1] * c1 + uu[3 * aa + 2] * c2);
+                    }
                 }
             }
-            double* out = ipart + (int64_t)K * NIMG;
-            const int tri0 = a * (a + 1) / 2;  // lower entries (a, b <= a) at tri0 + b
 #pragma unroll
-            for (int b = 0; b < 6; ++b)
-                if (b <= a) out[tri0 + b] = d[b];
-            out[21 + a] = r;
-#pragma unroll
-            for (int q = 0; q < CW; ++q) out[27 + 6 * q + a] = ic[q];
-        } else {
-            const int K = kp0 + (it - n2) / 6, a = (it - n2) % 6;
-            double acc[6];
-#pragma unroll
-            for (int b = 0; b < 6; ++b) acc[b] = 0.0;
-            for (int q = pkt[K - kp0] - toff; q < pkt[K - kp0 + 1] - toff; ++q) {
-                const int tm = term[q];
-                const double* ui = Us + (tm & 0xffff) * US + 3 * a;
-                const double* uj = Us + (tm >> 16) * US;
-                const double i0 = ui[0], i1 = ui[1], i2 = ui[2];
-#pragma unroll
-                for (int b = 0; b < 6; ++b) acc[b] += i0 * uj[3 * b] + i1 * uj[3 * b + 1] + i2 * uj[3 * b + 2];
+            for (int q = 0; q < IV; ++q) {  // fixed butterfly over the group's 8 lanes
+                double w = v[q];
+                w += __shfl_xor(w, 4, 8);
+                w += __shfl_xor(w, 2, 8);
+                w += __shfl_xor(w, 1, 8);
+                v[q] = w;
             }
-            double* out = ppart + (int64_t)K * 36 + 6 * a;
+            double* out = ipart + (int64_t)K * NIMG;
+            if (part == 0) {
 #pragma unroll
-            for (int b = 0; b < 6; ++b) out[b] = -acc[b];
+                for (int q = 0; q < 27; ++q)
+                    if ((q & 7) == g8) out[q] = v[q];
+            } else {
+                const int q0 = (part - 1) * HALF;
+#pragma unroll
+                for (int q = 0; q < HALF; ++q)
+#pragma unroll
+                    for (int aa = 0; aa < 6; ++aa)
+                        if (q0 + q < CW && ((6 * q + aa) & 7) == g8) out[27 + 6 * (q0 + q) + aa] = v[6 * q + aa];
+            }
         }
+    }
+    // pair keys: one thread per (key, rows 2h, 2h+1) of the pair block, outputs in registers; the term
+    // lists from LDS (staged above) or, for a chunk of one very large point, from HBM
+    // (thread numbering rotated so that the threads the image units left idle start on the pairs)
+    const int rot = (8 * 3 * (ki1 - ki0)) % LR_THREADS;
+    auto pair_items = [&](const int* __restrict__ pk, const int* __restrict__ tr, int toff_) {
+        const int n3 = 3 * (kp1 - kp0);
+        for (int it = (t + LR_THREADS - rot) % LR_THREADS; it < n3; it += LR_THREADS) {
+            const int K = kp0 + it / 3, a0 = 2 * (it % 3);
+            double acc[12];
+#pragma unroll
+            for (int q = 0; q < 12; ++q) acc[q] = 0.0;
+            for (int q = pk[K - kp0] - toff_; q < pk[K - kp0 + 1] - toff_; ++q) {
+                const int tm = tr[q];
+                const double* ui = Us + (tm & 0xffff) * US + 3 * a0;
+                const double* uj = Us + (tm >> 16) * US;
+                double vi[6], vj[18];
+#pragma unroll
+                for (int m = 0; m < 6; ++m) vi[m] = ui[m];
+#pragma unroll
+                for (int m = 0; m < 18; ++m) vj[m] = uj[m];
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int b = 0; b < 6; ++b)
+                        acc[6 * h + b] += vi[3 * h] * vj[3 * b] + vi[3 * h + 1] * vj[3 * b + 1] + vi[3 * h + 2] * vj[3 * b + 2];
+            }
+            double* out = ppart + (int64_t)K * 36 + 6 * a0;
+#pragma unroll
+            for (int q = 0; q < 12; ++q) out[q] = -acc[q];
+        }
+    };
+    if (!(dbg & 2)) {  // FBA_LR_SKIP (profiling only): bit 2 leaves out the pair items
+        if (stage_terms) pair_items(s_pkt, s_term, 0);
+        else pair_items(A + plan.pk_t + kp0, A + plan.pk_term + tb0, tb0);
     }
     __syncthreads();
     stamp(5);
@@ -1106,7 +1161,8 @@ int launch_accumulate(Ctx& c) {
     k_lin_reduce<NKV><<<(unsigned)c.n_chunks, LR_THREADS, LR<NKV>::LDS, c.stream>>>(                              \
         c.d_xy, c.d_img, c.d_cam, c.d_pt, c.d_lp_tie, c.d_ctl, c.d_xfull, c.d_img_tab, c.d_cam_tab,                \
         c.d_chunk_obs, c.d_chunk_pt, c.d_lp_start, c.d_acc, c.acc, c.d_WT, c.d_pt_tab, c.d_ppart, c.d_ipart,       \
-        c.d_cpart, c.L.u_c, c.set.type, c.cam_tab_stride, em, cm, px, py, c.d_lrprof);                            \
+        c.d_cpart, c.L.u_c, c.set.type, c.cam_tab_stride, em, cm, px, py, c.d_lrprof,                              \
+        c.d_lrprof && getenv("FBA_LR_SKIP") ? atoi(getenv("FBA_LR_SKIP")) : 0);                            \
     if (c.n_pairs > 0)                                                                                            \
         k_red_pairs<<<(unsigned)((c.n_pairs + 3) / 4), 256, 0, c.stream>>>(c.d_ppart, c.d_acc, c.acc, c.d_S, L.ld, \
                                                                          c.n_pairs);                              \
