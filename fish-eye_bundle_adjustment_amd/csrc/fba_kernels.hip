@@ -393,7 +393,7 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     constexpr int CW = LY::CW, NJ = LY::NJ, PS = LY::PS;
     constexpr int ES = R_::ES, US = R_::US, PPS = R_::PPS, NIMG = R_::NIMG, NCAM = R_::NCAM;
     constexpr int CAM_SPLIT = R_::CAM_SPLIT;
-    static_assert(LR_THREADS >= 512 && LR_THREADS >= CHUNK_OBS && LR_THREADS >= 8 * CHUNK_PTS, "thread roles");
+    static_assert(LR_THREADS >= 512 && LR_THREADS >= CHUNK_OBS, "thread roles");
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* QE = lds;                                  // [CHUNK_OBS][ES]
     double* Us = QE + CHUNK_OBS * ES;                  // [CHUNK_OBS][US]
@@ -441,76 +441,64 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     if (t < CHUNK_OBS) pl[t] = (active && p >= 0) ? p - p0 : -1;
     __syncthreads();
     stamp(1);
-    // (B) one 8-lane group per point: each lane sums every 8th observation of the point, a fixed
-    // xor-butterfly adds the 8 partial sums, then the lanes share the point's outputs
-    if ((t >> 3) < p1 - p0) {
-        const int lp = p0 + (t >> 3), g8 = t & 7;
+    // (B)
+    if (t < p1 - p0) {
+        const int lp = p0 + t;
         const int a0 = lp_start[lp] - o0, a1 = lp_start[lp + 1] - o0;
-        constexpr int NV = 9 + 3 * CW;  // V (6) | b (3) | Wc (3 CW)
-        double sv[NV];
+        double V00 = 0, V01 = 0, V02 = 0, V11 = 0, V12 = 0, V22 = 0, b0 = 0, b1 = 0, b2 = 0;
+        double Wc[CW][3];
 #pragma unroll
-        for (int q = 0; q < NV; ++q) sv[q] = 0.0;
-        for (int i = a0 + g8; i < a1; i += 8) {
+        for (int q = 0; q < CW; ++q) Wc[q][0] = Wc[q][1] = Wc[q][2] = 0.0;
+        for (int i = a0; i < a1; ++i) {
             const double* r = QE + i * ES;
 #pragma unroll
             for (int row = 0; row < 2; ++row) {
                 const double pr = row ? py : px;
                 const double j0 = r[3 * row], j1 = r[3 * row + 1], j2 = r[3 * row + 2], wv = r[6 + row];
                 const double q0 = pr * j0, q1 = pr * j1, q2 = pr * j2;
-                sv[0] += q0 * j0; sv[1] += q0 * j1; sv[2] += q0 * j2;
-                sv[3] += q1 * j1; sv[4] += q1 * j2; sv[5] += q2 * j2;
-                sv[6] += q0 * wv; sv[7] += q1 * wv; sv[8] += q2 * wv;
+                V00 += q0 * j0; V01 += q0 * j1; V02 += q0 * j2;
+                V11 += q1 * j1; V12 += q1 * j2; V22 += q2 * j2;
+                b0 += q0 * wv; b1 += q1 * wv; b2 += q2 * wv;
 #pragma unroll
                 for (int q = 0; q < CW; ++q) {
                     const double jc = r[8 + row * CW + q];
-                    sv[9 + 3 * q] += jc * q0; sv[10 + 3 * q] += jc * q1; sv[11 + 3 * q] += jc * q2;
+                    Wc[q][0] += jc * q0; Wc[q][1] += jc * q1; Wc[q][2] += jc * q2;
                 }
             }
         }
-#pragma unroll
-        for (int q = 0; q < NV; ++q) {
-            double w = sv[q];
-            w += __shfl_xor(w, 4, 8);
-            w += __shfl_xor(w, 2, 8);
-            w += __shfl_xor(w, 1, 8);
-            sv[q] = w;
-        }
-        const double V00 = sv[0], V01 = sv[1], V02 = sv[2], V11 = sv[3], V12 = sv[4], V22 = sv[5];
-        const double b0 = sv[6], b1 = sv[7], b2 = sv[8];
         // symmetric 3x3 inverse (adjugate)
         const double c00 = V11 * V22 - V12 * V12, c01 = V02 * V12 - V01 * V22, c02 = V01 * V12 - V02 * V11;
         const double id = 1.0 / (V00 * c00 + V01 * c01 + V02 * c02);
         const double I00 = c00 * id, I01 = c01 * id, I02 = c02 * id;
         const double I11 = (V00 * V22 - V02 * V02) * id, I12 = (V01 * V02 - V00 * V12) * id,
                      I22 = (V00 * V11 - V01 * V01) * id;
+        double* P = PT + (int64_t)lp * PS;
+        P[6] = I00 * b0 + I01 * b1 + I02 * b2;
+        P[7] = I01 * b0 + I11 * b1 + I12 * b2;
+        P[8] = I02 * b0 + I12 * b1 + I22 * b2;
+#pragma unroll
+        for (int q = 0; q < CW; ++q) {
+            P[12 + 3 * CW + 3 * q] = Wc[q][0] * I00 + Wc[q][1] * I01 + Wc[q][2] * I02;
+            P[13 + 3 * CW + 3 * q] = Wc[q][0] * I01 + Wc[q][1] * I11 + Wc[q][2] * I12;
+            P[14 + 3 * CW + 3 * q] = Wc[q][0] * I02 + Wc[q][1] * I12 + Wc[q][2] * I22;
+        }
         // V = L L', R = L^-T (upper): r00 = m00, r01 = m10, r02 = m20, r11 = m11, r12 = m21, r22 = m22
         const double l00 = sqrt(V00), l10 = V01 / l00, l20 = V02 / l00;
         const double l11 = sqrt(V11 - l10 * l10), l21 = (V12 - l20 * l10) / l11;
         const double l22 = sqrt(V22 - l20 * l20 - l21 * l21);
         const double m00 = 1.0 / l00, m11 = 1.0 / l11, m22 = 1.0 / l22;
         const double m10 = -l10 * m00 * m11, m21 = -l21 * m11 * m22, m20 = -(l20 * m00 + l21 * m10) * m22;
-        double* P = PT + (int64_t)lp * PS;
-        double* pp = PP + (t >> 3) * PPS;
-        if (g8 == 0) {
-            P[6] = I00 * b0 + I01 * b1 + I02 * b2;
-            P[7] = I01 * b0 + I11 * b1 + I12 * b2;
-            P[8] = I02 * b0 + I12 * b1 + I22 * b2;
-            pp[0] = I00; pp[1] = I01; pp[2] = I02; pp[3] = I11; pp[4] = I12; pp[5] = I22;
-            pp[6] = m00; pp[7] = m10; pp[8] = m20; pp[9] = m11; pp[10] = m21; pp[11] = m22;
-            pp[12] = m00 * b0;
-            pp[13] = m10 * b0 + m11 * b1;
-            pp[14] = m20 * b0 + m21 * b1 + m22 * b2;
-        }
+        double* pp = PP + t * PPS;
+        pp[0] = I00; pp[1] = I01; pp[2] = I02; pp[3] = I11; pp[4] = I12; pp[5] = I22;
+        pp[6] = m00; pp[7] = m10; pp[8] = m20; pp[9] = m11; pp[10] = m21; pp[11] = m22;
+        pp[12] = m00 * b0;
+        pp[13] = m10 * b0 + m11 * b1;
+        pp[14] = m20 * b0 + m21 * b1 + m22 * b2;
 #pragma unroll
         for (int q = 0; q < CW; ++q) {
-            if ((q & 7) != g8) continue;
-            const double w0 = sv[9 + 3 * q], w1 = sv[10 + 3 * q], w2 = sv[11 + 3 * q];
-            P[12 + 3 * CW + 3 * q] = w0 * I00 + w1 * I01 + w2 * I02;
-            P[13 + 3 * CW + 3 * q] = w0 * I01 + w1 * I11 + w2 * I12;
-            P[14 + 3 * CW + 3 * q] = w0 * I02 + w1 * I12 + w2 * I22;
-            pp[15 + 3 * q] = w0 * m00;
-            pp[16 + 3 * q] = w0 * m10 + w1 * m11;
-            pp[17 + 3 * q] = w0 * m20 + w1 * m21 + w2 * m22;
+            pp[15 + 3 * q] = Wc[q][0] * m00;
+            pp[16 + 3 * q] = Wc[q][0] * m10 + Wc[q][1] * m11;
+            pp[17 + 3 * q] = Wc[q][0] * m20 + Wc[q][1] * m21 + Wc[q][2] * m22;
         }
     }
     __syncthreads();
