@@ -671,11 +671,9 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     }
     // pair keys: one thread per (key, rows 2h, 2h+1) of the pair block, outputs in registers; the term
     // lists from LDS (staged above) or, for a chunk of one very large point, from HBM
-    // (thread numbering rotated so that the threads the image units left idle start on the pairs)
-    const int rot = (8 * 3 * (ki1 - ki0)) % LR_THREADS;
     auto pair_items = [&](const int* __restrict__ pk, const int* __restrict__ tr, int toff_) {
         const int n3 = 3 * (kp1 - kp0);
-        for (int it = (t + LR_THREADS - rot) % LR_THREADS; it < n3; it += LR_THREADS) {
+        for (int it = t; it < n3; it += LR_THREADS) {
             const int K = kp0 + it / 3, a0 = 2 * (it % 3);
             double acc[12];
 #pragma unroll
