@@ -105,6 +105,8 @@ def main():
 
     folder = scene_folder(args.config, rank, world)
     ds = fba.load_folder(folder)
+    if world > 1:  # a dedicated stream (capturable: the iteration replays as HIP graphs), RCCL on it too
+        torch.cuda.set_stream(torch.cuda.Stream(dev))
     stream = torch.cuda.current_stream(dev).cuda_stream if world > 1 else None
     ctx = fba.capi.Context(ds.pack(), fba.capi.make_settings(ds.settings), device=local, rank=rank, world=world,
                            stream=stream, verbose=args.verbose)

@@ -597,7 +597,7 @@ static inline void mark(Ctx* c, int i) {
 
 static bool graph_eligible(const Ctx* c) {
     static const bool off = getenv("FBA_NO_GRAPH") && atoi(getenv("FBA_NO_GRAPH")) != 0;
-    return !off && c->graphs_ok && c->own_stream && !c->timing && !c->probe && !c->d_lrprof;
+    return !off && c->graphs_ok && c->stream && !c->timing && !c->probe && !c->d_lrprof;
 }
 
 // run body() on the context's stream, through a graph captured from its first run when eligible
@@ -605,7 +605,11 @@ template <class F>
 static int run_graph(Ctx* c, int which, F&& body) {
     if (!graph_eligible(c)) return body();
     if (!c->graph[which]) {
-        FBA_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        if (hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+            (void)hipGetLastError();  // e.g. a stream that cannot be captured: launch eagerly from now on
+            c->graphs_ok = false;
+            return body();
+        }
         const int rc = body();
         hipGraph_t g = nullptr;
         const hipError_t e = hipStreamEndCapture(c->stream, &g);
@@ -631,8 +635,7 @@ static int run_graph(Ctx* c, int which, F&& body) {
 static int accumulate_body(Ctx* c) {
     int rc;
     mark(c, 0);
-    if ((rc = launch_params(*c))) return rc;
-    FBA_HIP(hipMemcpyAsync(c->d_xlin, c->d_xfull, sizeof(double) * c->L.u_full, hipMemcpyDeviceToDevice, c->stream));
+    if ((rc = launch_params(*c, nullptr, c->d_xlin))) return rc;  // tables + the linearisation point
     mark(c, 1);
     mark(c, 2);
     if ((rc = launch_accumulate(*c))) return rc;

@@ -95,8 +95,8 @@ struct Ctx {
     Layout L;
     hipStream_t stream = nullptr;
     bool own_stream = false;
-    // the two halves of an iteration captured once as HIP graphs (own stream, no timing / probe /
-    // profile events; FBA_NO_GRAPH=1 disables): [0] linearise + accumulate, [1] solve + update
+    // the two halves of an iteration captured once as HIP graphs (a capturable stream, no timing /
+    // probe / profile events; FBA_NO_GRAPH=1 disables): [0] linearise + accumulate, [1] solve + update
     hipGraphExec_t graph[2] = {nullptr, nullptr};
     bool graphs_ok = true;
     int device = 0;
@@ -204,7 +204,8 @@ void set_error(const std::string& msg);
 // kernel launchers (fba_kernels.hip / fba_chol.hip)
 std::vector<int32_t> camera_order(const fba_problem* p);  // internal image slot -> EXT row or -1 (fba_order.cpp)
 void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pairs);  // pairs: (e1, e2) slots, e1 > e2
-int launch_params(Ctx& c, const double* x = nullptr);     // x: parameters (default d_xfull)
+int launch_params(Ctx& c, const double* x = nullptr, double* copy_to = nullptr);  // x: parameters (default d_xfull),
+                                                                                   // also copied to copy_to
 int launch_linearize(Ctx& c, const double* x = nullptr);  // Jacobian rows to d_J (residuals, dense AwG)
 int launch_accumulate(Ctx& c);   // zero S, image, pair, camera blocks, unit diagonal for unused
 int launch_border(Ctx& c);       // alpha, G G^T border, RHS rows

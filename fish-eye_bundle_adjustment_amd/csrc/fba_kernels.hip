@@ -30,8 +30,10 @@ namespace fba {
 __global__ void k_params(const double* __restrict__ xfull, const double* __restrict__ caminfo,
                          double* __restrict__ img_tab, double* __restrict__ cam_tab, double* __restrict__ G,
                          const uint8_t* __restrict__ active, int n_img, int n_cam, int nk, int cw, int cam_stride,
-                         int ic) {
+                         int ic, double* __restrict__ xcopy, int64_t n_copy) {
     int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (xcopy)  // the linearisation point (main.m:569 uses it for v), copied by the whole grid
+        for (int64_t i = t; i < n_copy; i += (int64_t)gridDim.x * blockDim.x) xcopy[i] = xfull[i];
     if (t < n_img) {
         const double* e = xfull + 6 * (int64_t)t;
         double Xc = e[0], Yc = e[1], Zc = e[2], w = e[3], p = e[4], k = e[5];
@@ -69,6 +71,7 @@ __global__ void k_params(const double* __restrict__ xfull, const double* __restr
                 0, 0, 0, 0, -cos(w), -sin(w), 0,
                 0, 0, 0, 0, sin(w) * secp, -cos(w) * secp, 0};
             const bool slot = active[6 * (int64_t)t];  // padding slots (fba_order.cpp) carry no constraint
+#pragma unroll
             for (int i = 0; i < 42; ++i) g[i] = slot ? rows[i] : 0.0;
         }
     } else if (t < n_img + n_cam) {
@@ -713,9 +716,18 @@ __global__ __launch_bounds__(256) void k_red_pairs(const double* __restrict__ pp
     const int64_t pr = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (pr >= n_pairs || lane >= 36) return;
+    // the partials in chunk order, 4 loads in flight (fixed association: ((s + p0) + p1) + ...)
+    const int q0 = A[plan.rp_start + pr], q1 = A[plan.rp_start + pr + 1];
     double s = 0.0;
-    for (int q = A[plan.rp_start + pr]; q < A[plan.rp_start + pr + 1]; ++q)
-        s += ppart[(int64_t)A[plan.rp_list + q] * 36 + lane];
+    int q = q0;
+    for (; q + 4 <= q1; q += 4) {
+        const int i0 = A[plan.rp_list + q], i1 = A[plan.rp_list + q + 1], i2 = A[plan.rp_list + q + 2],
+                  i3 = A[plan.rp_list + q + 3];
+        const double p0 = ppart[(int64_t)i0 * 36 + lane], p1 = ppart[(int64_t)i1 * 36 + lane],
+                     p2 = ppart[(int64_t)i2 * 36 + lane], p3 = ppart[(int64_t)i3 * 36 + lane];
+        s = (((s + p0) + p1) + p2) + p3;
+    }
+    for (; q < q1; ++q) s += ppart[(int64_t)A[plan.rp_list + q] * 36 + lane];
     const int64_t e1 = A[plan.rp_e + 2 * pr], e2 = A[plan.rp_e + 2 * pr + 1];
     S[(6 * e1 + lane / 6) * ld + 6 * e2 + lane % 6] = s;
 }
@@ -1112,11 +1124,13 @@ static inline unsigned cam_mask(const fba_settings& s, int nk) {
 static inline double px_of(const Ctx& c) { return 1.0 / (c.set.meas_std_x * c.set.meas_std_x); }
 static inline double py_of(const Ctx& c) { return 1.0 / (c.set.meas_std_y * c.set.meas_std_y); }
 
-int launch_params(Ctx& c, const double* x) {
+int launch_params(Ctx& c, const double* x, double* copy_to) {
     const int n = c.L.n_img + c.L.n_cam;
-    k_params<<<(n + 63) / 64, 64, 0, c.stream>>>(x ? x : c.d_xfull, c.d_caminfo, c.d_img_tab, c.d_cam_tab, c.d_G, c.d_active,
-                                                   c.L.n_img, c.L.n_cam, c.L.nk, c.L.cw, c.cam_tab_stride,
-                                                   c.set.inner_constraints);
+    const int64_t blocks = copy_to ? std::max<int64_t>((n + 63) / 64, std::min<int64_t>(1024, (c.L.u_full + 255) / 256))
+                                   : (n + 63) / 64;
+    k_params<<<(unsigned)blocks, 64, 0, c.stream>>>(x ? x : c.d_xfull, c.d_caminfo, c.d_img_tab, c.d_cam_tab, c.d_G,
+                                                    c.d_active, c.L.n_img, c.L.n_cam, c.L.nk, c.L.cw, c.cam_tab_stride,
+                                                    c.set.inner_constraints, copy_to, c.L.u_full);
     FBA_HIP(hipGetLastError());
     return FBA_OK;
 }
