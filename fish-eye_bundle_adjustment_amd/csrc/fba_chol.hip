@@ -48,6 +48,29 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     return __hiloint2double(hi, lo);
 }
 
+// In-launch hand-off of a factored diagonal block (k_panel): the potrf workgroup stores L_kk and its
+// leaf inverses WRITE-THROUGH (sc1, buffer stores on a descriptor based at the block), drains its
+// stores in every wave, and one lane sets the column's flag with an agent-scope atomic; the panel
+// workgroups poll that flag relaxed and read the payload with sc1 loads (no stale L1/L2 copies on any
+// XCD).  Flags are zeroed by a memset node ahead of the factorisation (one epoch per launch).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+constexpr int SC1 = 16;  // buffer aux bits: sc1 (write-through / L1 bypass)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t block_rsrc(const void* base, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, int64_t off_bytes, double2 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off_bytes, 0, SC1);
+}
+__device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, int64_t off_bytes, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, (int)off_bytes, 0, SC1);
+}
+__device__ __forceinline__ double2 ld_sc1(__amdgpu_buffer_rsrc_t r, int64_t off_bytes) {
+    return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off_bytes, 0, SC1));
+}
+constexpr unsigned FLAG_SPINS = 1u << 22;  // bounded poll (s_sleep 1 per spin): ~0.3 s, then give up
+
 // 1/sqrt(d) from v_rsq_f64 refined by two Newton steps (full double precision), no IEEE divide
 __device__ __forceinline__ double rsqrt_d(double d) {
     double r = __builtin_amdgcn_rsq(d);
@@ -175,14 +198,15 @@ constexpr size_t POTRF_LDS = sizeof(double) * (POTRF_NT + CB / IB) * IB * 17;  /
 
 // TS: shader-clock stamps of wave 0's critical path into ts[] (calibration builds only,
 // scripts/ubench/chol_ubench.hip)
+// potrf_body: factor the 128x128 diagonal block of column col (512 threads); flag != nullptr: publish
+// it (k_panel hand-off)
 template <bool TS>
-__global__ __launch_bounds__(POTRF_THREADS) void k_potrf128(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ cols,
-                                                  double* __restrict__ dinv, double* __restrict__ scal,
-                                                  unsigned long long* __restrict__ ts) {
+__device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, int col, double* __restrict__ dinv,
+                                           double* __restrict__ scal, unsigned long long* __restrict__ ts,
+                                           unsigned* __restrict__ flag, double* __restrict__ smem) {
 #define POTRF_TS(i) do { if (TS && threadIdx.x == 0 && blockIdx.x == 0) ts[i] = __builtin_amdgcn_s_memtime(); } while (0)
     POTRF_TS(0);
-    const int64_t k0 = (int64_t)cols[blockIdx.x] * CB;  // one diagonal block per workgroup (one level)
-    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int64_t k0 = (int64_t)col * CB;
     // lower-triangle tiles only (80 KB, so the kernel fits beside a bulk-update workgroup on a CU):
     // element (r, c), r/16 >= c/16, at tile (r/16)(r/16+1)/2 + c/16, row r%16 (stride 17), col c%16
 #define AT(r, c) smem[(((r) >> 4) * (((r) >> 4) + 1) / 2 + ((c) >> 4)) * (IB * 17) + ((r) & 15) * 17 + ((c) & 15)]
@@ -194,18 +218,19 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_potrf128(double* __restrict__
     bool ok = true;
     // store the final tiles (t, sc), t >= sc, of block column sc (diagonal tile: lower part only);
     // item i -> tile row t = sc + (i >> 7), row (i >> 3) & 15, columns 2 (i & 7)
+    const __amdgpu_buffer_rsrc_t rL = block_rsrc(S + k0 * ld + k0, ((int64_t)(CB - 1) * ld + CB) * 8);
     auto store_col = [&](int sc, int t0, int nthr) {
         for (int i = t0; i < (CB / IB - sc) * 128; i += nthr) {
             const int ti = sc + (i >> 7), n = (i >> 3) & 15, m = (i & 7) * 2;
-            double* g = S + (k0 + ti * IB + n) * ld + k0 + sc * IB + m;
+            const int64_t off = ((int64_t)(ti * IB + n) * ld + sc * IB + m) * 8;
             const double* t = smem + (ti * (ti + 1) / 2 + sc) * IB * 17 + n * 17 + m;
             if (ti > sc || m + 1 <= n) {
                 double2 v;
                 v.x = t[0];
                 v.y = t[1];
-                *reinterpret_cast<double2*>(g) = v;
+                st_sc1(rL, off, v);
             } else if (m == n) {
-                g[0] = t[0];
+                st_sc1(rL, off, t[0]);
             }
         }
     };
@@ -343,11 +368,31 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_potrf128(double* __restrict__
     }
     if (!ok && lane == 0 && scal[1] == 0.0) scal[1] = (double)(k0 + 1);
     store_col(CB / IB - 1, tid, POTRF_THREADS);
-    for (int i = tid; i < (CB / IB) * IB * IB; i += POTRF_THREADS)  // the leaf inverses, row-major 16x16 each
-        dinv[dbase + i] = Dall[(i >> 8) * IB * 17 + ((i >> 4) & 15) * 17 + (i & 15)];
+    {   // the leaf inverses, row-major 16x16 each, two per thread-store
+        const __amdgpu_buffer_rsrc_t rD = block_rsrc(dinv + dbase, (CB / IB) * IB * IB * 8);
+        for (int i = 2 * tid; i < (CB / IB) * IB * IB; i += 2 * POTRF_THREADS) {
+            double2 v;
+            v.x = Dall[(i >> 8) * IB * 17 + ((i >> 4) & 15) * 17 + (i & 15)];
+            v.y = Dall[(i >> 8) * IB * 17 + ((i >> 4) & 15) * 17 + (i & 15) + 1];
+            st_sc1(rD, (int64_t)i * 8, v);
+        }
+    }
     POTRF_TS(40);
+    if (flag) {  // publish: every storing wave drains, the barrier, then one lane's flag
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 #undef AT
 #undef POTRF_TS
+}
+
+template <bool TS>
+__global__ __launch_bounds__(POTRF_THREADS) void k_potrf128(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ cols,
+                                                            double* __restrict__ dinv, double* __restrict__ scal,
+                                                            unsigned long long* __restrict__ ts) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    potrf_body<TS>(S, ld, cols[blockIdx.x], dinv, scal, ts, nullptr, smem);
 }
 
 
@@ -363,46 +408,66 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_potrf128(double* __restrict__
 constexpr int TRSM_NT = (CB / IB) * (CB / IB - 1) / 2;  // 28 off-diagonal tiles
 constexpr size_t TRSM_LDS = sizeof(double) * (4 * IB * LDA + 4 * IB * 17 + (TRSM_NT + CB / IB) * IB * 17);
 
-__global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ tasks,
-                                                 const double* __restrict__ dinv) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
+// trsm_body: threads 0..255 (4 waves x 16 rows) solve one record; flag != nullptr: the factor of
+// column k comes from a potrf workgroup of the same launch (wait for its flag, sc1 loads); the threads
+// 256.. of a 512-thread workgroup only take part in the barriers
+__device__ __forceinline__ void trsm_body(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ rec,
+                                          const double* __restrict__ dinv, const unsigned* __restrict__ flag,
+                                          double* __restrict__ scal, double* __restrict__ smem) {
     double* X = smem;                       // [4][IB][LDA]   panel rows of each wave
     double* T = X + 4 * IB * LDA;           // [4][IB][17]    per-wave 16x16 staging
     double* Lt = T + 4 * IB * 17;           // [28][IB][17]   L_st, p = s(s-1)/2 + t
     double* Dt = Lt + TRSM_NT * IB * 17;    // [8][IB][17]    D_s
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int lr = lane & 15, lk = lane >> 4;
+    const bool worker = tid < 256;
     // record (column k, 2 r + h): rows 64 h .. 64 h + 63 of panel block (r, k)
-    const int64_t k0 = (int64_t)tasks[2 * blockIdx.x] * CB;
-    const int rh = tasks[2 * blockIdx.x + 1];
+    const int64_t k0 = (int64_t)rec[0] * CB;
+    const int rh = rec[1];
     const int64_t rbase = (int64_t)(rh >> 1) * CB + (rh & 1) * 64 + wave * IB;
     double* Xw = X + wave * IB * LDA;
     double* Tw = T + wave * IB * 17;
     const double* L = S + k0 * ld + k0;
     const double* Dk = dinv + (k0 / CB) * (CB / IB) * (IB * IB);
-    {
-        double2 v[16], lv[14], dv[4];
+    if (worker) {  // the panel rows (written by earlier launches): plain loads, issued first
+        double2 v[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int idx = lane + 64 * q, r = idx >> 6, c = (idx & 63) * 2;
             v[q] = *reinterpret_cast<const double2*>(S + (rbase + r) * ld + k0 + c);
         }
-        // off-diagonal tiles: item i -> tile p = i >> 7, row n = (i >> 3) & 15, columns 2*(i & 7)
-#pragma unroll
-        for (int q = 0; q < 14; ++q) {
-            const int i = tid + 256 * q, p = i >> 7, n = (i >> 3) & 15, kc = (i & 7) * 2;
-            int sr = 1, pp = p;
-            while (pp >= sr) { pp -= sr; ++sr; }
-            lv[q] = *reinterpret_cast<const double2*>(L + (int64_t)(sr * IB + n) * ld + pp * IB + kc);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) dv[q] = *reinterpret_cast<const double2*>(Dk + 2 * (tid + 256 * q));
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int idx = lane + 64 * q, r = idx >> 6, c = (idx & 63) * 2;
             Xw[r * LDA + c] = v[q].x;
             Xw[r * LDA + c + 1] = v[q].y;
         }
+    }
+    if (flag) {  // wait for the factor of column k: one lane polls, relaxed, bounded
+        if (tid == 0) {
+            unsigned spins = 0;
+            while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1u) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }  // hand-off timeout (host reports it)
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the payload loads below the poll
+        __syncthreads();
+    }
+    if (worker) {  // the factor: off-diagonal tiles of L_kk and the leaf inverses, sc1 loads
+        const __amdgpu_buffer_rsrc_t rL = block_rsrc(L, ((int64_t)(CB - 1) * ld + CB) * 8);
+        const __amdgpu_buffer_rsrc_t rD = block_rsrc(Dk, (CB / IB) * IB * IB * 8);
+        double2 lv[14], dv[4];
+        // off-diagonal tiles: item i -> tile p = i >> 7, row n = (i >> 3) & 15, columns 2*(i & 7)
+#pragma unroll
+        for (int q = 0; q < 14; ++q) {
+            const int i = tid + 256 * q, p = i >> 7, n = (i >> 3) & 15, kc = (i & 7) * 2;
+            int sr = 1, pp = p;
+            while (pp >= sr) { pp -= sr; ++sr; }
+            lv[q] = ld_sc1(rL, ((int64_t)(sr * IB + n) * ld + pp * IB + kc) * 8);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dv[q] = ld_sc1(rD, (int64_t)(2 * (tid + 256 * q)) * 8);
 #pragma unroll
         for (int q = 0; q < 14; ++q) {
             const int i = tid + 256 * q, p = i >> 7, n = (i >> 3) & 15, kc = (i & 7) * 2;
@@ -417,6 +482,7 @@ __global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t
         }
     }
     __syncthreads();
+    if (!worker) return;
 #pragma unroll
     for (int s = 0; s < CB / IB; ++s) {
         const int c0 = s * IB;
@@ -462,6 +528,30 @@ __global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t
         v.x = Xw[r * LDA + c];
         v.y = Xw[r * LDA + c + 1];
         *reinterpret_cast<double2*>(S + (rbase + r) * ld + k0 + c) = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ tasks,
+                                                 const double* __restrict__ dinv) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    trsm_body(S, ld, tasks + 2 * blockIdx.x, dinv, nullptr, nullptr, smem);
+}
+
+// k_panel: one level's diagonal factorisations and panel solves in ONE launch: workgroups
+// 0 .. ncol-1 factor the level's diagonal blocks (potrf_body) and publish them, the rest solve the
+// panel halves (trsm_body) as soon as their column's factor is published.  Every workgroup of the
+// launch is resident at once (<= 8 + 2 * panel blocks workgroups, one per CU), so the waits end.
+__global__ __launch_bounds__(POTRF_THREADS) void k_panel(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ cols,
+                                                         int ncol, const int32_t* __restrict__ trsm,
+                                                         double* __restrict__ dinv, double* __restrict__ scal,
+                                                         unsigned* __restrict__ flags) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    if ((int)blockIdx.x < ncol) {
+        const int col = cols[blockIdx.x];
+        potrf_body<false>(S, ld, col, dinv, scal, nullptr, flags + col, smem);
+    } else {
+        const int32_t* rec = trsm + 2 * (blockIdx.x - ncol);
+        trsm_body(S, ld, rec, dinv, flags + rec[0], scal, smem);
     }
 }
 
@@ -826,11 +916,17 @@ __global__ void k_neg_copy(const double* __restrict__ X, double* __restrict__ de
 int launch_cholesky(Ctx& c) {
     const int64_t ld = c.L.ld;
     const Sched& s = c.sched;
+    FBA_HIP(hipMemsetAsync(c.d_flags, 0, c.flags_bytes, c.stream));  // k_panel hand-off flags (one epoch)
     for (int w = 0; w < s.n_waves; ++w) {
         const Sched::Wave& W = s.w[w];
-        k_potrf128<false><<<(unsigned)W.ncol, POTRF_THREADS, POTRF_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.cols, c.d_dinv, c.d_scal,
-                                                                          nullptr);
-        k_trsm128<<<(unsigned)W.ntrsm, 256, TRSM_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.trsm, c.d_dinv);
+        if (W.ncol + W.ntrsm <= c.n_cu) {  // one launch: every workgroup resident (one per CU)
+            k_panel<<<(unsigned)(W.ncol + W.ntrsm), POTRF_THREADS, TRSM_LDS, c.stream>>>(
+                c.d_S, ld, c.d_sched + W.cols, W.ncol, c.d_sched + W.trsm, c.d_dinv, c.d_scal, c.d_flags);
+        } else {
+            k_potrf128<false><<<(unsigned)W.ncol, POTRF_THREADS, POTRF_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.cols,
+                                                                                      c.d_dinv, c.d_scal, nullptr);
+            k_trsm128<<<(unsigned)W.ntrsm, 256, TRSM_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.trsm, c.d_dinv);
+        }
         if (W.ntask == 0) continue;
         const bool pr = c.probe && c.probe_n < (int)c.probe_ev.size() / 2;
         if (pr) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
@@ -870,6 +966,13 @@ int launch_backward(Ctx& c) {
 int chol_setup(Ctx& c) {
     FBA_HIP(hipFuncSetAttribute((const void*)k_potrf128<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)POTRF_LDS));
     FBA_HIP(hipFuncSetAttribute((const void*)k_trsm128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRSM_LDS));
+    FBA_HIP(hipFuncSetAttribute((const void*)k_panel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRSM_LDS));
+    static_assert(TRSM_LDS >= POTRF_LDS, "k_panel LDS");
+    hipDeviceProp_t prop;
+    FBA_HIP(hipGetDeviceProperties(&prop, c.device));
+    c.n_cu = prop.multiProcessorCount;
+    c.flags_bytes = (size_t)((c.L.n_pad / CB + 3) / 4 * 4) * sizeof(unsigned);  // multiple of 16 bytes
+    FBA_HIP(hipMalloc((void**)&c.d_flags, c.flags_bytes));
     FBA_HIP(hipFuncSetAttribute((const void*)k_trtri128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRTRI_LDS));
 
     c.probe_ev.assign(2 * std::max(c.sched.n_waves, 1), nullptr);

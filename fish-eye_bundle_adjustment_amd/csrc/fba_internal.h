@@ -161,6 +161,9 @@ struct Ctx {
     int pt_comp = 0;
     int64_t n_lp_pad = 0;
     double* d_P = nullptr;       // [Sched::n_scratch][64*64] partial sums of split update targets
+    unsigned* d_flags = nullptr; // [nb] k_panel hand-off flags (zeroed before each factorisation)
+    size_t flags_bytes = 0;
+    int n_cu = 0;                // compute units (k_panel needs its whole grid resident)
     double* d_S = nullptr;       // [(n_pad+NB)*ld] normal matrix (lower) + RHS rows
     double* d_X = nullptr;       // [n_pad] solution of the bordered solve
     double* d_dinv = nullptr;    // [(n_pad/NB)*8*256] inverses of the 16x16 diagonal blocks of L
