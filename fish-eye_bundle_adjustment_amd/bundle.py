@@ -100,10 +100,13 @@ class Adjustment:
     rms: tuple               # RMSx, RMSy, RMS
     sigma02: float
     seconds: float
+    cx_diag: np.ndarray = None   # diag of the final Cx (sigma02-scaled, distortions de-scaled)
+    corr: np.ndarray = None      # (numImg, u_img+u_cam, u_img+u_cam) EOP/IOP Correlation sub-blocks
 
 
-def adjust(data: Dataset, device=0, verbose=False) -> Adjustment:
-    """main.m:386-602 on one GPU: Buildxhat, the Gauss-Newton loop, residuals and sigma0^2."""
+def adjust(data: Dataset, device=0, verbose=False, covariance=True) -> Adjustment:
+    """main.m:386-602 on one GPU: Buildxhat, the Gauss-Newton loop, residuals, sigma0^2 and (with
+    covariance=True) the post-fit Cx diagonal and correlation sub-blocks (main.m:428-482, :602)."""
     t0 = time.perf_counter()
     ctx = capi.Context(data.pack(), capi.make_settings(data.settings), device=device, verbose=verbose)
     try:
@@ -111,44 +114,22 @@ def adjust(data: Dataset, device=0, verbose=False) -> Adjustment:
         t1 = time.perf_counter()
         xhat = ctx.get_xhat()
         v, rsd, st = ctx.residuals()
+        cxd, corr = ctx.covariance(st[3]) if covariance else (None, None)
     finally:
         ctx.close()
     return Adjustment(xhat=xhat, xhatnames=xhat_names(data), iterations=it, deltasum=hist, v=v, rsd=rsd,
-                      rms=(st[0], st[1], st[2]), sigma02=st[3], seconds=t1 - t0)
+                      rms=(st[0], st[1], st[2]), sigma02=st[3], seconds=t1 - t0, cx_diag=cxd, corr=corr)
 
 
 def write_outputs(data: Dataset, res: Adjustment, folder):
-    """Minimal .out summary (main.m:646-682 fields) and the .rsd table (main.m:957, BuildRSD.m:6)."""
-    s = data.settings
-    name = os.path.splitext(s["Output_Filename"])[0]
-    out = os.path.join(folder, s["Output_Filename"])
-    ic = int(s["Inner_Constraints"])
-    with open(out, "w") as fh:
-        fh.write("Fish-eye model Bundle Adjustment (MI355X HIP path)\n\n")
-        fh.write(f"Time Taken:\t\t{res.seconds:.6f} seconds\nIterations:\t\t{res.iterations}\n"
-                 f"Model Used:\t\t{s['type']}\n\nSettings used:\n")
-        for k, v in s.items():
-            fh.write(f"{k}\t\t{v}\n")
-        fh.write("\nObservations/Unknowns Summary\n\n")
-        rows = [("Number of Photos", data.numImg), ("Number of Cameras", data.numCam),
-                ("Number of tie/control points", data.numGCP),
-                ("Number of tie/control points to be estimated", data.numtie), ("Total Unknowns", len(res.xhat)),
-                ("Number of image points", data.n_pts), ("Total number of observations", data.n),
-                ("Number of Inner Constraints", 7 * ic),
-                ("Total Number of Observations", data.n + 7 * ic),
-                ("Total Degrees of Freedom", data.n + 7 * ic - len(res.xhat)),
-                ("A-Posteriori", f"{res.sigma02:.10g}"), ("RMSx", f"{res.rms[0]:.10g}"),
-                ("RMSy", f"{res.rms[1]:.10g}"), ("RMS", f"{res.rms[2]:.10g}")]
-        for k, v in rows:
-            fh.write(f"{k}\t{v}\n")
-        fh.write("\nEstimated unknowns\n")
-        for nm, x in zip(res.xhatnames, res.xhat):
-            fh.write(f"{nm}\t{x:.10g}\n")
-    with open(os.path.join(folder, name + ".rsd"), "w") as fh:
-        for i in range(data.n_pts):
-            r = res.rsd[i]
-            fh.write(f"{data.pho_target[i]}\t{data.pho_image[i]}\t{data.xy[i, 0]:.10g}\t{data.xy[i, 1]:.10g}\t"
-                     f"{r[0]:.10g}\t{r[1]:.10g}\t{r[2]:.10g}\t{r[3]:.10g}\t{r[4]:.10g}\n")
+    """main.m:631-958: the .out report, the .rsd residual table and the .par camera file
+    (fba_amd/report.py)."""
+    from . import report
+    name = os.path.splitext(data.settings["Output_Filename"])[0]
+    out = os.path.join(folder, data.settings["Output_Filename"])
+    par = report.write_out(out, data, res, res.seconds)
+    report.write_rsd(os.path.join(folder, name + ".rsd"), data, res.rsd)
+    report.write_par(os.path.join(folder, name + ".par"), par)
     return out
 
 

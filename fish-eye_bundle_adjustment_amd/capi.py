@@ -22,7 +22,7 @@ EXPORTS = (
     "fba_last_error", "fba_abi_version", "fba_count_unknowns", "fba_partition", "fba_create",
     "fba_destroy", "fba_buildxhat", "fba_set_xhat", "fba_get_xhat", "fba_build_awg",
     "fba_accumulate", "fba_reduce_buffer", "fba_synchronize", "fba_solve_update", "fba_step", "fba_adjust",
-    "fba_residuals", "fba_finish_stats", "fba_last_timings", "fba_set_timing", "fba_set_probe",
+    "fba_residuals", "fba_finish_stats", "fba_covariance", "fba_last_timings", "fba_set_timing", "fba_set_probe",
     "fba_probe_stats",
 )
 
@@ -77,6 +77,7 @@ def _load():
         "fba_adjust": ([P, P, P], C.c_int),
         "fba_residuals": ([P, P, P, P], C.c_int),
         "fba_finish_stats": ([P, P, P, D, P], C.c_int),
+        "fba_covariance": ([P, D, P, P], C.c_int),
         "fba_last_timings": ([P, P], C.c_int),
         "fba_set_timing": ([P, I], C.c_int),
         "fba_set_probe": ([P, I], C.c_int),
@@ -230,6 +231,20 @@ class Context:
         st = np.zeros(6)
         check(lib.fba_residuals(self.h, ptr(v), ptr(rsd), ptr(st)))
         return v, rsd, st
+
+    def covariance(self, sigma02, corr=True):
+        """fba_covariance: diag of the reference's final Cx (main.m:428-482, :602) in xhat order, and
+        per EXT image the Correlation sub-matrix over [its estimated EOPs, its camera's estimated
+        IOPs] (main.m:446-456, :831-840), shape (n_img, u_img + u_cam, u_img + u_cam)."""
+        st = self.settings
+        u_img = sum(int(x) for x in (st.est_Xc, st.est_Yc, st.est_Zc, st.est_omega, st.est_phi, st.est_kappa))
+        u_cam = (int(st.est_xp) + int(st.est_yp) + int(st.est_c) + int(st.est_radial) * int(st.num_radial)
+                 + 2 * int(st.est_decent))
+        mu = u_img + u_cam
+        d = np.zeros(max(int(self.u), 1))
+        cr = np.zeros((max(self.packed.n_img, 1), mu, mu)) if corr else None
+        check(lib.fba_covariance(self.h, float(sigma02), ptr(d), ptr(cr)))
+        return d[: int(self.u)], (cr[: self.packed.n_img] if corr else None)
 
     def set_timing(self, on=True):
         check(lib.fba_set_timing(self.h, int(on)))

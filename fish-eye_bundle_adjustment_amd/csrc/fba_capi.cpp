@@ -206,6 +206,8 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     for (int e = 0; e < L.n_img; ++e)
         if (c->img_ord[e] >= 0) c->img_new[c->img_ord[e]] = e;
     full_to_ref_map(s, L, c->img_ord, c->full_to_ref);
+    c->ref_img_cam.assign(L.n_img_ref, -1);
+    for (int64_t i = 0; i < p->n_pts; ++i) c->ref_img_cam[p->img[i]] = p->cam[i];
 
     FBA_HIP(hipSetDevice(opt.device));
     c->device = opt.device;
@@ -659,6 +661,7 @@ static int accumulate_body(Ctx* c) {
 }
 
 static int accumulate(Ctx* c) {
+    c->have_factor = false;
     const int rc = run_graph(c, 0, [&] { return accumulate_body(c); });
     if (rc == FBA_OK) c->have_lin = true;
     return rc;
@@ -697,6 +700,7 @@ static int solve_update(Ctx* c, double* dsum) {
         c->last_ms[7] = ms;
     }
     c->have_delta = true;
+    c->have_factor = true;
     c->iterations++;
     const double info = c->h_pinned[1];
     *dsum = c->h_pinned[2];
@@ -931,6 +935,85 @@ int fba_residuals(fba_ctx* ctx, double* v, double* rsd, double* stats) {
         }
         stats[4] = sp;
         stats[5] = nu;
+    }
+    return FBA_OK;
+}
+
+int fba_covariance(fba_ctx* ctx, double sigma02, double* cx_diag, double* corr) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }
+    if (!c->have_factor || !c->have_delta) {
+        set_error("fba_covariance needs the factor of the last solve (call it once, right after the iterations)");
+        return FBA_ERR_ARG;
+    }
+    const Layout& L = c->L;
+    const int m = 6 + L.cw;
+    double *d_cdiag = nullptr, *d_pdiag = nullptr, *d_iblk = nullptr;
+    int32_t *d_islot = nullptr, *d_icam = nullptr;
+    std::vector<int32_t> islot(std::max(L.n_img_ref, 1), 0), icam(std::max(L.n_img_ref, 1), 0);
+    for (int e = 0; e < L.n_img_ref; ++e) {
+        islot[e] = c->img_new[e];
+        icam[e] = std::max(c->ref_img_cam[e], 0);
+    }
+    auto release = [&]() {
+        for (void* q : {(void*)d_cdiag, (void*)d_pdiag, (void*)d_iblk, (void*)d_islot, (void*)d_icam})
+            if (q) (void)hipFree(q);
+    };
+    int rc;
+    if ((rc = dalloc(&d_cdiag, (size_t)L.u_c)) || (rc = dalloc(&d_pdiag, 3 * (size_t)std::max(L.n_tie, 1))) ||
+        (corr && (rc = dalloc(&d_iblk, (size_t)std::max(L.n_img_ref, 1) * m * m))) || (rc = upload(&d_islot, islot)) ||
+        (rc = upload(&d_icam, icam))) {
+        release();
+        return rc;
+    }
+    if (hipMemsetAsync(d_pdiag, 0, sizeof(double) * 3 * std::max(L.n_tie, 1), c->stream) != hipSuccess) {
+        release();
+        set_error("hipMemsetAsync failed");
+        return FBA_ERR_HIP;
+    }
+    if ((rc = launch_covariance(*c, d_cdiag, d_pdiag, d_iblk, d_islot, d_icam, corr ? L.n_img_ref : 0))) {
+        release();
+        return rc;
+    }
+    std::vector<double> cd(L.u_c), pd(3 * (size_t)L.n_tie), ib(corr ? (size_t)L.n_img_ref * m * m : 0);
+    const hipError_t e1 = hipMemcpy(cd.data(), d_cdiag, sizeof(double) * cd.size(), hipMemcpyDeviceToHost);
+    const hipError_t e2 = pd.empty() ? hipSuccess : hipMemcpy(pd.data(), d_pdiag, sizeof(double) * pd.size(), hipMemcpyDeviceToHost);
+    const hipError_t e3 = ib.empty() ? hipSuccess : hipMemcpy(ib.data(), d_iblk, sizeof(double) * ib.size(), hipMemcpyDeviceToHost);
+    release();
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+        set_error("HIP error copying the covariance back");
+        return FBA_ERR_HIP;
+    }
+    if (cx_diag) {
+        std::fill(cx_diag, cx_diag + L.u_ref, 0.0);
+        for (int64_t i = 0; i < L.u_full; ++i) {
+            const int64_t r = c->full_to_ref[i];
+            if (r < 0 || (i >= L.u_c && !c->full_owned[i])) continue;
+            cx_diag[r] = sigma02 * (i < L.u_c ? cd[i] : pd[i - L.u_c]);  // main.m:602: Cx = sigma02 .* Cx
+        }
+    }
+    if (corr) {
+        // the reference's Correlation (main.m:446-456, before the distortion de-scaling) over
+        // [the image's estimated EOPs, its camera's estimated IOPs] (main.m:831-840), in xhat order
+        const int mu = L.u_img + L.u_cam;
+        std::vector<int> sel;
+        const int ee[6] = {c->set.est_Xc, c->set.est_Yc, c->set.est_Zc, c->set.est_omega, c->set.est_phi, c->set.est_kappa};
+        for (int a = 0; a < 6; ++a)
+            if (ee[a]) sel.push_back(a);
+        const int64_t cb = 6 * (int64_t)L.n_img;
+        for (int q = 0; q < L.cw; ++q)
+            if (L.n_cam > 0 && c->full_to_ref[cb + q] >= 0) sel.push_back(6 + q);
+        for (int e = 0; e < L.n_img_ref; ++e) {
+            const double* b = ib.data() + (size_t)e * m * m;
+            double* out = corr + (size_t)e * mu * mu;
+            for (int a = 0; a < (int)sel.size(); ++a)
+                for (int q = 0; q < (int)sel.size(); ++q) {
+                    const int ra = sel[a], rq = sel[q];
+                    out[a * mu + q] = c->ref_img_cam[e] < 0
+                                          ? 0.0
+                                          : b[ra * m + rq] / (std::sqrt(b[ra * m + ra]) * std::sqrt(b[rq * m + rq]));
+                }
+        }
     }
     return FBA_OK;
 }

@@ -870,7 +870,7 @@ __device__ __forceinline__ double gemv_t128(const double* __restrict__ M, int64_
 // i = srcs[b] of the level, x_i = Linv_i' y_i (y_i is final: its contributions came from higher
 // levels).  Workgroup nsrc + t: target column j = tgts[t], y_j -= sum_i L(i,j)' x_i over its sources
 // (ascending; x_i recomputed locally from y_i, one 128x128 GEMV, instead of a second launch).
-__global__ __launch_bounds__(256) void k_bwd_wave(double* __restrict__ S, int64_t ld, int64_t n_pad,
+__global__ __launch_bounds__(256) void k_bwd_wave(double* __restrict__ S, int64_t ld, int64_t yrow,
                                                   const double* __restrict__ linv, double* __restrict__ X,
                                                   const int32_t* __restrict__ srcs, int nsrc,
                                                   const int32_t* __restrict__ tgts, const int32_t* __restrict__ tstart,
@@ -879,7 +879,7 @@ __global__ __launch_bounds__(256) void k_bwd_wave(double* __restrict__ S, int64_
     __shared__ double xs[CB];
     __shared__ double red[512];
     const int tid = threadIdx.x;
-    double* y = S + n_pad * ld;
+    double* y = S + yrow * ld;  // the right-hand-side row (n_pad: the solve; n_pad + a: border column a)
     if ((int)blockIdx.x < nsrc) {
         const int64_t i = srcs[blockIdx.x];
         if (tid < CB) ys[tid] = y[i * CB + tid];
@@ -939,6 +939,29 @@ int launch_cholesky(Ctx& c) {
         if (W.ncomb > 0)
             k_syrk_combine<<<(unsigned)W.ncomb, 256, 0, c.stream>>>(c.d_S, ld, c.d_sched + W.comb, c.d_P);
     }
+    FBA_HIP(hipGetLastError());
+    return FBA_OK;
+}
+
+// backward solves of the forward-solved right-hand-side rows row0 .. row0+nrows-1 (covariance,
+// fba_cov.hip); X + r n_pad receives the solution of row row0 + r.  The rows are consumed.
+int launch_backward_rows(Ctx& c, int row0, int nrows, double* X) {
+    const int64_t ld = c.L.ld;
+    const Sched& s = c.sched;
+    for (int r = 0; r < nrows; ++r)
+        for (int w = s.n_waves - 1; w >= 0; --w) {
+            const Sched::BWave& B = s.b[w];
+            k_bwd_wave<<<(unsigned)(B.nsrc + B.ntgt), 256, 0, c.stream>>>(
+                c.d_S, ld, c.L.n_pad + row0 + r, c.d_linv, X + (int64_t)r * c.L.n_pad, c.d_sched + B.srcs, B.nsrc,
+                c.d_sched + B.tgts, c.d_sched + B.src_start, c.d_sched + B.src);
+        }
+    FBA_HIP(hipGetLastError());
+    return FBA_OK;
+}
+
+int launch_border_gram(Ctx& c, double* gpart, int* nseg) {
+    k_border_gram<<<GRAM_SEG, 256, 0, c.stream>>>(c.d_S, c.L.ld, c.L.n_pad, gpart);
+    *nseg = GRAM_SEG;
     FBA_HIP(hipGetLastError());
     return FBA_OK;
 }

@@ -1,0 +1,429 @@
+// fba_cov.hip -- post-fit covariance of the unknowns on the device (gfx950 / MI355X).
+//
+// The reference keeps Cx = the (bordered) inverse of the normal matrix of the last iteration
+// (main.m:428-444), its correlation matrix (main.m:446-456, before the distortion de-scaling), the
+// diagonal de-scaling of Cx for the distortion terms (main.m:460-482) and Cx *= sigma0^2 (main.m:602);
+// the .out/.par writers read sqrt(diag Cx) and small correlation sub-blocks (main.m:711-880).  Dense,
+// that is a u x u inverse (u = 156,010 at config 4).  Here only the entries those outputs read are
+// formed, from the block Cholesky factor M = L L' the last iteration left in S (fba_chol.hip):
+//
+//   selected inversion  Q = M^-1 on the block pattern of L (Takahashi recurrence), top level first:
+//                         Y_i  = L_ik L_kk^-1                       (i in R_k, the block rows of column k)
+//                         Q_ik = -sum_{j in R_k} Q_ij Y_j            (Q_ij of higher levels, already formed)
+//                         Q_kk = L_kk^-T L_kk^-1 - sum_i Y_i' Q_ik
+//                       written over L in place (a level only reads columns of higher levels);
+//   border (inner constraints)  the bordered inverse's camera block is C = Q - Z H^-1 Z' with
+//                       Z = L^-T [A~ B~] (14 backward solves of the forward-solved border rows) and H the
+//                       14x14 matrix k_border_combine solves with (derivation: u = (I - F H^-1 F') y);
+//                       without inner constraints C = Q;
+//   camera side         diag C, and per image the (6 + cw)^2 block over its EOPs and its camera's
+//                       unknowns (the reference's EOP/IOP correlation sub-matrices);
+//   tie points          Cx_pp = V^-1 + T' C T with T = W V^-1 of the point's observations and camera
+//                       (the Schur identity for the eliminated points), diagonal only.
+// All sums run in a fixed order (no atomics).  The factor in S is consumed; the next iteration
+// re-accumulates S from scratch (k_zero_blocks), so nothing else is affected.
+#include "fba_internal.h"
+
+#include <algorithm>
+#include <vector>
+
+namespace fba {
+
+constexpr int CB = NB;  // 128
+
+// ------------------------------------------------------------------------------------------------
+// k_blk_gemm: one workgroup per task, C(128x128) = sum_t sign_t op(A_t) op(B_t), terms in list order.
+// Operand/output bases: 0 = S (leading dimension ld), 1 = linv, 2 = Y scratch (both 128).
+// Thread (ty, tx) of a 16x16 grid owns rows ty + 16 a, columns tx + 16 b (a, b < 8); K in slices of
+// 16 staged through LDS.
+// task record (int64): out offset, out base, first term, end term
+// term record (int64): A offset, B offset, flags = baseA | baseB << 2 | tA << 4 | tB << 5 | neg << 6
+// ------------------------------------------------------------------------------------------------
+constexpr int KS = 16;
+constexpr int LP = CB + 4;
+
+__global__ __launch_bounds__(256) void k_blk_gemm(const int64_t* __restrict__ tasks, const int64_t* __restrict__ terms,
+                                                  double* __restrict__ S, int64_t ld, const double* __restrict__ linv,
+                                                  double* __restrict__ Y) {
+    __shared__ double As[KS][LP];
+    __shared__ double Bs[KS][LP];
+    const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+    const int64_t* tk = tasks + 4 * (int64_t)blockIdx.x;
+    double acc[8][8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[a][b] = 0.0;
+    for (int64_t t = tk[2]; t < tk[3]; ++t) {
+        const int64_t* tr = terms + 3 * t;
+        const int fl = (int)tr[2];
+        const int ba = fl & 3, bb = (fl >> 2) & 3, ta = (fl >> 4) & 1, tb = (fl >> 5) & 1;
+        const double sg = (fl >> 6) & 1 ? -1.0 : 1.0;
+        const double* A = (ba == 0 ? S : ba == 1 ? linv : Y) + tr[0];
+        const double* B = (bb == 0 ? S : bb == 1 ? linv : Y) + tr[1];
+        const int64_t lda = ba == 0 ? ld : CB, ldb = bb == 0 ? ld : CB;
+        for (int k0 = 0; k0 < CB; k0 += KS) {
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int idx = tid + 256 * q;
+                int r, kk;
+                double v;
+                if (!ta) { r = idx >> 4; kk = idx & 15; v = A[(int64_t)r * lda + k0 + kk]; }
+                else { kk = idx >> 7; r = idx & 127; v = A[(int64_t)(k0 + kk) * lda + r]; }
+                As[kk][r] = sg * v;
+                int c;
+                if (!tb) { kk = idx >> 7; c = idx & 127; v = B[(int64_t)(k0 + kk) * ldb + c]; }
+                else { c = idx >> 4; kk = idx & 15; v = B[(int64_t)c * ldb + k0 + kk]; }
+                Bs[kk][c] = v;
+            }
+            __syncthreads();
+#pragma unroll 4
+            for (int kk = 0; kk < KS; ++kk) {
+                double av[8], bv[8];
+#pragma unroll
+                for (int a = 0; a < 8; ++a) av[a] = As[kk][ty + 16 * a];
+#pragma unroll
+                for (int b = 0; b < 8; ++b) bv[b] = Bs[kk][tx + 16 * b];
+#pragma unroll
+                for (int a = 0; a < 8; ++a)
+#pragma unroll
+                    for (int b = 0; b < 8; ++b) acc[a][b] += av[a] * bv[b];
+            }
+        }
+    }
+    double* C = (tk[1] == 0 ? S : Y) + tk[0];
+    const int64_t ldc = tk[1] == 0 ? ld : CB;
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) C[(int64_t)(ty + 16 * a) * ldc + tx + 16 * b] = acc[a][b];
+}
+
+// H^-1 of the 14x14 border system (k_border_combine's H = [[A'A - I, A'B], [B'A, B'B]] from the Gram of
+// the forward-solved rows 1..14), Gauss-Jordan with partial pivoting, one wave; gpart as k_border_gram
+__global__ __launch_bounds__(64) void k_border_hinv(const double* __restrict__ gpart, int nseg, double* __restrict__ hinv) {
+    __shared__ double g[15][15];
+    __shared__ double H[14][28];
+    const int tid = threadIdx.x;
+    for (int e = tid; e < 120; e += 64) {
+        int a = 0, rem = e;
+        while (rem >= 15 - a) { rem -= 15 - a; ++a; }
+        const int b = a + rem;
+        double v = 0.0;
+        for (int q = 0; q < nseg; ++q) v += gpart[q * 120 + e];
+        g[a][b] = g[b][a] = v;
+    }
+    __syncthreads();
+    for (int i = tid; i < 14 * 28; i += 64) {
+        const int r = i / 28, q = i % 28;
+        H[r][q] = q < 14 ? g[1 + r][1 + q] - ((r == q && r < 7) ? 1.0 : 0.0) : (q - 14 == r ? 1.0 : 0.0);
+    }
+    __syncthreads();
+    for (int col = 0; col < 14; ++col) {
+        if (tid == 0) {
+            int p = col;
+            for (int r = col + 1; r < 14; ++r)
+                if (fabs(H[r][col]) > fabs(H[p][col])) p = r;
+            if (p != col)
+                for (int q = 0; q < 28; ++q) { const double t = H[col][q]; H[col][q] = H[p][q]; H[p][q] = t; }
+        }
+        __syncthreads();
+        const double piv = H[col][col];
+        __syncthreads();
+        if (tid < 28) H[col][tid] /= piv;
+        __syncthreads();
+        for (int i = tid; i < 14 * 28; i += 64) {
+            const int r = i / 28, q = i % 28;
+            if (r != col && q != col) H[r][q] -= H[r][col] * H[col][q];
+        }
+        __syncthreads();
+        if (tid < 14 && tid != col) H[tid][col] = 0.0;
+        __syncthreads();
+    }
+    for (int i = tid; i < 196; i += 64) hinv[i] = H[i / 14][14 + i % 14];
+}
+
+// Wz[a][i] = sum_b Hinv[a][b] Z[b][i]
+__global__ void k_border_wz(const double* __restrict__ Z, const double* __restrict__ hinv, double* __restrict__ Wz,
+                            int64_t n_pad) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_pad) return;
+    double z[14];
+#pragma unroll
+    for (int b = 0; b < 14; ++b) z[b] = Z[b * n_pad + i];
+#pragma unroll
+    for (int a = 0; a < 14; ++a) {
+        double s = 0.0;
+#pragma unroll
+        for (int b = 0; b < 14; ++b) s += hinv[a * 14 + b] * z[b];
+        Wz[a * n_pad + i] = s;
+    }
+}
+
+// C(r, c) of the camera-side system: Q from the selected inverse in S (lower blocks; diagonal blocks
+// full), minus the border's low-rank term when nz = 14
+__device__ __forceinline__ double cget(const double* __restrict__ S, int64_t ld, const double* __restrict__ Z,
+                                       const double* __restrict__ Wz, int nz, int64_t n_pad, int64_t r, int64_t c) {
+    const int64_t rr = (r / CB >= c / CB) ? r : c, cc = (r / CB >= c / CB) ? c : r;
+    double v = S[rr * ld + cc];
+    for (int a = 0; a < nz; ++a) v -= Z[a * n_pad + r] * Wz[a * n_pad + c];
+    return v;
+}
+
+// camera side: diag C (de-scaled as main.m:460-482) and the (6+cw)^2 block of every image slot
+__global__ void k_cov_cam(const double* __restrict__ S, int64_t ld, const double* __restrict__ Z,
+                          const double* __restrict__ Wz, int nz, int64_t n_pad, int64_t u_c, int n_img, int cw, int nk,
+                          const double* __restrict__ cam_tab, int cam_stride, double* __restrict__ cdiag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= u_c) return;
+    double v = cget(S, ld, Z, Wz, nz, n_pad, i, i);
+    const int64_t cb = 6 * (int64_t)n_img;
+    if (i >= cb) {
+        const int64_t k = (i - cb) / cw;
+        const int q = (int)((i - cb) % cw);
+        const double* ct = cam_tab + k * cam_stride;
+        if (q >= 3 && q < 3 + nk) { const double s = ct[CAM_TAB_HDR + nk + (q - 3)]; v /= s * s; }
+        else if (q >= 3 + nk) { const double s = ct[6]; v /= s * s; }
+    }
+    cdiag[i] = v;
+}
+
+__global__ __launch_bounds__(256) void k_cov_img(const double* __restrict__ S, int64_t ld, const double* __restrict__ Z,
+                                                 const double* __restrict__ Wz, int nz, int64_t n_pad,
+                                                 const int32_t* __restrict__ slots, const int32_t* __restrict__ cams,
+                                                 int n_img, int cw, double* __restrict__ blk) {
+    const int e = blockIdx.x;
+    const int m = 6 + cw;
+    const int64_t s = slots[e], k = cams[e];
+    for (int idx = threadIdx.x; idx < m * m; idx += blockDim.x) {
+        const int a = idx / m, b = idx % m;
+        const int64_t r = a < 6 ? 6 * s + a : 6 * (int64_t)n_img + k * cw + (a - 6);
+        const int64_t c = b < 6 ? 6 * s + b : 6 * (int64_t)n_img + k * cw + (b - 6);
+        blk[(int64_t)e * m * m + idx] = cget(S, ld, Z, Wz, nz, n_pad, r, c);
+    }
+}
+
+// tie points: one wave per local point.  Row groups g = 0..m-1 (observation g: 6 rows of its image,
+// T = WT[o]), g = m (the camera: cw rows, Tc).  Lane pairs (g, h) of groups add sum T_g' C_gh T_h
+// (diagonal of the 3x3 only); lanes a < nz add the border term (Z_a' T)(Wz_a' T).  Fixed-order
+// wave reduction.
+__global__ __launch_bounds__(256) void k_cov_pts(const double* __restrict__ S, int64_t ld, const double* __restrict__ Z,
+                                                 const double* __restrict__ Wz, int nz, int64_t n_pad,
+                                                 const double* __restrict__ WT, const double* __restrict__ PT, int ps,
+                                                 const int32_t* __restrict__ lp_start, const int32_t* __restrict__ lp_tie,
+                                                 const int32_t* __restrict__ lp_cam, const int32_t* __restrict__ img,
+                                                 int64_t n_lp, int n_img, int cw, int64_t u_c, double* __restrict__ pdiag) {
+    const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (p >= n_lp) return;
+    const int o0 = lp_start[p], m = lp_start[p + 1] - o0;
+    const double* P = PT + p * ps;
+    const double* Tc = P + 12 + 3 * cw;
+    const int64_t cam0 = 6 * (int64_t)n_img + (int64_t)lp_cam[p] * cw;
+    auto grp_rows = [&](int g, int64_t& r0, int& n, const double*& T) {
+        if (g < m) { r0 = 6 * (int64_t)img[o0 + g]; n = 6; T = WT + (int64_t)(o0 + g) * 18; }
+        else { r0 = cam0; n = cw; T = Tc; }
+    };
+    double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+    const int ng = m + 1;
+    for (int pr = lane; pr < ng * ng; pr += 64) {
+        const int g = pr / ng, h = pr % ng;
+        int64_t r0, c0;
+        int nr, nc;
+        const double *Tg, *Th;
+        grp_rows(g, r0, nr, Tg);
+        grp_rows(h, c0, nc, Th);
+        for (int a = 0; a < nr; ++a) {
+            double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+            for (int b = 0; b < nc; ++b) {
+                const int64_t r = r0 + a, c = c0 + b;
+                const int64_t rr = (r / CB >= c / CB) ? r : c, cc = (r / CB >= c / CB) ? c : r;
+                const double q = S[rr * ld + cc];
+                s0 += q * Th[3 * b]; s1 += q * Th[3 * b + 1]; s2 += q * Th[3 * b + 2];
+            }
+            acc0 += Tg[3 * a] * s0; acc1 += Tg[3 * a + 1] * s1; acc2 += Tg[3 * a + 2] * s2;
+        }
+    }
+    if (lane < nz) {
+        double z0 = 0, z1 = 0, z2 = 0, w0 = 0, w1 = 0, w2 = 0;
+        for (int g = 0; g < ng; ++g) {
+            int64_t r0;
+            int nr;
+            const double* Tg;
+            grp_rows(g, r0, nr, Tg);
+            for (int a = 0; a < nr; ++a) {
+                const double zv = Z[lane * n_pad + r0 + a], wv = Wz[lane * n_pad + r0 + a];
+                z0 += zv * Tg[3 * a]; z1 += zv * Tg[3 * a + 1]; z2 += zv * Tg[3 * a + 2];
+                w0 += wv * Tg[3 * a]; w1 += wv * Tg[3 * a + 1]; w2 += wv * Tg[3 * a + 2];
+            }
+        }
+        acc0 -= z0 * w0; acc1 -= z1 * w1; acc2 -= z2 * w2;
+    }
+#pragma unroll
+    for (int w = 32; w > 0; w >>= 1) {
+        acc0 += __shfl_xor(acc0, w, 64);
+        acc1 += __shfl_xor(acc1, w, 64);
+        acc2 += __shfl_xor(acc2, w, 64);
+    }
+    if (lane == 0) {
+        double* out = pdiag + 3 * (int64_t)lp_tie[p];
+        out[0] = P[0] + acc0;
+        out[1] = P[3] + acc1;
+        out[2] = P[5] + acc2;
+    }
+}
+
+// backward solve of one right-hand-side row (fba_chol.hip)
+int launch_backward_rows(Ctx& c, int row0, int nrows, double* X);
+int launch_border_gram(Ctx& c, double* gpart, int* nseg);
+
+// ------------------------------------------------------------------------------------------------
+// driver: rebuilds the last linearisation's point tables (k_lin_point), the 14 border columns, the
+// selected inverse level by level (top down), then the requested diagonals / blocks.
+// Outputs (device, internal order): cdiag [u_c] (de-scaled camera-side diag C), pdiag [3 n_tie]
+// (tie points of this rank), iblk [n_img_ref][(6+cw)^2] (raw C blocks per reference image).
+// ------------------------------------------------------------------------------------------------
+int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, const int32_t* d_islot,
+                      const int32_t* d_icam, int n_iblk) {
+    const Layout& L = c.L;
+    const int64_t ld = L.ld, n_pad = L.n_pad, nb = n_pad / CB;
+    const Sched& s = c.sched;
+    int rc;
+    // point tables of the last linearisation (V^-1, T, Tc), as fba_residuals does
+    if ((rc = launch_params(c, c.d_xlin)) || (rc = launch_linearize(c, c.d_xlin))) return rc;
+
+    const int nz = L.nrhs > 1 ? 14 : 0;
+    double *d_Z = nullptr, *d_Wz = nullptr, *d_h = nullptr, *d_g = nullptr;
+    std::vector<void*> tmp;
+    auto alloc = [&](double** p, size_t n) -> int {
+        FBA_HIP(hipMalloc((void**)p, sizeof(double) * std::max<size_t>(n, 1)));
+        tmp.push_back(*p);
+        return FBA_OK;
+    };
+    auto cleanup = [&]() { for (void* q : tmp) (void)hipFree(q); tmp.clear(); };
+    if (nz) {
+        if ((rc = alloc(&d_Z, 14 * (size_t)n_pad)) || (rc = alloc(&d_Wz, 14 * (size_t)n_pad)) ||
+            (rc = alloc(&d_h, 196)) || (rc = alloc(&d_g, 64 * 120))) { cleanup(); return rc; }
+        int nseg = 0;
+        if ((rc = launch_border_gram(c, d_g, &nseg)) || (rc = launch_backward_rows(c, 1, 14, d_Z))) { cleanup(); return rc; }
+        k_border_hinv<<<1, 64, 0, c.stream>>>(d_g, nseg, d_h);
+        k_border_wz<<<(unsigned)((n_pad + 255) / 256), 256, 0, c.stream>>>(d_Z, d_h, d_Wz, n_pad);
+    }
+
+    // block rows R_k of every column (from the panel-solve records, half 0), RHS block row excluded
+    std::vector<std::vector<int32_t>> R(nb);
+    for (int w = 0; w < s.n_waves; ++w) {
+        const int32_t* tr = s.buf.data() + s.w[w].trsm;
+        for (int t = 0; t < s.w[w].ntrsm; ++t) {
+            const int32_t k = tr[2 * t], r2 = tr[2 * t + 1];
+            if ((r2 & 1) == 0 && r2 / 2 < nb) R[k].push_back(r2 / 2);
+        }
+    }
+    size_t ymax = 1;
+    for (int w = 0; w < s.n_waves; ++w) {
+        size_t n = 0;
+        const int32_t* cols = s.buf.data() + s.w[w].cols;
+        for (int q = 0; q < s.w[w].ncol; ++q) n += R[cols[q]].size();
+        ymax = std::max(ymax, n);
+    }
+    double* d_Y = nullptr;
+    int64_t *d_tasks = nullptr, *d_terms = nullptr;
+    if ((rc = alloc(&d_Y, ymax * CB * CB))) { cleanup(); return rc; }
+    // generous task/term buffers: sized by the largest level
+    size_t tmax = 1, rmax = 1;
+    for (int w = 0; w < s.n_waves; ++w) {
+        size_t nt = 0, nr = 0;
+        const int32_t* cols = s.buf.data() + s.w[w].cols;
+        for (int q = 0; q < s.w[w].ncol; ++q) {
+            const size_t r = R[cols[q]].size();
+            nt += 2 * r + 1;
+            nr += r + r * r + 1 + r;
+        }
+        tmax = std::max(tmax, nt);
+        rmax = std::max(rmax, nr);
+    }
+    if ((rc = alloc((double**)&d_tasks, 4 * tmax)) || (rc = alloc((double**)&d_terms, 3 * rmax))) { cleanup(); return rc; }
+
+    auto blk = [&](int64_t i, int64_t j) { return i * CB * ld + j * CB; };
+    std::vector<int64_t> tasks, terms;
+    auto launch = [&]() -> int {
+        if (tasks.empty()) return FBA_OK;
+        FBA_HIP(hipMemcpyAsync(d_tasks, tasks.data(), sizeof(int64_t) * tasks.size(), hipMemcpyHostToDevice, c.stream));
+        FBA_HIP(hipMemcpyAsync(d_terms, terms.data(), sizeof(int64_t) * std::max<size_t>(terms.size(), 1),
+                               hipMemcpyHostToDevice, c.stream));
+        k_blk_gemm<<<(unsigned)(tasks.size() / 4), 256, 0, c.stream>>>(d_tasks, d_terms, c.d_S, ld, c.d_linv, d_Y);
+        FBA_HIP(hipGetLastError());
+        FBA_HIP(hipStreamSynchronize(c.stream));  // host lists are rebuilt for the next launch
+        tasks.clear();
+        terms.clear();
+        return FBA_OK;
+    };
+    auto task = [&](int64_t out, int base) {
+        tasks.insert(tasks.end(), {out, (int64_t)base, (int64_t)terms.size() / 3, 0});
+    };
+    auto term = [&](int64_t a, int64_t b, int fl) { terms.insert(terms.end(), {a, b, (int64_t)fl}); };
+    auto close_task = [&]() { tasks.back() = (int64_t)terms.size() / 3; };
+    enum { BS = 0, BL = 1, BY = 2 };
+    for (int w = s.n_waves - 1; w >= 0; --w) {
+        const int32_t* cols = s.buf.data() + s.w[w].cols;
+        const int ncol = s.w[w].ncol;
+        std::vector<size_t> ybase(ncol);
+        size_t ny = 0;
+        for (int q = 0; q < ncol; ++q) { ybase[q] = ny; ny += R[cols[q]].size(); }
+        // (1) Y_i = L_ik Linv_k
+        for (int q = 0; q < ncol; ++q) {
+            const int64_t k = cols[q];
+            for (size_t a = 0; a < R[k].size(); ++a) {
+                task((int64_t)(ybase[q] + a) * CB * CB, BY);
+                term(blk(R[k][a], k), k * CB * CB, BS | BL << 2);
+                close_task();
+            }
+        }
+        if ((rc = launch())) { cleanup(); return rc; }
+        // (2) Q_ik = -sum_j Q_ij Y_j
+        for (int q = 0; q < ncol; ++q) {
+            const int64_t k = cols[q];
+            for (size_t a = 0; a < R[k].size(); ++a) {
+                const int64_t i = R[k][a];
+                task(blk(i, k), BS);
+                for (size_t b = 0; b < R[k].size(); ++b) {
+                    const int64_t j = R[k][b];
+                    const int64_t y = (int64_t)(ybase[q] + b) * CB * CB;
+                    if (i >= j) term(blk(i, j), y, BS | BY << 2 | 1 << 6);
+                    else term(blk(j, i), y, BS | BY << 2 | 1 << 4 | 1 << 6);
+                }
+                close_task();
+            }
+        }
+        if ((rc = launch())) { cleanup(); return rc; }
+        // (3) Q_kk = Linv_k' Linv_k - sum_i Y_i' Q_ik
+        for (int q = 0; q < ncol; ++q) {
+            const int64_t k = cols[q];
+            task(blk(k, k), BS);
+            term(k * CB * CB, k * CB * CB, BL | BL << 2 | 1 << 4);
+            for (size_t a = 0; a < R[k].size(); ++a)
+                term((int64_t)(ybase[q] + a) * CB * CB, blk(R[k][a], k), BY | BS << 2 | 1 << 4 | 1 << 6);
+            close_task();
+        }
+        if ((rc = launch())) { cleanup(); return rc; }
+    }
+
+    if (d_cdiag)
+        k_cov_cam<<<(unsigned)((L.u_c + 255) / 256), 256, 0, c.stream>>>(c.d_S, ld, d_Z, d_Wz, nz, n_pad, L.u_c, L.n_img,
+                                                                         L.cw, L.nk, c.d_cam_tab, c.cam_tab_stride, d_cdiag);
+    if (d_iblk && n_iblk > 0)
+        k_cov_img<<<(unsigned)n_iblk, 256, 0, c.stream>>>(c.d_S, ld, d_Z, d_Wz, nz, n_pad, d_islot, d_icam, L.n_img, L.cw,
+                                                          d_iblk);
+    if (d_pdiag && c.n_lp > 0)
+        k_cov_pts<<<(unsigned)((c.n_lp + 3) / 4), 256, 0, c.stream>>>(c.d_S, ld, d_Z, d_Wz, nz, n_pad, c.d_WT, c.d_pt_tab,
+                                                                      c.pt_comp, c.d_lp_start, c.d_lp_tie, c.d_lp_cam,
+                                                                      c.d_img, c.n_lp, L.n_img, L.cw, L.u_c, d_pdiag);
+    FBA_HIP(hipGetLastError());
+    FBA_HIP(hipStreamSynchronize(c.stream));
+    cleanup();
+    c.have_factor = false;
+    return FBA_OK;
+}
+
+}  // namespace fba

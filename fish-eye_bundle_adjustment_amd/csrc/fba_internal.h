@@ -181,6 +181,8 @@ struct Ctx {
     // state
     bool have_lin = false;       // d_J holds a linearisation
     bool have_delta = false;
+    bool have_factor = false;    // d_S holds the factor of the last solve (fba_covariance consumes it)
+    std::vector<int32_t> ref_img_cam;  // [n_img_ref] camera of each EXT image (-1: no observation)
     int iterations = 0;
     bool timing = false;
     // kernel probe (fba_set_probe): HIP events around every bulk trailing-update launch
@@ -219,6 +221,8 @@ int launch_cholesky(Ctx& c);     // factor + forward solve of RHS rows
 int launch_backward(Ctx& c);     // border combine + backward solve -> delta_c
 int launch_backsub_update(Ctx& c);
 int launch_residuals(Ctx& c);    // v per obs, partial sums
+int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, const int32_t* d_islot,
+                      const int32_t* d_icam, int n_iblk);  // post-fit covariance (fba_cov.hip)
 int launch_dense_awg(Ctx& c, double* dA, double* dG, const int64_t* d_map, int64_t n_rows, int64_t u_ref);
 
 }  // namespace fba

@@ -99,10 +99,12 @@ def parse_settings(cfg_rows, folder):
         s["Meas_std"] = float(v)
         vy, oky = find_setting(cfg_rows, "Meas_std_y")
         s["Meas_std_y"] = float(vy) if oky else float(v)  # main.m:397-402
+        s["no_std_y"] = 0 if oky else 1                     # main.m:129 (the .out settings list)
     else:
         # main.m:125-127 sets sigma = 1 (the reference then trips over rmfield at main.m:399)
         s["Meas_std"] = 1.0
         s["Meas_std_y"] = 1.0
+        s["no_std_y"] = 1
     v, ok = find_setting(cfg_rows, "Type")
     s["type"] = v if ok else "fisheye"
     v, ok = find_setting(cfg_rows, "Check_Points", True)

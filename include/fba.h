@@ -167,6 +167,18 @@ int fba_residuals(fba_ctx* ctx, double* v, double* rsd, double* stats);
 int fba_finish_stats(const fba_problem* p, const fba_settings* s, const double* sums /*[2]: sum vx^2, sum vy^2*/,
                      double vtpv, double* stats /*[6]*/);
 
+/* Post-fit covariance of the unknowns (main.m:428-456, :460-482, :602): from the factor of the LAST
+ * solve (call right after the iterations, before any further fba_accumulate / fba_step; the factor is
+ * consumed).  sigma02 is the a-posteriori variance factor (fba_residuals stats[3] or fba_finish_stats).
+ *   cx_diag [u] (may be NULL): diag(Cx) of the reference's final Cx = sigma02 * (bordered) inverse of
+ *           the last normal matrix, distortion entries de-scaled by dist_scaling^2 (main.m:460-482,
+ *           diagonal only, as the reference); xhat order.  With world > 1 the tie entries of other
+ *           ranks are 0 (camera entries are replicated).
+ *   corr [n_img][(u_img+u_cam)^2] (may be NULL): per EXT image, the reference's Correlation matrix
+ *           (main.m:446-456) restricted to [the image's estimated EOPs, its camera's estimated
+ *           IOP/distortion unknowns] in xhat order, full symmetric, row-major (main.m:831-840). */
+int fba_covariance(fba_ctx* ctx, double sigma02, double* cx_diag, double* corr);
+
 /* Per-phase device timings of the last fba_step / fba_accumulate+fba_solve_update, in ms:
  * [0] params+linearize, [1] point-side, [2] image/pair/camera accumulation, [3] border,
  * [4] Cholesky+forward, [5] backward+border solve, [6] back-substitution+update, [7] total. */

@@ -651,6 +651,29 @@ def adjust(data, solver=None, max_iter=None):
                   rms=(rmsx, rmsy, math.sqrt(rmsx ** 2 + rmsy ** 2)), sigma02=sigma02, w0=w0)
 
 
+def covariance(data, res):
+    """The reference's post-fit covariance, restated from the last iteration's A, w, G:
+    Cx = the (bordered) inverse (main.m:428-444), Correlation = Cx / sqrt(diag x diag) before the
+    de-scaling (main.m:446-456), the diagonal de-scaling of the distortion entries (main.m:460-482)
+    and Cx = sigma02 * Cx (main.m:602).  Returns (diag of the final Cx, Correlation)."""
+    s = data.settings
+    _, Cx = solve_dense(data, res.A, res.w, res.G, weights(data))
+    d = np.sqrt(np.diag(Cx))
+    corr = Cx / np.outer(d, d)
+    diag = np.diag(Cx).copy()
+    ds = res.dist_scaling
+    for i in range(ds.shape[0]):
+        if s["Estimate_radial"]:
+            ri = int(ds[i, 0]) - 1
+            for j in range(s["Num_Radial_Distortions"]):
+                diag[ri + j] /= ds[i, 2 + j] ** 2
+        if s["Estimate_decent"]:
+            di = int(ds[i, 1]) - 1
+            diag[di] /= ds[i, 2] ** 2
+            diag[di + 1] /= ds[i, 2] ** 2
+    return res.sigma02 * diag, corr
+
+
 def build_rsd(data, v, xhat):
     """BuildRSD.m:1-43: per point [r, vx, vy, vr, vt] (ids / x / y are carried by the caller)."""
     s = data.settings

@@ -226,3 +226,41 @@ def test_sharded_step_over_rccl_and_device_views(fba, cam0_folders):
     for c in ranks:
         c.close()
     ref.close()
+
+
+def _check_cov(res, od, ro, oracle, rtol=1e-7, atol_corr=1e-7):
+    """diag(Cx) and the EOP/IOP correlation sub-blocks of fba_covariance against the oracle's dense
+    bordered inverse of the last normal matrix (main.m:428-482, :602)."""
+    cdo, corro = oracle.covariance(od, ro)
+    np.testing.assert_allclose(res.cx_diag, cdo, rtol=rtol, atol=0)
+    u_img, u_cam = oracle.counts(od.settings)
+    for e in range(od.numImg):
+        idx = list(range(e * u_img, (e + 1) * u_img))
+        k = int(od.cam_num[np.nonzero(od.ext_index == e)[0][0]])
+        idx += list(range(u_img * od.numImg + k * u_cam, u_img * od.numImg + (k + 1) * u_cam))
+        np.testing.assert_allclose(res.corr[e], corro[np.ix_(idx, idx)], rtol=0, atol=atol_corr)
+
+
+@pytest.mark.parametrize("variant", ["stage3_pinhole", "stage1_pinhole", "stage3_noic_pinhole", "stage3_sigy_pinhole"])
+def test_covariance_cam0(fba, oracle, cam0_folders, variant):
+    """Post-fit covariance on cam0: selected inverse of the block Cholesky factor + the border's
+    low-rank correction + the tie-point Schur identity, against the reference's explicit inverse."""
+    ds = fba.load_folder(cam0_folders[variant])
+    od = oracle.load_folder(cam0_folders[variant])
+    ro = oracle.adjust(od)
+    res = fba.adjust(ds)
+    _check_cov(res, od, ro, oracle)
+
+
+@pytest.mark.parametrize("n_control", [0, 12])
+def test_covariance_synthetic(fba, oracle, tmp_path, n_control):
+    """Free-network fish-eye scene (inner constraints) and a scene whose datum comes from control
+    points (no inner constraints): every estimated unknown's variance, tie points included."""
+    from fba_amd import synth
+    sc = synth.generate(14, 260, seed=23, typ="fisheye", n_control=n_control)
+    folder = synth.write_folder(sc, str(tmp_path / f"c{n_control}"))
+    ds = fba.load_folder(folder)
+    od = oracle.load_folder(folder)
+    ro = oracle.adjust(od)
+    res = fba.adjust(ds)
+    _check_cov(res, od, ro, oracle)
