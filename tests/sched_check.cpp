@@ -137,6 +137,17 @@ int main(int argc, char** argv) {
             printf("\n");
         }
         printf("scratch quarters %d\n", s.n_scratch);
+        // work of the covariance's selected inversion (fba_cov.hip): per column k, |R_k| + |R_k|^2 + |R_k| + 1
+        // 128^3 block products (R_k = the block rows below k, RHS row excluded)
+        std::vector<int64_t> nr(L.n_pad / NB, 0);
+        for (int w = 0; w < s.n_waves; ++w) {
+            const int32_t* tr = s.buf.data() + s.w[w].trsm;
+            for (int t = 0; t < s.w[w].ntrsm; ++t)
+                if ((tr[2 * t + 1] & 1) == 0 && tr[2 * t + 1] / 2 < L.n_pad / NB) nr[tr[2 * t]]++;
+        }
+        double prods = 0.0;
+        for (int64_t r : nr) prods += (double)(2 * r + r * r + 1);
+        printf("selected inversion: %.0f block products, %.1f GFLOP\n", prods, prods * 2.0 * NB * NB * NB * 1e-9);
         return 0;
     }
     const int64_t n = L.n_pad, nb = n / NB, nr = n + NB;  // rows: matrix + RHS block row

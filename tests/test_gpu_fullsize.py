@@ -16,7 +16,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import dist_scaling_of, group_rel_err
+from conftest import dist_scaling_of, distortion_scale, group_rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -72,6 +72,37 @@ def test_control_points_adjust_matches_oracle(fba, fbo, oracle, tmp_path):
     _check_adjust(fba, fbo, oracle, folder)
 
 
+def test_config3_covariance_matches_oracle(fba, fbo, oracle, scenes):
+    """fba_covariance at config 3 (u = 16,210): the camera-side diagonal of Cx and the EOP/IOP
+    correlation blocks against the dense inverse of the C oracle's last bordered reduced system
+    [S G; G' 0] (the camera block of the bordered inverse of the full normal matrix, main.m:432);
+    every tie-point variance positive and finite."""
+    import scipy.linalg as sla
+    folder = _scene(3, scenes)
+    ds = fba.load_folder(folder)
+    od = oracle.load_folder(folder)
+    ref = fbo.CpuAdjustment(od, solver="kkt")
+    ref.adjust()
+    _, s02 = ref.residuals()
+    uc = ref.u_c
+    K = np.zeros((uc + 7, uc + 7))
+    K[:uc, :uc] = ref.S
+    K[:uc, uc:] = ref.G
+    K[uc:, :uc] = ref.G.T
+    C = sla.inv(K)[:uc, :uc]
+    sc = distortion_scale(ref.names[:uc], dist_scaling_of(od))
+    res = fba.adjust(ds)
+    np.testing.assert_allclose(res.cx_diag[:uc], s02 * np.diag(C) / sc ** 2, rtol=1e-7)
+    d = np.sqrt(np.diag(C))
+    corr = C / np.outer(d, d)
+    cam = 6 * od.numImg
+    for e in range(0, od.numImg, 17):
+        idx = list(range(6 * e, 6 * e + 6)) + list(range(cam, cam + 10))
+        np.testing.assert_allclose(res.corr[e], corr[np.ix_(idx, idx)], rtol=0, atol=1e-7)
+    tie = res.cx_diag[uc:]
+    assert np.isfinite(tie).all() and (tie > 0).all()
+
+
 def test_config4_first_iterations_match_oracle(fba, fbo, oracle, scenes):
     folder = _scene(4, scenes)
     ds = fba.load_folder(folder)
@@ -108,3 +139,4 @@ def test_config5_properties(fba, scenes):
     assert (np.diff(d[:3]) < 0).all()
     assert abs(res.sigma02 - 1.0) <= 0.05, res.sigma02
     assert np.isfinite(res.xhat).all()
+    assert np.isfinite(res.cx_diag).all() and (res.cx_diag > 0).all()  # fba_covariance at 2M image points
