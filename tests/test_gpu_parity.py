@@ -264,3 +264,26 @@ def test_covariance_synthetic(fba, oracle, tmp_path, n_control):
     ro = oracle.adjust(od)
     res = fba.adjust(ds)
     _check_cov(res, od, ro, oracle)
+
+
+def test_batch_main_writes_reference_outputs(fba, oracle, tmp_path):
+    """BatchRun.m -> main(folder) on the device path: .out / .par / .rsd written next to the data, the
+    standard deviations in the .out being sqrt of the device Cx diagonal."""
+    import os
+    import shutil
+    from conftest import CAM0
+    from fba_amd import batch
+    folder = tmp_path / "proj" / "cam0"
+    shutil.copytree(CAM0, folder)
+    done = batch.batch_run([str(tmp_path / "proj")])
+    assert done == [(str(folder), 0)]
+    for ext in (".out", ".par", ".rsd"):
+        assert os.path.getsize(folder / ("cam0" + ext)) > 0
+    lines = (folder / "cam0.out").read_text().splitlines()
+    dof = next(x for x in lines if x.startswith("Total Degrees of Freedom"))
+    assert dof.split()[-1] == "1485"
+    od = oracle.load_folder(str(folder))
+    ro = oracle.adjust(od)
+    cdo, _ = oracle.covariance(od, ro)
+    xc = next(x for x in lines if x.startswith("Xc "))
+    assert float(xc.split()[2]) == pytest.approx(np.sqrt(cdo[0]), abs=2e-5)

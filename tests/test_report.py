@@ -100,3 +100,25 @@ def test_par_and_rsd(cam0_outputs):
     f = rsd[0].split("\t")
     assert f[:2] == [ds.pho_target[0], ds.pho_image[0]]
     np.testing.assert_allclose([float(x) for x in f[4:]], res.rsd[0], rtol=1e-14)
+
+
+def test_batch_find_folders(fba, tmp_path):
+    """BatchRun.m's findfiles: complete folders found recursively, partial ones reported and skipped,
+    a duplicate extension warns and clears the found list (BatchRun.m:92-96)."""
+    from fba_amd import batch
+    import shutil
+    a = tmp_path / "a"
+    shutil.copytree(CAM0, a)
+    (tmp_path / "b").mkdir()
+    for ext in (".pho", ".ext"):
+        (tmp_path / "b" / ("x" + ext)).write_text("")
+    shutil.copytree(CAM0, tmp_path / "b" / "deep")
+    c = tmp_path / "c"
+    shutil.copytree(CAM0, c)
+    (c / "zz.pho").write_text("")
+    msgs = []
+    found = batch.find_folders(str(tmp_path), log=msgs.append)
+    assert found == [str(a), str(tmp_path / "b" / "deep")]
+    assert any(m.startswith("Error: .ext and .pho were found in") and m.endswith("but not .cnt and .int. This folder "
+                                                                                    "will be skipped") for m in msgs)
+    assert any(m.startswith("Warning: More than 1 .pho file was found in") for m in msgs)
