@@ -152,23 +152,27 @@ def main():
     ms = {n: float(v) for n, v in zip(names, phases)}
     t, chol_flops, lin_bytes = phase_roofline(ds, ms, n_phase)
 
-    # roofline of the dominant kernel, outside the timed region: one more step with HIP events
-    # around every launch of the Cholesky trailing update (k_syrk_multi, one per elimination-tree
-    # level) on the stream it runs on
-    ctx.set_probe(True)
-    step()
-    pr = ctx.probe_stats()
-    ctx.set_probe(False)
-    avg_s = pr["ms"] * 1e-3 / max(pr["launches"], 1)
-    flops_launch = pr["flops"] / max(pr["launches"], 1)
-    traffic = pmc_traffic(args.config, "k_syrk_multi")
-    roof = {"bound": "mfma", "kernel": "k_syrk_multi (Cholesky trailing update of one tree level, 64x64 f64 MFMA "
-                                       "tiles, K = 128 per source column)",
-            "achieved": flops_launch / avg_s / 1e12 if avg_s > 0 else None, "peak": FP64_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "launches": pr["launches"], "avg_launch_us": avg_s * 1e6,
-            "flops_per_launch": flops_launch,
-            "traffic": traffic}
-    roof["frac"] = roof["achieved"] / roof["peak"] if roof["achieved"] else None
+    # rooflines, outside the timed region: one more step per probed kernel, HIP events around each of
+    # its launches on the stream it runs on.  k_panel (one launch per elimination-tree level: the
+    # level's 128x128 diagonal factorisations and panel solves) has the largest share of GPU time, so
+    # it is `roofline`; k_syrk_multi (the level's bulk trailing update, 64x64 f64 MFMA tiles) follows.
+    def probe(kind, name, note):
+        ctx.set_probe(kind)
+        step()
+        pr = ctx.probe_stats()
+        ctx.set_probe(0)
+        avg_s = pr["ms"] * 1e-3 / max(pr["launches"], 1)
+        flops_launch = pr["flops"] / max(pr["launches"], 1)
+        r = {"bound": "mfma", "kernel": f"{name} ({note})",
+             "achieved": flops_launch / avg_s / 1e12 if avg_s > 0 else None, "peak": FP64_PEAK_TFLOPS,
+             "unit": "TFLOP/s", "launches": pr["launches"], "avg_launch_us": avg_s * 1e6,
+             "flops_per_launch": flops_launch, "traffic": pmc_traffic(args.config, name)}
+        r["frac"] = r["achieved"] / r["peak"] if r["achieved"] else None
+        return r
+    roof = probe(2, "k_panel", "diagonal-block potrf + panel solves of one elimination-tree level, 128x128 f64 "
+                               "blocks; a latency-bound dependency chain: 18 levels in series at config 4")
+    roof_bulk = probe(1, "k_syrk_multi", "Cholesky trailing update of one tree level, 64x64 f64 MFMA tiles, "
+                                         "K = 128 per source column")
     phase_roof = {"cholesky_dense_equiv_TFLOPs": chol_flops / (t["cholesky"] * 1e-3) / 1e12,
                   "linearize_accumulate_GBs": lin_bytes / ((t["linearize"] + t["accumulate"]) * 1e-3) / 1e9}
     value = args.steps / dt
@@ -185,6 +189,7 @@ def main():
         "phase_ms": {k: t[k] for k in names},
         "deltasum_last": dsum[-1] if dsum else None,
         "roofline": roof,
+        "roofline_bulk_update": roof_bulk,
         "phase_roofline": phase_roof,
     }
     ctx.close()

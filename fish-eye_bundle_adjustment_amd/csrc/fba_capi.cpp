@@ -167,7 +167,7 @@ static void destroy(Ctx* c) {
     if (!c) return;
     void* ptrs[] = {c->d_chunk_obs, c->d_chunk_pt, c->d_xy, c->d_img, c->d_cam, c->d_pt, c->d_ctl, c->d_lp_tie, c->d_lp_start, c->d_lp_cam,
                     c->d_acc, c->d_ppart, c->d_ipart, c->d_cpart, c->d_cseg, c->d_bscr, c->d_lrprof, c->d_gpairs, c->d_red, c->d_xfull, c->d_xlin, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
-                    c->d_pt_tab, c->d_P, c->d_flags, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
+                    c->d_pt_tab, c->d_P, c->d_flags, c->d_bflags, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
                     c->d_active, c->d_counted, c->d_obs_pho, c->d_sched};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
@@ -705,7 +705,8 @@ static int solve_update(Ctx* c, double* dsum) {
     const double info = c->h_pinned[1];
     *dsum = c->h_pinned[2];
     if (info < 0.0) {
-        set_error("device hand-off timeout in the block Cholesky (a workgroup of k_panel was not resident)");
+        set_error("device hand-off timeout in the block Cholesky / backward solve (a workgroup of k_panel or "
+                  "k_bwd_flow was not resident)");
         return FBA_ERR_HIP;
     }
     if (info != 0.0) {
@@ -1040,7 +1041,8 @@ int fba_last_timings(fba_ctx* ctx, double* ms) {
 int fba_set_probe(fba_ctx* ctx, int32_t enabled) {
     Ctx* c = reinterpret_cast<Ctx*>(ctx);
     if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }
-    c->probe = enabled != 0;
+    if (enabled < 0 || enabled > 2) { set_error("fba_set_probe: 0 (off), 1 (k_syrk_multi) or 2 (k_panel)"); return FBA_ERR_ARG; }
+    c->probe = enabled;
     c->probe_n = 0;
     c->probe_flops = 0.0;
     return FBA_OK;

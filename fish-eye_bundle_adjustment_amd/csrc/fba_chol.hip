@@ -780,7 +780,7 @@ __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, 
     }
 }
 
-constexpr size_t TRTRI_LDS = sizeof(double) * (CB * LDA + 4 * IB * 17);
+constexpr size_t TRTRI_LDS = sizeof(double) * (CB * LDA + 4 * IB * 17 + IB * LDA);  // X, per-wave staging, L row block
 
 // ------------------------------------------------------------------------------------------------
 // k_trtri128: inverse of the 128x128 diagonal blocks (the listed columns, or all; one workgroup per
@@ -801,15 +801,36 @@ __global__ __launch_bounds__(256) void k_trtri128(const double* __restrict__ S, 
         const int r = idx >> 7, c = idx & 127;
         X[r * LDA + c] = ((r >> 4) == (c >> 4)) ? Dk[(r >> 4) * IB * IB + (r & 15) * IB + (c & 15)] : 0.0;
     }
+    // row block i of L (16 x 128) staged in LDS for step i; the next one is loaded into registers
+    // while step i computes (the row reads were the latency of every step)
+    double* Lr = Y + 4 * IB * 17;       // [16][LDA]
+    double lpre[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int idx = tid + 256 * q;
+        lpre[q] = L[(int64_t)(IB + (idx >> 7)) * ld + (idx & 127)];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int idx = tid + 256 * q;
+        Lr[(idx >> 7) * LDA + (idx & 127)] = lpre[q];
+    }
     __syncthreads();
     double* Yw = Y + wave * IB * 17;
     for (int i = 1; i < CB / IB; ++i) {
+        if (i + 1 < CB / IB) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int idx = tid + 256 * q;
+                lpre[q] = L[(int64_t)(IB * (i + 1) + (idx >> 7)) * ld + (idx & 127)];
+            }
+        }
         for (int j = wave; j < i; j += 4) {
             dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
             for (int k = j; k < i; ++k) {
 #pragma unroll
                 for (int kk = 0; kk < IB; kk += 4) {
-                    const double av = L[(int64_t)(IB * i + lr) * ld + IB * k + kk + lk];
+                    const double av = Lr[lr * LDA + IB * k + kk + lk];
                     const double bv = X[(IB * k + kk + lk) * LDA + IB * j + lr];
                     acc = mfma(av, bv, acc);
                 }
@@ -821,7 +842,7 @@ __global__ __launch_bounds__(256) void k_trtri128(const double* __restrict__ S, 
             dbl4 out = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int kk = 0; kk < IB; kk += 4) {
-                const double av = -Dk[i * IB * IB + lr * IB + kk + lk];
+                const double av = -X[(IB * i + lr) * LDA + IB * i + kk + lk];  // D_i, the diagonal tile of X
                 const double bv = Yw[(kk + lk) * 17 + lr];
                 out = mfma(av, bv, out);
             }
@@ -831,6 +852,14 @@ __global__ __launch_bounds__(256) void k_trtri128(const double* __restrict__ S, 
             __builtin_amdgcn_wave_barrier();
         }
         __syncthreads();
+        if (i + 1 < CB / IB) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int idx = tid + 256 * q;
+                Lr[(idx >> 7) * LDA + (idx & 127)] = lpre[q];
+            }
+            __syncthreads();
+        }
     }
     double* out = linv + (int64_t)kb * CB * CB;
     for (int idx = tid; idx < CB * CB; idx += 256) out[idx] = X[(idx >> 7) * LDA + (idx & 127)];
@@ -903,6 +932,96 @@ __global__ __launch_bounds__(256) void k_bwd_wave(double* __restrict__ S, int64_
     if (tid < CB) y[j * CB + tid] -= acc;
 }
 
+// k_bwd_flow: the whole backward solve L' x = y in ONE launch, dataflow-ordered: workgroup b owns
+// block column j = nb-1-b; it stages Linv_j in LDS, then for each source block row i of column j
+// (descending: the order the x_i are published in) streams L(i,j) into registers, waits for x_i's
+// flag, reads x_i (sc1) and adds L(i,j)' x_i; then x_j = Linv_j' (y_j - sum), published write-through
+// with an agent-scope flag, and delta_c = -x_j stored (k_neg_copy fused).  Waits only point to higher
+// blocks and every workgroup is resident (nb <= CUs, checked by the host), so they end; polls are
+// bounded (scal[1] = -1 on timeout, reported by the host).
+constexpr size_t BWD_LDS = sizeof(double) * (CB * CB + 2 * CB + 512);
+
+__global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, int64_t ld, int64_t n_pad,
+                                                  const double* __restrict__ linv, double* __restrict__ X,
+                                                  double* __restrict__ delta, int64_t u_c,
+                                                  const int32_t* __restrict__ src_start, const int32_t* __restrict__ src,
+                                                  unsigned* __restrict__ flags, double* __restrict__ scal) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* Li = smem;              // [128][128] Linv_j
+    double* xs = Li + CB * CB;      // [128] x_i of the current source
+    double* ys = xs + CB;           // [128]
+    double* red = ys + CB;          // [512]
+    const int tid = threadIdx.x;
+    const int nb = (int)(n_pad / CB);
+    const int j = nb - 1 - (int)blockIdx.x;
+    const int c2 = tid & 63, h = tid >> 6;  // gemv_t128's thread map: columns 2 c2 + {0,1}, rows 32 h ..
+    {
+        const double2* Lg = reinterpret_cast<const double2*>(linv + (int64_t)j * CB * CB);
+        double2* Ls = reinterpret_cast<double2*>(Li);
+        for (int q = tid; q < CB * CB / 2; q += 256) Ls[q] = Lg[q];
+    }
+    double a0 = 0.0, a1 = 0.0;
+    const __amdgpu_buffer_rsrc_t rX = block_rsrc(X, n_pad * 8);
+    for (int q = src_start[j]; q < src_start[j + 1]; ++q) {
+        const int i = src[q];
+        const double* M = S + (int64_t)i * CB * ld + (int64_t)j * CB;  // L(i, j), written by earlier launches
+        double2 m[32];
+#pragma unroll
+        for (int r = 0; r < 32; ++r) m[r] = *reinterpret_cast<const double2*>(M + (int64_t)(h * 32 + r) * ld + 2 * c2);
+        if (tid == 0) {
+            unsigned spins = 0;
+            while (__hip_atomic_load(flags + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1u) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __syncthreads();
+        if (tid < CB / 2) {
+            const double2 v = ld_sc1(rX, ((int64_t)i * CB + 2 * tid) * 8);
+            xs[2 * tid] = v.x;
+            xs[2 * tid + 1] = v.y;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            const double xr = xs[h * 32 + r];
+            a0 += m[r].x * xr;
+            a1 += m[r].y * xr;
+        }
+        __syncthreads();  // xs is rewritten by the next source
+    }
+    red[h * 128 + 2 * c2] = a0;
+    red[h * 128 + 2 * c2 + 1] = a1;
+    __syncthreads();
+    if (tid < CB) {
+        const double s = (red[tid] + red[128 + tid]) + (red[256 + tid] + red[384 + tid]);
+        ys[tid] = S[n_pad * ld + (int64_t)j * CB + tid] - s;
+    }
+    __syncthreads();
+    // x_j = Linv_j' y_j from LDS
+    double b0 = 0.0, b1 = 0.0;
+#pragma unroll 8
+    for (int r = 0; r < 32; ++r) {
+        const double yr = ys[h * 32 + r];
+        const double2 l = *reinterpret_cast<const double2*>(Li + (h * 32 + r) * CB + 2 * c2);
+        b0 += l.x * yr;
+        b1 += l.y * yr;
+    }
+    red[h * 128 + 2 * c2] = b0;
+    red[h * 128 + 2 * c2 + 1] = b1;
+    __syncthreads();
+    if (tid < CB) {
+        const double x = (red[tid] + red[128 + tid]) + (red[256 + tid] + red[384 + tid]);
+        st_sc1(rX, ((int64_t)j * CB + tid) * 8, x);
+        const int64_t g = (int64_t)j * CB + tid;
+        if (g < u_c) delta[g] = -x;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(flags + j, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ void k_neg_copy(const double* __restrict__ X, double* __restrict__ delta, int64_t u_c) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < u_c) delta[i] = -X[i];
@@ -919,6 +1038,8 @@ int launch_cholesky(Ctx& c) {
     FBA_HIP(hipMemsetAsync(c.d_flags, 0, c.flags_bytes, c.stream));  // k_panel hand-off flags (one epoch)
     for (int w = 0; w < s.n_waves; ++w) {
         const Sched::Wave& W = s.w[w];
+        const bool pp = c.probe == 2 && c.probe_n < (int)c.probe_ev.size() / 2;
+        if (pp) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
         if (W.ncol + W.ntrsm <= c.n_cu) {  // one launch: every workgroup resident (one per CU)
             k_panel<<<(unsigned)(W.ncol + W.ntrsm), POTRF_THREADS, TRSM_LDS, c.stream>>>(
                 c.d_S, ld, c.d_sched + W.cols, W.ncol, c.d_sched + W.trsm, c.d_dinv, c.d_scal, c.d_flags);
@@ -927,8 +1048,13 @@ int launch_cholesky(Ctx& c) {
                                                                                       c.d_dinv, c.d_scal, nullptr);
             k_trsm128<<<(unsigned)W.ntrsm, 256, TRSM_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.trsm, c.d_dinv);
         }
+        if (pp) {
+            FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], c.stream));
+            c.probe_flops += W.pflops;
+            ++c.probe_n;
+        }
         if (W.ntask == 0) continue;
-        const bool pr = c.probe && c.probe_n < (int)c.probe_ev.size() / 2;
+        const bool pr = c.probe == 1 && c.probe_n < (int)c.probe_ev.size() / 2;
         if (pr) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
         k_syrk_multi<<<(unsigned)W.ntask, 256, 0, c.stream>>>(c.d_S, ld, c.d_sched + W.tasks, c.d_sched + W.src, c.d_P);
         if (pr) {
@@ -969,12 +1095,23 @@ int launch_border_gram(Ctx& c, double* gpart, int* nseg) {
 int launch_backward(Ctx& c) {
     const int64_t ld = c.L.ld;
     if (c.set.inner_constraints) {
+        // (running k_trtri128 on a forked stream concurrently with these two measured slower: a forked
+        // iteration graph adds cross-queue waits to every launch of the Cholesky chain)
         k_border_gram<<<GRAM_SEG, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_bscr + 32 * 14);
         k_border_combine<<<(unsigned)((c.L.n_pad + 255) / 256), 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad,
                                                                                    c.d_bscr + 32 * 14);
     }
     k_trtri128<<<(unsigned)(c.L.n_pad / CB), 256, TRTRI_LDS, c.stream>>>(c.d_S, ld, nullptr, c.d_dinv, c.d_linv);
     const Sched& s = c.sched;
+    const int64_t nb = c.L.n_pad / CB;
+    if (c.bwd_flow && nb <= c.n_cu) {  // one launch, every workgroup resident
+        FBA_HIP(hipMemsetAsync(c.d_bflags, 0, c.flags_bytes, c.stream));
+        k_bwd_flow<<<(unsigned)nb, 256, BWD_LDS, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_linv, c.d_X, c.d_delta, c.L.u_c,
+                                                           c.d_sched + s.bf_start, c.d_sched + s.bf_src, c.d_bflags,
+                                                           c.d_scal);
+        FBA_HIP(hipGetLastError());
+        return FBA_OK;
+    }
     for (int w = s.n_waves - 1; w >= 0; --w) {
         const Sched::BWave& B = s.b[w];
         k_bwd_wave<<<(unsigned)(B.nsrc + B.ntgt), 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_linv, c.d_X,
@@ -996,6 +1133,9 @@ int chol_setup(Ctx& c) {
     c.n_cu = prop.multiProcessorCount;
     c.flags_bytes = (size_t)((c.L.n_pad / CB + 3) / 4 * 4) * sizeof(unsigned);  // multiple of 16 bytes
     FBA_HIP(hipMalloc((void**)&c.d_flags, c.flags_bytes));
+    FBA_HIP(hipMalloc((void**)&c.d_bflags, c.flags_bytes));
+    FBA_HIP(hipFuncSetAttribute((const void*)k_bwd_flow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)BWD_LDS));
+    c.bwd_flow = !(getenv("FBA_BWD_LEVELS") && atoi(getenv("FBA_BWD_LEVELS")) != 0);
     FBA_HIP(hipFuncSetAttribute((const void*)k_trtri128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRTRI_LDS));
 
     c.probe_ev.assign(2 * std::max(c.sched.n_waves, 1), nullptr);

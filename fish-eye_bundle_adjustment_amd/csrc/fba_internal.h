@@ -52,6 +52,7 @@ struct Sched {
         int64_t cols = 0, trsm = 0, tasks = 0, src = 0, comb = 0;  // offsets
         int ncol = 0, ntrsm = 0, ntask = 0, ncomb = 0;
         double flops = 0.0;       // trailing-update flops of the level (kernel probe)
+        double pflops = 0.0;      // diagonal factorisations + panel solves of the level (kernel probe)
     };
     struct BWave {
         int64_t srcs = 0, tgts = 0, src_start = 0, src = 0;
@@ -59,6 +60,8 @@ struct Sched {
     };
     int n_waves = 0;
     int64_t n_tiles = 0;
+    int64_t bf_start = 0, bf_src = 0;  // backward dataflow (k_bwd_flow): per block column j, the block
+                                       // rows i > j of its panel, descending (offsets)
     int64_t zero = 0;             // (block row, block column) of every block of the factor's pattern
     int nzero = 0;                // (diagonal, panel and RHS blocks): zeroed before each accumulation
     int n_scratch = 0;            // 64x64 scratch quarters of the split targets (max over levels)
@@ -162,6 +165,8 @@ struct Ctx {
     int64_t n_lp_pad = 0;
     double* d_P = nullptr;       // [Sched::n_scratch][64*64] partial sums of split update targets
     unsigned* d_flags = nullptr; // [nb] k_panel hand-off flags (zeroed before each factorisation)
+    unsigned* d_bflags = nullptr; // [nb] k_bwd_flow hand-off flags (zeroed before each backward solve)
+    bool bwd_flow = true;         // one-launch backward solve (FBA_BWD_LEVELS=1: one launch per level)
     size_t flags_bytes = 0;
     int n_cu = 0;                // compute units (k_panel needs its whole grid resident)
     double* d_S = nullptr;       // [(n_pad+NB)*ld] normal matrix (lower) + RHS rows
@@ -185,8 +190,9 @@ struct Ctx {
     std::vector<int32_t> ref_img_cam;  // [n_img_ref] camera of each EXT image (-1: no observation)
     int iterations = 0;
     bool timing = false;
-    // kernel probe (fba_set_probe): HIP events around every bulk trailing-update launch
-    bool probe = false;
+    // kernel probe (fba_set_probe): HIP events around every launch of one Cholesky kernel
+    // (1: k_syrk_multi, the bulk trailing update; 2: k_panel, the diagonal factorisations + panel solves)
+    int probe = 0;
     std::vector<hipEvent_t> probe_ev;  // [2*nb]
     int probe_n = 0;
     double probe_flops = 0.0;

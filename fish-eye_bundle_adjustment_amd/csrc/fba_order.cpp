@@ -374,6 +374,8 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
                 for (int h = 0; h < 2; ++h)
                     if (h == 0 || real_rows(r) > NB / 2) { buf.push_back(k); buf.push_back(2 * r + h); }
         W.ntrsm = (int)((at() - W.trsm) / 2);
+        // potrf of each 128 block (NB^3/3) + the triangular solve of each 64-row half panel (64 NB^2)
+        W.pflops = (double)W.ncol * NB * NB * NB / 3.0 + (double)W.ntrsm * 64.0 * NB * NB;
         // trailing-update targets (i, j), j < nb, with their source columns in ascending order
         std::map<std::pair<int32_t, int32_t>, std::vector<int32_t>> tg;
         for (int32_t k : wave[w])
@@ -451,6 +453,20 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
         B.src = at();
         for (auto& t : tg) buf.insert(buf.end(), t.second.begin(), t.second.end());
     }
+    // backward dataflow lists: the sources of every block column, descending
+    s.bf_start = at();
+    {
+        int32_t acc = 0;
+        for (int64_t j = 0; j < nb; ++j) {
+            buf.push_back(acc);
+            for (int32_t i : R[j]) acc += i < nb ? 1 : 0;
+        }
+        buf.push_back(acc);
+    }
+    s.bf_src = at();
+    for (int64_t j = 0; j < nb; ++j)
+        for (auto it = R[j].rbegin(); it != R[j].rend(); ++it)
+            if (*it < nb) buf.push_back(*it);
     // the blocks the factorisation touches (everything else in S stays zero from fba_create on)
     s.zero = at();
     for (int64_t k = 0; k < nb; ++k) {

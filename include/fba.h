@@ -185,11 +185,12 @@ int fba_covariance(fba_ctx* ctx, double sigma02, double* cx_diag, double* corr);
 int fba_last_timings(fba_ctx* ctx, double* ms /*[8]*/);
 int fba_set_timing(fba_ctx* ctx, int32_t enabled);
 
-/* Kernel probe (measurement only; no reference counterpart): while enabled, every launch of the
- * bulk trailing-update kernel of the Cholesky (k_syrk_q64, the dominant kernel) is bracketed by HIP
- * events on the stream it runs on.  fba_probe_stats synchronises and returns, over the launches since
- * the probe was enabled: out[0] launches, out[1] summed kernel ms, out[2] algorithmic flops,
- * out[3] reserved.  The probe records at most one step's worth of launches (one factorisation). */
+/* Kernel probe (measurement only; no reference counterpart): while enabled, every launch of one
+ * Cholesky kernel is bracketed by HIP events on the stream it runs on -- enabled = 1: k_syrk_multi (the
+ * bulk trailing update of a tree level), 2: k_panel (the level's diagonal-block factorisations and
+ * panel solves, the critical path); 0 turns the probe off.  fba_probe_stats synchronises and returns,
+ * over the launches since the probe was enabled: out[0] launches, out[1] summed kernel ms, out[2]
+ * algorithmic flops, out[3] reserved.  The probe records at most one step's worth of launches. */
 int fba_set_probe(fba_ctx* ctx, int32_t enabled);
 int fba_probe_stats(fba_ctx* ctx, double* out /*[4]*/);
 
