@@ -912,33 +912,52 @@ __global__ __launch_bounds__(256) void k_finish_rhs(double* __restrict__ S, cons
 // ------------------------------------------------------------------------------------------------
 // back-substitution of tie points: dp = -(vb + sum_o T_o^T d_e(o) + Tc^T d_cam)
 // ------------------------------------------------------------------------------------------------
+// one workgroup per chunk (<= 256 observations of <= 64 whole tie points): thread per observation
+// u_o = T_o' d_e(o) into LDS (contiguous 144-byte T records, coalesced across the wave), then thread
+// per point d_p = -(vb + sum_o u_o + Tc' d_cam), its observations summed in order
 template <int NK>
-__global__ void k_backsub(const double* __restrict__ WT, const double* __restrict__ PT,
-                          const int32_t* __restrict__ lp_start, const int32_t* __restrict__ lp_tie,
-                          const int32_t* __restrict__ lp_cam, const int32_t* __restrict__ img,
-                          double* __restrict__ delta, int64_t n_lp, int64_t u_c, int n_img) {
+__global__ __launch_bounds__(256) void k_backsub(const double* __restrict__ WT, const double* __restrict__ PT,
+                                                 const int32_t* __restrict__ chunk_obs, const int32_t* __restrict__ chunk_pt,
+                                                 const int32_t* __restrict__ lp_start, const int32_t* __restrict__ lp_tie,
+                                                 const int32_t* __restrict__ lp_cam, const int32_t* __restrict__ img,
+                                                 double* __restrict__ delta, int64_t u_c, int n_img) {
     using LY = Lay<NK>;
     constexpr int CW = LY::CW, PS = LY::PS;
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n_lp) return;
-    const double* P = PT + p * PS;
-    double d0 = P[6], d1 = P[7], d2 = P[8];
-    for (int o = lp_start[p]; o < lp_start[p + 1]; ++o) {
+    __shared__ double u[CHUNK_OBS][3];
+    const int c = blockIdx.x, t = threadIdx.x;
+    const int p0 = chunk_pt[c], p1 = chunk_pt[c + 1];
+    if (p1 == p0) return;  // control chunk (uniform)
+    const int o0 = chunk_obs[c], o = o0 + t;
+    if (o < chunk_obs[c + 1]) {
+        const double2* T = reinterpret_cast<const double2*>(WT + (int64_t)o * 18);
+        double2 tv[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) tv[k] = T[k];
         const double* de = delta + 6 * (int64_t)img[o];
-        const double* T = WT + (int64_t)o * 18;
+        const double* tf = reinterpret_cast<const double*>(tv);
+        double d0 = 0.0, d1 = 0.0, d2 = 0.0;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
-            d0 += T[3 * a] * de[a]; d1 += T[3 * a + 1] * de[a]; d2 += T[3 * a + 2] * de[a];
+            const double e = de[a];
+            d0 += tf[3 * a] * e; d1 += tf[3 * a + 1] * e; d2 += tf[3 * a + 2] * e;
         }
+        u[t][0] = d0; u[t][1] = d1; u[t][2] = d2;
     }
-    const double* dk = delta + 6 * (int64_t)n_img + (int64_t)lp_cam[p] * CW;
-    const double* Tc = P + 12 + 3 * CW;
+    __syncthreads();
+    const int p = p0 + t;
+    if (p < p1) {
+        const double* P = PT + (int64_t)p * PS;
+        double d0 = P[6], d1 = P[7], d2 = P[8];
+        for (int q = lp_start[p] - o0; q < lp_start[p + 1] - o0; ++q) { d0 += u[q][0]; d1 += u[q][1]; d2 += u[q][2]; }
+        const double* dk = delta + 6 * (int64_t)n_img + (int64_t)lp_cam[p] * CW;
+        const double* Tc = P + 12 + 3 * CW;
 #pragma unroll
-    for (int c = 0; c < CW; ++c) {
-        d0 += Tc[3 * c] * dk[c]; d1 += Tc[3 * c + 1] * dk[c]; d2 += Tc[3 * c + 2] * dk[c];
+        for (int k = 0; k < CW; ++k) {
+            d0 += Tc[3 * k] * dk[k]; d1 += Tc[3 * k + 1] * dk[k]; d2 += Tc[3 * k + 2] * dk[k];
+        }
+        double* out = delta + u_c + 3 * (int64_t)lp_tie[p];
+        out[0] = -d0; out[1] = -d1; out[2] = -d2;
     }
-    double* out = delta + u_c + 3 * (int64_t)lp_tie[p];
-    out[0] = -d0; out[1] = -d1; out[2] = -d2;
 }
 
 
@@ -1215,10 +1234,10 @@ int launch_border(Ctx& c) {
 int launch_backsub_update(Ctx& c) {
     const Layout& L = c.L;
     if (c.n_lp > 0) {
-        const int blocks = (int)((c.n_lp + 255) / 256);
-#define BS(NKV)                                                                                               \
-    k_backsub<NKV><<<blocks, 256, 0, c.stream>>>(c.d_WT, c.d_pt_tab, c.d_lp_start, c.d_lp_tie, c.d_lp_cam,    \
-                                                 c.d_img, c.d_delta, c.n_lp, L.u_c, L.n_img)
+#define BS(NKV)                                                                                                    \
+    k_backsub<NKV><<<(unsigned)c.n_chunks, 256, 0, c.stream>>>(c.d_WT, c.d_pt_tab, c.d_chunk_obs, c.d_chunk_pt,       \
+                                                              c.d_lp_start, c.d_lp_tie, c.d_lp_cam, c.d_img, c.d_delta, \
+                                                              L.u_c, L.n_img)
         FBA_NK_DISPATCH(L.nk, BS);
 #undef BS
         FBA_HIP(hipGetLastError());
