@@ -18,7 +18,7 @@
 //                   X_s = (A_s - sum_{t<s} X_t L_st^T) D_s^T: all MFMA, 16 rows per wave
 //     k_syrk_multi  the trailing updates of the level, C -= sum_k X_ik X_jk^T, 64x64 quarters, K = 128
 //                   per source column staged through LDS in 32-deep slices; targets with many sources
-//                   split into groups (scratch quarters, k_syrk_combine adds them in order)
+//                   split into groups (scratch quarters; the last group to arrive adds them in order)
 //   forward solve   the right-hand sides [r | A | B] (B = G D, D an equilibration over all images)
 //                   are stored as extra ROWS below M (one extra block row, in every panel), so the
 //                   panel solves compute Y' = (L^-1 [r A B])' as a by-product
@@ -558,8 +558,8 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_panel(double* __restrict__ S,
 // ------------------------------------------------------------------------------------------------
 // k_syrk_multi: the trailing updates of one level, one 64x64 output quarter per workgroup (task record,
 // Sched): C(i,j) -= sum_k X_ik X_jk^T over the task's source columns k (ascending), or, for a split
-// target, the partial sum of a group of sources into a scratch quarter (k_syrk_combine adds the groups
-// in order): the result does not depend on the schedule.  K = 128 per source column staged through
+// target, the partial sum of a group of sources into a scratch quarter (the last group to arrive adds
+// the groups in slot order): the result does not depend on the schedule.  K = 128 per source column staged through
 // LDS in 32-deep slices, the next slice prefetched into registers while the MFMAs of the current one
 // run.
 // ------------------------------------------------------------------------------------------------
@@ -567,9 +567,11 @@ constexpr int KS = 32;
 constexpr int LDK = 34;   // LDS stride of a 32-deep slice: bank = (4r + 2k) mod 64, conflict-free
 
 __global__ __launch_bounds__(256) void k_syrk_multi(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ tasks,
-                                                    const int32_t* __restrict__ src, double* __restrict__ P) {
+                                                    const int32_t* __restrict__ src, double* __restrict__ P,
+                                                    const int32_t* __restrict__ comb, unsigned* __restrict__ cnt) {
     __shared__ __attribute__((aligned(16))) double As[64][LDK];
     __shared__ __attribute__((aligned(16))) double Bs[64][LDK];
+    __shared__ unsigned last;
     const int32_t* tk = tasks + Sched::SYRK_REC * blockIdx.x;
     const int64_t bi = tk[0], bj = tk[1];
     const int qr = tk[2] >> 1, qc = tk[2] & 1, s0 = tk[3], slot = tk[5];
@@ -631,39 +633,55 @@ __global__ __launch_bounds__(256) void k_syrk_multi(double* __restrict__ S, int6
                 for (int b = 0; b < 2; ++b) acc[a][b] = mfma(av[a], bv[b], acc[a][b]);
         }
     }
+    if (slot < 0) {
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+            for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) Cp[(a * 16 + 4 * r) * ldc + b * 16] = acc[a][b][r];
-}
-
-// k_syrk_combine: C quarter += the scratch quarters of a split target in slot order (each holds the
-// negated partial sum of its source group)
-__global__ __launch_bounds__(256) void k_syrk_combine(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ comb,
-                                                      const double* __restrict__ P) {
-    const int32_t* cb = comb + Sched::COMB_REC * blockIdx.x;
-    const int64_t r0 = (int64_t)cb[0] * CB + (cb[2] >> 1) * 64, c0 = (int64_t)cb[1] * CB + (cb[2] & 1) * 64;
+                for (int r = 0; r < 4; ++r) Cp[(a * 16 + 4 * r) * ldc + b * 16] = acc[a][b][r];
+        return;
+    }
+    // split target: this group's partial goes to its scratch quarter write-through; the group that
+    // arrives last (agent-scope counter) adds all groups' partials to C in slot order -- the same
+    // arithmetic as a separate combine launch, so the result does not depend on the arrival order
+    {
+        const __amdgpu_buffer_rsrc_t rP = block_rsrc(P + (int64_t)slot * 4096, 4096 * 8);
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    st_sc1(rP, (int64_t)((wr + lk + a * 16 + 4 * r) * 64 + wc + lr + b * 16) * 8, acc[a][b][r]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int32_t* cb = comb + Sched::COMB_REC * tk[6];
+    if (tid == 0)
+        last = __hip_atomic_fetch_add(cnt + tk[6], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(cb[4] - 1);
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const int first = cb[3], n = cb[4];
     double2 v[8];
-    double2* cp[8];
+    double2* cq[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {  // thread -> 8 double2 of the quarter, all loads of a round in flight
-        const int e = 2 * (threadIdx.x + 256 * q), r = e >> 6, cl = e & 63;
-        cp[q] = reinterpret_cast<double2*>(S + (r0 + r) * ld + c0 + cl);
-        v[q] = *cp[q];
+    for (int q = 0; q < 8; ++q) {
+        const int e = 2 * (tid + 256 * q), r = e >> 6, cl = e & 63;
+        cq[q] = reinterpret_cast<double2*>(S + (r0 + r) * ld + c0 + cl);
+        v[q] = *cq[q];
     }
     for (int g = 0; g < n; ++g) {
-        const double* pg = P + (int64_t)(first + g) * 4096;
-        double2 p[8];
+        const __amdgpu_buffer_rsrc_t rg = block_rsrc(P + (int64_t)(first + g) * 4096, 4096 * 8);
+        double2 pv[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) p[q] = *reinterpret_cast<const double2*>(pg + 2 * (threadIdx.x + 256 * q));
+        for (int q = 0; q < 8; ++q) pv[q] = ld_sc1(rg, (int64_t)(2 * (tid + 256 * q)) * 8);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) { v[q].x += p[q].x; v[q].y += p[q].y; }
+        for (int q = 0; q < 8; ++q) { v[q].x += pv[q].x; v[q].y += pv[q].y; }
     }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) *cp[q] = v[q];
+    for (int q = 0; q < 8; ++q) *cq[q] = v[q];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1035,7 +1053,7 @@ __global__ void k_neg_copy(const double* __restrict__ X, double* __restrict__ de
 int launch_cholesky(Ctx& c) {
     const int64_t ld = c.L.ld;
     const Sched& s = c.sched;
-    FBA_HIP(hipMemsetAsync(c.d_flags, 0, c.flags_bytes, c.stream));  // k_panel hand-off flags (one epoch)
+    // the k_panel / k_bwd_flow hand-off flags and the split-target counters were zeroed by k_finish_rhs
     for (int w = 0; w < s.n_waves; ++w) {
         const Sched::Wave& W = s.w[w];
         const bool pp = c.probe == 2 && c.probe_n < (int)c.probe_ev.size() / 2;
@@ -1056,14 +1074,13 @@ int launch_cholesky(Ctx& c) {
         if (W.ntask == 0) continue;
         const bool pr = c.probe == 1 && c.probe_n < (int)c.probe_ev.size() / 2;
         if (pr) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
-        k_syrk_multi<<<(unsigned)W.ntask, 256, 0, c.stream>>>(c.d_S, ld, c.d_sched + W.tasks, c.d_sched + W.src, c.d_P);
+        k_syrk_multi<<<(unsigned)W.ntask, 256, 0, c.stream>>>(c.d_S, ld, c.d_sched + W.tasks, c.d_sched + W.src, c.d_P,
+                                                               c.d_sched + W.comb, c.d_counters + W.cbase);
         if (pr) {
             FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], c.stream));
             c.probe_flops += W.flops;
             ++c.probe_n;
         }
-        if (W.ncomb > 0)
-            k_syrk_combine<<<(unsigned)W.ncomb, 256, 0, c.stream>>>(c.d_S, ld, c.d_sched + W.comb, c.d_P);
     }
     FBA_HIP(hipGetLastError());
     return FBA_OK;
@@ -1105,7 +1122,6 @@ int launch_backward(Ctx& c) {
     const Sched& s = c.sched;
     const int64_t nb = c.L.n_pad / CB;
     if (c.bwd_flow && nb <= c.n_cu) {  // one launch, every workgroup resident
-        FBA_HIP(hipMemsetAsync(c.d_bflags, 0, c.flags_bytes, c.stream));
         k_bwd_flow<<<(unsigned)nb, 256, BWD_LDS, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_linv, c.d_X, c.d_delta, c.L.u_c,
                                                            c.d_sched + s.bf_start, c.d_sched + s.bf_src, c.d_bflags,
                                                            c.d_scal);
@@ -1132,8 +1148,12 @@ int chol_setup(Ctx& c) {
     FBA_HIP(hipGetDeviceProperties(&prop, c.device));
     c.n_cu = prop.multiProcessorCount;
     c.flags_bytes = (size_t)((c.L.n_pad / CB + 3) / 4 * 4) * sizeof(unsigned);  // multiple of 16 bytes
-    FBA_HIP(hipMalloc((void**)&c.d_flags, c.flags_bytes));
-    FBA_HIP(hipMalloc((void**)&c.d_bflags, c.flags_bytes));
+    const size_t nf = c.flags_bytes / sizeof(unsigned);
+    c.n_sync = (int64_t)(2 * nf + std::max(c.sched.n_counters, 1));
+    FBA_HIP(hipMalloc((void**)&c.d_flags, sizeof(unsigned) * c.n_sync));
+    FBA_HIP(hipMemset(c.d_flags, 0, sizeof(unsigned) * c.n_sync));
+    c.d_bflags = c.d_flags + nf;
+    c.d_counters = c.d_bflags + nf;
     FBA_HIP(hipFuncSetAttribute((const void*)k_bwd_flow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)BWD_LDS));
     c.bwd_flow = !(getenv("FBA_BWD_LEVELS") && atoi(getenv("FBA_BWD_LEVELS")) != 0);
     FBA_HIP(hipFuncSetAttribute((const void*)k_trtri128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRTRI_LDS));

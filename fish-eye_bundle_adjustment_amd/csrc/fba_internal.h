@@ -42,15 +42,17 @@ struct Layout {
 // Block schedule of the reduced-system Cholesky (fba_order.cpp): one batched step per level of the
 // elimination tree.  All offsets index the int32 device buffer Ctx::d_sched.
 //   trsm records  (k, 2 r + h): panel block (r, k), row half h (halves of padding rows are skipped)
-//   task records  SYRK_REC ints: (i, j, quarter 2 qr + qc, s0, s1, slot): C(i,j) quarter -= sum of
-//                 X_ik X_jk' over the sources src[s0..s1) (ascending); slot >= 0: the sum goes to the
-//                 scratch quarter `slot` instead (split targets), combined by a COMB_REC record
+//   task records  SYRK_REC ints: (i, j, quarter 2 qr + qc, s0, s1, slot, comb): C(i,j) quarter -= sum
+//                 of X_ik X_jk' over the sources src[s0..s1) (ascending); slot >= 0: the sum goes to the
+//                 scratch quarter `slot` instead (split targets), and the last group to arrive (counter
+//                 cbase + comb) applies the COMB_REC record `comb` of the level
 //                 (i, j, quarter, first slot, slots): C -= P_first - ... in slot order
 struct Sched {
-    static constexpr int SYRK_REC = 6, COMB_REC = 5;
+    static constexpr int SYRK_REC = 7, COMB_REC = 5;
     struct Wave {
         int64_t cols = 0, trsm = 0, tasks = 0, src = 0, comb = 0;  // offsets
         int ncol = 0, ntrsm = 0, ntask = 0, ncomb = 0;
+        int cbase = 0;            // first arrival counter of the level's split targets (k_syrk_multi)
         double flops = 0.0;       // trailing-update flops of the level (kernel probe)
         double pflops = 0.0;      // diagonal factorisations + panel solves of the level (kernel probe)
     };
@@ -65,6 +67,7 @@ struct Sched {
     int64_t zero = 0;             // (block row, block column) of every block of the factor's pattern
     int nzero = 0;                // (diagonal, panel and RHS blocks): zeroed before each accumulation
     int n_scratch = 0;            // 64x64 scratch quarters of the split targets (max over levels)
+    int n_counters = 0;           // split-target arrival counters, all levels
     std::vector<Wave> w;          // factorisation, level 0 up
     std::vector<BWave> b;         // backward solve, indexed by level (run top down)
     std::vector<int32_t> buf;     // host image of the lists (uploaded to Ctx::d_sched)
@@ -166,6 +169,9 @@ struct Ctx {
     double* d_P = nullptr;       // [Sched::n_scratch][64*64] partial sums of split update targets
     unsigned* d_flags = nullptr; // [nb] k_panel hand-off flags (zeroed before each factorisation)
     unsigned* d_bflags = nullptr; // [nb] k_bwd_flow hand-off flags (zeroed before each backward solve)
+    unsigned* d_counters = nullptr; // [Sched::n_counters] split-target arrival counters
+    int64_t n_sync = 0;           // unsigned words of flags + bflags + counters (one allocation at d_flags,
+                                  // zeroed by k_finish_rhs ahead of every factorisation)
     bool bwd_flow = true;         // one-launch backward solve (FBA_BWD_LEVELS=1: one launch per level)
     size_t flags_bytes = 0;
     int n_cu = 0;                // compute units (k_panel needs its whole grid resident)

@@ -888,10 +888,13 @@ __global__ __launch_bounds__(256) void k_border(double* __restrict__ S, const do
 __global__ __launch_bounds__(256) void k_finish_rhs(double* __restrict__ S, const double* __restrict__ G,
                                                     double* __restrict__ scal, const double* __restrict__ part,
                                                     const uint8_t* __restrict__ active, int64_t ld, int64_t n_pad,
-                                                    int64_t u_c, int n_img, int n_loc, int ic) {
+                                                    int64_t u_c, int n_img, int n_loc, int ic,
+                                                    unsigned* __restrict__ sync, int64_t n_sync) {
     __shared__ double w[14];
     if (ic) border_weights_lds(part, w);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // the hand-off flags and split-target counters of the factorisation / backward solve that follow
+    for (int64_t q = i; q < n_sync; q += (int64_t)gridDim.x * blockDim.x) sync[q] = 0u;
     if (ic && blockIdx.x == 0 && threadIdx.x < 14) scal[8 + (threadIdx.x / 7) * 8 + threadIdx.x % 7] = w[threadIdx.x];
     if (i >= n_pad) return;
     if (i >= u_c || !active[i]) {
@@ -1226,7 +1229,8 @@ int launch_border(Ctx& c) {
         FBA_HIP(hipGetLastError());
     }
     k_finish_rhs<<<(unsigned)((L.n_pad + 255) / 256), 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, c.d_bscr, c.d_active,
-                                                                           L.ld, L.n_pad, L.u_c, L.n_img, c.n_loc, ic);
+                                                                           L.ld, L.n_pad, L.u_c, L.n_img, c.n_loc, ic,
+                                                                           c.d_flags, c.n_sync);
     FBA_HIP(hipGetLastError());
     return FBA_OK;
 }

@@ -387,7 +387,7 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
         // consecutive sources summed into scratch quarters and combined in group order afterwards,
         // so no workgroup runs more than SPLIT * 128 deep (the long poles of a level)
         constexpr int SPLIT = 2;
-        struct Task { int32_t i, j, q, s0, s1, slot; };
+        struct Task { int32_t i, j, q, s0, s1, slot, comb; };
         std::vector<Task> tasks;
         std::vector<int32_t> src, comb;
         int slots = 0, ncomb = 0;
@@ -403,10 +403,11 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
                 if (i == j && qr == 0 && qc == 1) continue;  // strictly upper quarter of a diagonal block
                 if ((qr == 1 && real_rows(i) <= NB / 2) || (qc == 1 && real_rows(j) <= NB / 2)) continue;
                 if (!split) {
-                    tasks.push_back({i, j, q, s0, s0 + ns, -1});
+                    tasks.push_back({i, j, q, s0, s0 + ns, -1, -1});
                 } else {
                     const int first = slots;
-                    for (int32_t g = 0; g < ns; g += SPLIT) tasks.push_back({i, j, q, s0 + g, s0 + std::min(ns, g + SPLIT), slots++});
+                    for (int32_t g = 0; g < ns; g += SPLIT)
+                        tasks.push_back({i, j, q, s0 + g, s0 + std::min(ns, g + SPLIT), slots++, ncomb});
                     comb.insert(comb.end(), {i, j, q, first, slots - first});
                     ++ncomb;
                 }
@@ -422,9 +423,11 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
         buf.insert(buf.end(), src.begin(), src.end());
         W.tasks = at();
         W.ntask = (int)tasks.size();
-        for (auto& t : tasks) buf.insert(buf.end(), {t.i, t.j, t.q, t.s0, t.s1, t.slot});
+        for (auto& t : tasks) buf.insert(buf.end(), {t.i, t.j, t.q, t.s0, t.s1, t.slot, t.comb});
         W.comb = at();
         W.ncomb = ncomb;
+        W.cbase = s.n_counters;
+        s.n_counters += ncomb;
         buf.insert(buf.end(), comb.begin(), comb.end());
         s.n_scratch = std::max(s.n_scratch, slots);
         ntile_total += (int64_t)tg.size();
