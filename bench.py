@@ -95,11 +95,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
     import torch
+    # FBA_BENCH_BACKEND=gloo rehearses the multi-rank path with every rank on the one GPU of a test box
+    # (device = local rank modulo the visible GPUs); the real runs use RCCL ("nccl"), one rank per GPU
+    backend = os.environ.get("FBA_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     import fba_import
     fba = fba_import.load()
 
