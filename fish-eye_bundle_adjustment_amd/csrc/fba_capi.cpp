@@ -637,10 +637,10 @@ static int run_graph(Ctx* c, int which, F&& body) {
 static int accumulate_body(Ctx* c) {
     int rc;
     mark(c, 0);
-    if ((rc = launch_params(*c, nullptr, c->d_xlin))) return rc;  // tables + the linearisation point
+    if ((rc = launch_params_zero(*c, c->d_xlin))) return rc;  // tables + the linearisation point + zero S
     mark(c, 1);
     mark(c, 2);
-    if ((rc = launch_accumulate(*c))) return rc;
+    if ((rc = launch_accumulate(*c, true))) return rc;
     if (c->d_lrprof) {  // FBA_LR_PROFILE: per-phase averages of k_lin_reduce (us)
         std::vector<uint64_t> tp(8 * c->n_chunks);
         FBA_HIP(hipMemcpyAsync(tp.data(), c->d_lrprof, sizeof(uint64_t) * tp.size(), hipMemcpyDeviceToHost, c->stream));
@@ -675,7 +675,9 @@ static int solve_body(Ctx* c) {
     mark(c, 4);
     if ((rc = launch_cholesky(*c))) return rc;
     mark(c, 5);
-    if (L.u_full > L.u_c)  // (a zero-byte memset is not a valid graph node)
+    // tie-point corrections of other ranks' points stay zero (a single rank writes every one of them in
+    // k_backsub; a zero-byte memset is not a valid graph node)
+    if (L.u_full > L.u_c && c->opt.world > 1)
         FBA_HIP(hipMemsetAsync(c->d_delta + L.u_c, 0, sizeof(double) * (L.u_full - L.u_c), c->stream));
     if ((rc = launch_backward(*c))) return rc;
     mark(c, 6);

@@ -537,24 +537,6 @@ __global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t
     trsm_body(S, ld, tasks + 2 * blockIdx.x, dinv, nullptr, nullptr, smem);
 }
 
-// k_panel: one level's diagonal factorisations and panel solves in ONE launch: workgroups
-// 0 .. ncol-1 factor the level's diagonal blocks (potrf_body) and publish them, the rest solve the
-// panel halves (trsm_body) as soon as their column's factor is published.  Every workgroup of the
-// launch is resident at once (<= 8 + 2 * panel blocks workgroups, one per CU), so the waits end.
-__global__ __launch_bounds__(POTRF_THREADS) void k_panel(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ cols,
-                                                         int ncol, const int32_t* __restrict__ trsm,
-                                                         double* __restrict__ dinv, double* __restrict__ scal,
-                                                         unsigned* __restrict__ flags) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    if ((int)blockIdx.x < ncol) {
-        const int col = cols[blockIdx.x];
-        potrf_body<false>(S, ld, col, dinv, scal, nullptr, flags + col, smem);
-    } else {
-        const int32_t* rec = trsm + 2 * (blockIdx.x - ncol);
-        trsm_body(S, ld, rec, dinv, flags + rec[0], scal, smem);
-    }
-}
-
 // ------------------------------------------------------------------------------------------------
 // k_syrk_multi: the trailing updates of one level, one 64x64 output quarter per workgroup (task record,
 // Sched): C(i,j) -= sum_k X_ik X_jk^T over the task's source columns k (ascending), or, for a split
@@ -805,82 +787,122 @@ constexpr size_t TRTRI_LDS = sizeof(double) * (CB * LDA + 4 * IB * 17 + IB * LDA
 // block, after the factorisation): block forward substitution on the 8x8 grid of 16x16 tiles,
 // X_ii = D_i, X_ij = -D_i sum_{k=j}^{i-1} L_ik X_kj, on v_mfma_f64_16x16x4_f64.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_trtri128(const double* __restrict__ S, int64_t ld, const int32_t* __restrict__ cols,
-                                                  const double* __restrict__ dinv, double* __restrict__ linv) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
+// trtri_body: threads 0..255 of the workgroup invert block kb; threads 256.. (a k_panel workgroup
+// has 512) only take part in the barriers
+__device__ __forceinline__ void trtri_body(const double* __restrict__ S, int64_t ld, int kb,
+                                           const double* __restrict__ dinv, double* __restrict__ linv,
+                                           double* __restrict__ smem) {
     double* X = smem;                   // [128][LDA]
     double* Y = smem + CB * LDA;        // [4 waves][16][17]
-    const int kb = cols ? cols[blockIdx.x] : (int)blockIdx.x;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, wave = (tid & 255) >> 6, lane = tid & 63;
+    const bool worker = tid < 256;
     const int lr = lane & 15, lk = lane >> 4;
     const double* L = S + (int64_t)kb * CB * ld + (int64_t)kb * CB;
     const double* Dk = dinv + (int64_t)kb * (CB / IB) * (IB * IB);
-    for (int idx = tid; idx < CB * CB; idx += 256) {
-        const int r = idx >> 7, c = idx & 127;
-        X[r * LDA + c] = ((r >> 4) == (c >> 4)) ? Dk[(r >> 4) * IB * IB + (r & 15) * IB + (c & 15)] : 0.0;
-    }
     // row block i of L (16 x 128) staged in LDS for step i; the next one is loaded into registers
     // while step i computes (the row reads were the latency of every step)
     double* Lr = Y + 4 * IB * 17;       // [16][LDA]
     double lpre[8];
+    if (worker) {
+        for (int idx = tid; idx < CB * CB; idx += 256) {
+            const int r = idx >> 7, c = idx & 127;
+            X[r * LDA + c] = ((r >> 4) == (c >> 4)) ? Dk[(r >> 4) * IB * IB + (r & 15) * IB + (c & 15)] : 0.0;
+        }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int idx = tid + 256 * q;
-        lpre[q] = L[(int64_t)(IB + (idx >> 7)) * ld + (idx & 127)];
-    }
+        for (int q = 0; q < 8; ++q) {
+            const int idx = tid + 256 * q;
+            lpre[q] = L[(int64_t)(IB + (idx >> 7)) * ld + (idx & 127)];
+        }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int idx = tid + 256 * q;
-        Lr[(idx >> 7) * LDA + (idx & 127)] = lpre[q];
+        for (int q = 0; q < 8; ++q) {
+            const int idx = tid + 256 * q;
+            Lr[(idx >> 7) * LDA + (idx & 127)] = lpre[q];
+        }
     }
     __syncthreads();
     double* Yw = Y + wave * IB * 17;
     for (int i = 1; i < CB / IB; ++i) {
-        if (i + 1 < CB / IB) {
+        if (worker) {
+            if (i + 1 < CB / IB) {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int idx = tid + 256 * q;
-                lpre[q] = L[(int64_t)(IB * (i + 1) + (idx >> 7)) * ld + (idx & 127)];
-            }
-        }
-        for (int j = wave; j < i; j += 4) {
-            dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
-            for (int k = j; k < i; ++k) {
-#pragma unroll
-                for (int kk = 0; kk < IB; kk += 4) {
-                    const double av = Lr[lr * LDA + IB * k + kk + lk];
-                    const double bv = X[(IB * k + kk + lk) * LDA + IB * j + lr];
-                    acc = mfma(av, bv, acc);
+                for (int q = 0; q < 8; ++q) {
+                    const int idx = tid + 256 * q;
+                    lpre[q] = L[(int64_t)(IB * (i + 1) + (idx >> 7)) * ld + (idx & 127)];
                 }
             }
+            for (int j = wave; j < i; j += 4) {
+                dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+                for (int k = j; k < i; ++k) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) Yw[(lk + 4 * r) * 17 + lr] = acc[r];
-            __builtin_amdgcn_s_waitcnt(0xC07F);
-            __builtin_amdgcn_wave_barrier();
-            dbl4 out = dbl4{0.0, 0.0, 0.0, 0.0};
+                    for (int kk = 0; kk < IB; kk += 4) {
+                        const double av = Lr[lr * LDA + IB * k + kk + lk];
+                        const double bv = X[(IB * k + kk + lk) * LDA + IB * j + lr];
+                        acc = mfma(av, bv, acc);
+                    }
+                }
 #pragma unroll
-            for (int kk = 0; kk < IB; kk += 4) {
-                const double av = -X[(IB * i + lr) * LDA + IB * i + kk + lk];  // D_i, the diagonal tile of X
-                const double bv = Yw[(kk + lk) * 17 + lr];
-                out = mfma(av, bv, out);
+                for (int r = 0; r < 4; ++r) Yw[(lk + 4 * r) * 17 + lr] = acc[r];
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                __builtin_amdgcn_wave_barrier();
+                dbl4 out = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int kk = 0; kk < IB; kk += 4) {
+                    const double av = -X[(IB * i + lr) * LDA + IB * i + kk + lk];  // D_i, the diagonal tile of X
+                    const double bv = Yw[(kk + lk) * 17 + lr];
+                    out = mfma(av, bv, out);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) X[(IB * i + lk + 4 * r) * LDA + IB * j + lr] = out[r];
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                __builtin_amdgcn_wave_barrier();
             }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) X[(IB * i + lk + 4 * r) * LDA + IB * j + lr] = out[r];
-            __builtin_amdgcn_s_waitcnt(0xC07F);
-            __builtin_amdgcn_wave_barrier();
         }
         __syncthreads();
         if (i + 1 < CB / IB) {
+            if (worker)
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int idx = tid + 256 * q;
-                Lr[(idx >> 7) * LDA + (idx & 127)] = lpre[q];
-            }
+                for (int q = 0; q < 8; ++q) {
+                    const int idx = tid + 256 * q;
+                    Lr[(idx >> 7) * LDA + (idx & 127)] = lpre[q];
+                }
             __syncthreads();
         }
     }
-    double* out = linv + (int64_t)kb * CB * CB;
-    for (int idx = tid; idx < CB * CB; idx += 256) out[idx] = X[(idx >> 7) * LDA + (idx & 127)];
+    if (worker) {
+        double* out = linv + (int64_t)kb * CB * CB;
+        for (int idx = tid; idx < CB * CB; idx += 256) out[idx] = X[(idx >> 7) * LDA + (idx & 127)];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_trtri128(const double* __restrict__ S, int64_t ld, const int32_t* __restrict__ cols,
+                                                  const double* __restrict__ dinv, double* __restrict__ linv) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    trtri_body(S, ld, cols ? cols[blockIdx.x] : (int)blockIdx.x, dinv, linv, smem);
+}
+
+// k_panel: one level's diagonal factorisations and panel solves in ONE launch: workgroups
+// 0 .. ncol-1 factor the level's diagonal blocks (potrf_body) and publish them, the next ntrsm solve
+// the panel halves (trsm_body) as soon as their column's factor is published, and the last nprev
+// invert the diagonal blocks of the PREVIOUS level (trtri_body; final since the last launch) for the
+// backward solve, off the critical path.  Every workgroup of the launch is resident at once (<= 8 +
+// 2 * panel blocks + 8 workgroups, one per CU), so the waits end.
+constexpr size_t PANEL_LDS = TRSM_LDS > TRTRI_LDS ? TRSM_LDS : TRTRI_LDS;
+
+__global__ __launch_bounds__(POTRF_THREADS) void k_panel(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ cols,
+                                                         int ncol, const int32_t* __restrict__ trsm, int ntrsm,
+                                                         const int32_t* __restrict__ prev, double* __restrict__ dinv,
+                                                         double* __restrict__ linv, double* __restrict__ scal,
+                                                         unsigned* __restrict__ flags) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    if ((int)blockIdx.x < ncol) {
+        const int col = cols[blockIdx.x];
+        potrf_body<false>(S, ld, col, dinv, scal, nullptr, flags + col, smem);
+    } else if ((int)blockIdx.x < ncol + ntrsm) {
+        const int32_t* rec = trsm + 2 * (blockIdx.x - ncol);
+        trsm_body(S, ld, rec, dinv, flags + rec[0], scal, smem);
+    } else {
+        trtri_body(S, ld, prev[blockIdx.x - ncol - ntrsm], dinv, linv, smem);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -957,26 +979,36 @@ __global__ __launch_bounds__(256) void k_bwd_wave(double* __restrict__ S, int64_
 // with an agent-scope flag, and delta_c = -x_j stored (k_neg_copy fused).  Waits only point to higher
 // blocks and every workgroup is resident (nb <= CUs, checked by the host), so they end; polls are
 // bounded (scal[1] = -1 on timeout, reported by the host).
-constexpr size_t BWD_LDS = sizeof(double) * (CB * CB + 2 * CB + 512);
+constexpr size_t BWD_LDS = sizeof(double) * (CB * CB + (CB / IB) * IB * IB + 2 * CB + 512);
 
 __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, int64_t ld, int64_t n_pad,
-                                                  const double* __restrict__ linv, double* __restrict__ X,
+                                                  const double* __restrict__ linv, const double* __restrict__ dinv,
+                                                  double* __restrict__ X,
                                                   double* __restrict__ delta, int64_t u_c,
                                                   const int32_t* __restrict__ src_start, const int32_t* __restrict__ src,
                                                   unsigned* __restrict__ flags, double* __restrict__ scal) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    double* Li = smem;              // [128][128] Linv_j
-    double* xs = Li + CB * CB;      // [128] x_i of the current source
+    double* Li = smem;              // [128][128] Linv_j, or L_jj for a root column
+    double* Dt = Li + CB * CB;      // [8][16][16] the leaf inverses of a root column
+    double* xs = Dt + (CB / IB) * IB * IB;  // [128] x_i of the current source
     double* ys = xs + CB;           // [128]
     double* red = ys + CB;          // [512]
     const int tid = threadIdx.x;
     const int nb = (int)(n_pad / CB);
     const int j = nb - 1 - (int)blockIdx.x;
     const int c2 = tid & 63, h = tid >> 6;  // gemv_t128's thread map: columns 2 c2 + {0,1}, rows 32 h ..
+    // a root of the elimination tree (no source blocks: the top level) is solved by substitution with
+    // its factor and leaf inverses, so its Linv (k_trtri128, 30 us) is off the critical path
+    const bool root = src_start[j] == src_start[j + 1];
     {
-        const double2* Lg = reinterpret_cast<const double2*>(linv + (int64_t)j * CB * CB);
+        const double2* Lg = root ? nullptr : reinterpret_cast<const double2*>(linv + (int64_t)j * CB * CB);
         double2* Ls = reinterpret_cast<double2*>(Li);
-        for (int q = tid; q < CB * CB / 2; q += 256) Ls[q] = Lg[q];
+        for (int q = tid; q < CB * CB / 2; q += 256) {
+            const int r = q >> 6, cc = (q & 63) * 2;
+            Ls[q] = root ? *reinterpret_cast<const double2*>(S + ((int64_t)j * CB + r) * ld + (int64_t)j * CB + cc) : Lg[q];
+        }
+        if (root)
+            for (int q = tid; q < (CB / IB) * IB * IB; q += 256) Dt[q] = dinv[(int64_t)j * (CB / IB) * IB * IB + q];
     }
     double a0 = 0.0, a1 = 0.0;
     const __amdgpu_buffer_rsrc_t rX = block_rsrc(X, n_pad * 8);
@@ -1017,6 +1049,39 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
         ys[tid] = S[n_pad * ld + (int64_t)j * CB + tid] - s;
     }
     __syncthreads();
+    if (root) {
+        // x = L^-T y: tiles s = 7 .. 0, x_s = D_s' (y_s - sum_{t>s} L_ts' x_t); thread (c, part) sums rows
+        // part, part + 16, .. of the tiles below s for column c, 16 parts added in order
+        const int c = tid & 15, part = tid >> 4;
+        for (int sb = CB / IB - 1; sb >= 0; --sb) {
+            double a = 0.0;
+            for (int r = IB * (sb + 1) + part; r < CB; r += 16) a += Li[r * CB + IB * sb + c] * xs[r];
+            red[part * 16 + c] = a;
+            __syncthreads();
+            if (tid < IB) {
+                double rs = ys[IB * sb + tid];
+                for (int q = 0; q < 16; ++q) rs -= red[q * 16 + tid];
+                red[256 + tid] = rs;
+            }
+            __syncthreads();
+            if (tid < IB) {
+                double x = 0.0;
+                for (int r = 0; r < IB; ++r) x += Dt[sb * IB * IB + r * IB + tid] * red[256 + r];  // (D_s' r)[tid]
+                xs[IB * sb + tid] = x;
+            }
+            __syncthreads();
+        }
+        if (tid < CB) {
+            const double x = xs[tid];
+            st_sc1(rX, ((int64_t)j * CB + tid) * 8, x);
+            const int64_t g = (int64_t)j * CB + tid;
+            if (g < u_c) delta[g] = -x;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(flags + j, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     // x_j = Linv_j' y_j from LDS
     double b0 = 0.0, b1 = 0.0;
 #pragma unroll 8
@@ -1058,13 +1123,18 @@ int launch_cholesky(Ctx& c) {
         const Sched::Wave& W = s.w[w];
         const bool pp = c.probe == 2 && c.probe_n < (int)c.probe_ev.size() / 2;
         if (pp) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
-        if (W.ncol + W.ntrsm <= c.n_cu) {  // one launch: every workgroup resident (one per CU)
-            k_panel<<<(unsigned)(W.ncol + W.ntrsm), POTRF_THREADS, TRSM_LDS, c.stream>>>(
-                c.d_S, ld, c.d_sched + W.cols, W.ncol, c.d_sched + W.trsm, c.d_dinv, c.d_scal, c.d_flags);
+        const int nprev = w > 0 ? s.w[w - 1].ncol : 0;  // the previous level's blocks, inverted alongside
+        const int32_t* prev = c.d_sched + (w > 0 ? s.w[w - 1].cols : 0);
+        if (W.ncol + W.ntrsm + nprev <= c.n_cu) {  // one launch: every workgroup resident (one per CU)
+            k_panel<<<(unsigned)(W.ncol + W.ntrsm + nprev), POTRF_THREADS, PANEL_LDS, c.stream>>>(
+                c.d_S, ld, c.d_sched + W.cols, W.ncol, c.d_sched + W.trsm, W.ntrsm, prev, c.d_dinv, c.d_linv, c.d_scal,
+                c.d_flags);
         } else {
             k_potrf128<false><<<(unsigned)W.ncol, POTRF_THREADS, POTRF_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.cols,
                                                                                       c.d_dinv, c.d_scal, nullptr);
             k_trsm128<<<(unsigned)W.ntrsm, 256, TRSM_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.trsm, c.d_dinv);
+            if (nprev > 0)
+                k_trtri128<<<(unsigned)nprev, 256, TRTRI_LDS, c.stream>>>(c.d_S, ld, prev, c.d_dinv, c.d_linv);
         }
         if (pp) {
             FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], c.stream));
@@ -1109,7 +1179,18 @@ int launch_border_gram(Ctx& c, double* gpart, int* nseg) {
     return FBA_OK;
 }
 
+// the diagonal-block inverses of the last level (the others come from the next level's k_panel)
+int launch_trtri_last(Ctx& c) {
+    const Sched& s = c.sched;
+    if (s.n_waves > 0)
+        k_trtri128<<<(unsigned)s.w[s.n_waves - 1].ncol, 256, TRTRI_LDS, c.stream>>>(
+            c.d_S, c.L.ld, c.d_sched + s.w[s.n_waves - 1].cols, c.d_dinv, c.d_linv);
+    FBA_HIP(hipGetLastError());
+    return FBA_OK;
+}
+
 int launch_backward(Ctx& c) {
+    int rc;
     const int64_t ld = c.L.ld;
     if (c.set.inner_constraints) {
         // (running k_trtri128 on a forked stream concurrently with these two measured slower: a forked
@@ -1118,16 +1199,16 @@ int launch_backward(Ctx& c) {
         k_border_combine<<<(unsigned)((c.L.n_pad + 255) / 256), 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad,
                                                                                    c.d_bscr + 32 * 14);
     }
-    k_trtri128<<<(unsigned)(c.L.n_pad / CB), 256, TRTRI_LDS, c.stream>>>(c.d_S, ld, nullptr, c.d_dinv, c.d_linv);
     const Sched& s = c.sched;
     const int64_t nb = c.L.n_pad / CB;
-    if (c.bwd_flow && nb <= c.n_cu) {  // one launch, every workgroup resident
-        k_bwd_flow<<<(unsigned)nb, 256, BWD_LDS, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_linv, c.d_X, c.d_delta, c.L.u_c,
+    if (c.bwd_flow && nb <= c.n_cu) {  // one launch, every workgroup resident; roots solve by substitution
+        k_bwd_flow<<<(unsigned)nb, 256, BWD_LDS, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_linv, c.d_dinv, c.d_X, c.d_delta, c.L.u_c,
                                                            c.d_sched + s.bf_start, c.d_sched + s.bf_src, c.d_bflags,
                                                            c.d_scal);
         FBA_HIP(hipGetLastError());
         return FBA_OK;
     }
+    if ((rc = launch_trtri_last(c))) return rc;
     for (int w = s.n_waves - 1; w >= 0; --w) {
         const Sched::BWave& B = s.b[w];
         k_bwd_wave<<<(unsigned)(B.nsrc + B.ntgt), 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_linv, c.d_X,
@@ -1142,7 +1223,7 @@ int launch_backward(Ctx& c) {
 int chol_setup(Ctx& c) {
     FBA_HIP(hipFuncSetAttribute((const void*)k_potrf128<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)POTRF_LDS));
     FBA_HIP(hipFuncSetAttribute((const void*)k_trsm128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRSM_LDS));
-    FBA_HIP(hipFuncSetAttribute((const void*)k_panel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRSM_LDS));
+    FBA_HIP(hipFuncSetAttribute((const void*)k_panel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)PANEL_LDS));
     static_assert(TRSM_LDS >= POTRF_LDS, "k_panel LDS");
     hipDeviceProp_t prop;
     FBA_HIP(hipGetDeviceProperties(&prop, c.device));

@@ -276,6 +276,7 @@ __global__ __launch_bounds__(256) void k_cov_pts(const double* __restrict__ S, i
 
 // backward solve of one right-hand-side row (fba_chol.hip)
 int launch_backward_rows(Ctx& c, int row0, int nrows, double* X);
+int launch_trtri_last(Ctx& c);
 int launch_border_gram(Ctx& c, double* gpart, int* nseg);
 
 // ------------------------------------------------------------------------------------------------
@@ -293,6 +294,8 @@ int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, 
     // point tables of the last linearisation (V^-1, T, Tc), as fba_residuals does
     if ((rc = launch_params(c, c.d_xlin)) || (rc = launch_linearize(c, c.d_xlin))) return rc;
 
+    // the last level's diagonal-block inverses (the iteration's backward solve does without them)
+    if ((rc = launch_trtri_last(c))) return rc;
     const int nz = L.nrhs > 1 ? 14 : 0;
     double *d_Z = nullptr, *d_Wz = nullptr, *d_h = nullptr, *d_g = nullptr;
     std::vector<void*> tmp;

@@ -224,7 +224,9 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
 int launch_params(Ctx& c, const double* x = nullptr, double* copy_to = nullptr);  // x: parameters (default d_xfull),
                                                                                    // also copied to copy_to
 int launch_linearize(Ctx& c, const double* x = nullptr);  // Jacobian rows to d_J (residuals, dense AwG)
-int launch_accumulate(Ctx& c);   // zero S, image, pair, camera blocks, unit diagonal for unused
+int launch_params_zero(Ctx& c, double* copy_to);  // k_params (+ copy of the linearisation point) and the
+                                                   // zeroing of the factor's pattern blocks, one launch
+int launch_accumulate(Ctx& c, bool zeroed = false);  // zero S (unless zeroed), image, pair, camera blocks
 int launch_border(Ctx& c);       // alpha, G G^T border, RHS rows
 int chol_setup(Ctx& c);
 int acc_setup(Ctx& c);            // kernel attributes of the accumulation kernels          // one-time kernel attributes, streams, events

@@ -27,13 +27,13 @@ namespace fba {
 // ------------------------------------------------------------------------------------------------
 // k_params: per-image and per-camera tables
 // ------------------------------------------------------------------------------------------------
-__global__ void k_params(const double* __restrict__ xfull, const double* __restrict__ caminfo,
-                         double* __restrict__ img_tab, double* __restrict__ cam_tab, double* __restrict__ G,
-                         const uint8_t* __restrict__ active, int n_img, int n_cam, int nk, int cw, int cam_stride,
-                         int ic, double* __restrict__ xcopy, int64_t n_copy) {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void params_body(int t, int nthreads, const double* __restrict__ xfull,
+                                            const double* __restrict__ caminfo, double* __restrict__ img_tab,
+                                            double* __restrict__ cam_tab, double* __restrict__ G,
+                                            const uint8_t* __restrict__ active, int n_img, int n_cam, int nk, int cw,
+                                            int cam_stride, int ic, double* __restrict__ xcopy, int64_t n_copy) {
     if (xcopy)  // the linearisation point (main.m:569 uses it for v), copied by the whole grid
-        for (int64_t i = t; i < n_copy; i += (int64_t)gridDim.x * blockDim.x) xcopy[i] = xfull[i];
+        for (int64_t i = t; i < n_copy; i += nthreads) xcopy[i] = xfull[i];
     if (t < n_img) {
         const double* e = xfull + 6 * (int64_t)t;
         double Xc = e[0], Yc = e[1], Zc = e[2], w = e[3], p = e[4], k = e[5];
@@ -93,6 +93,38 @@ __global__ void k_params(const double* __restrict__ xfull, const double* __restr
             o[CAM_TAB_HDR + nk + j - 1] = pow(rmax, 2.0 * j);    // rmax^(2j), BuildAwG.m:424-426
         }
         o[6] = o[CAM_TAB_HDR + nk];                              // rmax^2
+    }
+}
+
+__global__ void k_params(const double* __restrict__ xfull, const double* __restrict__ caminfo,
+                         double* __restrict__ img_tab, double* __restrict__ cam_tab, double* __restrict__ G,
+                         const uint8_t* __restrict__ active, int n_img, int n_cam, int nk, int cw, int cam_stride,
+                         int ic, double* __restrict__ xcopy, int64_t n_copy) {
+    params_body(blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x, xfull, caminfo, img_tab, cam_tab, G,
+                active, n_img, n_cam, nk, cw, cam_stride, ic, xcopy, n_copy);
+}
+
+// the per-iteration head of the accumulation in one launch: workgroups < npb build the parameter
+// tables and copy the linearisation point (k_params), the rest zero the factor's pattern blocks
+// (8 workgroups of 16 rows per 128x128 block, Sched::zero)
+__global__ __launch_bounds__(256) void k_params_zero(const double* __restrict__ xfull, const double* __restrict__ caminfo,
+                                                     double* __restrict__ img_tab, double* __restrict__ cam_tab,
+                                                     double* __restrict__ G, const uint8_t* __restrict__ active, int n_img,
+                                                     int n_cam, int nk, int cw, int cam_stride, int ic,
+                                                     double* __restrict__ xcopy, int64_t n_copy, int npb,
+                                                     double* __restrict__ S, int64_t ld, const int32_t* __restrict__ blk) {
+    if ((int)blockIdx.x < npb) {
+        params_body(blockIdx.x * 256 + threadIdx.x, npb * 256, xfull, caminfo, img_tab, cam_tab, G, active, n_img, n_cam,
+                    nk, cw, cam_stride, ic, xcopy, n_copy);
+        return;
+    }
+    const int zb = blockIdx.x - npb, b = zb >> 3;
+    const int64_t r0 = (int64_t)blk[2 * b] * NB + (zb & 7) * 16, c0 = (int64_t)blk[2 * b + 1] * NB;
+    const double2 z = {0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int i = threadIdx.x + 256 * q, r = i >> 6, c = (i & 63) * 2;
+        *reinterpret_cast<double2*>(S + (r0 + r) * ld + c0 + c) = z;
     }
 }
 
@@ -1146,6 +1178,17 @@ static inline unsigned cam_mask(const fba_settings& s, int nk) {
 static inline double px_of(const Ctx& c) { return 1.0 / (c.set.meas_std_x * c.set.meas_std_x); }
 static inline double py_of(const Ctx& c) { return 1.0 / (c.set.meas_std_y * c.set.meas_std_y); }
 
+// k_params (with the linearisation-point copy) and k_zero_blocks in one launch (fba_step's accumulation)
+int launch_params_zero(Ctx& c, double* copy_to) {
+    const int n = c.L.n_img + c.L.n_cam;
+    const int npb = (int)std::max<int64_t>((n + 255) / 256, std::min<int64_t>(256, (c.L.u_full + 255) / 256));
+    k_params_zero<<<(unsigned)(npb + 8 * c.sched.nzero), 256, 0, c.stream>>>(
+        c.d_xfull, c.d_caminfo, c.d_img_tab, c.d_cam_tab, c.d_G, c.d_active, c.L.n_img, c.L.n_cam, c.L.nk, c.L.cw,
+        c.cam_tab_stride, c.set.inner_constraints, copy_to, c.L.u_full, npb, c.d_S, c.L.ld, c.d_sched + c.sched.zero);
+    FBA_HIP(hipGetLastError());
+    return FBA_OK;
+}
+
 int launch_params(Ctx& c, const double* x, double* copy_to) {
     const int n = c.L.n_img + c.L.n_cam;
     const int64_t blocks = copy_to ? std::max<int64_t>((n + 63) / 64, std::min<int64_t>(1024, (c.L.u_full + 255) / 256))
@@ -1184,9 +1227,9 @@ __global__ __launch_bounds__(256) void k_zero_blocks(double* __restrict__ S, int
     }
 }
 
-int launch_accumulate(Ctx& c) {
+int launch_accumulate(Ctx& c, bool zeroed) {
     const Layout& L = c.L;
-    if (c.sched.nzero > 0)
+    if (c.sched.nzero > 0 && !zeroed)
         k_zero_blocks<<<(unsigned)(8 * c.sched.nzero), 256, 0, c.stream>>>(c.d_S, L.ld, c.d_sched + c.sched.zero);
     if (c.n_chunks == 0) return FBA_OK;
     const unsigned em = eop_mask(c.set), cm = cam_mask(c.set, c.L.nk);
@@ -1247,6 +1290,7 @@ int launch_backsub_update(Ctx& c) {
         FBA_HIP(hipGetLastError());
     }
     const int nblk = (int)((L.u_full + 255) / 256);
+    // (forming deltasum in k_update's last-arriving workgroup measured slower: 612 agent-scope atomics)
     k_update<<<nblk, 256, 0, c.stream>>>(c.d_xfull, c.d_delta, c.d_cam_tab, c.d_counted, c.d_part, L.u_full,
                                          L.n_img, L.n_cam, L.nk, L.cw, c.cam_tab_stride);
     FBA_HIP(hipGetLastError());
