@@ -178,7 +178,7 @@ def main():
         r["frac"] = r["achieved"] / r["peak"] if r["achieved"] else None
         return r
     roof = probe(2, "k_panel", "diagonal-block potrf + panel solves of one elimination-tree level, 128x128 f64 "
-                               "blocks; a latency-bound dependency chain: 18 levels in series at config 4")
+                               "blocks; a latency-bound dependency chain: one launch per level, in series")
     roof_bulk = probe(1, "k_syrk_multi", "Cholesky trailing update of one tree level, 64x64 f64 MFMA tiles, "
                                          "K = 128 per source column")
     phase_roof = {"cholesky_dense_equiv_TFLOPs": chol_flops / (t["cholesky"] * 1e-3) / 1e12,

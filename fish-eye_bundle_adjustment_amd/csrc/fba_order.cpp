@@ -286,7 +286,9 @@ class Dissection {
 
 std::vector<int32_t> camera_order(const fba_problem* p) {
     const char* le = getenv("FBA_ND_LEAF");
-    int leaf = le ? atoi(le) : 150;  // levels at configs 4 / 5: leaf 150 -> 18 / 35, 250 -> 20 / 36, 400 -> 22 / 40
+    // levels at configs 3 / 4 / 5: leaf 100 -> 9 / 17 / 33, 150 -> 8 / 18 / 35, 250 -> - / 20 / 36, 400 -> - / 22 / 40;
+    // config 4 measured 726 iter/s at 100 and 120, 711 at 150, 708 at 75
+    int leaf = le ? atoi(le) : 100;
     if (leaf <= 0) leaf = p->n_img;  // 0: reverse Cuthill-McKee only
     Graph g = covis_graph(p);
     std::vector<int32_t> all(p->n_img), out;
