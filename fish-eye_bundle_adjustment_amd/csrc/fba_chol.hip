@@ -1050,27 +1050,31 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
     }
     __syncthreads();
     if (root) {
-        // x = L^-T y: tiles s = 7 .. 0, x_s = D_s' (y_s - sum_{t>s} L_ts' x_t); thread (c, part) sums rows
-        // part, part + 16, .. of the tiles below s for column c, 16 parts added in order
-        const int c = tid & 15, part = tid >> 4;
-        for (int sb = CB / IB - 1; sb >= 0; --sb) {
-            double a = 0.0;
-            for (int r = IB * (sb + 1) + part; r < CB; r += 16) a += Li[r * CB + IB * sb + c] * xs[r];
-            red[part * 16 + c] = a;
-            __syncthreads();
-            if (tid < IB) {
-                double rs = ys[IB * sb + tid];
-                for (int q = 0; q < 16; ++q) rs -= red[q * 16 + tid];
-                red[256 + tid] = rs;
-            }
-            __syncthreads();
-            if (tid < IB) {
+        // x = L^-T y by substitution in wave 0 alone (no workgroup barriers): tiles s = 7 .. 0,
+        // x_s = D_s' (y_s - sum_{t>s} L_ts' x_t); lane (c = lane & 15, quarter g = lane >> 4) sums the
+        // rows g, g+4, .. below tile s for column c, the quarters added by a fixed xor butterfly
+        if (tid < 64) {
+            const int c = tid & 15, g = tid >> 4;
+            for (int sb = CB / IB - 1; sb >= 0; --sb) {
+                double a = 0.0;
+                for (int r = IB * (sb + 1) + g; r < CB; r += 4) a += Li[r * CB + IB * sb + c] * xs[r];
+                a += __shfl_xor(a, 16, 64);
+                a += __shfl_xor(a, 32, 64);
+                const double rs = ys[IB * sb + c] - a;  // every quarter holds r_s[c]
                 double x = 0.0;
-                for (int r = 0; r < IB; ++r) x += Dt[sb * IB * IB + r * IB + tid] * red[256 + r];  // (D_s' r)[tid]
-                xs[IB * sb + tid] = x;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {             // (D_s' r)[c] = sum_r D_s[r][c] r[r], r = 4 g + q
+                    const int r = 4 * g + q;
+                    x += Dt[sb * IB * IB + r * IB + c] * __shfl(rs, r, 64);
+                }
+                x += __shfl_xor(x, 16, 64);
+                x += __shfl_xor(x, 32, 64);
+                if (g == 0) xs[IB * sb + c] = x;
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                __builtin_amdgcn_wave_barrier();
             }
-            __syncthreads();
         }
+        __syncthreads();
         if (tid < CB) {
             const double x = xs[tid];
             st_sc1(rX, ((int64_t)j * CB + tid) * 8, x);
