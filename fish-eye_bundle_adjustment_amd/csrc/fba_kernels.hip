@@ -742,10 +742,9 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
 }
 
 // k_red_pairs: S(e1, e2) = the sum of the pair's partials in chunk order (one wave per pair)
-__global__ __launch_bounds__(256) void k_red_pairs(const double* __restrict__ ppart, const int32_t* __restrict__ A,
-                                                   const AccPlan plan, double* __restrict__ S, int64_t ld,
-                                                   int64_t n_pairs) {
-    const int64_t pr = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+__device__ __forceinline__ void red_pairs_body(int blk, const double* __restrict__ ppart, const int32_t* __restrict__ A,
+                                               const AccPlan& plan, double* __restrict__ S, int64_t ld, int64_t n_pairs) {
+    const int64_t pr = (int64_t)blk * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (pr >= n_pairs || lane >= 36) return;
     // the partials in chunk order, 4 loads in flight (fixed association: ((s + p0) + p1) + ...)
@@ -766,11 +765,11 @@ __global__ __launch_bounds__(256) void k_red_pairs(const double* __restrict__ pp
 
 // k_red_images: the diagonal block, RHS and image-camera block of image e from its partials
 template <int NK>
-__global__ __launch_bounds__(128) void k_red_images(const double* __restrict__ ipart, const int32_t* __restrict__ A,
-                                                    const AccPlan plan, double* __restrict__ S, int64_t ld,
-                                                    int64_t n_pad, int n_img) {
+__device__ __forceinline__ void red_images_body(int e, int q, const double* __restrict__ ipart,
+                                                const int32_t* __restrict__ A, const AccPlan& plan,
+                                                double* __restrict__ S, int64_t ld, int64_t n_pad, int n_img) {
     constexpr int CW = 5 + NK, NIMG = LR<NK>::NIMG;
-    const int e = blockIdx.x, q = threadIdx.x;
+    if (e >= n_img) return;
     const int r0 = A[plan.ri_start + e], r1 = A[plan.ri_start + e + 1];
     if (r0 == r1 || q >= NIMG) return;
     double s = 0.0;
@@ -791,12 +790,13 @@ __global__ __launch_bounds__(128) void k_red_images(const double* __restrict__ i
 constexpr int CAM_SEG = 64;
 
 template <int NK>
-__global__ __launch_bounds__(128) void k_red_cam_seg(const double* __restrict__ cpart, const int32_t* __restrict__ A,
-                                                     const AccPlan plan, double* __restrict__ cseg) {
+__device__ __forceinline__ void red_cam_seg_body(int sg, int q, int n_cam, const double* __restrict__ cpart,
+                                                 const int32_t* __restrict__ A, const AccPlan& plan,
+                                                 double* __restrict__ cseg) {
     constexpr int NCAM = LR<NK>::NCAM;
     static_assert(NCAM <= 128, "one thread per camera entry");
-    const int k = blockIdx.x / CAM_SEG, g = blockIdx.x % CAM_SEG, q = threadIdx.x;
-    if (q >= NCAM) return;
+    const int k = sg / CAM_SEG, g = sg % CAM_SEG;
+    if (q >= NCAM || k >= n_cam) return;
     const int x0 = A[plan.rc_start + k], n = A[plan.rc_start + k + 1] - x0;
     const int y0 = x0 + (int)((int64_t)n * g / CAM_SEG), y1 = x0 + (int)((int64_t)n * (g + 1) / CAM_SEG);
     double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
@@ -809,6 +809,24 @@ __global__ __launch_bounds__(128) void k_red_cam_seg(const double* __restrict__ 
     }
     for (; x < y1; ++x) s0 += cpart[(int64_t)A[plan.rc_list + x] * NCAM + q];
     cseg[((int64_t)k * CAM_SEG + g) * NCAM + q] = (s0 + s1) + (s2 + s3);
+}
+
+// the three independent reductions in one launch: workgroups [0, npb) the image pairs (4 per
+// workgroup), then two images per workgroup (128 threads each), then two camera segments per workgroup
+template <int NK>
+__global__ __launch_bounds__(256) void k_red_blocks(const double* __restrict__ ppart, const double* __restrict__ ipart,
+                                                    const double* __restrict__ cpart, const int32_t* __restrict__ A,
+                                                    const AccPlan plan, double* __restrict__ S, int64_t ld,
+                                                    int64_t n_pairs, int64_t n_pad, int n_img, int n_cam, int npb,
+                                                    int nib, double* __restrict__ cseg) {
+    const int b = blockIdx.x;
+    if (b < npb) {
+        red_pairs_body(b, ppart, A, plan, S, ld, n_pairs);
+    } else if (b < npb + nib) {
+        red_images_body<NK>(2 * (b - npb) + (threadIdx.x >> 7), threadIdx.x & 127, ipart, A, plan, S, ld, n_pad, n_img);
+    } else {
+        red_cam_seg_body<NK>(2 * (b - npb - nib) + (threadIdx.x >> 7), threadIdx.x & 127, n_cam, cpart, A, plan, cseg);
+    }
 }
 
 template <int NK>
@@ -1240,12 +1258,12 @@ int launch_accumulate(Ctx& c, bool zeroed) {
         c.d_chunk_obs, c.d_chunk_pt, c.d_lp_start, c.d_acc, c.acc, c.d_WT, c.d_pt_tab, c.d_ppart, c.d_ipart,       \
         c.d_cpart, c.L.u_c, c.set.type, c.cam_tab_stride, em, cm, px, py, c.d_lrprof,                              \
         c.d_lrprof && getenv("FBA_LR_SKIP") ? atoi(getenv("FBA_LR_SKIP")) : 0);                            \
-    if (c.n_pairs > 0)                                                                                            \
-        k_red_pairs<<<(unsigned)((c.n_pairs + 3) / 4), 256, 0, c.stream>>>(c.d_ppart, c.d_acc, c.acc, c.d_S, L.ld, \
-                                                                         c.n_pairs);                              \
-    k_red_images<NKV><<<(unsigned)L.n_img, 128, 0, c.stream>>>(c.d_ipart, c.d_acc, c.acc, c.d_S, L.ld, L.n_pad,   \
-                                                               L.n_img);                                          \
-    k_red_cam_seg<NKV><<<(unsigned)(L.n_cam * CAM_SEG), 128, 0, c.stream>>>(c.d_cpart, c.d_acc, c.acc, c.d_cseg);  \
+    {                                                                                                             \
+        const int npb = (int)((c.n_pairs + 3) / 4), nib = (L.n_img + 1) / 2, ncb = (L.n_cam * CAM_SEG + 1) / 2;   \
+        k_red_blocks<NKV><<<(unsigned)(npb + nib + ncb), 256, 0, c.stream>>>(                                     \
+            c.d_ppart, c.d_ipart, c.d_cpart, c.d_acc, c.acc, c.d_S, L.ld, c.n_pairs, L.n_pad, L.n_img, L.n_cam, npb, \
+            nib, c.d_cseg);                                                                                       \
+    }                                                                                                             \
     k_red_cam<NKV><<<(unsigned)L.n_cam, 128, 0, c.stream>>>(c.d_cseg, c.d_S, L.ld, L.n_pad, L.n_img)
     FBA_NK_DISPATCH(L.nk, ACC);
 #undef ACC
