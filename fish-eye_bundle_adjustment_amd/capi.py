@@ -21,7 +21,8 @@ NK_MAX = 8
 EXPORTS = (
     "fba_last_error", "fba_abi_version", "fba_count_unknowns", "fba_partition", "fba_create",
     "fba_destroy", "fba_buildxhat", "fba_set_xhat", "fba_get_xhat", "fba_build_awg",
-    "fba_accumulate", "fba_reduce_buffer", "fba_synchronize", "fba_solve_update", "fba_step", "fba_adjust",
+    "fba_accumulate", "fba_reduce_buffer", "fba_synchronize", "fba_solve_update", "fba_solve_update_async",
+    "fba_deltasum_device", "fba_solve_finish", "fba_step", "fba_adjust",
     "fba_residuals", "fba_finish_stats", "fba_covariance", "fba_last_timings", "fba_set_timing", "fba_set_probe",
     "fba_probe_stats",
 )
@@ -73,6 +74,9 @@ def _load():
         "fba_reduce_buffer": ([P, P, P], C.c_int),
         "fba_synchronize": ([P], C.c_int),
         "fba_solve_update": ([P, P], C.c_int),
+        "fba_solve_update_async": ([P], C.c_int),
+        "fba_deltasum_device": ([P, P], C.c_int),
+        "fba_solve_finish": ([P, P], C.c_int),
         "fba_step": ([P, P], C.c_int),
         "fba_adjust": ([P, P, P], C.c_int),
         "fba_residuals": ([P, P, P, P], C.c_int),
@@ -210,6 +214,19 @@ class Context:
     def solve_update(self):
         d = C.c_double()
         check(lib.fba_solve_update(self.h, C.byref(d)))
+        return d.value
+
+    def solve_update_async(self):
+        check(lib.fba_solve_update_async(self.h))
+
+    def deltasum_device(self):
+        p = C.c_void_p()
+        check(lib.fba_deltasum_device(self.h, C.byref(p)))
+        return p.value
+
+    def solve_finish(self):
+        d = C.c_double()
+        check(lib.fba_solve_finish(self.h, C.byref(d)))
         return d.value
 
     def step(self):

@@ -687,10 +687,15 @@ static int solve_body(Ctx* c) {
     return FBA_OK;
 }
 
-static int solve_update(Ctx* c, double* dsum) {
-    int rc;
+static int solve_enqueue(Ctx* c) {
     if (!c->have_lin) { set_error("fba_solve_update before fba_accumulate"); return FBA_ERR_ARG; }
-    if ((rc = run_graph(c, 1, [&] { return solve_body(c); }))) return rc;
+    return run_graph(c, 1, [&] { return solve_body(c); });
+}
+
+// wait for the solve, read scal (again from the device when `recopy`: a caller may have all-reduced
+// the deltasum share in place after the graph's own copy), check the failure flags
+static int solve_finish(Ctx* c, double* dsum, bool recopy) {
+    if (recopy) FBA_HIP(hipMemcpyAsync(c->h_pinned, c->d_scal, sizeof(double) * 4, hipMemcpyDeviceToHost, c->stream));
     FBA_HIP(hipStreamSynchronize(c->stream));
     if (c->timing) {
         float ms;
@@ -720,6 +725,12 @@ static int solve_update(Ctx* c, double* dsum) {
     }
     if (!std::isfinite(*dsum)) { set_error("non-finite correction vector"); return FBA_ERR_NONFINITE; }
     return FBA_OK;
+}
+
+static int solve_update(Ctx* c, double* dsum) {
+    int rc;
+    if ((rc = solve_enqueue(c))) return rc;
+    return solve_finish(c, dsum, false);
 }
 
 }  // namespace fba
@@ -868,6 +879,32 @@ int fba_solve_update(fba_ctx* ctx, double* deltasum_part) {
     double d = 0.0;
     int rc = solve_update(c, &d);
     if (deltasum_part) *deltasum_part = d;
+    return rc;
+}
+
+int fba_solve_update_async(fba_ctx* ctx) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }
+    const int rc = solve_enqueue(c);
+    if (rc == FBA_OK) c->pending = true;
+    return rc;
+}
+
+int fba_deltasum_device(fba_ctx* ctx, void** dev_ptr) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c || !dev_ptr) { set_error("NULL argument"); return FBA_ERR_ARG; }
+    *dev_ptr = c->d_scal + 2;
+    return FBA_OK;
+}
+
+int fba_solve_finish(fba_ctx* ctx, double* deltasum) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }
+    if (!c->pending) { set_error("fba_solve_finish without fba_solve_update_async"); return FBA_ERR_ARG; }
+    c->pending = false;
+    double d = 0.0;
+    const int rc = solve_finish(c, &d, true);
+    if (deltasum) *deltasum = d;
     return rc;
 }
 

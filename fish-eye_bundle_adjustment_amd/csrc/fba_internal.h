@@ -192,7 +192,8 @@ struct Ctx {
     // state
     bool have_lin = false;       // d_J holds a linearisation
     bool have_delta = false;
-    bool have_factor = false;    // d_S holds the factor of the last solve (fba_covariance consumes it)
+    bool have_factor = false;
+    bool pending = false;        // fba_solve_update_async enqueued, fba_solve_finish not yet called    // d_S holds the factor of the last solve (fba_covariance consumes it)
     std::vector<int32_t> ref_img_cam;  // [n_img_ref] camera of each EXT image (-1: no observation)
     int iterations = 0;
     bool timing = false;

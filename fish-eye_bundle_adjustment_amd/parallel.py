@@ -3,9 +3,10 @@
 
     rank r:  fba_accumulate      linearise + point-reduce its own observations (no communication)
              all_reduce(S, r)    the only data-path collective: the reduced camera system
-             fba_solve_update    replicated factor/solve (identical on every rank), back-substitution
-                                 of the rank's own tie points, xhat update
-             all_reduce(share)   this rank's share of sumabs(delta) -> the reference's deltasum
+             fba_solve_update_async  replicated factor/solve (identical on every rank), back-substitution
+                                 of the rank's own tie points, xhat update (enqueued, no host wait)
+             all_reduce(share)   this rank's share of sumabs(delta), in place on the device
+             fba_solve_finish    the one host synchronisation: the reference's deltasum
 
 torch.distributed is plumbing here (backend "nccl" = RCCL on ROCm, "gloo" on CPU); the compute is
 libfba.so.  The context runs on torch's current stream so the collective is ordered after the
@@ -46,14 +47,24 @@ class ShardedStep:
         else:
             self.buf = buffer
             self.device = buffer.device
-        self.share = torch.zeros(1, dtype=torch.float64, device=self.device)
+        # a device context: this rank's deltasum share is all-reduced in place on the device right after
+        # the solve, so an iteration has one host round trip (fba_solve_finish); an engine without
+        # device memory (the C oracle in tests/test_multirank.py) hands its share over on the host
+        self.on_device = hasattr(ctx, "deltasum_device")
+        if self.on_device:
+            self.share = device_view(ctx.deltasum_device(), 1, self.device)
+        else:
+            self.share = torch.zeros(1, dtype=torch.float64, device=self.device)
 
     def __call__(self):
         import torch.distributed as dist
         self.ctx.accumulate()
         dist.all_reduce(self.buf, group=self.group)
-        part = self.ctx.solve_update()
-        self.share.fill_(part)
+        if self.on_device:
+            self.ctx.solve_update_async()
+            dist.all_reduce(self.share, group=self.group)
+            return self.ctx.solve_finish()
+        self.share.fill_(self.ctx.solve_update())
         dist.all_reduce(self.share, group=self.group)
         return float(self.share.item())
 

@@ -152,6 +152,13 @@ int fba_reduce_buffer(fba_ctx* ctx, void** dev_ptr, int64_t* n_doubles);
  * caller touches the reduce buffer from another stream or the host). */
 int fba_synchronize(fba_ctx* ctx);
 int fba_solve_update(fba_ctx* ctx, double* deltasum_part);
+/* The same split without the host round trip in the middle (multi-GPU): fba_solve_update_async only
+ * enqueues the solve on the context's stream; fba_deltasum_device gives the device address of this
+ * rank's deltasum share (one double), which the caller may all-reduce in place on that stream;
+ * fba_solve_finish synchronises, checks the solve and returns that (reduced) value. */
+int fba_solve_update_async(fba_ctx* ctx);
+int fba_deltasum_device(fba_ctx* ctx, void** dev_ptr);
+int fba_solve_finish(fba_ctx* ctx, double* deltasum);
 int fba_step(fba_ctx* ctx, double* deltasum);
 
 /* main.m:407-494: iterate while deltasum > threshold, at most iteration_cap times.
