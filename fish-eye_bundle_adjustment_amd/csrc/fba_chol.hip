@@ -288,11 +288,13 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
         POTRF_TS(3 + 4 * s);
         Dl = Dall + s * IB * 17;
         if (s == CB / IB - 1) break;
-        // panel solve X_t = A_ts D_s^T: wave 0 tile s+1, waves 1..7 tiles s+2..7
+        // panel solve X_t = A_ts D_s^T: wave 0 tile s+1, waves 1..7 tiles s+2..7 (with a flag, wave 4 is the
+        // publisher and the other six take tiles s+2..7, one each)
         {
-            const int t0 = (wave == 0) ? s + 1 : s + 1 + wave;
-            const int step = (wave == 0) ? CB : POTRF_NW - 1;
-            for (int t = t0; t < CB / IB; t += step) {
+            const int wb = flag ? (wave < 4 ? wave : wave - 1) : wave;
+            const int t0 = (wave == 0) ? s + 1 : s + 1 + wb;
+            const int step = (wave == 0) ? CB : (flag ? POTRF_NW - 2 : POTRF_NW - 1);
+            for (int t = t0; t < CB / IB && !(flag && wave == 4); t += step) {
                 const int r0 = t * IB;
                 dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -304,7 +306,20 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
         }
         __syncthreads();  // B2: panel column s solved
         POTRF_TS(4 + 4 * s);
-        if (wave == 0) {
+        if (flag && wave == 4) {
+            // progressive hand-off: block column s of L and the leaf inverse D_s are final; store them
+            // write-through, drain, then flag = s + 1 (the panel solves' step s needs columns < s and D_s)
+            store_col(s, lane, 64);
+            const __amdgpu_buffer_rsrc_t rD = block_rsrc(dinv + dbase, (CB / IB) * IB * IB * 8);
+            for (int i = 2 * lane; i < IB * IB; i += 128) {
+                double2 v;
+                v.x = Dall[s * IB * 17 + (i >> 4) * 17 + (i & 15)];
+                v.y = Dall[s * IB * 17 + (i >> 4) * 17 + (i & 15) + 1];
+                st_sc1(rD, (int64_t)(s * IB * IB + i) * 8, v);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_store(flag, (unsigned)(s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (wave == 0) {
             // next diagonal tile, then its leaf factor
             const int R = c0 + IB;
             dbl4 acc;
@@ -363,14 +378,14 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
                         for (int r = 0; r < 4; ++r) AT((R + lk + 4 * r), C + IB + lr) = acc2[r];
                 }
             }
-            store_col(s, tid - 64, POTRF_THREADS - 64);  // block column s is final: written behind the update
+            if (!flag) store_col(s, tid - 64, POTRF_THREADS - 64);  // block column s is final: written behind the update
         }
     }
     if (!ok && lane == 0 && scal[1] == 0.0) scal[1] = (double)(k0 + 1);
     store_col(CB / IB - 1, tid, POTRF_THREADS);
-    {   // the leaf inverses, row-major 16x16 each, two per thread-store
+    {   // the leaf inverses, row-major 16x16 each, two per thread-store (with a flag only D_7 is left)
         const __amdgpu_buffer_rsrc_t rD = block_rsrc(dinv + dbase, (CB / IB) * IB * IB * 8);
-        for (int i = 2 * tid; i < (CB / IB) * IB * IB; i += 2 * POTRF_THREADS) {
+        for (int i = 2 * tid + (flag ? (CB / IB - 1) * IB * IB : 0); i < (CB / IB) * IB * IB; i += 2 * POTRF_THREADS) {
             double2 v;
             v.x = Dall[(i >> 8) * IB * 17 + ((i >> 4) & 15) * 17 + (i & 15)];
             v.y = Dall[(i >> 8) * IB * 17 + ((i >> 4) & 15) * 17 + (i & 15) + 1];
@@ -381,7 +396,7 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
     if (flag) {  // publish: every storing wave drains, the barrier, then one lane's flag
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) __hip_atomic_store(flag, (unsigned)(CB / IB), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #undef AT
 #undef POTRF_TS
@@ -408,12 +423,64 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_potrf128(double* __restrict__
 constexpr int TRSM_NT = (CB / IB) * (CB / IB - 1) / 2;  // 28 off-diagonal tiles
 constexpr size_t TRSM_LDS = sizeof(double) * (4 * IB * LDA + 4 * IB * 17 + (TRSM_NT + CB / IB) * IB * 17);
 
+// one substitution step of a wave's 16 panel rows: X_s = (A_s - sum_{t<s} X_t L_st^T) D_s^T
+__device__ __forceinline__ void trsm_step(const int s, double* __restrict__ Xw, double* __restrict__ Tw,
+                                          const double* __restrict__ Lt, const double* __restrict__ Dt, int lr, int lk) {
+    const int c0 = s * IB;
+    // Z = A_s - sum_{t<s} X_t L_st^T : output 16x16, K = 16 s.  All operands of the step are read
+    // from LDS in one batch, then two independent MFMA chains.
+    double av[CB / 4], bv[CB / 4];
+#pragma unroll
+    for (int t = 0; t < s; ++t) {
+        const double* Lst = Lt + (s * (s - 1) / 2 + t) * IB * 17;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {  // B[k][n] = L[c0+n][t*16+k]
+            av[4 * t + kk] = Xw[lr * LDA + t * IB + 4 * kk + lk];
+            bv[4 * t + kk] = Lst[lr * 17 + 4 * kk + lk];
+        }
+    }
+    dbl4 p0 = dbl4{0.0, 0.0, 0.0, 0.0}, p1 = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 4 * s; q += 2) {
+        p0 = mfma(av[q], bv[q], p0);
+        p1 = mfma(av[q + 1], bv[q + 1], p1);
+    }
+    dbl4 acc;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = Xw[(lk + 4 * r) * LDA + c0 + lr] - (p0[r] + p1[r]);
+    // Z (D layout) -> LDS, then X_s = Z D_s^T
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Tw[(lk + 4 * r) * 17 + lr] = acc[r];
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    dbl4 out = dbl4{0.0, 0.0, 0.0, 0.0};
+    const double* Ds = Dt + s * IB * 17;
+#pragma unroll
+    for (int kk = 0; kk < IB; kk += 4) out = mfma(Tw[lr * 17 + kk + lk], Ds[lr * 17 + kk + lk], out);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Xw[(lk + 4 * r) * LDA + c0 + lr] = out[r];
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ void trsm_store(double* __restrict__ S, int64_t ld, int64_t rbase, int64_t k0,
+                                           const double* __restrict__ Xw, int lane) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int idx = lane + 64 * q, r = idx >> 6, c = (idx & 63) * 2;
+        double2 v;
+        v.x = Xw[r * LDA + c];
+        v.y = Xw[r * LDA + c + 1];
+        *reinterpret_cast<double2*>(S + (rbase + r) * ld + k0 + c) = v;
+    }
+}
+
 // trsm_body: threads 0..255 (4 waves x 16 rows) solve one record; flag != nullptr: the factor of
 // column k comes from a potrf workgroup of the same launch (wait for its flag, sc1 loads); the threads
 // 256.. of a 512-thread workgroup only take part in the barriers
 __device__ __forceinline__ void trsm_body(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ rec,
                                           const double* __restrict__ dinv, const unsigned* __restrict__ flag,
-                                          double* __restrict__ scal, double* __restrict__ smem) {
+                                          double* __restrict__ scal, double* __restrict__ smem, bool progressive) {
     double* X = smem;                       // [4][IB][LDA]   panel rows of each wave
     double* T = X + 4 * IB * LDA;           // [4][IB][17]    per-wave 16x16 staging
     double* Lt = T + 4 * IB * 17;           // [28][IB][17]   L_st, p = s(s-1)/2 + t
@@ -443,20 +510,51 @@ __device__ __forceinline__ void trsm_body(double* __restrict__ S, int64_t ld, co
             Xw[r * LDA + c + 1] = v[q].y;
         }
     }
-    if (flag) {  // wait for the factor of column k: one lane polls, relaxed, bounded
+    const __amdgpu_buffer_rsrc_t rL = block_rsrc(L, ((int64_t)(CB - 1) * ld + CB) * 8);
+    const __amdgpu_buffer_rsrc_t rD = block_rsrc(Dk, (CB / IB) * IB * IB * 8);
+    auto wait_flag = [&](unsigned v) {  // one lane polls, relaxed, bounded; then the whole workgroup
         if (tid == 0) {
             unsigned spins = 0;
-            while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1u) {
+            while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }  // hand-off timeout (host reports it)
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the payload loads below the poll
         __syncthreads();
+    };
+    if (flag && progressive) {
+        // progressive hand-off (k_panel): step st starts as soon as the potrf workgroup has published
+        // block columns < st and D_st (flag >= st + 1): the row-st tiles L_st,t (t < st) and D_st, sc1 loads
+        __syncthreads();  // the panel rows are in LDS
+#pragma unroll
+        for (int st = 0; st < CB / IB; ++st) {
+            wait_flag((unsigned)(st + 1));
+            if (worker) {
+                // items: st tiles x 16 rows x 8 double2 + D_st (128 double2)
+                for (int i = tid; i < (st + 1) * 128; i += 256) {
+                    const int p = i >> 7, n = (i >> 3) & 15, kc = (i & 7) * 2;
+                    if (p < st) {
+                        const double2 v = ld_sc1(rL, ((int64_t)(st * IB + n) * ld + p * IB + kc) * 8);
+                        double* dst = Lt + ((st * (st - 1) / 2 + p) * IB + n) * 17 + kc;
+                        dst[0] = v.x;
+                        dst[1] = v.y;
+                    } else {
+                        const double2 v = ld_sc1(rD, (int64_t)(st * IB * IB + n * IB + kc) * 8);
+                        double* dst = Dt + (st * IB + n) * 17 + kc;
+                        dst[0] = v.x;
+                        dst[1] = v.y;
+                    }
+                }
+            }
+            __syncthreads();
+            if (worker) trsm_step(st, Xw, Tw, Lt, Dt, lr, lk);
+        }
+        if (worker) trsm_store(S, ld, rbase, k0, Xw, lane);
+        return;
     }
+    if (flag) wait_flag((unsigned)(CB / IB));  // the whole factor
     if (worker) {  // the factor: off-diagonal tiles of L_kk and the leaf inverses, sc1 loads
-        const __amdgpu_buffer_rsrc_t rL = block_rsrc(L, ((int64_t)(CB - 1) * ld + CB) * 8);
-        const __amdgpu_buffer_rsrc_t rD = block_rsrc(Dk, (CB / IB) * IB * IB * 8);
         double2 lv[14], dv[4];
         // off-diagonal tiles: item i -> tile p = i >> 7, row n = (i >> 3) & 15, columns 2*(i & 7)
 #pragma unroll
@@ -484,57 +582,14 @@ __device__ __forceinline__ void trsm_body(double* __restrict__ S, int64_t ld, co
     __syncthreads();
     if (!worker) return;
 #pragma unroll
-    for (int s = 0; s < CB / IB; ++s) {
-        const int c0 = s * IB;
-        // Z = A_s - sum_{t<s} X_t L_st^T : output 16x16, K = 16 s.  All operands of the step are read
-        // from LDS in one batch, then two independent MFMA chains.
-        double av[CB / 4], bv[CB / 4];
-#pragma unroll
-        for (int t = 0; t < s; ++t) {
-            const double* Lst = Lt + (s * (s - 1) / 2 + t) * IB * 17;
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {  // B[k][n] = L[c0+n][t*16+k]
-                av[4 * t + kk] = Xw[lr * LDA + t * IB + 4 * kk + lk];
-                bv[4 * t + kk] = Lst[lr * 17 + 4 * kk + lk];
-            }
-        }
-        dbl4 p0 = dbl4{0.0, 0.0, 0.0, 0.0}, p1 = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int q = 0; q < 4 * s; q += 2) {
-            p0 = mfma(av[q], bv[q], p0);
-            p1 = mfma(av[q + 1], bv[q + 1], p1);
-        }
-        dbl4 acc;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r] = Xw[(lk + 4 * r) * LDA + c0 + lr] - (p0[r] + p1[r]);
-        // Z (D layout) -> LDS, then X_s = Z D_s^T
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Tw[(lk + 4 * r) * 17 + lr] = acc[r];
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_wave_barrier();
-        dbl4 out = dbl4{0.0, 0.0, 0.0, 0.0};
-        const double* Ds = Dt + s * IB * 17;
-#pragma unroll
-        for (int kk = 0; kk < IB; kk += 4) out = mfma(Tw[lr * 17 + kk + lk], Ds[lr * 17 + kk + lk], out);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Xw[(lk + 4 * r) * LDA + c0 + lr] = out[r];
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_wave_barrier();
-    }
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int idx = lane + 64 * q, r = idx >> 6, c = (idx & 63) * 2;
-        double2 v;
-        v.x = Xw[r * LDA + c];
-        v.y = Xw[r * LDA + c + 1];
-        *reinterpret_cast<double2*>(S + (rbase + r) * ld + k0 + c) = v;
-    }
+    for (int st = 0; st < CB / IB; ++st) trsm_step(st, Xw, Tw, Lt, Dt, lr, lk);
+    trsm_store(S, ld, rbase, k0, Xw, lane);
 }
 
 __global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ tasks,
                                                  const double* __restrict__ dinv) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    trsm_body(S, ld, tasks + 2 * blockIdx.x, dinv, nullptr, nullptr, smem);
+    trsm_body(S, ld, tasks + 2 * blockIdx.x, dinv, nullptr, nullptr, smem, false);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -892,14 +947,14 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_panel(double* __restrict__ S,
                                                          int ncol, const int32_t* __restrict__ trsm, int ntrsm,
                                                          const int32_t* __restrict__ prev, double* __restrict__ dinv,
                                                          double* __restrict__ linv, double* __restrict__ scal,
-                                                         unsigned* __restrict__ flags) {
+                                                         unsigned* __restrict__ flags, int progressive) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     if ((int)blockIdx.x < ncol) {
         const int col = cols[blockIdx.x];
         potrf_body<false>(S, ld, col, dinv, scal, nullptr, flags + col, smem);
     } else if ((int)blockIdx.x < ncol + ntrsm) {
         const int32_t* rec = trsm + 2 * (blockIdx.x - ncol);
-        trsm_body(S, ld, rec, dinv, flags + rec[0], scal, smem);
+        trsm_body(S, ld, rec, dinv, flags + rec[0], scal, smem, progressive != 0);
     } else {
         trtri_body(S, ld, prev[blockIdx.x - ncol - ntrsm], dinv, linv, smem);
     }
@@ -1132,7 +1187,7 @@ int launch_cholesky(Ctx& c) {
         if (W.ncol + W.ntrsm + nprev <= c.n_cu) {  // one launch: every workgroup resident (one per CU)
             k_panel<<<(unsigned)(W.ncol + W.ntrsm + nprev), POTRF_THREADS, PANEL_LDS, c.stream>>>(
                 c.d_S, ld, c.d_sched + W.cols, W.ncol, c.d_sched + W.trsm, W.ntrsm, prev, c.d_dinv, c.d_linv, c.d_scal,
-                c.d_flags);
+                c.d_flags, (int)c.panel_progressive);
         } else {
             k_potrf128<false><<<(unsigned)W.ncol, POTRF_THREADS, POTRF_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.cols,
                                                                                       c.d_dinv, c.d_scal, nullptr);
@@ -1241,6 +1296,7 @@ int chol_setup(Ctx& c) {
     c.d_counters = c.d_bflags + nf;
     FBA_HIP(hipFuncSetAttribute((const void*)k_bwd_flow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)BWD_LDS));
     c.bwd_flow = !(getenv("FBA_BWD_LEVELS") && atoi(getenv("FBA_BWD_LEVELS")) != 0);
+    c.panel_progressive = !(getenv("FBA_PANEL_PROGRESSIVE") && atoi(getenv("FBA_PANEL_PROGRESSIVE")) == 0);
     FBA_HIP(hipFuncSetAttribute((const void*)k_trtri128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRTRI_LDS));
 
     c.probe_ev.assign(2 * std::max(c.sched.n_waves, 1), nullptr);

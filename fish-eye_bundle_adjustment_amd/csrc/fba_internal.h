@@ -172,7 +172,9 @@ struct Ctx {
     unsigned* d_counters = nullptr; // [Sched::n_counters] split-target arrival counters
     int64_t n_sync = 0;           // unsigned words of flags + bflags + counters (one allocation at d_flags,
                                   // zeroed by k_finish_rhs ahead of every factorisation)
-    bool bwd_flow = true;         // one-launch backward solve (FBA_BWD_LEVELS=1: one launch per level)
+    bool bwd_flow = true;
+    bool panel_progressive = true;  // k_panel: panel solves step with the potrf's published column blocks
+                                    // (FBA_PANEL_PROGRESSIVE=0: wait for the whole factor)         // one-launch backward solve (FBA_BWD_LEVELS=1: one launch per level)
     size_t flags_bytes = 0;
     int n_cu = 0;                // compute units (k_panel needs its whole grid resident)
     double* d_S = nullptr;       // [(n_pad+NB)*ld] normal matrix (lower) + RHS rows
