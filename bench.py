@@ -177,10 +177,11 @@ def main():
              "flops_per_launch": flops_launch, "traffic": pmc_traffic(args.config, name)}
         r["frac"] = r["achieved"] / r["peak"] if r["achieved"] else None
         return r
-    roof = probe(2, "k_panel", "diagonal-block potrf + panel solves of one elimination-tree level, 128x128 f64 "
-                               "blocks; a latency-bound dependency chain: one launch per level, in series")
-    roof_bulk = probe(1, "k_syrk_multi", "Cholesky trailing update of one tree level, 64x64 f64 MFMA tiles, "
-                                         "K = 128 per source column")
+    roof = probe(2, "k_panel", "one elimination-tree level: the 128x128 f64 diagonal-block potrf, the panel "
+                               "solves and (levels of <= 450 update tasks) the previous level's trailing updates "
+                               "as in-launch dataflow; a latency-bound chain, one launch per level")
+    roof_bulk = probe(1, "k_syrk_multi", "Cholesky trailing update of one of the large tree levels (> 450 "
+                                         "tasks, own launch), 64x64 f64 MFMA tiles, K = 128 per source column")
     phase_roof = {"cholesky_dense_equiv_TFLOPs": chol_flops / (t["cholesky"] * 1e-3) / 1e12,
                   "linearize_accumulate_GBs": lin_bytes / ((t["linearize"] + t["accumulate"]) * 1e-3) / 1e9}
     value = args.steps / dt

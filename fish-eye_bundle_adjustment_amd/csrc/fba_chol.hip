@@ -200,6 +200,23 @@ constexpr size_t POTRF_LDS = sizeof(double) * (POTRF_NT + CB / IB) * IB * 17;  /
 // scripts/ubench/chol_ubench.hip)
 // potrf_body: factor the 128x128 diagonal block of column col (512 threads); flag != nullptr: publish
 // it (k_panel hand-off)
+// wait until every flag of a list is set (merged launch: the previous level's updates of this
+// workgroup's blocks); one lane polls, bounded, then the whole workgroup
+__device__ __forceinline__ void wait_list(const int32_t* __restrict__ wl, int n, unsigned* __restrict__ tflags,
+                                          double* __restrict__ scal) {
+    if (n <= 0) return;
+    if (threadIdx.x == 0)
+        for (int q = 0; q < n; ++q) {
+            unsigned spins = 0;
+            while (__hip_atomic_load(tflags + wl[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }
+            }
+        }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __syncthreads();
+}
+
 template <bool TS>
 __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, int col, double* __restrict__ dinv,
                                            double* __restrict__ scal, unsigned long long* __restrict__ ts,
@@ -239,10 +256,11 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
         // starts after one load latency); the other 35 lower tiles go through LDS: item i -> tile
         // p = 1 + (i >> 7), row (i >> 3) & 15, columns 2 (i & 7), all of a thread's loads in flight
         double a[IB], x[IB];
+        // sc1 loads: in a merged launch the block was just updated by another workgroup
         if (wave == 0) {
 #pragma unroll
             for (int h = 0; h < IB / 2; ++h) {
-                const double2 v = *reinterpret_cast<const double2*>(S + (k0 + lr) * ld + k0 + 2 * h);
+                const double2 v = ld_sc1(rL, ((int64_t)lr * ld + 2 * h) * 8);
                 a[2 * h] = v.x;
                 a[2 * h + 1] = v.y;
             }
@@ -257,7 +275,7 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
             while (pp > ti) { pp -= ti + 1; ++ti; }
             off[q] = -1;
             if (p < POTRF_NT) {
-                v[q] = *reinterpret_cast<const double2*>(S + (k0 + ti * IB + n) * ld + k0 + pp * IB + m);
+                v[q] = ld_sc1(rL, ((int64_t)(ti * IB + n) * ld + pp * IB + m) * 8);
                 off[q] = p * IB * 17 + n * 17 + m;
             }
         }
@@ -496,12 +514,13 @@ __device__ __forceinline__ void trsm_body(double* __restrict__ S, int64_t ld, co
     double* Tw = T + wave * IB * 17;
     const double* L = S + k0 * ld + k0;
     const double* Dk = dinv + (k0 / CB) * (CB / IB) * (IB * IB);
-    if (worker) {  // the panel rows (written by earlier launches): plain loads, issued first
+    if (worker) {  // the panel rows, issued first (sc1: in a merged launch just updated by another workgroup)
+        const __amdgpu_buffer_rsrc_t rA = block_rsrc(S + rbase * ld + k0, ((int64_t)(IB - 1) * ld + CB) * 8);
         double2 v[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int idx = lane + 64 * q, r = idx >> 6, c = (idx & 63) * 2;
-            v[q] = *reinterpret_cast<const double2*>(S + (rbase + r) * ld + k0 + c);
+            v[q] = ld_sc1(rA, ((int64_t)r * ld + c) * 8);
         }
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
@@ -603,19 +622,24 @@ __global__ __launch_bounds__(256) void k_trsm128(double* __restrict__ S, int64_t
 constexpr int KS = 32;
 constexpr int LDK = 34;   // LDS stride of a 32-deep slice: bank = (4r + 2k) mod 64, conflict-free
 
-__global__ __launch_bounds__(256) void k_syrk_multi(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ tasks,
-                                                    const int32_t* __restrict__ src, double* __restrict__ P,
-                                                    const int32_t* __restrict__ comb, unsigned* __restrict__ cnt) {
-    __shared__ __attribute__((aligned(16))) double As[64][LDK];
-    __shared__ __attribute__((aligned(16))) double Bs[64][LDK];
-    __shared__ unsigned last;
-    const int32_t* tk = tasks + Sched::SYRK_REC * blockIdx.x;
+// syrk_body: one quarter task; threads 0..255 work, threads 256.. (a 512-thread k_panel workgroup) only
+// take part in the barriers.  tflags != nullptr: the task runs inside the next level's k_panel, so the
+// target quarter is written through (sc1) and its completion flag raised for the potrf / panel-solve
+// workgroups of that launch that consume it.
+__device__ __forceinline__ void syrk_body(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ tk,
+                                          const int32_t* __restrict__ src, double* __restrict__ P,
+                                          const int32_t* __restrict__ comb, unsigned* __restrict__ cnt,
+                                          unsigned* __restrict__ tflags, double* __restrict__ smem) {
+    double (*As)[LDK] = reinterpret_cast<double (*)[LDK]>(smem);
+    double (*Bs)[LDK] = reinterpret_cast<double (*)[LDK]>(smem + 64 * LDK);
+    unsigned* last = reinterpret_cast<unsigned*>(smem + 128 * LDK);
     const int64_t bi = tk[0], bj = tk[1];
     const int qr = tk[2] >> 1, qc = tk[2] & 1, s0 = tk[3], slot = tk[5];
     const int nsl = 4 * (tk[4] - s0);
     const int32_t* ks_src = src + s0;
     const int64_t r0 = bi * CB + qr * 64, c0 = bj * CB + qc * 64;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, wave = (tid & 255) >> 6, lane = tid & 63;
+    const bool worker = tid < 256;
     const int lr = lane & 15, lk = lane >> 4;
     const int wr = (wave >> 1) * 32, wc = (wave & 1) * 32;
     // output: the C quarter in place, or scratch quarter `slot` (row-major 64x64, starts from zero)
@@ -627,12 +651,12 @@ __global__ __launch_bounds__(256) void k_syrk_multi(double* __restrict__ S, int6
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc[a][b][r] = slot < 0 ? Cp[(a * 16 + 4 * r) * ldc + b * 16] : 0.0;
-    const int rr = tid >> 2, cc = (tid & 3) * 8;
+            for (int r = 0; r < 4; ++r) acc[a][b][r] = (slot < 0 && worker) ? Cp[(a * 16 + 4 * r) * ldc + b * 16] : 0.0;
+    const int rr = (tid & 255) >> 2, cc = (tid & 3) * 8;
     const double* ga = S + (r0 + rr) * ld + cc;
     const double* gb = S + (c0 + rr) * ld + cc;
     double2 pa[4], pb[4];
-    {
+    if (worker) {
         const int64_t kc = (int64_t)ks_src[0] * CB;
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
@@ -642,47 +666,64 @@ __global__ __launch_bounds__(256) void k_syrk_multi(double* __restrict__ S, int6
     }
     for (int sl = 0; sl < nsl; ++sl) {
         __syncthreads();
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-            As[rr][cc + 2 * h] = pa[h].x; As[rr][cc + 2 * h + 1] = pa[h].y;
-            Bs[rr][cc + 2 * h] = pb[h].x; Bs[rr][cc + 2 * h + 1] = pb[h].y;
-        }
-        __syncthreads();
-        if (sl + 1 < nsl) {
-            const int64_t kc = (int64_t)ks_src[(sl + 1) >> 2] * CB + ((sl + 1) & 3) * KS;
+        if (worker) {
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
-                pa[h] = *reinterpret_cast<const double2*>(ga + kc + 2 * h);
-                pb[h] = *reinterpret_cast<const double2*>(gb + kc + 2 * h);
+                As[rr][cc + 2 * h] = pa[h].x; As[rr][cc + 2 * h + 1] = pa[h].y;
+                Bs[rr][cc + 2 * h] = pb[h].x; Bs[rr][cc + 2 * h + 1] = pb[h].y;
             }
         }
+        __syncthreads();
+        if (worker) {
+            if (sl + 1 < nsl) {
+                const int64_t kc = (int64_t)ks_src[(sl + 1) >> 2] * CB + ((sl + 1) & 3) * KS;
 #pragma unroll
-        for (int kk = 0; kk < KS; kk += 4) {
-            double av[2], bv[2];
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                av[q] = -As[wr + q * 16 + lr][kk + lk];
-                bv[q] = Bs[wc + q * 16 + lr][kk + lk];
+                for (int h = 0; h < 4; ++h) {
+                    pa[h] = *reinterpret_cast<const double2*>(ga + kc + 2 * h);
+                    pb[h] = *reinterpret_cast<const double2*>(gb + kc + 2 * h);
+                }
             }
+#pragma unroll
+            for (int kk = 0; kk < KS; kk += 4) {
+                double av[2], bv[2];
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    av[q] = -As[wr + q * 16 + lr][kk + lk];
+                    bv[q] = Bs[wc + q * 16 + lr][kk + lk];
+                }
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b) acc[a][b] = mfma(av[a], bv[b], acc[a][b]);
+            }
+        }
+    }
+    const __amdgpu_buffer_rsrc_t rC = block_rsrc(S + r0 * ld + c0, ((int64_t)63 * ld + 64) * 8);
+    if (slot < 0) {
+        if (worker) {
 #pragma unroll
             for (int a = 0; a < 2; ++a)
 #pragma unroll
-                for (int b = 0; b < 2; ++b) acc[a][b] = mfma(av[a], bv[b], acc[a][b]);
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        if (tflags)
+                            st_sc1(rC, ((int64_t)(wr + lk + a * 16 + 4 * r) * ld + wc + lr + b * 16) * 8, acc[a][b][r]);
+                        else
+                            Cp[(a * 16 + 4 * r) * ldc + b * 16] = acc[a][b][r];
+                    }
         }
-    }
-    if (slot < 0) {
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) Cp[(a * 16 + 4 * r) * ldc + b * 16] = acc[a][b][r];
+        if (tflags) {  // publish the quarter
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(tflags + tk[7], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         return;
     }
     // split target: this group's partial goes to its scratch quarter write-through; the group that
     // arrives last (agent-scope counter) adds all groups' partials to C in slot order -- the same
     // arithmetic as a separate combine launch, so the result does not depend on the arrival order
-    {
+    if (worker) {
         const __amdgpu_buffer_rsrc_t rP = block_rsrc(P + (int64_t)slot * 4096, 4096 * 8);
 #pragma unroll
         for (int a = 0; a < 2; ++a)
@@ -696,29 +737,45 @@ __global__ __launch_bounds__(256) void k_syrk_multi(double* __restrict__ S, int6
     __syncthreads();
     const int32_t* cb = comb + Sched::COMB_REC * tk[6];
     if (tid == 0)
-        last = __hip_atomic_fetch_add(cnt + tk[6], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(cb[4] - 1);
+        *last = __hip_atomic_fetch_add(cnt + tk[6], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(cb[4] - 1);
     __syncthreads();
-    if (!last) return;
+    if (!*last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const int first = cb[3], n = cb[4];
-    double2 v[8];
-    double2* cq[8];
+    if (worker) {
+        double2 v[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int e = 2 * (tid + 256 * q), r = e >> 6, cl = e & 63;
-        cq[q] = reinterpret_cast<double2*>(S + (r0 + r) * ld + c0 + cl);
-        v[q] = *cq[q];
+        for (int q = 0; q < 8; ++q) {
+            const int e = 2 * (tid + 256 * q), r = e >> 6, cl = e & 63;
+            v[q] = *reinterpret_cast<const double2*>(S + (r0 + r) * ld + c0 + cl);
+        }
+        for (int g = 0; g < n; ++g) {
+            const __amdgpu_buffer_rsrc_t rg = block_rsrc(P + (int64_t)(first + g) * 4096, 4096 * 8);
+            double2 pv[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) pv[q] = ld_sc1(rg, (int64_t)(2 * (tid + 256 * q)) * 8);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) { v[q].x += pv[q].x; v[q].y += pv[q].y; }
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int e = 2 * (tid + 256 * q), r = e >> 6, cl = e & 63;
+            if (tflags) st_sc1(rC, ((int64_t)r * ld + cl) * 8, v[q]);
+            else *reinterpret_cast<double2*>(S + (r0 + r) * ld + c0 + cl) = v[q];
+        }
     }
-    for (int g = 0; g < n; ++g) {
-        const __amdgpu_buffer_rsrc_t rg = block_rsrc(P + (int64_t)(first + g) * 4096, 4096 * 8);
-        double2 pv[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) pv[q] = ld_sc1(rg, (int64_t)(2 * (tid + 256 * q)) * 8);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) { v[q].x += pv[q].x; v[q].y += pv[q].y; }
+    if (tflags) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(tflags + tk[7], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) *cq[q] = v[q];
+}
+
+__global__ __launch_bounds__(256) void k_syrk_multi(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ tasks,
+                                                    const int32_t* __restrict__ src, double* __restrict__ P,
+                                                    const int32_t* __restrict__ comb, unsigned* __restrict__ cnt) {
+    __shared__ __attribute__((aligned(16))) double sm[128 * LDK + 2];
+    syrk_body(S, ld, tasks + Sched::SYRK_REC * blockIdx.x, src, P, comb, cnt, nullptr, sm);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -947,16 +1004,33 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_panel(double* __restrict__ S,
                                                          int ncol, const int32_t* __restrict__ trsm, int ntrsm,
                                                          const int32_t* __restrict__ prev, double* __restrict__ dinv,
                                                          double* __restrict__ linv, double* __restrict__ scal,
-                                                         unsigned* __restrict__ flags, int progressive) {
+                                                         unsigned* __restrict__ flags, int progressive,
+                                                         const int32_t* __restrict__ tasks, int ntask, int ndiag,
+                                                         const int32_t* __restrict__ src, double* __restrict__ P,
+                                                         const int32_t* __restrict__ comb, unsigned* __restrict__ cnt,
+                                                         unsigned* __restrict__ tflags, const int32_t* __restrict__ wstart,
+                                                         const int32_t* __restrict__ wlist) {
+    // workgroup order (every wait points to a lower index, so in-order dispatch always progresses):
+    // [the previous level's updates of this level's diagonal blocks][potrf][the other updates]
+    // [panel solves][inverses of the previous level's blocks]
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    if ((int)blockIdx.x < ncol) {
-        const int col = cols[blockIdx.x];
+    const int b = blockIdx.x;
+    if (b < ndiag) {
+        syrk_body(S, ld, tasks + Sched::SYRK_REC * b, src, P, comb, cnt, tflags, smem);
+    } else if (b < ndiag + ncol) {
+        const int c = b - ndiag;
+        if (ntask > 0) wait_list(wlist + wstart[c], wstart[c + 1] - wstart[c], tflags, scal);
+        const int col = cols[c];
         potrf_body<false>(S, ld, col, dinv, scal, nullptr, flags + col, smem);
-    } else if ((int)blockIdx.x < ncol + ntrsm) {
-        const int32_t* rec = trsm + 2 * (blockIdx.x - ncol);
+    } else if (b < ntask + ncol) {
+        syrk_body(S, ld, tasks + Sched::SYRK_REC * (b - ncol), src, P, comb, cnt, tflags, smem);
+    } else if (b < ntask + ncol + ntrsm) {
+        const int t = b - ntask - ncol;
+        if (ntask > 0) wait_list(wlist + wstart[ncol + t], wstart[ncol + t + 1] - wstart[ncol + t], tflags, scal);
+        const int32_t* rec = trsm + 2 * t;
         trsm_body(S, ld, rec, dinv, flags + rec[0], scal, smem, progressive != 0);
     } else {
-        trtri_body(S, ld, prev[blockIdx.x - ncol - ntrsm], dinv, linv, smem);
+        trtri_body(S, ld, prev[b - ntask - ncol - ntrsm], dinv, linv, smem);
     }
 }
 
@@ -1177,17 +1251,39 @@ __global__ void k_neg_copy(const double* __restrict__ X, double* __restrict__ de
 int launch_cholesky(Ctx& c) {
     const int64_t ld = c.L.ld;
     const Sched& s = c.sched;
-    // the k_panel / k_bwd_flow hand-off flags and the split-target counters were zeroed by k_finish_rhs
+    // the k_panel / k_bwd_flow hand-off flags, the split-target counters and the update flags were
+    // zeroed by k_finish_rhs
+    int pend = -1;  // a level whose trailing updates run inside the next level's k_panel
+    auto updates = [&](int v) -> int {  // a level's trailing updates as their own launch
+        const Sched::Wave& V = s.w[v];
+        const bool pr = c.probe == 1 && c.probe_n < (int)c.probe_ev.size() / 2;
+        if (pr) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
+        k_syrk_multi<<<(unsigned)V.ntask, 256, 0, c.stream>>>(c.d_S, ld, c.d_sched + V.tasks, c.d_sched + V.src, c.d_P,
+                                                               c.d_sched + V.comb, c.d_counters + V.cbase);
+        if (pr) {
+            FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], c.stream));
+            c.probe_flops += V.flops;
+            ++c.probe_n;
+        }
+        return FBA_OK;
+    };
     for (int w = 0; w < s.n_waves; ++w) {
         const Sched::Wave& W = s.w[w];
-        const bool pp = c.probe == 2 && c.probe_n < (int)c.probe_ev.size() / 2;
-        if (pp) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
         const int nprev = w > 0 ? s.w[w - 1].ncol : 0;  // the previous level's blocks, inverted alongside
         const int32_t* prev = c.d_sched + (w > 0 ? s.w[w - 1].cols : 0);
-        if (W.ncol + W.ntrsm + nprev <= c.n_cu) {  // one launch: every workgroup resident (one per CU)
-            k_panel<<<(unsigned)(W.ncol + W.ntrsm + nprev), POTRF_THREADS, PANEL_LDS, c.stream>>>(
+        const bool fits = W.ncol + W.ntrsm + nprev <= c.n_cu;  // potrf + panel solves resident (one per CU)
+        if (pend >= 0 && !fits) { updates(pend); pend = -1; }
+        const Sched::Wave* U = pend >= 0 ? &s.w[pend] : nullptr;
+        const bool pp = c.probe == 2 && c.probe_n < (int)c.probe_ev.size() / 2;
+        if (pp) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
+        if (fits) {
+            // one launch: [U's updates of this level's diagonal blocks][potrf][U's other updates]
+            // [panel solves][inverses of the previous level's blocks]; U = the previous level (merged)
+            k_panel<<<(unsigned)(W.ncol + W.ntrsm + nprev + (U ? U->ntask : 0)), POTRF_THREADS, PANEL_LDS, c.stream>>>(
                 c.d_S, ld, c.d_sched + W.cols, W.ncol, c.d_sched + W.trsm, W.ntrsm, prev, c.d_dinv, c.d_linv, c.d_scal,
-                c.d_flags, (int)c.panel_progressive);
+                c.d_flags, (int)c.panel_progressive, U ? c.d_sched + U->tasks : nullptr, U ? U->ntask : 0,
+                U ? U->ndiag : 0, U ? c.d_sched + U->src : nullptr, c.d_P, U ? c.d_sched + U->comb : nullptr,
+                U ? c.d_counters + U->cbase : nullptr, c.d_tflags, c.d_sched + W.wstart, c.d_sched + W.wlist);
         } else {
             k_potrf128<false><<<(unsigned)W.ncol, POTRF_THREADS, POTRF_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.cols,
                                                                                       c.d_dinv, c.d_scal, nullptr);
@@ -1197,20 +1293,15 @@ int launch_cholesky(Ctx& c) {
         }
         if (pp) {
             FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], c.stream));
-            c.probe_flops += W.pflops;
+            c.probe_flops += W.pflops + (U ? U->flops : 0.0);
             ++c.probe_n;
         }
+        pend = -1;
         if (W.ntask == 0) continue;
-        const bool pr = c.probe == 1 && c.probe_n < (int)c.probe_ev.size() / 2;
-        if (pr) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
-        k_syrk_multi<<<(unsigned)W.ntask, 256, 0, c.stream>>>(c.d_S, ld, c.d_sched + W.tasks, c.d_sched + W.src, c.d_P,
-                                                               c.d_sched + W.comb, c.d_counters + W.cbase);
-        if (pr) {
-            FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], c.stream));
-            c.probe_flops += W.flops;
-            ++c.probe_n;
-        }
+        if (c.merge_updates && W.ntask <= c.merge_max) pend = w;  // into the next level's k_panel
+        else updates(w);
     }
+    if (pend >= 0) updates(pend);
     FBA_HIP(hipGetLastError());
     return FBA_OK;
 }
@@ -1289,14 +1380,17 @@ int chol_setup(Ctx& c) {
     c.n_cu = prop.multiProcessorCount;
     c.flags_bytes = (size_t)((c.L.n_pad / CB + 3) / 4 * 4) * sizeof(unsigned);  // multiple of 16 bytes
     const size_t nf = c.flags_bytes / sizeof(unsigned);
-    c.n_sync = (int64_t)(2 * nf + std::max(c.sched.n_counters, 1));
+    c.n_sync = (int64_t)(2 * nf + std::max(c.sched.n_counters, 1) + std::max(c.sched.n_tflags, 1));
     FBA_HIP(hipMalloc((void**)&c.d_flags, sizeof(unsigned) * c.n_sync));
     FBA_HIP(hipMemset(c.d_flags, 0, sizeof(unsigned) * c.n_sync));
     c.d_bflags = c.d_flags + nf;
     c.d_counters = c.d_bflags + nf;
+    c.d_tflags = c.d_counters + std::max(c.sched.n_counters, 1);
     FBA_HIP(hipFuncSetAttribute((const void*)k_bwd_flow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)BWD_LDS));
     c.bwd_flow = !(getenv("FBA_BWD_LEVELS") && atoi(getenv("FBA_BWD_LEVELS")) != 0);
     c.panel_progressive = !(getenv("FBA_PANEL_PROGRESSIVE") && atoi(getenv("FBA_PANEL_PROGRESSIVE")) == 0);
+    c.merge_updates = !(getenv("FBA_MERGE_UPDATES") && atoi(getenv("FBA_MERGE_UPDATES")) == 0);
+    c.merge_max = getenv("FBA_MERGE_MAX") ? atoi(getenv("FBA_MERGE_MAX")) : 450;  // config 4: 0 -> 752, 300 -> 762, 400-500 -> 764, all -> 733 iter/s
     FBA_HIP(hipFuncSetAttribute((const void*)k_trtri128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRTRI_LDS));
 
     c.probe_ev.assign(2 * std::max(c.sched.n_waves, 1), nullptr);

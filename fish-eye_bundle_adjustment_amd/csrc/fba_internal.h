@@ -42,17 +42,21 @@ struct Layout {
 // Block schedule of the reduced-system Cholesky (fba_order.cpp): one batched step per level of the
 // elimination tree.  All offsets index the int32 device buffer Ctx::d_sched.
 //   trsm records  (k, 2 r + h): panel block (r, k), row half h (halves of padding rows are skipped)
-//   task records  SYRK_REC ints: (i, j, quarter 2 qr + qc, s0, s1, slot, comb): C(i,j) quarter -= sum
+//   task records  SYRK_REC ints: (i, j, quarter 2 qr + qc, s0, s1, slot, comb, fidx): C(i,j) quarter -= sum
 //                 of X_ik X_jk' over the sources src[s0..s1) (ascending); slot >= 0: the sum goes to the
 //                 scratch quarter `slot` instead (split targets), and the last group to arrive (counter
 //                 cbase + comb) applies the COMB_REC record `comb` of the level
-//                 (i, j, quarter, first slot, slots): C -= P_first - ... in slot order
+//                 (i, j, quarter, first slot, slots): C -= P_first - ... in slot order; fidx: the target
+//                 quarter's completion flag when the update runs inside the next level's k_panel
 struct Sched {
-    static constexpr int SYRK_REC = 7, COMB_REC = 5;
+    static constexpr int SYRK_REC = 8, COMB_REC = 5;
     struct Wave {
         int64_t cols = 0, trsm = 0, tasks = 0, src = 0, comb = 0;  // offsets
         int ncol = 0, ntrsm = 0, ntask = 0, ncomb = 0;
         int cbase = 0;            // first arrival counter of the level's split targets (k_syrk_multi)
+        int ndiag = 0;            // the level's first ndiag tasks update next-level diagonal blocks
+        int64_t wstart = 0, wlist = 0;  // merged launch: wait lists (flags of the previous level's
+                                        // updates) of this level's potrf columns then panel halves
         double flops = 0.0;       // trailing-update flops of the level (kernel probe)
         double pflops = 0.0;      // diagonal factorisations + panel solves of the level (kernel probe)
     };
@@ -68,6 +72,7 @@ struct Sched {
     int nzero = 0;                // (diagonal, panel and RHS blocks): zeroed before each accumulation
     int n_scratch = 0;            // 64x64 scratch quarters of the split targets (max over levels)
     int n_counters = 0;           // split-target arrival counters, all levels
+    int n_tflags = 0;             // completion flags of the update targets (quarters), all levels
     std::vector<Wave> w;          // factorisation, level 0 up
     std::vector<BWave> b;         // backward solve, indexed by level (run top down)
     std::vector<int32_t> buf;     // host image of the lists (uploaded to Ctx::d_sched)
@@ -170,9 +175,13 @@ struct Ctx {
     unsigned* d_flags = nullptr; // [nb] k_panel hand-off flags (zeroed before each factorisation)
     unsigned* d_bflags = nullptr; // [nb] k_bwd_flow hand-off flags (zeroed before each backward solve)
     unsigned* d_counters = nullptr; // [Sched::n_counters] split-target arrival counters
+    unsigned* d_tflags = nullptr;   // [Sched::n_tflags] update-target completion flags (merged k_panel)
     int64_t n_sync = 0;           // unsigned words of flags + bflags + counters (one allocation at d_flags,
                                   // zeroed by k_finish_rhs ahead of every factorisation)
     bool bwd_flow = true;
+    int merge_max = 450;            // ... for levels of at most this many update tasks (FBA_MERGE_MAX)
+    bool merge_updates = true;      // a level's trailing updates inside the next level's k_panel
+                                    // (FBA_MERGE_UPDATES=0: their own k_syrk_multi launch)
     bool panel_progressive = true;  // k_panel: panel solves step with the potrf's published column blocks
                                     // (FBA_PANEL_PROGRESSIVE=0: wait for the whole factor)         // one-launch backward solve (FBA_BWD_LEVELS=1: one launch per level)
     size_t flags_bytes = 0;

@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <deque>
 #include <map>
+#include <tuple>
 
 #include "fba_internal.h"
 
@@ -364,6 +365,7 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
     std::vector<int32_t> buf;  // device image
     auto at = [&]() { return (int64_t)buf.size(); };
     s.w.resize(nw);
+    std::vector<std::map<std::tuple<int32_t, int32_t, int32_t>, int32_t>> tflag(nw);  // (i, j, quarter) -> flag
     int64_t ntile_total = 0;
     for (int w = 0; w < nw; ++w) {
         Sched::Wave& W = s.w[w];
@@ -389,11 +391,18 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
         // consecutive sources summed into scratch quarters and combined in group order afterwards,
         // so no workgroup runs more than SPLIT * 128 deep (the long poles of a level)
         constexpr int SPLIT = 2;
-        struct Task { int32_t i, j, q, s0, s1, slot, comb; };
+        struct Task { int32_t i, j, q, s0, s1, slot, comb, fidx, rank; };
         std::vector<Task> tasks;
         std::vector<int32_t> src, comb;
         int slots = 0, ncomb = 0;
         W.flops = 0.0;
+        // completion flag of every target quarter (the in-launch hand-off to the next level's k_panel);
+        // rank: 0 a diagonal block of a next-level column, 1 a panel block of one, 2 the rest
+        std::map<std::tuple<int32_t, int32_t, int32_t>, int32_t>& fmap = tflag[w];
+        auto rank_of = [&](int32_t i, int32_t j) {
+            if (w + 1 >= nw || level[j] != w + 1) return 2;
+            return i == j ? 0 : 1;
+        };
         for (auto& t : tg) {
             const int32_t i = t.first.first, j = t.first.second;
             const int32_t s0 = (int32_t)src.size();
@@ -404,28 +413,35 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
                 const int qr = q >> 1, qc = q & 1;
                 if (i == j && qr == 0 && qc == 1) continue;  // strictly upper quarter of a diagonal block
                 if ((qr == 1 && real_rows(i) <= NB / 2) || (qc == 1 && real_rows(j) <= NB / 2)) continue;
+                const int32_t fidx = s.n_tflags++;
+                fmap[std::make_tuple(i, j, q)] = fidx;
+                const int32_t rk = rank_of(i, j);
                 if (!split) {
-                    tasks.push_back({i, j, q, s0, s0 + ns, -1, -1});
+                    tasks.push_back({i, j, q, s0, s0 + ns, -1, -1, fidx, rk});
                 } else {
                     const int first = slots;
                     for (int32_t g = 0; g < ns; g += SPLIT)
-                        tasks.push_back({i, j, q, s0 + g, s0 + std::min(ns, g + SPLIT), slots++, ncomb});
+                        tasks.push_back({i, j, q, s0 + g, s0 + std::min(ns, g + SPLIT), slots++, ncomb, fidx, rk});
                     comb.insert(comb.end(), {i, j, q, first, slots - first});
                     ++ncomb;
                 }
                 W.flops += (double)ns * 2.0 * 64 * 64 * NB;
             }
         }
-        // longest (most sources) first, then by block column: the long workgroups start early
+        // the next level's diagonal blocks first, then its panel blocks (their consumers wait in the merged
+        // launch), then the rest; within a rank longest (most sources) first, then by block column
         std::stable_sort(tasks.begin(), tasks.end(), [](const Task& a, const Task& b) {
+            if (a.rank != b.rank) return a.rank < b.rank;
             if (a.s1 - a.s0 != b.s1 - b.s0) return a.s1 - a.s0 > b.s1 - b.s0;
             return a.j != b.j ? a.j < b.j : a.i < b.i;
         });
+        W.ndiag = 0;
+        for (auto& t : tasks) W.ndiag += t.rank == 0 ? 1 : 0;
         W.src = at();
         buf.insert(buf.end(), src.begin(), src.end());
         W.tasks = at();
         W.ntask = (int)tasks.size();
-        for (auto& t : tasks) buf.insert(buf.end(), {t.i, t.j, t.q, t.s0, t.s1, t.slot, t.comb});
+        for (auto& t : tasks) buf.insert(buf.end(), {t.i, t.j, t.q, t.s0, t.s1, t.slot, t.comb, t.fidx});
         W.comb = at();
         W.ncomb = ncomb;
         W.cbase = s.n_counters;
@@ -433,6 +449,36 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
         buf.insert(buf.end(), comb.begin(), comb.end());
         s.n_scratch = std::max(s.n_scratch, slots);
         ntile_total += (int64_t)tg.size();
+    }
+    // wait lists of the merged launches: level v's potrf workgroups wait for the flags of level v-1's
+    // updates of their diagonal block, its panel-solve halves (k, 2 r + h) for those of quarters
+    // (r, k, 2 h + 0/1)
+    for (int v = 1; v < nw; ++v) {
+        Sched::Wave& W = s.w[v];
+        const auto& fm = tflag[v - 1];
+        std::vector<int32_t> start, list;
+        auto add = [&](int32_t i, int32_t j, int32_t q) {
+            auto it = fm.find(std::make_tuple(i, j, q));
+            if (it != fm.end()) list.push_back(it->second);
+        };
+        for (int32_t k : wave[v]) {
+            start.push_back((int32_t)list.size());
+            for (int q : {0, 2, 3}) add(k, k, q);
+        }
+        const int32_t* tr = buf.data() + W.trsm;
+        std::vector<std::pair<int32_t, int32_t>> recs;
+        for (int t = 0; t < W.ntrsm; ++t) recs.push_back({tr[2 * t], tr[2 * t + 1]});
+        for (auto& rc : recs) {
+            start.push_back((int32_t)list.size());
+            const int32_t k = rc.first, r = rc.second >> 1, h = rc.second & 1;
+            add(r, k, 2 * h);  // (r = nb: the RHS block row, updated like any other)
+            add(r, k, 2 * h + 1);
+        }
+        start.push_back((int32_t)list.size());
+        W.wstart = at();
+        buf.insert(buf.end(), start.begin(), start.end());
+        W.wlist = at();
+        buf.insert(buf.end(), list.begin(), list.end());
     }
     // backward solve L' x = y by levels, top down: the columns of level w get x = Linv' y; every
     // column j whose panel holds one of them gets y_j -= sum_i L(i,j)' x_i (i ascending)
