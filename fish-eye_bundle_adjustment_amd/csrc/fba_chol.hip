@@ -1002,35 +1002,40 @@ constexpr size_t PANEL_LDS = TRSM_LDS > TRTRI_LDS ? TRSM_LDS : TRTRI_LDS;
 
 __global__ __launch_bounds__(POTRF_THREADS) void k_panel(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ cols,
                                                          int ncol, const int32_t* __restrict__ trsm, int ntrsm,
-                                                         const int32_t* __restrict__ prev, double* __restrict__ dinv,
+                                                         const int32_t* __restrict__ prev, int nprev,
+                                                         double* __restrict__ dinv,
                                                          double* __restrict__ linv, double* __restrict__ scal,
                                                          unsigned* __restrict__ flags, int progressive,
                                                          const int32_t* __restrict__ tasks, int ntask, int ndiag,
-                                                         const int32_t* __restrict__ src, double* __restrict__ P,
-                                                         const int32_t* __restrict__ comb, unsigned* __restrict__ cnt,
-                                                         unsigned* __restrict__ tflags, const int32_t* __restrict__ wstart,
+                                                         int npanel, const int32_t* __restrict__ src,
+                                                         double* __restrict__ P, const int32_t* __restrict__ comb,
+                                                         unsigned* __restrict__ cnt, unsigned* __restrict__ tflags,
+                                                         const int32_t* __restrict__ wstart,
                                                          const int32_t* __restrict__ wlist) {
     // workgroup order (every wait points to a lower index, so in-order dispatch always progresses):
-    // [the previous level's updates of this level's diagonal blocks][potrf][the other updates]
-    // [panel solves][inverses of the previous level's blocks]
+    // [the previous level's updates of this level's diagonal blocks][potrf][its updates of this level's
+    // panel blocks][panel solves][inverses of the previous level's blocks][its updates of later levels'
+    // blocks, which nothing in this launch waits for]
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int b = blockIdx.x;
-    if (b < ndiag) {
+    const int e1 = ndiag, e2 = e1 + ncol, e3 = e2 + npanel, e4 = e3 + ntrsm, e5 = e4 + nprev;
+    if (b < e1) {
         syrk_body(S, ld, tasks + Sched::SYRK_REC * b, src, P, comb, cnt, tflags, smem);
-    } else if (b < ndiag + ncol) {
-        const int c = b - ndiag;
+    } else if (b < e2) {
+        const int c = b - e1;
         if (ntask > 0) wait_list(wlist + wstart[c], wstart[c + 1] - wstart[c], tflags, scal);
-        const int col = cols[c];
-        potrf_body<false>(S, ld, col, dinv, scal, nullptr, flags + col, smem);
-    } else if (b < ntask + ncol) {
+        potrf_body<false>(S, ld, cols[c], dinv, scal, nullptr, flags + cols[c], smem);
+    } else if (b < e3) {
         syrk_body(S, ld, tasks + Sched::SYRK_REC * (b - ncol), src, P, comb, cnt, tflags, smem);
-    } else if (b < ntask + ncol + ntrsm) {
-        const int t = b - ntask - ncol;
+    } else if (b < e4) {
+        const int t = b - e3;
         if (ntask > 0) wait_list(wlist + wstart[ncol + t], wstart[ncol + t + 1] - wstart[ncol + t], tflags, scal);
         const int32_t* rec = trsm + 2 * t;
         trsm_body(S, ld, rec, dinv, flags + rec[0], scal, smem, progressive != 0);
+    } else if (b < e5) {
+        trtri_body(S, ld, prev[b - e4], dinv, linv, smem);
     } else {
-        trtri_body(S, ld, prev[b - ntask - ncol - ntrsm], dinv, linv, smem);
+        syrk_body(S, ld, tasks + Sched::SYRK_REC * (b - e5 + ndiag + npanel), src, P, comb, cnt, tflags, smem);
     }
 }
 
@@ -1280,9 +1285,10 @@ int launch_cholesky(Ctx& c) {
             // one launch: [U's updates of this level's diagonal blocks][potrf][U's other updates]
             // [panel solves][inverses of the previous level's blocks]; U = the previous level (merged)
             k_panel<<<(unsigned)(W.ncol + W.ntrsm + nprev + (U ? U->ntask : 0)), POTRF_THREADS, PANEL_LDS, c.stream>>>(
-                c.d_S, ld, c.d_sched + W.cols, W.ncol, c.d_sched + W.trsm, W.ntrsm, prev, c.d_dinv, c.d_linv, c.d_scal,
-                c.d_flags, (int)c.panel_progressive, U ? c.d_sched + U->tasks : nullptr, U ? U->ntask : 0,
-                U ? U->ndiag : 0, U ? c.d_sched + U->src : nullptr, c.d_P, U ? c.d_sched + U->comb : nullptr,
+                c.d_S, ld, c.d_sched + W.cols, W.ncol, c.d_sched + W.trsm, W.ntrsm, prev, nprev, c.d_dinv, c.d_linv,
+                c.d_scal, c.d_flags, (int)c.panel_progressive, U ? c.d_sched + U->tasks : nullptr, U ? U->ntask : 0,
+                U ? U->ndiag : 0, U ? U->npanel : 0, U ? c.d_sched + U->src : nullptr, c.d_P,
+                U ? c.d_sched + U->comb : nullptr,
                 U ? c.d_counters + U->cbase : nullptr, c.d_tflags, c.d_sched + W.wstart, c.d_sched + W.wlist);
         } else {
             k_potrf128<false><<<(unsigned)W.ncol, POTRF_THREADS, POTRF_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.cols,

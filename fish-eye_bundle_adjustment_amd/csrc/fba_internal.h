@@ -54,7 +54,8 @@ struct Sched {
         int64_t cols = 0, trsm = 0, tasks = 0, src = 0, comb = 0;  // offsets
         int ncol = 0, ntrsm = 0, ntask = 0, ncomb = 0;
         int cbase = 0;            // first arrival counter of the level's split targets (k_syrk_multi)
-        int ndiag = 0;            // the level's first ndiag tasks update next-level diagonal blocks
+        int ndiag = 0;            // the level's first ndiag tasks update next-level diagonal blocks,
+        int npanel = 0;           // the next npanel next-level panel blocks, the rest later levels' blocks
         int64_t wstart = 0, wlist = 0;  // merged launch: wait lists (flags of the previous level's
                                         // updates) of this level's potrf columns then panel halves
         double flops = 0.0;       // trailing-update flops of the level (kernel probe)

@@ -435,8 +435,11 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
             if (a.s1 - a.s0 != b.s1 - b.s0) return a.s1 - a.s0 > b.s1 - b.s0;
             return a.j != b.j ? a.j < b.j : a.i < b.i;
         });
-        W.ndiag = 0;
-        for (auto& t : tasks) W.ndiag += t.rank == 0 ? 1 : 0;
+        W.ndiag = W.npanel = 0;
+        for (auto& t : tasks) {
+            W.ndiag += t.rank == 0 ? 1 : 0;
+            W.npanel += t.rank == 1 ? 1 : 0;
+        }
         W.src = at();
         buf.insert(buf.end(), src.begin(), src.end());
         W.tasks = at();
