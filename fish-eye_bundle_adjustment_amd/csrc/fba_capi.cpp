@@ -554,7 +554,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         (rc = dalloc(&c->d_ipart, (size_t)A.n_ik * (27 + 6 * L.cw))) ||
         (rc = dalloc(&c->d_cpart, (size_t)c->n_chunks * npk)) ||
         (rc = dalloc(&c->d_cseg, (size_t)std::max(L.n_cam, 1) * 64 * npk)) ||
-        (rc = dalloc(&c->d_bscr, (size_t)(32 * 14 + 16 * 120))) ||  // k_border_weights / k_border_gram segments
+        (rc = dalloc(&c->d_bscr, (size_t)(32 * 14 + 16 * 120 + 16))) ||  // k_border_weights / k_border_gram segments, combine coefficients
         (rc = dalloc(&c->d_S, (size_t)(L.n_pad + NB) * L.ld)) ||
         (rc = dalloc(&c->d_P, (size_t)std::max(c->sched.n_scratch, 1) * 4096)) || (rc = dalloc(&c->d_X, (size_t)L.n_pad)) ||
         (rc = dalloc(&c->d_dinv, (size_t)(L.n_pad / NB) * 8 * 256)) ||

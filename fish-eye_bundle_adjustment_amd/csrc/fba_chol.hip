@@ -823,7 +823,7 @@ __global__ __launch_bounds__(256) void k_border_gram(const double* __restrict__ 
 // [[A'A - I, A'B], [B'A, B'B]] [z; k] = -[A'y; B'y] (14x14, partial pivoting, wave 0 alone) and forms
 // u = y + A z + B k on its 256 entries of the RHS row (derivation in fba_kernels.hip, border section)
 __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, int64_t ld, int64_t n_pad,
-                                                        const double* __restrict__ gpart) {
+                                                        const double* __restrict__ gpart, double* __restrict__ coef_out) {
     __shared__ double g[15][15];
     __shared__ double H[14][16];
     __shared__ double coef[14];
@@ -882,6 +882,10 @@ __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, 
 #undef WSYNC
     }
     __syncthreads();
+    if (coef_out) {  // one workgroup: the 14 coefficients only (k_bwd_flow applies them)
+        if (tid < 14) coef_out[tid] = coef[tid];
+        return;
+    }
     const int64_t i = (int64_t)blockIdx.x * 256 + tid;
     if (i < n_pad) {
         double* yw = S + n_pad * ld;
@@ -1120,7 +1124,8 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
                                                   double* __restrict__ X,
                                                   double* __restrict__ delta, int64_t u_c,
                                                   const int32_t* __restrict__ src_start, const int32_t* __restrict__ src,
-                                                  unsigned* __restrict__ flags, double* __restrict__ scal) {
+                                                  unsigned* __restrict__ flags, double* __restrict__ scal,
+                                                  const double* __restrict__ coef) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* Li = smem;              // [128][128] Linv_j, or L_jj for a root column
     double* Dt = Li + CB * CB;      // [8][16][16] the leaf inverses of a root column
@@ -1180,7 +1185,12 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
     __syncthreads();
     if (tid < CB) {
         const double s = (red[tid] + red[128 + tid]) + (red[256 + tid] + red[384 + tid]);
-        ys[tid] = S[n_pad * ld + (int64_t)j * CB + tid] - s;
+        // u_j = y_j + F_j c (the inner-constraint combine, coefficients from k_border_combine), then - s
+        double u = S[n_pad * ld + (int64_t)j * CB + tid];
+        if (coef)
+#pragma unroll
+            for (int m = 0; m < 14; ++m) u += S[(n_pad + 1 + m) * ld + (int64_t)j * CB + tid] * coef[m];
+        ys[tid] = u - s;
     }
     __syncthreads();
     if (root) {
@@ -1348,19 +1358,24 @@ int launch_trtri_last(Ctx& c) {
 int launch_backward(Ctx& c) {
     int rc;
     const int64_t ld = c.L.ld;
+    const Sched& s = c.sched;
+    const int64_t nb = c.L.n_pad / CB;
+    const bool flow = c.bwd_flow && nb <= c.n_cu;
+    double* coef = c.d_bscr + 32 * 14 + 16 * 120;
     if (c.set.inner_constraints) {
         // (running k_trtri128 on a forked stream concurrently with these two measured slower: a forked
         // iteration graph adds cross-queue waits to every launch of the Cholesky chain)
         k_border_gram<<<GRAM_SEG, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_bscr + 32 * 14);
-        k_border_combine<<<(unsigned)((c.L.n_pad + 255) / 256), 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad,
-                                                                                   c.d_bscr + 32 * 14);
+        if (flow)  // the 14 coefficients only; k_bwd_flow applies them to its block
+            k_border_combine<<<1, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_bscr + 32 * 14, coef);
+        else
+            k_border_combine<<<(unsigned)((c.L.n_pad + 255) / 256), 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad,
+                                                                                       c.d_bscr + 32 * 14, nullptr);
     }
-    const Sched& s = c.sched;
-    const int64_t nb = c.L.n_pad / CB;
-    if (c.bwd_flow && nb <= c.n_cu) {  // one launch, every workgroup resident; roots solve by substitution
+    if (flow) {  // one launch, every workgroup resident; roots solve by substitution
         k_bwd_flow<<<(unsigned)nb, 256, BWD_LDS, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_linv, c.d_dinv, c.d_X, c.d_delta, c.L.u_c,
                                                            c.d_sched + s.bf_start, c.d_sched + s.bf_src, c.d_bflags,
-                                                           c.d_scal);
+                                                           c.d_scal, c.set.inner_constraints ? coef : nullptr);
         FBA_HIP(hipGetLastError());
         return FBA_OK;
     }
