@@ -114,7 +114,7 @@ int main() {
         const float tt = time_us([&] { k_trsm128<<<(unsigned)(2 * nt), 256, TRSM_LDS>>>(dS, ld, dl + 2, dinv); }, 10);
         printf("k_trsm128 %2d blocks  %8.2f us\n", nt, tt);
     }
-    const float ts1 = time_us([&] { k_syrk_multi<<<1, 256>>>(dS, ld, dl + 400, dl + 410, nullptr); }, 10);
+    const float ts1 = time_us([&] { k_syrk_multi<<<1, 256>>>(dS, ld, dl + 400, dl + 410, nullptr, nullptr, nullptr); }, 10);
     printf("k_syrk_multi 1 quarter %7.2f us (K = 128)\n", ts1);
     const float te = time_us([&] { k_neg_copy<<<1, 64>>>(dinv, dinv + 64, 1); }, 20);
     printf("empty-ish launch      %8.2f us\n", te);
