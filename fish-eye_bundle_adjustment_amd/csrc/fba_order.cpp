@@ -14,10 +14,12 @@
 // Trailing-update targets that several columns of a level update are summed in one workgroup in
 // ascending column order, so results do not depend on the schedule (no floating-point atomics).
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <deque>
+#include <functional>
 #include <map>
 #include <tuple>
 
@@ -172,42 +174,110 @@ class Dissection {
             nn = std::sqrt(nn);
             for (int a = 0; a < 3; ++a) ax[a] = y[a] / nn;
         }
-        std::vector<std::pair<double, int32_t>> pr(n);
-        for (size_t q = 0; q < n; ++q) {
-            const int32_t v = verts[q];
-            double x = 0.0;
-            for (int d = 0; d < 3; ++d) x += (pos_[3 * v + d] - mu[d]) * ax[d];
-            pr[q] = {x, v};
-        }
-        std::sort(pr.begin(), pr.end());
-        for (size_t q = 0; q < n; ++q) lev_[pr[q].second] = (int)q;  // rank along the axis
-        size_t best_cut = n / 2, best_sep = n + 1;
-        bool best_left = true;
-        for (int f = 40; f <= 60; f += 2) {
-            const size_t cut = n * f / 100;
-            if (cut == 0 || cut >= n) continue;
-            size_t sl = 0, sr = 0;  // left vertices with a right neighbour, and vice versa
+        // candidate cut directions: the principal axis, the coordinate axes of the plane and the two
+        // diagonals (a near-square block has no meaningful principal axis; a diagonal cut is ~1.4x longer)
+        std::vector<std::array<double, 3>> axes{{ax[0], ax[1], ax[2]}, {1, 0, 0}, {0, 1, 0},
+                                                {0.7071067811865476, 0.7071067811865476, 0},
+                                                {0.7071067811865476, -0.7071067811865476, 0}};
+        // separator of a cut (vertices of rank < cut on the left): a minimum vertex cover of the cut
+        // edges (Koenig, from a maximum matching of the bipartite graph left- x right-boundary), never
+        // larger than either side's boundary; returns the cover as a flag per vertex of `sep`
+        std::vector<int> slot(g_.n, -1);
+        auto cover = [&](const std::vector<std::pair<double, int32_t>>& ord, size_t cut, std::vector<int32_t>& sep) {
+            std::vector<int32_t> lb, rb;
             for (size_t q = 0; q < n; ++q) {
-                const int32_t v = pr[q].second;
+                const int32_t v = ord[q].second;
                 const bool left = q < cut;
-                for (int32_t e = g_.start[v]; e < g_.start[v + 1]; ++e) {
+                bool cross = false;
+                for (int32_t e = g_.start[v]; e < g_.start[v + 1] && !cross; ++e) {
                     const int w = g_.adj[e];
-                    if (tag_[w] != t) continue;
-                    if (((size_t)lev_[w] < cut) != left) { (left ? sl : sr)++; break; }
+                    cross = tag_[w] == t && (((size_t)lev_[w] < cut) != left);
+                }
+                if (cross) (left ? lb : rb).push_back(v);
+            }
+            for (size_t a = 0; a < lb.size(); ++a) slot[lb[a]] = (int)a;
+            for (size_t b = 0; b < rb.size(); ++b) slot[rb[b]] = (int)b;
+            std::vector<std::vector<int>> nbr(lb.size());
+            for (size_t a = 0; a < lb.size(); ++a)
+                for (int32_t e = g_.start[lb[a]]; e < g_.start[lb[a] + 1]; ++e) {
+                    const int w = g_.adj[e];
+                    if (tag_[w] == t && (size_t)lev_[w] >= cut) nbr[a].push_back(slot[w]);
+                }
+            std::vector<int> ml(lb.size(), -1), mr(rb.size(), -1), seen(rb.size(), -1);
+            std::function<bool(int, int)> augment = [&](int a, int stamp) -> bool {
+                for (int b : nbr[a]) {
+                    if (seen[b] == stamp) continue;
+                    seen[b] = stamp;
+                    if (mr[b] < 0 || augment(mr[b], stamp)) { ml[a] = b; mr[b] = a; return true; }
+                }
+                return false;
+            };
+            for (size_t a = 0; a < lb.size(); ++a) augment((int)a, (int)a);
+            // Z = reachable from unmatched left vertices by alternating paths; cover = (L \ Z) + (R & Z)
+            std::vector<char> zl(lb.size(), 0), zr(rb.size(), 0);
+            std::vector<int> stack;
+            for (size_t a = 0; a < lb.size(); ++a)
+                if (ml[a] < 0) { zl[a] = 1; stack.push_back((int)a); }
+            while (!stack.empty()) {
+                const int a = stack.back();
+                stack.pop_back();
+                for (int b : nbr[a]) {
+                    if (zr[b]) continue;
+                    zr[b] = 1;
+                    if (mr[b] >= 0 && !zl[mr[b]]) { zl[mr[b]] = 1; stack.push_back(mr[b]); }
                 }
             }
-            if (std::min(sl, sr) < best_sep) { best_sep = std::min(sl, sr); best_cut = cut; best_left = sl <= sr; }
-        }
-        for (size_t q = 0; q < n; ++q) {
-            const int32_t v = pr[q].second;
-            const bool left = q < best_cut;
-            bool cross = false;
-            for (int32_t e = g_.start[v]; e < g_.start[v + 1] && !cross; ++e) {
-                const int w = g_.adj[e];
-                cross = tag_[w] == t && (((size_t)lev_[w] < best_cut) != left);
+            sep.clear();
+            for (size_t a = 0; a < lb.size(); ++a)
+                if (!zl[a]) sep.push_back(lb[a]);
+            for (size_t b = 0; b < rb.size(); ++b)
+                if (zr[b]) sep.push_back(rb[b]);
+            for (int32_t v : lb) slot[v] = -1;
+            for (int32_t v : rb) slot[v] = -1;
+        };
+        std::vector<std::pair<double, int32_t>> pr(n), best_pr;
+        std::vector<int32_t> best_sep_v;
+        size_t best_cut = n / 2, best_sep = n + 1;
+        for (const auto& a3 : axes) {
+            for (size_t q = 0; q < n; ++q) {
+                const int32_t v = verts[q];
+                double x = 0.0;
+                for (int d = 0; d < 3; ++d) x += (pos_[3 * v + d] - mu[d]) * a3[d];
+                pr[q] = {x, v};
             }
-            if (cross && left == best_left) S.push_back(v);
-            else (left ? A : B).push_back(v);
+            std::sort(pr.begin(), pr.end());
+            for (size_t q = 0; q < n; ++q) lev_[pr[q].second] = (int)q;  // rank along the axis
+            // the cut is chosen by the smaller one-sided boundary (choosing by the cover size measured
+            // worse: it favours unbalanced cuts and deeper trees); its separator is then the cover
+            for (int f = 40; f <= 60; f += 2) {
+                const size_t cut = n * f / 100;
+                if (cut == 0 || cut >= n) continue;
+                size_t sl = 0, sr = 0;  // left vertices with a right neighbour, and vice versa
+                for (size_t q = 0; q < n; ++q) {
+                    const int32_t v = pr[q].second;
+                    const bool left = q < cut;
+                    for (int32_t e = g_.start[v]; e < g_.start[v + 1]; ++e) {
+                        const int w = g_.adj[e];
+                        if (tag_[w] != t) continue;
+                        if (((size_t)lev_[w] < cut) != left) { (left ? sl : sr)++; break; }
+                    }
+                }
+                if (std::min(sl, sr) < best_sep) {
+                    best_sep = std::min(sl, sr);
+                    best_cut = cut;
+                    best_pr = pr;
+                }
+            }
+        }
+        if (best_pr.empty()) return false;
+        for (size_t q = 0; q < n; ++q) lev_[best_pr[q].second] = (int)q;
+        cover(best_pr, best_cut, best_sep_v);
+        std::vector<char> insep(g_.n, 0);
+        for (int32_t v : best_sep_v) insep[v] = 1;
+        for (size_t q = 0; q < n; ++q) {
+            const int32_t v = best_pr[q].second;
+            if (insep[v]) S.push_back(v);
+            else (q < best_cut ? A : B).push_back(v);
         }
         clear_lev(verts);
         std::sort(A.begin(), A.end());
@@ -287,8 +357,9 @@ class Dissection {
 
 std::vector<int32_t> camera_order(const fba_problem* p) {
     const char* le = getenv("FBA_ND_LEAF");
-    // levels at configs 3 / 4 / 5: leaf 100 -> 9 / 17 / 33, 150 -> 8 / 18 / 35, 250 -> - / 20 / 36, 400 -> - / 22 / 40;
-    // config 4 measured 726 iter/s at 100 and 120, 711 at 150, 708 at 75
+    // levels at configs 3 / 4 / 5 (cuts along the best of five directions, minimum-vertex-cover
+    // separators): leaf 100 -> 7 / 16 / 31, 150 -> 7 / 17 / 31; config 4 measured 808-812 iter/s at 100,
+    // 804 at 120, 776-778 at 150
     int leaf = le ? atoi(le) : 100;
     if (leaf <= 0) leaf = p->n_img;  // 0: reverse Cuthill-McKee only
     Graph g = covis_graph(p);
