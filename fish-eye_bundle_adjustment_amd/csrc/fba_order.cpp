@@ -64,7 +64,17 @@ class Dissection {
   public:
     // pos: image centres (3 per image) for coordinate bisection, or empty (level-structure bisection)
     Dissection(const Graph& g, int leaf, std::vector<double> pos)
-        : g_(g), leaf_(leaf), pos_(std::move(pos)), tag_(g.n, -1), lev_(g.n, -1), deg_(g.n, 0) {}
+        : g_(g), leaf_(leaf), pos_(std::move(pos)), tag_(g.n, -1), lev_(g.n, -1), deg_(g.n, 0) {
+        // the split fractions tried by a bisection, in percent (FBA_ND_FRAC="lo,hi,step")
+        if (const char* fr = getenv("FBA_ND_FRAC")) {
+            int a = 0, b = 0, c = 0;
+            if (sscanf(fr, "%d,%d,%d", &a, &b, &c) == 3 && a > 0 && b < 100 && a <= b && c > 0) {
+                frac_lo_ = a;
+                frac_hi_ = b;
+                frac_step_ = c;
+            }
+        }
+    }
 
     // order the vertices (all of one tag), appending to out; -1 entries are padding slots
     void nd(std::vector<int32_t> verts, std::vector<int32_t>& out) {
@@ -89,6 +99,7 @@ class Dissection {
     int leaf_;
     std::vector<double> pos_;
     int next_ = 0;
+    int frac_lo_ = 45, frac_hi_ = 55, frac_step_ = 1;
     std::vector<int> tag_, lev_, deg_;
 
     int mark(const std::vector<int32_t>& verts) {
@@ -249,7 +260,7 @@ class Dissection {
             for (size_t q = 0; q < n; ++q) lev_[pr[q].second] = (int)q;  // rank along the axis
             // the cut is chosen by the smaller one-sided boundary (choosing by the cover size measured
             // worse: it favours unbalanced cuts and deeper trees); its separator is then the cover
-            for (int f = 40; f <= 60; f += 2) {
+            for (int f = frac_lo_; f <= frac_hi_; f += frac_step_) {
                 const size_t cut = n * f / 100;
                 if (cut == 0 || cut >= n) continue;
                 size_t sl = 0, sr = 0;  // left vertices with a right neighbour, and vice versa
