@@ -637,10 +637,13 @@ static int run_graph(Ctx* c, int which, F&& body) {
 static int accumulate_body(Ctx* c) {
     int rc;
     mark(c, 0);
-    if ((rc = launch_params_zero(*c, c->d_xlin))) return rc;  // tables + the linearisation point + zero S
+    // tables + the linearisation point; S's pattern is zeroed by k_lin_reduce's tail workgroups
+    // (FBA_ZERO_HEAD=1: by k_params_zero ahead of it, the previous arrangement)
+    static const bool zero_head = getenv("FBA_ZERO_HEAD") && atoi(getenv("FBA_ZERO_HEAD"));
+    if ((rc = zero_head ? launch_params_zero(*c, c->d_xlin) : launch_params(*c, nullptr, c->d_xlin))) return rc;
     mark(c, 1);
     mark(c, 2);
-    if ((rc = launch_accumulate(*c, true))) return rc;
+    if ((rc = launch_accumulate(*c, zero_head))) return rc;
     if (c->d_lrprof) {  // FBA_LR_PROFILE: per-phase averages of k_lin_reduce (us)
         std::vector<uint64_t> tp(8 * c->n_chunks);
         FBA_HIP(hipMemcpyAsync(tp.data(), c->d_lrprof, sizeof(uint64_t) * tp.size(), hipMemcpyDeviceToHost, c->stream));

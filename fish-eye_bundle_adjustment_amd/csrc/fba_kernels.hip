@@ -417,9 +417,22 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     const int32_t* __restrict__ chunk_obs, const int32_t* __restrict__ chunk_pt, const int32_t* __restrict__ lp_start,
     const int32_t* __restrict__ A, const AccPlan plan, double* __restrict__ WT, double* __restrict__ PT,
     double* __restrict__ ppart, double* __restrict__ ipart, double* __restrict__ cpart, int64_t u_c, int type,
-    int cam_stride, unsigned eop_mask, unsigned cam_mask, double px, double py, uint64_t* __restrict__ tprof, int dbg) {
+    int cam_stride, unsigned eop_mask, unsigned cam_mask, double px, double py, uint64_t* __restrict__ tprof, int dbg,
+    int n_chunks, double* __restrict__ S, int64_t ld, const int32_t* __restrict__ zblk) {
     using LY = Lay<NK>;
     using R_ = LR<NK>;
+    if ((int)blockIdx.x >= n_chunks) {  // tail workgroups: zero one 128x128 block of the factor's pattern
+        // (Sched::zero) each; they run on the CUs the last round of chunks leaves idle
+        const int b = blockIdx.x - n_chunks;
+        const int64_t r0 = (int64_t)zblk[2 * b] * NB, c0 = (int64_t)zblk[2 * b + 1] * NB;
+        const double2 z = {0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < NB * NB / 2 / LR_THREADS; ++q) {
+            const int i = threadIdx.x + LR_THREADS * q, r = i >> 6, cc = (i & 63) * 2;
+            *reinterpret_cast<double2*>(S + (r0 + r) * ld + c0 + cc) = z;
+        }
+        return;
+    }
     // optional phase timestamps (FBA_LR_PROFILE): 100 MHz wall clock at the phase boundaries
     auto stamp = [&](int i) {
         if (tprof && threadIdx.x == 0) tprof[(int64_t)blockIdx.x * 8 + i] = wall_clock64();
@@ -1247,17 +1260,20 @@ __global__ __launch_bounds__(256) void k_zero_blocks(double* __restrict__ S, int
 
 int launch_accumulate(Ctx& c, bool zeroed) {
     const Layout& L = c.L;
-    if (c.sched.nzero > 0 && !zeroed)
+    // the pattern is zeroed by tail workgroups of k_lin_reduce (it does not touch S), unless done already
+    const int ztail = (zeroed || c.n_chunks == 0) ? 0 : c.sched.nzero;
+    if (c.sched.nzero > 0 && !zeroed && c.n_chunks == 0)
         k_zero_blocks<<<(unsigned)(8 * c.sched.nzero), 256, 0, c.stream>>>(c.d_S, L.ld, c.d_sched + c.sched.zero);
     if (c.n_chunks == 0) return FBA_OK;
     const unsigned em = eop_mask(c.set), cm = cam_mask(c.set, c.L.nk);
     const double px = px_of(c), py = py_of(c);
 #define ACC(NKV)                                                                                                  \
-    k_lin_reduce<NKV><<<(unsigned)c.n_chunks, LR_THREADS, LR<NKV>::LDS, c.stream>>>(                              \
+    k_lin_reduce<NKV><<<(unsigned)(c.n_chunks + ztail), LR_THREADS, LR<NKV>::LDS, c.stream>>>(                    \
         c.d_xy, c.d_img, c.d_cam, c.d_pt, c.d_lp_tie, c.d_ctl, c.d_xfull, c.d_img_tab, c.d_cam_tab,                \
         c.d_chunk_obs, c.d_chunk_pt, c.d_lp_start, c.d_acc, c.acc, c.d_WT, c.d_pt_tab, c.d_ppart, c.d_ipart,       \
         c.d_cpart, c.L.u_c, c.set.type, c.cam_tab_stride, em, cm, px, py, c.d_lrprof,                              \
-        c.d_lrprof && getenv("FBA_LR_SKIP") ? atoi(getenv("FBA_LR_SKIP")) : 0);                            \
+        c.d_lrprof && getenv("FBA_LR_SKIP") ? atoi(getenv("FBA_LR_SKIP")) : 0, (int)c.n_chunks, c.d_S, L.ld,       \
+        c.d_sched + c.sched.zero);                                                                                \
     {                                                                                                             \
         const int npb = (int)((c.n_pairs + 3) / 4), nib = (L.n_img + 1) / 2, ncb = (L.n_cam * CAM_SEG + 1) / 2;   \
         k_red_blocks<NKV><<<(unsigned)(npb + nib + ncb), 256, 0, c.stream>>>(                                     \
