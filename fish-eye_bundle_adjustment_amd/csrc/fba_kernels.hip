@@ -760,10 +760,20 @@ __device__ __forceinline__ void red_pairs_body(int blk, const double* __restrict
     const int64_t pr = (int64_t)blk * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (pr >= n_pairs || lane >= 36) return;
-    // the partials in chunk order, 4 loads in flight (fixed association: ((s + p0) + p1) + ...)
+    // the partials in chunk order, 8 (then 4) loads in flight (fixed association: ((s + p0) + p1) + ...)
     const int q0 = A[plan.rp_start + pr], q1 = A[plan.rp_start + pr + 1];
     double s = 0.0;
     int q = q0;
+    for (; q + 8 <= q1; q += 8) {
+        int id[8];
+        double p[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) id[j] = A[plan.rp_list + q + j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p[j] = ppart[(int64_t)id[j] * 36 + lane];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += p[j];
+    }
     for (; q + 4 <= q1; q += 4) {
         const int i0 = A[plan.rp_list + q], i1 = A[plan.rp_list + q + 1], i2 = A[plan.rp_list + q + 2],
                   i3 = A[plan.rp_list + q + 3];
@@ -785,8 +795,21 @@ __device__ __forceinline__ void red_images_body(int e, int q, const double* __re
     if (e >= n_img) return;
     const int r0 = A[plan.ri_start + e], r1 = A[plan.ri_start + e + 1];
     if (r0 == r1 || q >= NIMG) return;
+    // the partials in chunk order with 8 loads in flight; same association as the plain running sum
+    // (((s + p0) + p1) + ...), so the result does not depend on the batching
     double s = 0.0;
-    for (int x = r0; x < r1; ++x) s += ipart[(int64_t)A[plan.ri_list + x] * NIMG + q];
+    int x = r0;
+    for (; x + 8 <= r1; x += 8) {
+        int id[8];
+        double p[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) id[j] = A[plan.ri_list + x + j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p[j] = ipart[(int64_t)id[j] * NIMG + q];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += p[j];
+    }
+    for (; x < r1; ++x) s += ipart[(int64_t)A[plan.ri_list + x] * NIMG + q];
     if (q < 21) {
         S[(6 * (int64_t)e + c_tri_a[q]) * ld + 6 * e + c_tri_b[q]] = s;
     } else if (q < 27) {
