@@ -825,7 +825,6 @@ __global__ __launch_bounds__(256) void k_border_gram(const double* __restrict__ 
 __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, int64_t ld, int64_t n_pad,
                                                         const double* __restrict__ gpart, double* __restrict__ coef_out) {
     __shared__ double g[15][15];
-    __shared__ double H[14][16];
     __shared__ double coef[14];
     const int tid = threadIdx.x;
     if (tid < 120) {
@@ -842,16 +841,22 @@ __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, 
     }
     __syncthreads();
     if (tid < 64) {
-        // wave 0: lanes 0..13 own the rows of H; LDS traffic ordered by lgkmcnt waits in one wave
-#define WSYNC() do { __builtin_amdgcn_s_waitcnt(0xC07F); __builtin_amdgcn_wave_barrier(); } while (0)
-        for (int i = tid; i < 14 * 15; i += 64) {
-            const int r = i / 15, q = i % 15;
-            H[r][q] = (q < 14) ? g[1 + r][1 + q] - ((r == q && r < 7) ? 1.0 : 0.0) : -g[1 + r][0];
+        // wave 0: lane r < 14 holds row r of the augmented H = [H | rhs] in registers; pivot rows move
+        // by cross-lane shuffles (no LDS round trips on the 14-column chain).  The arithmetic and its
+        // order are those of the plain row-by-row elimination and back substitution.
+        double h[15];
+        if (tid < 14) {
+#pragma unroll
+            for (int q = 0; q < 14; ++q) h[q] = g[1 + tid][1 + q] - ((tid == q && tid < 7) ? 1.0 : 0.0);
+            h[14] = -g[1 + tid][0];
+        } else {
+#pragma unroll
+            for (int q = 0; q < 15; ++q) h[q] = 0.0;
         }
-        WSYNC();
+#pragma unroll
         for (int col = 0; col < 14; ++col) {
             // pivot: the first row of maximal |H[r][col]|, r >= col (wave reduction, ties to the lower row)
-            double v = (tid >= col && tid < 14) ? fabs(H[tid][col]) : -1.0;
+            double v = (tid >= col && tid < 14) ? fabs(h[col]) : -1.0;
             int p = tid;
 #pragma unroll
             for (int w = 1; w < 16; w <<= 1) {
@@ -860,26 +865,35 @@ __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, 
                 if (ov > v || (ov == v && op < p)) { v = ov; p = op; }
             }
             p = __shfl(p, 0, 64);
-            if (p != col && tid < 15) {
-                const double t = H[col][tid];
-                H[col][tid] = H[p][tid];
-                H[p][tid] = t;
+            double piv[15];
+#pragma unroll
+            for (int q = col; q < 15; ++q) {
+                const double hp = __shfl(h[q], p, 64), hc = __shfl(h[q], col, 64);
+                if (tid == p) h[q] = hc;     // row swap (a no-op when p == col)
+                if (tid == col) h[q] = hp;
+                piv[q] = hp;                 // the pivot row after the swap
             }
-            WSYNC();
-            const double f = (tid > col && tid < 14) ? H[tid][col] / H[col][col] : 0.0;
-            WSYNC();
-            if (tid > col && tid < 14)
-                for (int q = col; q < 15; ++q) H[tid][q] -= f * H[col][q];
-            WSYNC();
-        }
-        if (tid == 0) {
-            for (int r = 13; r >= 0; --r) {
-                double v = H[r][14];
-                for (int q = r + 1; q < 14; ++q) v -= H[r][q] * coef[q];
-                coef[r] = v / H[r][r];
+            if (tid > col && tid < 14) {
+                const double f = h[col] / piv[col];
+#pragma unroll
+                for (int q = col; q < 15; ++q) h[q] -= f * piv[q];
             }
         }
-#undef WSYNC
+        // back substitution, rows 13..0, each row's sum in ascending column order
+        double c[14];
+#pragma unroll
+        for (int r = 13; r >= 0; --r) {
+            double v = h[14];
+#pragma unroll
+            for (int q = r + 1; q < 14; ++q) v -= h[q] * c[q];
+            c[r] = __shfl(v / h[r], r, 64);
+        }
+        if (tid < 14) {
+            double mine = c[0];
+#pragma unroll
+            for (int q = 1; q < 14; ++q) mine = (tid == q) ? c[q] : mine;
+            coef[tid] = mine;
+        }
     }
     __syncthreads();
     if (coef_out) {  // one workgroup: the 14 coefficients only (k_bwd_flow applies them)
