@@ -24,7 +24,7 @@ EXPORTS = (
     "fba_accumulate", "fba_reduce_buffer", "fba_synchronize", "fba_solve_update", "fba_solve_update_async",
     "fba_deltasum_device", "fba_solve_finish", "fba_step", "fba_adjust",
     "fba_residuals", "fba_finish_stats", "fba_covariance", "fba_last_timings", "fba_set_timing", "fba_set_probe",
-    "fba_probe_stats",
+    "fba_probe_stats", "fba_test_border_solve",
 )
 
 
@@ -86,6 +86,7 @@ def _load():
         "fba_set_timing": ([P, I], C.c_int),
         "fba_set_probe": ([P, I], C.c_int),
         "fba_probe_stats": ([P, P], C.c_int),
+        "fba_test_border_solve": ([I, P, P], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

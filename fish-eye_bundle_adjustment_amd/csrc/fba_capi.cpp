@@ -1107,6 +1107,11 @@ int fba_probe_stats(fba_ctx* ctx, double* out) {
     return FBA_OK;
 }
 
+int fba_test_border_solve(int32_t device, const double* gram, double* coef) {
+    if (!gram || !coef) { set_error("NULL argument"); return FBA_ERR_ARG; }
+    return border_solve_selftest(device, gram, coef);
+}
+
 int fba_set_timing(fba_ctx* ctx, int32_t enabled) {
     Ctx* c = reinterpret_cast<Ctx*>(ctx);
     if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }

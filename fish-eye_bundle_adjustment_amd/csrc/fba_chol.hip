@@ -856,8 +856,10 @@ __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, 
 #pragma unroll
         for (int col = 0; col < 14; ++col) {
             // pivot: the first row of maximal |H[r][col]|, r >= col (wave reduction, ties to the lower row)
+            // lanes outside [col, 14) seed p = col, so an all-NaN column keeps the pivot at col (as the
+            // serial search does) instead of pulling in a finished row
             double v = (tid >= col && tid < 14) ? fabs(h[col]) : -1.0;
-            int p = tid;
+            int p = (tid >= col && tid < 14) ? tid : col;
 #pragma unroll
             for (int w = 1; w < 16; w <<= 1) {
                 const double ov = __shfl_xor(v, w, 64);
@@ -1349,6 +1351,28 @@ int launch_backward_rows(Ctx& c, int row0, int nrows, double* X) {
                 c.d_sched + B.tgts, c.d_sched + B.src_start, c.d_sched + B.src);
         }
     FBA_HIP(hipGetLastError());
+    return FBA_OK;
+}
+
+// test hook (fba_test_border_solve): k_border_combine's 14x14 solve for a given 15x15 Gram matrix,
+// placed in Gram segment 0 (the other segments zero)
+int border_solve_selftest(int device, const double* gram, double* coef) {
+    FBA_HIP(hipSetDevice(device));
+    std::vector<double> gp((size_t)GRAM_SEG * 120, 0.0);
+    for (int e = 0, a = 0; a < 15; ++a)
+        for (int b = a; b < 15; ++b, ++e) gp[e] = gram[a * 15 + b];
+    double *dg = nullptr, *dc = nullptr;
+    FBA_HIP(hipMalloc((void**)&dg, gp.size() * sizeof(double)));
+    hipError_t e1 = hipMalloc((void**)&dc, 16 * sizeof(double));
+    if (e1 == hipSuccess) e1 = hipMemcpy(dg, gp.data(), gp.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (e1 == hipSuccess) {
+        k_border_combine<<<1, 256>>>(nullptr, 0, 0, dg, dc);
+        e1 = hipGetLastError();
+    }
+    if (e1 == hipSuccess) e1 = hipMemcpy(coef, dc, 14 * sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipFree(dg);
+    if (dc) (void)hipFree(dc);
+    FBA_HIP(e1);
     return FBA_OK;
 }
 

@@ -251,5 +251,6 @@ int launch_residuals(Ctx& c);    // v per obs, partial sums
 int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, const int32_t* d_islot,
                       const int32_t* d_icam, int n_iblk);  // post-fit covariance (fba_cov.hip)
 int launch_dense_awg(Ctx& c, double* dA, double* dG, const int64_t* d_map, int64_t n_rows, int64_t u_ref);
+int border_solve_selftest(int device, const double* gram, double* coef);  // fba_test_border_solve
 
 }  // namespace fba

@@ -422,7 +422,10 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     using LY = Lay<NK>;
     using R_ = LR<NK>;
     if ((int)blockIdx.x >= n_chunks) {  // tail workgroups: zero one 128x128 block of the factor's pattern
-        // (Sched::zero) each; they run on the CUs the last round of chunks leaves idle
+        // (Sched::zero) each; they run on the CUs the last round of chunks leaves idle.  They are
+        // launched with the chunk workgroups' dynamic LDS (LR<NK>::LDS) and thread count, so each takes
+        // a chunk-sized LDS allocation: a larger chunk footprint serialises them too.
+        static_assert(NB == 128 && (NB * NB / 2) % LR_THREADS == 0, "tail zeroing assumes 128x128 blocks");
         const int b = blockIdx.x - n_chunks;
         const int64_t r0 = (int64_t)zblk[2 * b] * NB, c0 = (int64_t)zblk[2 * b + 1] * NB;
         const double2 z = {0.0, 0.0};

@@ -201,6 +201,12 @@ int fba_set_timing(fba_ctx* ctx, int32_t enabled);
 int fba_set_probe(fba_ctx* ctx, int32_t enabled);
 int fba_probe_stats(fba_ctx* ctx, double* out /*[4]*/);
 
+/* Test hook (no reference counterpart): the 14x14 bordered solve of the inner-constraint combine
+ * (k_border_combine, one workgroup on `device`) for a given symmetric 15x15 Gram matrix of the
+ * forward-solved rows [y | A (7) | B (7)] (row-major): coef = [z; k] solving
+ * [[A'A - I, A'B], [B'A, B'B]] [z; k] = -[A'y; B'y]. */
+int fba_test_border_solve(int32_t device, const double* gram /*[225]*/, double* coef /*[14]*/);
+
 #ifdef __cplusplus
 }
 #endif

@@ -287,3 +287,37 @@ def test_batch_main_writes_reference_outputs(fba, oracle, tmp_path):
     cdo, _ = oracle.covariance(od, ro)
     xc = next(x for x in lines if x.startswith("Xc "))
     assert float(xc.split()[2]) == pytest.approx(np.sqrt(cdo[0]), abs=2e-5)
+
+
+def _border_gram(rng, n=200):
+    """A 15 x n stand-in for the forward-solved rows [y | A (7) | B (7)] and its Gram matrix."""
+    R = rng.standard_normal((15, n))
+    return R @ R.T
+
+
+def test_border_solve_matches_dense(fba):
+    """k_border_combine's in-register 14x14 solve (partial pivoting by wave shuffles) against a dense
+    solve of [[A'A - I, A'B], [B'A, B'B]] [z; k] = -[A'y; B'y] (the inner-constraint combine)."""
+    rng = np.random.default_rng(7)
+    for _ in range(3):
+        g = _border_gram(rng)
+        H = g[1:, 1:].copy()
+        H[np.arange(7), np.arange(7)] -= 1.0
+        ref = np.linalg.solve(H, -g[1:, 0])
+        coef = np.zeros(14)
+        fba.capi.check(fba.capi.lib.fba_test_border_solve(0, fba.capi.ptr(np.ascontiguousarray(g)),
+                                                          fba.capi.ptr(coef)))
+        np.testing.assert_allclose(coef, ref, rtol=1e-10, atol=1e-12 * np.abs(ref).max())
+
+
+def test_border_solve_nan_column_stays_local(fba):
+    """A NaN pivot column must not pull an already-finished row back into the elimination (the pivot
+    search keeps row `col` when no candidate compares): the solve returns without a hang and the NaN
+    shows up in the output rather than as silently wrong finite coefficients."""
+    rng = np.random.default_rng(8)
+    g = _border_gram(rng)
+    g[5, 5:] = np.nan
+    g[5:, 5] = np.nan
+    coef = np.zeros(14)
+    fba.capi.check(fba.capi.lib.fba_test_border_solve(0, fba.capi.ptr(np.ascontiguousarray(g)), fba.capi.ptr(coef)))
+    assert not np.isfinite(coef).all()
