@@ -155,31 +155,87 @@ __device__ __forceinline__ void fmac_bc(double& d, double s, double m, int l) {
     }
 }
 
+// d += s[lane l of this row] * (-m), one v_fmac_f64_dpp with a negated src1 (row_newbcast:l)
+__device__ __forceinline__ void fmac_bcn_first(double& d, double s, double m, int l) {
+    switch (l) {
+        case 1: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:1 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 2: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:2 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 3: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:3 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 4: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:4 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 5: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:5 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 6: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:6 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 7: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:7 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 8: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:8 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 9: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:9 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 10: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:10 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 11: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:11 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 12: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:12 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 13: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:13 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 14: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:14 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 15: asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:15 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        default: break;
+    }
+}
+__device__ __forceinline__ void fmac_bcn(double& d, double s, double m, int l) {
+    switch (l) {
+        case 1: asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:1 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 2: asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:2 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 3: asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:3 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 4: asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:4 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 5: asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:5 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 6: asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:6 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 7: asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:7 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 8: asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:8 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 9: asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:9 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 10: asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:10 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 11: asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:11 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 12: asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:12 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 13: asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:13 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 14: asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:14 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        case 15: asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:15 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(s), "v"(m)); break;
+        default: break;
+    }
+}
+
 // lane i (< 16) of a wave holds row i of a 16x16 SPD block in a[]; on return a[] holds row i of L
 // (lower part) and x[] COLUMN i of L^-1 (x[r] = (L^-1)[r][i]).  Every broadcast L[l][j] feeds both
 // the rank-1 update of the factor and the forward substitution of the inverse's columns, each as
-// one v_fmac_f64_dpp.  Returns false if a pivot was not positive.
-__device__ __forceinline__ bool leaf_factor(double (&a)[IB], double (&x)[IB], int lane16) {
+// one v_fmac_f64_dpp (negated src1: no separate negation).  The pivot chain per column is
+// broadcast -> v_rsq_f64 -> one third-order correction folded into L[i][j] -> the next column's
+// update: rsq is good to 2^-24 (measured), so e = d r^2 - 1 and r (1 - e/2 + 3e^2/8) is accurate to
+// rounding (max rel. error 2.7e-16 measured, vs 3.0e-16 for two Newton steps).  The pivot test is
+// off the chain: a non-positive pivot propagates NaN and is reported (returns false).
+// put(j): called once column j of L (a[j] on lanes >= j) and row j of L^-1 (x[j]) are final
+template <class PUT>
+__device__ __forceinline__ bool leaf_factor(double (&a)[IB], double (&x)[IB], int lane16, PUT&& put) {
     bool ok = true;
 #pragma unroll
     for (int r = 0; r < IB; ++r) x[r] = (r == lane16) ? 1.0 : 0.0;
 #pragma unroll
     for (int j = 0; j < IB; ++j) {
-        double d = bcl(a[j], j);
-        if (!(d > 0.0)) { ok = false; d = 1.0; }
-        const double inv = rsqrt_d(d);
-        a[j] *= inv;       // lane j: d * inv = sqrt(d); lanes > j: L[i][j]; lanes < j: unused
-        x[j] *= inv;       // (L^-1)[j][c] final
-        const double na = -a[j], nx = -x[j];
+        const double d = bcl(a[j], j);
+        ok &= d > 0.0;
+        const double r = __builtin_amdgcn_rsq(d);
+        const double ar = a[j] * r;
+        const double t = d * r;
+        const double e = __builtin_fma(t, r, -1.0);
+        const double p = __builtin_fma(e, 0.375, -0.5);
+        const double inv = __builtin_fma(r * e, p, r);
+        a[j] = __builtin_fma(ar * e, p, ar);  // lane j: sqrt(d); lanes > j: L[i][j]; lanes < j: unused
+        x[j] *= inv;                          // (L^-1)[j][c] final
 #pragma unroll
         for (int l = j + 1; l < IB; ++l) {
-            if (l == j + 1) fmac_bc_first(a[l], a[j], na, l);  // a[l] -= L[i][j] L[l][j]
-            else fmac_bc(a[l], a[j], na, l);
+            if (l == j + 1) fmac_bcn_first(a[l], a[j], a[j], l);  // a[l] -= L[i][j] L[l][j]
+            else fmac_bcn(a[l], a[j], a[j], l);
         }
 #pragma unroll
-        for (int l = j + 1; l < IB; ++l) fmac_bc(x[l], a[j], nx, l);  // x[l] -= L[l][j] x[j]
+        for (int l = j + 1; l < IB; ++l) fmac_bcn(x[l], a[j], x[j], l);  // x[l] -= L[l][j] x[j]
+        put(j);
     }
     return ok;
+}
+__device__ __forceinline__ bool leaf_factor(double (&a)[IB], double (&x)[IB], int lane16) {
+    return leaf_factor(a, x, lane16, [](int) {});
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -194,7 +250,7 @@ __device__ __forceinline__ bool leaf_factor(double (&a)[IB], double (&x)[IB], in
 constexpr int POTRF_NT = (CB / IB) * (CB / IB + 1) / 2;  // 36 lower tiles
 constexpr int POTRF_THREADS = 512;                          // wave 0: the leaf chain; waves 1-7: the bulk
 constexpr int POTRF_NW = POTRF_THREADS / 64;
-constexpr size_t POTRF_LDS = sizeof(double) * (POTRF_NT + CB / IB) * IB * 17;  // + the eight D_s
+constexpr size_t POTRF_LDS = sizeof(double) * (POTRF_NT + CB / IB) * IB * 17 + 32 * sizeof(int);  // + the eight D_s, counters
 
 // TS: shader-clock stamps of wave 0's critical path into ts[] (calibration builds only,
 // scripts/ubench/chol_ubench.hip)
@@ -218,7 +274,7 @@ __device__ __forceinline__ void wait_list(const int32_t* __restrict__ wl, int n,
 }
 
 template <bool TS>
-__device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, int col, double* __restrict__ dinv,
+__device__ __forceinline__ void potrf_body_sync(double* __restrict__ S, int64_t ld, int col, double* __restrict__ dinv,
                                            double* __restrict__ scal, unsigned long long* __restrict__ ts,
                                            unsigned* __restrict__ flag, double* __restrict__ smem) {
 #define POTRF_TS(i) do { if (TS && threadIdx.x == 0 && blockIdx.x == 0) ts[i] = __builtin_amdgcn_s_memtime(); } while (0)
@@ -418,6 +474,250 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
     }
 #undef AT
 #undef POTRF_TS
+}
+
+// potrf_body (dataflow): factor the 128x128 diagonal block of column col (512 threads); flag != nullptr:
+// publish it column by column (k_panel hand-off).  No workgroup barriers after the load: the waves
+// coordinate through LDS counters (workgroup-scope release / acquire), so wave 0 runs the critical
+// chain back to back:
+//   wave 0      leaf s (16x16 factor + inverse in registers, lane i = row i, DPP broadcasts; its
+//               columns stored to LDS as they finalise) -> panel tile (s+1, s) = A D_s' -> diagonal
+//               tile (s+1, s+1) -= X X' (v_mfma_f64_16x16x4_f64) -> leaf s+1
+//   bulk waves  (1-3, 5-7) after leaf s: the panel tiles (r, s), r >= s+2, then the trailing update of
+//               rows >= s+2 by column s, row s+2 (wave 0's next operands) first
+//   wave 4      (wave 0's SIMD, mostly asleep) stores block column s and D_s once column s is solved,
+//               and with a flag publishes them
+// Every wait points to work that does not wait for the waiter, so the chain always progresses; the
+// polls are bounded (scal[1] = -1 on timeout, reported by the host).
+template <bool TS>
+__device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, int col, double* __restrict__ dinv,
+                                           double* __restrict__ scal, unsigned long long* __restrict__ ts,
+                                           unsigned* __restrict__ flag, double* __restrict__ smem) {
+#define POTRF_TS(i) do { if (TS && threadIdx.x == 0 && blockIdx.x == 0) ts[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#define BULK_TS(i) do { if (TS && threadIdx.x == 64 && blockIdx.x == 0) ts[i] = __builtin_amdgcn_s_memtime(); } while (0)
+    POTRF_TS(0);
+    const int64_t k0 = (int64_t)col * CB;
+#define AT(r, c) smem[(((r) >> 4) * (((r) >> 4) + 1) / 2 + ((c) >> 4)) * (IB * 17) + ((r) & 15) * 17 + ((c) & 15)]
+    double* Dall = smem + POTRF_NT * IB * 17;  // [8][16][17] the leaf inverses D_s
+    int* sy = reinterpret_cast<int*>(Dall + (CB / IB) * IB * 17);
+    int* s_leaf = sy;       // leaves factored (L_ss and D_s in LDS; leaf 0 before the barrier)
+    int* s_pc = sy + 1;     // [7] panel tiles of column s solved (complete: 7 - s)
+    int* s_bc = sy + 8;     // [6] bulk waves done with the trailing update of step s (complete: 6)
+    int* s_cc = sy + 16;    // [6] row s+2 (tiles (s+2, s+1), (s+2, s+2)) updated by column s
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int lr = lane & 15, lk = lane >> 4;
+    const int64_t dbase = (k0 / CB) * (CB / IB) * (IB * IB);
+    constexpr int NBULK = 6;
+    bool ok = true;
+    auto wait_ge = [&](int* p, int v) {  // bounded (a lost update would be a bug: reported, not hung)
+        unsigned spins = 0;
+        while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }
+        }
+    };
+    auto bump = [&](int* p) {  // after this wave's LDS writes
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    if (tid < 32) sy[tid] = 0;
+    const __amdgpu_buffer_rsrc_t rL = block_rsrc(S + k0 * ld + k0, ((int64_t)(CB - 1) * ld + CB) * 8);
+    // wave 0's leaf s: column j of L and row j of D_s to LDS as soon as they are final
+    double a[IB], x[IB];
+    // (branch-free, so the scheduler can overlap them with the pivot chain: all four 16-lane rows of
+    // the wave hold the same leaf and store the same values; a[j] of lanes < j lands in the unused
+    // upper triangle of the diagonal tile, and x[j] is exactly zero there: (L^-1)[j][lane] = 0, j < lane)
+    auto leaf = [&](int s) {
+        const int R = s * IB;
+        double* Lw = &AT((R + lr), R);
+        double* Dw = Dall + s * IB * 17 + lr;
+        return leaf_factor(a, x, lr, [&](int j) {
+            Lw[j] = a[j];
+            Dw[j * 17] = x[j];  // (L^-1)[j][lane]
+        });
+    };
+    {
+        // wave 0 reads the rows of diagonal tile 0 straight into registers and factors leaf 0 while the
+        // other 35 lower tiles are on their way into LDS (sc1 loads: in a merged launch the block was
+        // just updated by another workgroup); item i -> tile p = 1 + (i >> 7), row (i >> 3) & 15,
+        // columns 2 (i & 7)
+        if (wave == 0) {
+#pragma unroll
+            for (int h = 0; h < IB / 2; ++h) {
+                const double2 v = ld_sc1(rL, ((int64_t)lr * ld + 2 * h) * 8);
+                a[2 * h] = v.x;
+                a[2 * h + 1] = v.y;
+            }
+        }
+        constexpr int NQ = ((POTRF_NT - 1) * 128 + POTRF_THREADS - 1) / POTRF_THREADS;
+        double2 v[NQ];
+        int off[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int i = tid + POTRF_THREADS * q, p = 1 + (i >> 7), n = (i >> 3) & 15, m = (i & 7) * 2;
+            int ti = 0, pp = p;
+            while (pp > ti) { pp -= ti + 1; ++ti; }
+            off[q] = -1;
+            if (p < POTRF_NT) {
+                v[q] = ld_sc1(rL, ((int64_t)(ti * IB + n) * ld + pp * IB + m) * 8);
+                off[q] = p * IB * 17 + n * 17 + m;
+            }
+        }
+        if (wave == 0) {
+            POTRF_TS(1);
+            ok = leaf(0);
+            POTRF_TS(2);
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            if (off[q] >= 0) {
+                smem[off[q]] = v[q].x;
+                smem[off[q] + 1] = v[q].y;
+            }
+        }
+    }
+    __syncthreads();  // all tiles, leaf 0 and the zeroed counters in LDS
+    if (tid == 0) __hip_atomic_store(s_leaf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    POTRF_TS(3);
+    if (wave == 0) {
+        // the critical chain
+        for (int s = 0; s < CB / IB - 1; ++s) {
+            const int c0 = s * IB, R = c0 + IB;
+            if (s > 0) wait_ge(s_cc + s - 1, 1);  // row s+1 updated through column s-1
+            POTRF_TS(4 + 4 * s);
+            const double* Dl = Dall + s * IB * 17;
+            dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0}, d;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) d[r] = AT((R + lk + 4 * r), R + lr);
+#pragma unroll
+            for (int kk = 0; kk < IB; kk += 4) acc = mfma(AT((R + lr), c0 + kk + lk), Dl[lr * 17 + kk + lk], acc);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) AT((R + lk + 4 * r), c0 + lr) = acc[r];  // X = A D_s'
+            __builtin_amdgcn_wave_barrier();
+            double xa[4];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) xa[kk] = AT((R + lr), c0 + 4 * kk + lk);
+            bump(s_pc + s);
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) d = mfma(-xa[kk], xa[kk], d);  // C -= X X'
+#pragma unroll
+            for (int r = 0; r < 4; ++r) AT((R + lk + 4 * r), R + lr) = d[r];
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int c = 0; c < IB; ++c) a[c] = AT((R + lr), R + c);
+            POTRF_TS(5 + 4 * s);
+            ok &= leaf(s + 1);
+            POTRF_TS(6 + 4 * s);
+            bump(s_leaf);
+            POTRF_TS(7 + 4 * s);
+        }
+    } else if (wave != 4) {
+        // bulk waves: the whole schedule unrolled (every tile index a compile-time constant, one
+        // uniform branch per unit on its owner), each unit's LDS operands loaded before its MFMAs
+        const int b = wave < 4 ? wave - 1 : wave - 2;
+        // C(R, C) -= X(R) X(C)' [and C(R, C + 16) -= X(R) X(C + 16)'], K = 16 from column c0
+        auto unit = [&](const int c0, const int R, const int C, const bool two) {
+            dbl4 acc1, acc2;
+            double av[4], b1[4], b2[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc1[r] = AT((R + lk + 4 * r), C + lr);
+            if (two)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc2[r] = AT((R + lk + 4 * r), C + IB + lr);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                av[k] = -AT((R + lr), c0 + 4 * k + lk);
+                b1[k] = AT((C + lr), c0 + 4 * k + lk);
+                if (two) b2[k] = AT((C + IB + lr), c0 + 4 * k + lk);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                acc1 = mfma(av[k], b1[k], acc1);
+                if (two) acc2 = mfma(av[k], b2[k], acc2);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) AT((R + lk + 4 * r), C + lr) = acc1[r];
+            if (two)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) AT((R + lk + 4 * r), C + IB + lr) = acc2[r];
+        };
+#pragma unroll
+        for (int s = 0; s < CB / IB - 2; ++s) {
+            const int c0 = s * IB;
+            wait_ge(s_leaf, s + 1);                   // L_ss, D_s
+            BULK_TS(41 + 3 * s);
+            if (s > 0) wait_ge(s_bc + s - 1, NBULK);  // every update of step s-1
+            BULK_TS(42 + 3 * s);
+            if (b < CB / IB - 2 - s) {                // panel tile (s+2+b, s)
+                const int r0 = (s + 2 + b) * IB;
+                const double* Dl = Dall + s * IB * 17;
+                double av[4], bv[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    av[k] = AT((r0 + lr), c0 + 4 * k + lk);
+                    bv[k] = Dl[lr * 17 + 4 * k + lk];
+                }
+                dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc = mfma(av[k], bv[k], acc);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) AT((r0 + lk + 4 * r), c0 + lr) = acc[r];
+                bump(s_pc + s);
+            }
+            wait_ge(s_pc + s, CB / IB - 1 - s);  // column s solved
+            // trailing update of rows s+2 .. 7 by column s: row s+2 (wave 0's next panel tile and
+            // diagonal tile) on bulk wave 0 first, then the other rows from the bottom, tiles in pairs
+            // sharing the A operand, dealt round-robin from bulk wave 1 on
+            if (b == 0) {
+                unit(c0, (s + 2) * IB, (s + 1) * IB, true);
+                bump(s_cc + s);
+                BULK_TS(43 + 3 * s);
+            }
+            int u = 0;
+#pragma unroll
+            for (int i = CB / IB - 1; i >= s + 3; --i)
+#pragma unroll
+                for (int C = c0 + IB; C <= i * IB; C += 2 * IB, ++u)
+                    if ((1 + u) % NBULK == b) unit(c0, i * IB, C, C + IB <= i * IB);
+            bump(s_bc + s);
+        }
+    } else {
+        // wave 4: block column s (tiles (s..7, s)) and D_s are final once column s is solved
+        const __amdgpu_buffer_rsrc_t rD = block_rsrc(dinv + dbase, (CB / IB) * IB * IB * 8);
+        for (int s = 0; s < CB / IB; ++s) {
+            if (s < CB / IB - 1) wait_ge(s_pc + s, CB / IB - 1 - s);
+            else wait_ge(s_leaf, CB / IB);
+            for (int i = lane; i < (CB / IB - s) * 128; i += 64) {
+                const int ti = s + (i >> 7), n = (i >> 3) & 15, m = (i & 7) * 2;
+                const int64_t off = ((int64_t)(ti * IB + n) * ld + s * IB + m) * 8;
+                const double* t = smem + (ti * (ti + 1) / 2 + s) * IB * 17 + n * 17 + m;
+                if (ti > s || m + 1 <= n) {
+                    double2 v;
+                    v.x = t[0];
+                    v.y = t[1];
+                    st_sc1(rL, off, v);
+                } else if (m == n) {
+                    st_sc1(rL, off, t[0]);
+                }
+            }
+            for (int i = 2 * lane; i < IB * IB; i += 128) {
+                double2 v;
+                v.x = Dall[s * IB * 17 + (i >> 4) * 17 + (i & 15)];
+                v.y = Dall[s * IB * 17 + (i >> 4) * 17 + (i & 15) + 1];
+                st_sc1(rD, (int64_t)(s * IB * IB + i) * 8, v);
+            }
+            if (flag) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0) __hip_atomic_store(flag, (unsigned)(s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    if (!ok && lane == 0 && scal[1] == 0.0) scal[1] = (double)(k0 + 1);
+    POTRF_TS(40);
+#undef AT
+#undef POTRF_TS
+#undef BULK_TS
 }
 
 template <bool TS>

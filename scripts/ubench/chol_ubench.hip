@@ -12,6 +12,35 @@
 namespace fba { void set_error(const std::string&) {} }
 using namespace fba;
 
+// the barrier-synchronised potrf (A/B against the dataflow one)
+__global__ __launch_bounds__(POTRF_THREADS) void k_potrf128_sync(double* S, int64_t ld, const int32_t* cols, double* dinv,
+                                                                 double* scal) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    potrf_body_sync<false>(S, ld, cols[blockIdx.x], dinv, scal, nullptr, nullptr, smem);
+}
+
+// |L L' - A| / |A| over the 128x128 block and max |D_s L_ss - I| over the eight leaf inverses
+static void check(const std::vector<double>& M, const std::vector<double>& L, const std::vector<double>& D, int64_t ld,
+                  const char* name, float us) {
+    const int n = 128;
+    double err = 0.0, nrm = 0.0, derr = 0.0;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j <= i; ++j) {
+            double v = 0;
+            for (int k = 0; k <= j; ++k) v += L[i * ld + k] * L[j * ld + k];
+            err = std::max(err, std::fabs(v - M[i * ld + j]));
+            nrm = std::max(nrm, std::fabs(M[i * ld + j]));
+        }
+    for (int s = 0; s < 8; ++s)
+        for (int i = 0; i < 16; ++i)
+            for (int j = 0; j < 16; ++j) {
+                double v = 0;
+                for (int k = 0; k < 16; ++k) v += D[s * 256 + i * 16 + k] * (k >= j ? L[(16 * s + k) * ld + 16 * s + j] : 0.0);
+                derr = std::max(derr, std::fabs(v - (i == j ? 1.0 : 0.0)));
+            }
+    printf("%-20s %8.2f us  |LL'-A|/|A| %.2e  max|D L - I| %.2e\n", name, us, err / nrm, derr);
+}
+
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
 
 template <class F>
@@ -72,23 +101,23 @@ int main() {
     CK(hipFuncSetAttribute((const void*)k_potrf128<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)POTRF_LDS));
     CK(hipFuncSetAttribute((const void*)k_trsm128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRSM_LDS));
     auto reset = [&]() { return hipMemcpy(dS, M.data(), M.size() * 8, hipMemcpyHostToDevice); };
-    CK(reset());
-    const float tp = time_us([&] { k_potrf128<false><<<1, POTRF_THREADS, POTRF_LDS>>>(dS, ld, dl, dinv, scal, nullptr); }, 20);
-    // check: L from the last run (factoring the original block every time: reset, run once)
-    CK(reset());
-    k_potrf128<false><<<1, POTRF_THREADS, POTRF_LDS>>>(dS, ld, dl, dinv, scal, nullptr);
-    CK(hipDeviceSynchronize());
-    std::vector<double> L((size_t)n * ld);
-    CK(hipMemcpy(L.data(), dS, L.size() * 8, hipMemcpyDeviceToHost));
-    double err = 0.0, nrm = 0.0;
-    for (int i = 0; i < n; ++i)
-        for (int j = 0; j <= i; ++j) {
-            double v = 0;
-            for (int k = 0; k <= j; ++k) v += L[i * ld + k] * L[j * ld + k];
-            err = std::max(err, std::fabs(v - M[i * ld + j]));
-            nrm = std::max(nrm, std::fabs(M[i * ld + j]));
-        }
-    printf("k_potrf128           %8.2f us  |LL'-A|/|A| %.2e\n", tp, err / nrm);
+    CK(hipFuncSetAttribute((const void*)k_potrf128_sync, hipFuncAttributeMaxDynamicSharedMemorySize, (int)POTRF_LDS));
+    std::vector<double> L((size_t)n * ld), D(8 * 256);
+    for (int variant = 0; variant < 2; ++variant) {
+        auto run = [&] {
+            if (variant) k_potrf128_sync<<<1, POTRF_THREADS, POTRF_LDS>>>(dS, ld, dl, dinv, scal);
+            else k_potrf128<false><<<1, POTRF_THREADS, POTRF_LDS>>>(dS, ld, dl, dinv, scal, nullptr);
+        };
+        CK(reset());
+        const float tp = time_us(run, 20);
+        CK(reset());  // check: factor the original block once
+        CK(hipMemset(dinv, 0, 8 * 256 * 8));
+        run();
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(L.data(), dS, L.size() * 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(D.data(), dinv, D.size() * 8, hipMemcpyDeviceToHost));
+        check(M, L, D, ld, variant ? "k_potrf128 (sync)" : "k_potrf128 (dataflow)", tp);
+    }
     CK(reset());
     k_potrf128<true><<<1, POTRF_THREADS, POTRF_LDS>>>(dS, ld, dl, dinv, scal, dts);
     CK(hipDeviceSynchronize());
@@ -96,17 +125,21 @@ int main() {
     const float tq = time_us([&] { k_potrf128<true><<<1, POTRF_THREADS, POTRF_LDS>>>(dS, ld, dl, dinv, scal, dts); }, 1);
     unsigned long long q[64];
     CK(hipMemcpy(q, dts, sizeof q, hipMemcpyDeviceToHost));
-    printf("k_potrf128<TS>       %8.2f us, %llu clocks = %.2f GHz\n", tq, q[40] - q[0], (q[40] - q[0]) / (1e3 * tq));
-    printf("  start->leaf0 %llu  leaf0 %llu  ->B1 %llu\n", q[1] - q[0], q[2] - q[1], q[3] - q[2]);
-    unsigned long long tl = q[2] - q[1], tpan = 0, tdiag = 0, tend = 0;
+    printf("k_potrf128<TS>       %8.2f us, %llu clocks (wave 0) = %.2f GHz\n", tq, q[40] - q[0], (q[40] - q[0]) / (1e3 * tq));
+    printf("  start->leaf0 %llu  leaf0 %llu  ->barrier %llu\n", q[1] - q[0], q[2] - q[1], q[3] - q[2]);
+    unsigned long long tl = q[2] - q[1], tw = 0, tpd = 0, tb = 0, prev = q[3];
     for (int t = 0; t < 7; ++t) {
-        const unsigned long long pan = q[4 + 4 * t] - q[3 + 4 * t], dg = q[5 + 4 * t] - q[4 + 4 * t],
-                                 lf = q[6 + 4 * t] - q[5 + 4 * t], e = q[7 + 4 * t] - q[6 + 4 * t];
-        tpan += pan; tdiag += dg; tl += lf; tend += e;
-        printf("  s%d: B1->B2 %5llu  B2->leaf %5llu  leaf %5llu  leaf->B1 %5llu\n", t, pan, dg, lf, e);
+        const unsigned long long w = q[4 + 4 * t] - prev, pd = q[5 + 4 * t] - q[4 + 4 * t],
+                                 lf = q[6 + 4 * t] - q[5 + 4 * t], bb = q[7 + 4 * t] - q[6 + 4 * t];
+        prev = q[7 + 4 * t];
+        tw += w; tpd += pd; tl += lf; tb += bb;
+        printf("  s%d: wait %5llu  panel+diag %5llu  leaf %5llu  publish %5llu\n", t, w, pd, lf, bb);
     }
-    printf("  totals: leaves %llu  panel(B1->B2) %llu  diag-update %llu  leaf->B1 %llu  final store %llu\n", tl, tpan,
-           tdiag, tend, q[40] - q[31]);
+    printf("  totals: leaves %llu  waits %llu  panel+diag %llu  publish %llu  end %llu\n", tl, tw, tpd, tb, q[40] - q[31]);
+    for (int t = 0; t < 6; ++t)  // bulk wave 1 (owner of the row-(s+2) unit), relative to wave 0's step starts
+        printf("  bulk s%d: leaf seen %6lld  step s-1 all done %6lld  row s+2 out %6lld   (wave 0 step s+1 ready %6lld)\n", t,
+               (long long)(q[41 + 3 * t] - q[3]), (long long)(q[42 + 3 * t] - q[3]), (long long)(q[43 + 3 * t] - q[3]),
+               (long long)((t + 1 < 7 ? q[4 + 4 * (t + 1)] : q[40]) - q[3]));
     // trsm: 61 panel blocks below the factored block (two workgroups each)
     CK(reset());
     k_potrf128<false><<<1, POTRF_THREADS, POTRF_LDS>>>(dS, ld, dl, dinv, scal, nullptr);
