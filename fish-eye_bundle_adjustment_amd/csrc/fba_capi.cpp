@@ -166,7 +166,7 @@ static void partition(const fba_problem* p, int world, std::vector<int32_t>& tie
 static void destroy(Ctx* c) {
     if (!c) return;
     void* ptrs[] = {c->d_chunk_obs, c->d_chunk_pt, c->d_xy, c->d_img, c->d_cam, c->d_pt, c->d_ctl, c->d_lp_tie, c->d_lp_start, c->d_lp_cam,
-                    c->d_acc, c->d_ppart, c->d_ipart, c->d_cpart, c->d_cseg, c->d_bscr, c->d_lrprof, c->d_gpairs, c->d_red, c->d_xfull, c->d_xlin, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
+                    c->d_acc, c->d_ppart, c->d_ipart, c->d_cpart, c->d_cseg, c->d_bscr, c->d_lrprof, c->d_ptrace, c->d_gpairs, c->d_red, c->d_xfull, c->d_xlin, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
                     c->d_pt_tab, c->d_P, c->d_flags, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
                     c->d_active, c->d_counted, c->d_obs_pho, c->d_sched};
     for (void* q : ptrs)
@@ -566,6 +566,11 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     }
     if ((rc = chol_setup(*c)) || (rc = acc_setup(*c))) { destroy(c); return rc; }
     if (getenv("FBA_LR_PROFILE") && c->n_chunks > 0) FBA_HIP(hipMalloc((void**)&c->d_lrprof, sizeof(uint64_t) * 8 * c->n_chunks));
+    if (getenv("FBA_PANEL_TRACE") && c->sched.n_waves > 0)
+    {
+        FBA_HIP(hipMalloc((void**)&c->d_ptrace, sizeof(uint64_t) * 8 * PTRACE_WG * c->sched.n_waves));
+        FBA_HIP(hipMemset(c->d_ptrace, 0, sizeof(uint64_t) * 8 * PTRACE_WG * c->sched.n_waves));
+    }
     FBA_HIP(hipMemset(c->d_delta, 0, sizeof(double) * L.u_full));
     // outside the factor's block pattern S stays zero; the pattern itself is zeroed per accumulation
     FBA_HIP(hipMemsetAsync(c->d_S, 0, sizeof(double) * (size_t)(L.n_pad + NB) * L.ld, c->stream));
@@ -599,7 +604,7 @@ static inline void mark(Ctx* c, int i) {
 
 static bool graph_eligible(const Ctx* c) {
     static const bool off = getenv("FBA_NO_GRAPH") && atoi(getenv("FBA_NO_GRAPH")) != 0;
-    return !off && c->graphs_ok && c->stream && !c->timing && !c->probe && !c->d_lrprof;
+    return !off && c->graphs_ok && c->stream && !c->timing && !c->probe && !c->d_lrprof && !c->d_ptrace;
 }
 
 // run body() on the context's stream, through a graph captured from its first run when eligible
@@ -697,9 +702,65 @@ static int solve_enqueue(Ctx* c) {
 
 // wait for the solve, read scal (again from the device when `recopy`: a caller may have all-reduced
 // the deltasum share in place after the graph's own copy), check the failure flags
+// FBA_PANEL_TRACE: one line per elimination-tree level, times in us from the first k_panel's start:
+// launch span, the gap after the previous launch, and per workgroup role the last end (diagonal-block
+// updates, potrf start / after its waits / end, panel solves, inverses, other updates)
+static void print_panel_trace(Ctx* c) {
+    const int nw = c->sched.n_waves;
+    std::vector<uint64_t> t((size_t)8 * PTRACE_WG * nw);
+    if (hipMemcpy(t.data(), c->d_ptrace, t.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return;
+    uint64_t t0 = UINT64_MAX, prev_end = 0;
+    for (int w = 0; w < nw; ++w)
+        for (int b = 0; b < PTRACE_WG; ++b)
+            if (t[(size_t)8 * (w * PTRACE_WG + b)] != 0) t0 = std::min(t0, t[(size_t)8 * (w * PTRACE_WG + b)]);
+    auto us = [&](uint64_t v) { return v ? (double)(v - t0) * 0.01 : -1.0; };
+    auto hi_trsm_end = [&](int w) {
+        uint64_t m = 0;
+        for (int b = 0; b < PTRACE_WG; ++b) {
+            const uint64_t* r = &t[(size_t)8 * (w * PTRACE_WG + b)];
+            if (r[0] != 0 && r[3] == 3) m = std::max(m, r[2]);
+        }
+        return m;
+    };
+    for (int w = 0; w < nw; ++w) {
+        uint64_t lo = UINT64_MAX, hi = 0, rend[6] = {0, 0, 0, 0, 0, 0}, pst = 0, prd = 0, tfirst = UINT64_MAX, tseen = 0;
+        int n = 0;
+        for (int b = 0; b < PTRACE_WG; ++b) {
+            const uint64_t* r = &t[(size_t)8 * (w * PTRACE_WG + b)];
+            if (r[0] == 0) continue;
+            ++n;
+            lo = std::min(lo, r[0]);
+            hi = std::max(hi, r[2]);
+            const int role = (int)r[3];
+            if (role >= 0 && role < 6) rend[role] = std::max(rend[role], r[2]);
+            if (role == 1) { pst = std::max(pst, r[0]); prd = std::max(prd, r[1]); }
+            if (role == 3) { tfirst = std::min(tfirst, r[0]); tseen = std::max(tseen, r[1]); }
+            if (role == 3 && getenv("FBA_PANEL_TRACE")[0] == '3' && r[2] == hi_trsm_end(w))
+                fprintf(stderr, "[fba]   level %2d last panel solve wg %4d: start %6.1f  step 6 done %6.1f  factor seen %6.1f  "
+                        "step 7 done %6.1f  end %6.1f  batches %llx\n", w, b, us(r[0]), us(r[5]), us(r[1]), us(r[6]), us(r[2]),
+                        (unsigned long long)r[4]);
+            if (role == 0 && getenv("FBA_PANEL_TRACE")[0] == '2')
+                fprintf(stderr, "[fba]   level %2d diag-update wg %3d: %2d sources%s  %6.1f .. %6.1f (%4.1f us)\n", w, b,
+                        (int)(r[1] & 0xff), (r[1] & 0x100) ? " (split group)" : "", us(r[0]), us(r[2]), (double)(r[2] - r[0]) * 0.01);
+            if (role == 0 && getenv("FBA_PANEL_TRACE")[0] == '2')
+                fprintf(stderr, "[fba]       loaded +%.1f  products +%.1f  published +%.1f\n", (double)(r[4] - r[0]) * 0.01,
+                        (double)(r[5] - r[0]) * 0.01, (double)(r[2] - r[0]) * 0.01);
+        }
+        if (n == 0) { fprintf(stderr, "[fba] level %2d: own k_potrf128/k_trsm128 launches (no trace)\n", w); continue; }
+        fprintf(stderr, "[fba] level %2d: %4d wg  span %7.1f .. %7.1f (%5.1f)  gap %5.1f | diag-upd end %7.1f | potrf %7.1f wait-end %7.1f "
+                "end %7.1f | panel-upd end %7.1f | trsm %7.1f .. (factor seen %7.1f) %7.1f | trtri end %7.1f | other-upd end %7.1f\n",
+                w, n, us(lo), us(hi), (double)(hi - lo) * 0.01, prev_end ? (double)(lo - prev_end) * 0.01 : 0.0, us(rend[0]),
+                us(pst), us(prd), us(rend[1]), us(rend[2]), tfirst == UINT64_MAX ? -1.0 : us(tfirst), us(tseen), us(rend[3]),
+                us(rend[4]), us(rend[5]));
+        prev_end = hi;
+    }
+    (void)hipMemset(c->d_ptrace, 0, t.size() * sizeof(uint64_t));
+}
+
 static int solve_finish(Ctx* c, double* dsum, bool recopy) {
     if (recopy) FBA_HIP(hipMemcpyAsync(c->h_pinned, c->d_scal, sizeof(double) * 4, hipMemcpyDeviceToHost, c->stream));
     FBA_HIP(hipStreamSynchronize(c->stream));
+    if (c->d_ptrace) print_panel_trace(c);
     if (c->timing) {
         float ms;
         for (int i = 0; i < 7; ++i) {

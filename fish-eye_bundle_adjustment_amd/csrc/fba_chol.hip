@@ -739,7 +739,7 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_potrf128(double* __restrict__
 // runs its eight sub-steps out of LDS only.
 // ------------------------------------------------------------------------------------------------
 constexpr int TRSM_NT = (CB / IB) * (CB / IB - 1) / 2;  // 28 off-diagonal tiles
-constexpr size_t TRSM_LDS = sizeof(double) * (4 * IB * LDA + 4 * IB * 17 + (TRSM_NT + CB / IB) * IB * 17);
+constexpr size_t TRSM_LDS = sizeof(double) * (4 * IB * LDA + 4 * IB * 17 + (TRSM_NT + CB / IB) * IB * 17 + 4);  // + the loaders' column flags
 
 // one substitution step of a wave's 16 panel rows: X_s = (A_s - sum_{t<s} X_t L_st^T) D_s^T
 __device__ __forceinline__ void trsm_step(const int s, double* __restrict__ Xw, double* __restrict__ Tw,
@@ -798,7 +798,8 @@ __device__ __forceinline__ void trsm_store(double* __restrict__ S, int64_t ld, i
 // 256.. of a 512-thread workgroup only take part in the barriers
 __device__ __forceinline__ void trsm_body(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ rec,
                                           const double* __restrict__ dinv, const unsigned* __restrict__ flag,
-                                          double* __restrict__ scal, double* __restrict__ smem, bool progressive) {
+                                          double* __restrict__ scal, double* __restrict__ smem, bool progressive,
+                                          uint64_t* __restrict__ tr = nullptr) {
     double* X = smem;                       // [4][IB][LDA]   panel rows of each wave
     double* T = X + 4 * IB * LDA;           // [4][IB][17]    per-wave 16x16 staging
     double* Lt = T + 4 * IB * 17;           // [28][IB][17]   L_st, p = s(s-1)/2 + t
@@ -843,33 +844,65 @@ __device__ __forceinline__ void trsm_body(double* __restrict__ S, int64_t ld, co
         __syncthreads();
     };
     if (flag && progressive) {
-        // progressive hand-off (k_panel): step st starts as soon as the potrf workgroup has published
-        // block columns < st and D_st (flag >= st + 1): the row-st tiles L_st,t (t < st) and D_st, sc1 loads
-        __syncthreads();  // the panel rows are in LDS
-#pragma unroll
-        for (int st = 0; st < CB / IB; ++st) {
-            wait_flag((unsigned)(st + 1));
-            if (worker) {
-                // items: st tiles x 16 rows x 8 double2 + D_st (128 double2)
-                for (int i = tid; i < (st + 1) * 128; i += 256) {
-                    const int p = i >> 7, n = (i >> 3) & 15, kc = (i & 7) * 2;
-                    if (p < st) {
-                        const double2 v = ld_sc1(rL, ((int64_t)(st * IB + n) * ld + p * IB + kc) * 8);
-                        double* dst = Lt + ((st * (st - 1) / 2 + p) * IB + n) * 17 + kc;
-                        dst[0] = v.x;
-                        dst[1] = v.y;
-                    } else {
-                        const double2 v = ld_sc1(rD, (int64_t)(st * IB * IB + n * IB + kc) * 8);
-                        double* dst = Dt + (st * IB + n) * 17 + kc;
-                        dst[0] = v.x;
-                        dst[1] = v.y;
+        // progressive hand-off (k_panel): step st needs block columns < st of L_kk and D_st, final
+        // once flag >= st + 1.  Waves 4-7 (idle otherwise: the solve uses waves 0-3) are loaders, wave
+        // 4 + t % 4 for block column t: it polls the flag, copies the column (tiles (r, t), r > t, and
+        // D_t; sc1 loads, 16 per lane in flight) into LDS and raises the column's LDS flag.  Four
+        // columns are in flight at once, so the load latency overlaps both the factorisation and the
+        // substitution steps; the solving waves wait on the LDS flags only.
+        int* s_col = reinterpret_cast<int*>(Dt + (CB / IB) * IB * 17);  // [8] column t in LDS
+        if (tid < CB / IB) s_col[tid] = 0;
+        __syncthreads();  // the panel rows are in LDS, the flags are zero
+        if (!worker) {
+            for (int t = wave - 4; t < CB / IB; t += 4) {
+                unsigned spins = 0;
+                while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(t + 1)) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins == FLAG_SPINS) {
+                        if (lane == 0) scal[1] = -1.0;  // hand-off timeout (host reports it)
+                        break;
                     }
                 }
+                double2 v[16];
+                double* dst[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {  // items (8 - t) * 128 double2
+                    const int i = lane + 64 * q, u = i >> 7, n = (i >> 3) & 15, kc = (i & 7) * 2;
+                    dst[q] = nullptr;
+                    if (u < CB / IB - 1 - t) {  // tile (r, t), r = t + 1 + u
+                        const int r = t + 1 + u;
+                        v[q] = ld_sc1(rL, ((int64_t)(r * IB + n) * ld + t * IB + kc) * 8);
+                        dst[q] = Lt + ((r * (r - 1) / 2 + t) * IB + n) * 17 + kc;
+                    } else if (u == CB / IB - 1 - t) {  // D_t
+                        v[q] = ld_sc1(rD, (int64_t)(t * IB * IB + n * IB + kc) * 8);
+                        dst[q] = Dt + (t * IB + n) * 17 + kc;
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    if (dst[q]) {
+                        dst[q][0] = v[q].x;
+                        dst[q][1] = v[q].y;
+                    }
+                __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's LDS writes done
+                __builtin_amdgcn_wave_barrier();
+                if (lane == 0) __hip_atomic_store(s_col + t, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (tr && lane == 0 && t == CB / IB - 1) tr[1] = wall_clock64();  // FBA_PANEL_TRACE: last column in
             }
-            __syncthreads();
-            if (worker) trsm_step(st, Xw, Tw, Lt, Dt, lr, lk);
+        } else {
+#pragma unroll
+            for (int st = 0; st < CB / IB; ++st) {
+                unsigned sp = 0;
+                while (__hip_atomic_load(s_col + st, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++sp == FLAG_SPINS) break;  // (the loader reports the timeout)
+                }
+                trsm_step(st, Xw, Tw, Lt, Dt, lr, lk);
+                if (tr && tid == 0 && st == CB / IB - 2) tr[5] = wall_clock64();
+            }
+            if (tr && tid == 0) tr[6] = wall_clock64();
+            trsm_store(S, ld, rbase, k0, Xw, lane);
         }
-        if (worker) trsm_store(S, ld, rbase, k0, Xw, lane);
         return;
     }
     if (flag) wait_flag((unsigned)(CB / IB));  // the whole factor
@@ -1063,6 +1096,142 @@ __device__ __forceinline__ void syrk_body(double* __restrict__ S, int64_t ld, co
             if (tflags) st_sc1(rC, ((int64_t)r * ld + cl) * 8, v[q]);
             else *reinterpret_cast<double2*>(S + (r0 + r) * ld + c0 + cl) = v[q];
         }
+    }
+    if (tflags) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(tflags + tk[7], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// syrk_body_wide: the same quarter task inside k_panel (512 threads, one workgroup per CU, its LDS
+// free): all eight waves compute (wave w: rows 16 (w >> 1), columns 32 (w & 1) of the quarter, two
+// 16x16 MFMA tiles), each source column's whole K = 128 panel of A and B (128 KB) is staged in LDS
+// with one round of loads (16 x 16 B per thread in flight) instead of 32-deep slices, and the next
+// source's panel is loaded into registers while the current one is multiplied.  Same sums in the
+// same order per output element as syrk_body (k ascending within a source, sources ascending).
+constexpr int LDW = 130;  // LDS row stride of a 128-deep panel (16-B aligned rows)
+constexpr size_t SYRKW_LDS = sizeof(double) * 2 * 64 * LDW + 16;
+__device__ __forceinline__ void syrk_body_wide(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ tk,
+                                               const int32_t* __restrict__ src, double* __restrict__ P,
+                                               const int32_t* __restrict__ comb, unsigned* __restrict__ cnt,
+                                               unsigned* __restrict__ tflags, double* __restrict__ smem,
+                                               uint64_t* __restrict__ tr = nullptr) {
+    double (*As)[LDW] = reinterpret_cast<double (*)[LDW]>(smem);
+    double (*Bs)[LDW] = reinterpret_cast<double (*)[LDW]>(smem + 64 * LDW);
+    unsigned* last = reinterpret_cast<unsigned*>(smem + 128 * LDW);
+    const int64_t bi = tk[0], bj = tk[1];
+    const int qr = tk[2] >> 1, qc = tk[2] & 1, s0 = tk[3], slot = tk[5];
+    const int ns = tk[4] - s0;
+    const int32_t* ks_src = src + s0;
+    const int64_t r0 = bi * CB + qr * 64, c0 = bj * CB + qc * 64;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int lr = lane & 15, lk = lane >> 4;
+    const int wr = (wave >> 1) * 16, wc = (wave & 1) * 32;
+    double* Cp = slot < 0 ? S + (r0 + wr + lk) * ld + c0 + wc + lr : P + (int64_t)slot * 4096 + (wr + lk) * 64 + wc + lr;
+    const int64_t ldc = slot < 0 ? ld : 64;
+    dbl4 acc[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[b][r] = slot < 0 ? Cp[(4 * r) * ldc + b * 16] : 0.0;
+    // loader mapping: thread t -> row t >> 3 of A and of B, columns 16 (t & 7) .. + 15
+    const int rr = tid >> 3, cc = (tid & 7) * 16;
+    const double* ga = S + (r0 + rr) * ld + cc;
+    const double* gb = S + (c0 + rr) * ld + cc;
+    double2 pa[8], pb[8];
+    auto load = [&](int k) {
+        const int64_t kc = (int64_t)ks_src[k] * CB;
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+            pa[h] = *reinterpret_cast<const double2*>(ga + kc + 2 * h);
+            pb[h] = *reinterpret_cast<const double2*>(gb + kc + 2 * h);
+        }
+    };
+    load(0);
+    for (int k = 0; k < ns; ++k) {
+        if (k > 0) __syncthreads();  // the previous source's panels are consumed
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {  // (component stores: a double2 struct copy kept the arrays in scratch)
+            As[rr][cc + 2 * h] = pa[h].x; As[rr][cc + 2 * h + 1] = pa[h].y;
+            Bs[rr][cc + 2 * h] = pb[h].x; Bs[rr][cc + 2 * h + 1] = pb[h].y;
+        }
+        __syncthreads();
+        if (tr && tid == 0 && k == 0) tr[4] = wall_clock64();  // FBA_PANEL_TRACE: first panels in LDS
+        if (k + 1 < ns) load(k + 1);  // the next source in flight while this one is multiplied
+#pragma unroll
+        for (int kb = 0; kb < CB; kb += 32) {  // operands of 8 k-steps read ahead of their MFMAs
+            double av[8], b0[8], b1[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                av[q] = -As[wr + lr][kb + 4 * q + lk];
+                b0[q] = Bs[wc + lr][kb + 4 * q + lk];
+                b1[q] = Bs[wc + 16 + lr][kb + 4 * q + lk];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                acc[0] = mfma(av[q], b0[q], acc[0]);
+                acc[1] = mfma(av[q], b1[q], acc[1]);
+            }
+        }
+    }
+    const __amdgpu_buffer_rsrc_t rC = block_rsrc(S + r0 * ld + c0, ((int64_t)63 * ld + 64) * 8);
+    if (tr && tid == 0) tr[5] = wall_clock64();  // products done (wave 0)
+    if (slot < 0) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (tflags)
+                    st_sc1(rC, ((int64_t)(wr + lk + 4 * r) * ld + wc + lr + b * 16) * 8, acc[b][r]);
+                else
+                    Cp[(4 * r) * ldc + b * 16] = acc[b][r];
+            }
+        if (tflags) {  // publish the quarter
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(tflags + tk[7], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+    // split target (as syrk_body): the partial to scratch write-through, the last group adds the groups
+    // in slot order
+    {
+        const __amdgpu_buffer_rsrc_t rP = block_rsrc(P + (int64_t)slot * 4096, 4096 * 8);
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                st_sc1(rP, (int64_t)((wr + lk + 4 * r) * 64 + wc + lr + b * 16) * 8, acc[b][r]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int32_t* cb = comb + Sched::COMB_REC * tk[6];
+    if (tid == 0)
+        *last = __hip_atomic_fetch_add(cnt + tk[6], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(cb[4] - 1);
+    __syncthreads();
+    if (!*last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const int first = cb[3], n = cb[4];
+    double2 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int e = 2 * (tid + 512 * q), r = e >> 6, cl = e & 63;
+        v[q] = *reinterpret_cast<const double2*>(S + (r0 + r) * ld + c0 + cl);
+    }
+    for (int g = 0; g < n; ++g) {
+        const __amdgpu_buffer_rsrc_t rg = block_rsrc(P + (int64_t)(first + g) * 4096, 4096 * 8);
+        double2 pv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pv[q] = ld_sc1(rg, (int64_t)(2 * (tid + 512 * q)) * 8);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { v[q].x += pv[q].x; v[q].y += pv[q].y; }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int e = 2 * (tid + 512 * q), r = e >> 6, cl = e & 63;
+        if (tflags) st_sc1(rC, ((int64_t)r * ld + cl) * 8, v[q]);
+        else *reinterpret_cast<double2*>(S + (r0 + r) * ld + c0 + cl) = v[q];
     }
     if (tflags) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1318,7 +1487,8 @@ __global__ __launch_bounds__(256) void k_trtri128(const double* __restrict__ S, 
 // invert the diagonal blocks of the PREVIOUS level (trtri_body; final since the last launch) for the
 // backward solve, off the critical path.  Every workgroup of the launch is resident at once (<= 8 +
 // 2 * panel blocks + 8 workgroups, one per CU), so the waits end.
-constexpr size_t PANEL_LDS = TRSM_LDS > TRTRI_LDS ? TRSM_LDS : TRTRI_LDS;
+constexpr size_t PANEL_LDS_ = TRSM_LDS > TRTRI_LDS ? TRSM_LDS : TRTRI_LDS;
+constexpr size_t PANEL_LDS = PANEL_LDS_ > SYRKW_LDS ? PANEL_LDS_ : SYRKW_LDS;
 
 __global__ __launch_bounds__(POTRF_THREADS) void k_panel(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ cols,
                                                          int ncol, const int32_t* __restrict__ trsm, int ntrsm,
@@ -1331,7 +1501,8 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_panel(double* __restrict__ S,
                                                          double* __restrict__ P, const int32_t* __restrict__ comb,
                                                          unsigned* __restrict__ cnt, unsigned* __restrict__ tflags,
                                                          const int32_t* __restrict__ wstart,
-                                                         const int32_t* __restrict__ wlist) {
+                                                         const int32_t* __restrict__ wlist,
+                                                         uint64_t* __restrict__ trace) {
     // workgroup order (every wait points to a lower index, so in-order dispatch always progresses):
     // [the previous level's updates of this level's diagonal blocks][potrf][its updates of this level's
     // panel blocks][panel solves][inverses of the previous level's blocks][its updates of later levels'
@@ -1339,23 +1510,45 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_panel(double* __restrict__ S,
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int b = blockIdx.x;
     const int e1 = ndiag, e2 = e1 + ncol, e3 = e2 + npanel, e4 = e3 + ntrsm, e5 = e4 + nprev;
+    // FBA_PANEL_TRACE: [start, after the waits, end, role, phase stamps] per workgroup (100 MHz wall clock)
+    uint64_t* tr = trace ? trace + 8 * (int64_t)b : nullptr;
+    if (tr && threadIdx.x == 0) tr[0] = wall_clock64();
+    int role;
     if (b < e1) {
-        syrk_body(S, ld, tasks + Sched::SYRK_REC * b, src, P, comb, cnt, tflags, smem);
+        role = 0;
+        if (tr && threadIdx.x == 0) {  // FBA_PANEL_TRACE: sources, split group
+            const int32_t* tk = tasks + Sched::SYRK_REC * b;
+            tr[1] = (uint64_t)(tk[4] - tk[3]) | (tk[5] >= 0 ? 0x100u : 0u);
+        }
+        syrk_body_wide(S, ld, tasks + Sched::SYRK_REC * b, src, P, comb, cnt, tflags, smem, tr);
     } else if (b < e2) {
+        role = 1;
         const int c = b - e1;
         if (ntask > 0) wait_list(wlist + wstart[c], wstart[c + 1] - wstart[c], tflags, scal);
+        if (tr && threadIdx.x == 0) tr[1] = wall_clock64();
         potrf_body<false>(S, ld, cols[c], dinv, scal, nullptr, flags + cols[c], smem);
     } else if (b < e3) {
-        syrk_body(S, ld, tasks + Sched::SYRK_REC * (b - ncol), src, P, comb, cnt, tflags, smem);
+        role = 2;
+        syrk_body_wide(S, ld, tasks + Sched::SYRK_REC * (b - ncol), src, P, comb, cnt, tflags, smem);
     } else if (b < e4) {
+        role = 3;
         const int t = b - e3;
         if (ntask > 0) wait_list(wlist + wstart[ncol + t], wstart[ncol + t + 1] - wstart[ncol + t], tflags, scal);
         const int32_t* rec = trsm + 2 * t;
-        trsm_body(S, ld, rec, dinv, flags + rec[0], scal, smem, progressive != 0);
+        trsm_body(S, ld, rec, dinv, flags + rec[0], scal, smem, progressive != 0, tr);
     } else if (b < e5) {
+        role = 4;
         trtri_body(S, ld, prev[b - e4], dinv, linv, smem);
     } else {
-        syrk_body(S, ld, tasks + Sched::SYRK_REC * (b - e5 + ndiag + npanel), src, P, comb, cnt, tflags, smem);
+        role = 5;
+        syrk_body_wide(S, ld, tasks + Sched::SYRK_REC * (b - e5 + ndiag + npanel), src, P, comb, cnt, tflags, smem);
+    }
+    if (tr) {  // uniform: the trace pointer is a kernel argument
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            tr[2] = wall_clock64();
+            tr[3] = (uint64_t)role;
+        }
     }
 }
 
@@ -1615,7 +1808,8 @@ int launch_cholesky(Ctx& c) {
                 c.d_scal, c.d_flags, (int)c.panel_progressive, U ? c.d_sched + U->tasks : nullptr, U ? U->ntask : 0,
                 U ? U->ndiag : 0, U ? U->npanel : 0, U ? c.d_sched + U->src : nullptr, c.d_P,
                 U ? c.d_sched + U->comb : nullptr,
-                U ? c.d_counters + U->cbase : nullptr, c.d_tflags, c.d_sched + W.wstart, c.d_sched + W.wlist);
+                U ? c.d_counters + U->cbase : nullptr, c.d_tflags, c.d_sched + W.wstart, c.d_sched + W.wlist,
+                c.d_ptrace ? c.d_ptrace + (int64_t)w * PTRACE_WG * 8 : nullptr);
         } else {
             k_potrf128<false><<<(unsigned)W.ncol, POTRF_THREADS, POTRF_LDS, c.stream>>>(c.d_S, ld, c.d_sched + W.cols,
                                                                                       c.d_dinv, c.d_scal, nullptr);

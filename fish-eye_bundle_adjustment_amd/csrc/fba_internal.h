@@ -17,6 +17,7 @@
 namespace fba {
 
 constexpr int NB = 128;       // Cholesky block size (rows/cols of one panel block, fba_chol.hip)
+constexpr int PTRACE_WG = 2048;  // FBA_PANEL_TRACE: workgroup slots per level
 constexpr int CHUNK_OBS = 256;  // observations per k_lin_reduce / k_lin_point workgroup (chunk)
 constexpr int CHUNK_PTS = 64;   // tie points per chunk
 constexpr int CHUNK_TERMS = 2048;  // co-visibility terms per chunk staged in LDS (a single larger point
@@ -142,6 +143,7 @@ struct Ctx {
     double* d_ppart = nullptr;       // [acc.n_pk][36] pair-block partials
     double* d_ipart = nullptr;       // [acc.n_ik][27 + 6 cw] image partials: diagonal block, RHS, image-camera
     uint64_t* d_lrprof = nullptr;    // FBA_LR_PROFILE: k_lin_reduce phase timestamps [n_chunks][8]
+    uint64_t* d_ptrace = nullptr;    // FBA_PANEL_TRACE: k_panel workgroup timestamps [level][PTRACE_WG][8]
     double* d_cpart = nullptr;       // [n_chunks][cw(cw+1)/2 + cw] camera-block partials
     int32_t* d_chunk_obs = nullptr;  // [n_chunks+1] observation range of each chunk
     int32_t* d_chunk_pt = nullptr;   // [n_chunks+1] local point range of each chunk
