@@ -162,8 +162,8 @@ def main():
 
     # rooflines, outside the timed region: one more step per probed kernel, HIP events around each of
     # its launches on the stream it runs on.  k_panel (one launch per elimination-tree level: the
-    # level's 128x128 diagonal factorisations and panel solves) has the largest share of GPU time, so
-    # it is `roofline`; k_syrk_multi (the level's bulk trailing update, 64x64 f64 MFMA tiles) follows.
+    # level's 128x128 diagonal factorisations, panel solves and the previous level's trailing updates)
+    # has the largest share of GPU time, so it is `roofline`.
     def probe(kind, name, note):
         ctx.set_probe(kind)
         step()
@@ -178,10 +178,14 @@ def main():
         r["frac"] = r["achieved"] / r["peak"] if r["achieved"] else None
         return r
     roof = probe(2, "k_panel", "one elimination-tree level: the 128x128 f64 diagonal-block potrf, the panel "
-                               "solves and (levels of <= 450 update tasks) the previous level's trailing updates "
-                               "as in-launch dataflow; a latency-bound chain, one launch per level")
-    roof_bulk = probe(1, "k_syrk_multi", "Cholesky trailing update of one of the large tree levels (> 450 "
-                                         "tasks, own launch), 64x64 f64 MFMA tiles, K = 128 per source column")
+                               "solves and the previous level's trailing updates as in-launch dataflow; a latency-"
+                               "bound chain, one launch per level")
+    # k_syrk_multi runs only for levels whose updates are not merged into the next level's k_panel
+    # (FBA_MERGE_MAX; by default every level's are)
+    roof_bulk = probe(1, "k_syrk_multi", "Cholesky trailing update of a level not merged into the next k_panel "
+                                         "(FBA_MERGE_MAX), 64x64 f64 MFMA tiles, K = 128 per source column")
+    if not roof_bulk["launches"]:
+        roof_bulk = None
     phase_roof = {"cholesky_dense_equiv_TFLOPs": chol_flops / (t["cholesky"] * 1e-3) / 1e12,
                   "linearize_accumulate_GBs": lin_bytes / ((t["linearize"] + t["accumulate"]) * 1e-3) / 1e9}
     value = args.steps / dt
@@ -198,7 +202,7 @@ def main():
         "phase_ms": {k: t[k] for k in names},
         "deltasum_last": dsum[-1] if dsum else None,
         "roofline": roof,
-        "roofline_bulk_update": roof_bulk,
+        **({"roofline_bulk_update": roof_bulk} if roof_bulk else {}),
         "phase_roofline": phase_roof,
     }
     ctx.close()

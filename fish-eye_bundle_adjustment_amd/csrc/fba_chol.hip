@@ -985,7 +985,9 @@ __device__ __forceinline__ void syrk_body(double* __restrict__ S, int64_t ld, co
         for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[a][b][r] = (slot < 0 && worker) ? Cp[(a * 16 + 4 * r) * ldc + b * 16] : 0.0;
-    const int rr = (tid & 255) >> 2, cc = (tid & 3) * 8;
+    // loader mapping: thread t of the first 256 -> rows (t >> 4) + 16 h, columns 2 (t & 15), 2 (t & 15) + 1 of
+    // the 32-deep slice: one wave instruction reads four whole 256-B row slices (8 cache lines)
+    const int rr = (tid & 255) >> 4, cc = (tid & 15) * 2;
     const double* ga = S + (r0 + rr) * ld + cc;
     const double* gb = S + (c0 + rr) * ld + cc;
     double2 pa[4], pb[4];
@@ -993,8 +995,8 @@ __device__ __forceinline__ void syrk_body(double* __restrict__ S, int64_t ld, co
         const int64_t kc = (int64_t)ks_src[0] * CB;
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
-            pa[h] = *reinterpret_cast<const double2*>(ga + kc + 2 * h);
-            pb[h] = *reinterpret_cast<const double2*>(gb + kc + 2 * h);
+            pa[h] = *reinterpret_cast<const double2*>(ga + (int64_t)(16 * h) * ld + kc);
+            pb[h] = *reinterpret_cast<const double2*>(gb + (int64_t)(16 * h) * ld + kc);
         }
     }
     for (int sl = 0; sl < nsl; ++sl) {
@@ -1002,8 +1004,8 @@ __device__ __forceinline__ void syrk_body(double* __restrict__ S, int64_t ld, co
         if (worker) {
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
-                As[rr][cc + 2 * h] = pa[h].x; As[rr][cc + 2 * h + 1] = pa[h].y;
-                Bs[rr][cc + 2 * h] = pb[h].x; Bs[rr][cc + 2 * h + 1] = pb[h].y;
+                As[rr + 16 * h][cc] = pa[h].x; As[rr + 16 * h][cc + 1] = pa[h].y;
+                Bs[rr + 16 * h][cc] = pb[h].x; Bs[rr + 16 * h][cc + 1] = pb[h].y;
             }
         }
         __syncthreads();
@@ -1012,8 +1014,8 @@ __device__ __forceinline__ void syrk_body(double* __restrict__ S, int64_t ld, co
                 const int64_t kc = (int64_t)ks_src[(sl + 1) >> 2] * CB + ((sl + 1) & 3) * KS;
 #pragma unroll
                 for (int h = 0; h < 4; ++h) {
-                    pa[h] = *reinterpret_cast<const double2*>(ga + kc + 2 * h);
-                    pb[h] = *reinterpret_cast<const double2*>(gb + kc + 2 * h);
+                    pa[h] = *reinterpret_cast<const double2*>(ga + (int64_t)(16 * h) * ld + kc);
+                    pb[h] = *reinterpret_cast<const double2*>(gb + (int64_t)(16 * h) * ld + kc);
                 }
             }
 #pragma unroll
@@ -1135,17 +1137,17 @@ __device__ __forceinline__ void syrk_body_wide(double* __restrict__ S, int64_t l
     for (int b = 0; b < 2; ++b)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[b][r] = slot < 0 ? Cp[(4 * r) * ldc + b * 16] : 0.0;
-    // loader mapping: thread t -> row t >> 3 of A and of B, columns 16 (t & 7) .. + 15
-    const int rr = tid >> 3, cc = (tid & 7) * 16;
-    const double* ga = S + (r0 + rr) * ld + cc;
-    const double* gb = S + (c0 + rr) * ld + cc;
+    // loader mapping: wave w loads rows w, w + 8, .. of A and of B, lane l columns 2l, 2l + 1: one wave
+    // instruction reads one whole 1 KB row (8 cache lines), 16 of them in flight per lane
+    const double* ga = S + (r0 + wave) * ld + 2 * lane;
+    const double* gb = S + (c0 + wave) * ld + 2 * lane;
     double2 pa[8], pb[8];
     auto load = [&](int k) {
         const int64_t kc = (int64_t)ks_src[k] * CB;
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
-            pa[h] = *reinterpret_cast<const double2*>(ga + kc + 2 * h);
-            pb[h] = *reinterpret_cast<const double2*>(gb + kc + 2 * h);
+            pa[h] = *reinterpret_cast<const double2*>(ga + (int64_t)(8 * h) * ld + kc);
+            pb[h] = *reinterpret_cast<const double2*>(gb + (int64_t)(8 * h) * ld + kc);
         }
     };
     load(0);
@@ -1153,8 +1155,8 @@ __device__ __forceinline__ void syrk_body_wide(double* __restrict__ S, int64_t l
         if (k > 0) __syncthreads();  // the previous source's panels are consumed
 #pragma unroll
         for (int h = 0; h < 8; ++h) {  // (component stores: a double2 struct copy kept the arrays in scratch)
-            As[rr][cc + 2 * h] = pa[h].x; As[rr][cc + 2 * h + 1] = pa[h].y;
-            Bs[rr][cc + 2 * h] = pb[h].x; Bs[rr][cc + 2 * h + 1] = pb[h].y;
+            As[wave + 8 * h][2 * lane] = pa[h].x; As[wave + 8 * h][2 * lane + 1] = pa[h].y;
+            Bs[wave + 8 * h][2 * lane] = pb[h].x; Bs[wave + 8 * h][2 * lane + 1] = pb[h].y;
         }
         __syncthreads();
         if (tr && tid == 0 && k == 0) tr[4] = wall_clock64();  // FBA_PANEL_TRACE: first panels in LDS
@@ -1943,7 +1945,11 @@ int chol_setup(Ctx& c) {
     c.bwd_flow = !(getenv("FBA_BWD_LEVELS") && atoi(getenv("FBA_BWD_LEVELS")) != 0);
     c.panel_progressive = !(getenv("FBA_PANEL_PROGRESSIVE") && atoi(getenv("FBA_PANEL_PROGRESSIVE")) == 0);
     c.merge_updates = !(getenv("FBA_MERGE_UPDATES") && atoi(getenv("FBA_MERGE_UPDATES")) == 0);
-    c.merge_max = getenv("FBA_MERGE_MAX") ? atoi(getenv("FBA_MERGE_MAX")) : 450;  // config 4: 0 -> 752, 300 -> 762, 400-500 -> 764, all -> 733 iter/s
+    // every level's trailing updates run inside the next level's k_panel (config 4: 968 iter/s merged
+    // at any size vs 931 with the levels of > 450 tasks in their own k_syrk_multi launch, now that the
+    // in-launch update runs on eight waves with coalesced whole-row loads; it measured the other way
+    // round with the earlier four-wave sliced update); FBA_MERGE_MAX caps the merged size
+    c.merge_max = getenv("FBA_MERGE_MAX") ? atoi(getenv("FBA_MERGE_MAX")) : (1 << 30);
     FBA_HIP(hipFuncSetAttribute((const void*)k_trtri128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRTRI_LDS));
 
     c.probe_ev.assign(2 * std::max(c.sched.n_waves, 1), nullptr);

@@ -182,7 +182,7 @@ struct Ctx {
     int64_t n_sync = 0;           // unsigned words of flags + bflags + counters (one allocation at d_flags,
                                   // zeroed by k_finish_rhs ahead of every factorisation)
     bool bwd_flow = true;
-    int merge_max = 450;            // ... for levels of at most this many update tasks (FBA_MERGE_MAX)
+    int merge_max = 1 << 30;        // ... for levels of at most this many update tasks (FBA_MERGE_MAX)
     bool merge_updates = true;      // a level's trailing updates inside the next level's k_panel
                                     // (FBA_MERGE_UPDATES=0: their own k_syrk_multi launch)
     bool panel_progressive = true;  // k_panel: panel solves step with the potrf's published column blocks
