@@ -653,15 +653,18 @@ static int accumulate_body(Ctx* c) {
         std::vector<uint64_t> tp(8 * c->n_chunks);
         FBA_HIP(hipMemcpyAsync(tp.data(), c->d_lrprof, sizeof(uint64_t) * tp.size(), hipMemcpyDeviceToHost, c->stream));
         FBA_HIP(hipStreamSynchronize(c->stream));
-        double ph[5] = {0, 0, 0, 0, 0};
+        double ph[6] = {0, 0, 0, 0, 0, 0};
         uint64_t lo = UINT64_MAX, hi = 0;
         for (int64_t ch = 0; ch < c->n_chunks; ++ch) {
-            for (int i = 0; i < 5; ++i) ph[i] += (double)(tp[8 * ch + i + 1] - tp[8 * ch + i]) * 0.01 / (double)c->n_chunks;
-            lo = std::min(lo, tp[8 * ch]);
-            hi = std::max(hi, tp[8 * ch + 5]);
+            const uint64_t* q = &tp[8 * ch];
+            for (int i = 0; i < 4; ++i) ph[i] += (double)(q[i + 1] - q[i]) * 0.01 / (double)c->n_chunks;
+            ph[4] += (double)(q[6] - q[4]) * 0.01 / (double)c->n_chunks;  // image keys
+            ph[5] += (double)(q[5] - q[6]) * 0.01 / (double)c->n_chunks;  // pair keys
+            lo = std::min(lo, q[0]);
+            hi = std::max(hi, q[5]);
         }
         fprintf(stderr, "[fba] k_lin_reduce per chunk (us): model %.2f points %.2f couplings %.2f stage+camera %.2f "
-                "items %.2f; span %.1f\n", ph[0], ph[1], ph[2], ph[3], ph[4], (double)(hi - lo) * 0.01);
+                "image keys %.2f pair keys %.2f; span %.1f\n", ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], (double)(hi - lo) * 0.01);
     }
     if (c->opt.world > 1 && (rc = launch_pack(*c, 0))) return rc;
     mark(c, 3);

@@ -23,6 +23,14 @@
 
 namespace fba {
 
+// lane-permuted copy of a double within rows of the wave (DPP control CTRL: quad_perm, row_half_mirror)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
 
 // ------------------------------------------------------------------------------------------------
 // k_params: per-image and per-camera tables
@@ -645,14 +653,15 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     // xor-butterfly over the 8 lanes; part-major unit order keeps the rows of a wave on one path
     constexpr int HALF = (CW + 1) / 2;
     constexpr int IV = 27 > 6 * HALF ? 27 : 6 * HALF;  // values per unit
+    constexpr int NV = (IV + 7) / 8 * 8, M = NV / 8;     // padded to the 8-lane reduce-scatter
     {
         const int nk = ki1 - ki0, nu = 3 * nk, g8 = t & 7;
         for (int ub = t >> 3; ub < nu && !(dbg & 1); ub += LR_THREADS / 8) {
             const int part = ub / nk, K = ki0 + ub % nk;
             const int x0 = s_iko[K - ki0], x1 = s_iko[K - ki0 + 1];
-            double v[IV];
+            double v[NV];
 #pragma unroll
-            for (int q = 0; q < IV; ++q) v[q] = 0.0;
+            for (int q = 0; q < NV; ++q) v[q] = 0.0;
             for (int x = x0 + g8; x < x1; x += 8) {
                 const int l = s_ikobs[x];
                 const double* E = QE + l * ES;
@@ -697,28 +706,40 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
                     }
                 }
             }
+            // reduce-scatter over the group's 8 lanes in three DPP exchange steps (partners 7 - i, i ^ 2,
+            // i ^ 1): each step a lane keeps half of its values, adds the partner's copy of that half and
+            // hands over the other half, so lane g8 ends with the M fully summed values
+            // q = 4M b2 + 2M b1 + M b0 + j (b = bits of g8), in a fixed order
+            double h4[4 * M], h2[2 * M], h1[M];
+            const bool bA = (g8 & 4) != 0, bB = (g8 & 2) != 0, bC = (g8 & 1) != 0;
 #pragma unroll
-            for (int q = 0; q < IV; ++q) {  // fixed butterfly over the group's 8 lanes
-                double w = v[q];
-                w += __shfl_xor(w, 4, 8);
-                w += __shfl_xor(w, 2, 8);
-                w += __shfl_xor(w, 1, 8);
-                v[q] = w;
+            for (int j = 0; j < 4 * M; ++j) {
+                const double keep = bA ? v[4 * M + j] : v[j], give = bA ? v[j] : v[4 * M + j];
+                h4[j] = keep + dpp_d<0x141>(give);  // row_half_mirror
             }
-            double* out = ipart + (int64_t)K * NIMG;
-            if (part == 0) {
 #pragma unroll
-                for (int q = 0; q < 27; ++q)
-                    if ((q & 7) == g8) out[q] = v[q];
-            } else {
-                const int q0 = (part - 1) * HALF;
-#pragma unroll
-                for (int q = 0; q < HALF; ++q)
-#pragma unroll
-                    for (int aa = 0; aa < 6; ++aa)
-                        if (q0 + q < CW && ((6 * q + aa) & 7) == g8) out[27 + 6 * (q0 + q) + aa] = v[6 * q + aa];
+            for (int j = 0; j < 2 * M; ++j) {
+                const double keep = bB ? h4[2 * M + j] : h4[j], give = bB ? h4[j] : h4[2 * M + j];
+                h2[j] = keep + dpp_d<0x4E>(give);  // quad_perm [2,3,0,1]
             }
+#pragma unroll
+            for (int j = 0; j < M; ++j) {
+                const double keep = bC ? h2[M + j] : h2[j], give = bC ? h2[j] : h2[M + j];
+                h1[j] = keep + dpp_d<0xB1>(give);  // quad_perm [1,0,3,2]
+            }
+            const int q0 = (bA ? 4 * M : 0) + (bB ? 2 * M : 0) + (bC ? M : 0);
+            // part 0: the 27 values at out[0 ..]; parts 1, 2: the 6 nq values of cameras columns
+            // (part - 1) HALF .. at out[27 + 6 (part - 1) HALF ..]
+            const int nval = part == 0 ? 27 : 6 * min(HALF, CW - (part - 1) * HALF);
+            double* out = ipart + (int64_t)K * NIMG + (part == 0 ? 0 : 27 + 6 * (part - 1) * HALF);
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+                if (q0 + j < nval) out[q0 + j] = h1[j];
         }
+    }
+    if (tprof) {  // FBA_LR_PROFILE: image keys and pair keys timed apart (a barrier the real run does not have)
+        __syncthreads();
+        stamp(6);
     }
     // pair keys: one thread per (key, rows 2h, 2h+1) of the pair block, outputs in registers; the term
     // lists from LDS (staged above) or, for a chunk of one very large point, from HBM
