@@ -469,6 +469,39 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     const int p0 = chunk_pt[c], p1 = chunk_pt[c + 1];
     const int o = o0 + t;
     const bool active = t < CHUNK_OBS && o < o1;
+    // the chunk's plan lists, staged in LDS for (D) (every inner loop then runs out of LDS; the terms
+    // of a chunk holding one point with more than CHUNK_TERMS of them stay in HBM) by the threads
+    // (A) leaves idle, while (A) runs
+    const int kp0 = A[plan.ck_pk + c], kp1 = A[plan.ck_pk + c + 1];
+    const int ki0 = A[plan.ck_ik + c], ki1 = A[plan.ck_ik + c + 1];
+    const int tb0 = A[plan.pk_t + kp0], ntm = A[plan.pk_t + kp1] - tb0;
+    const int ob0 = A[plan.ik_o + ki0], nio = A[plan.ik_o + ki1] - ob0;
+    const bool stage_terms = ntm <= CHUNK_TERMS;
+    if (t >= CHUNK_OBS) {  // the threads the linearisation leaves idle, 8 loads each in flight
+        constexpr int NS = LR_THREADS - CHUNK_OBS;
+        const int u = t - CHUNK_OBS;
+        auto stage = [&](int n, const int32_t* __restrict__ src, int sub, int* __restrict__ dst) {
+            for (int i0 = 0; i0 < n; i0 += 8 * NS) {
+                int v[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int i = i0 + u + NS * q;
+                    v[q] = i < n ? src[i] : 0;
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int i = i0 + u + NS * q;
+                    if (i < n) dst[i] = v[q] - sub;
+                }
+            }
+        };
+        if (stage_terms) {
+            stage(kp1 - kp0 + 1, A + plan.pk_t + kp0, tb0, s_pkt);
+            stage(ntm, A + plan.pk_term + tb0, 0, s_term);
+        }
+        stage(ki1 - ki0 + 1, A + plan.ik_o + ki0, ob0, s_iko);
+        stage(nio, A + plan.ik_obs + ob0, 0, s_ikobs);
+    }
     double jr[2][NJ];
     double w0 = 0.0, w1 = 0.0;
     int p = -1;
@@ -500,24 +533,29 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     if (t < CHUNK_OBS) pl[t] = (active && p >= 0) ? p - p0 : -1;
     __syncthreads();
     stamp(1);
-    // (B)
-    if (t < p1 - p0) {
-        const int lp = p0 + t;
+    // (B) four lanes per point (g = t & 3): lane g accumulates the point's observations g, g + 4, ..;
+    // V and b are all-reduced over the four lanes, the camera couplings Wc reduce-scattered (lane g
+    // keeps camera columns [CWQ g', CWQ g' + CWQ)), each by two DPP exchange steps in a fixed order;
+    // every lane then forms V^-1 and the factor R, and the outputs of its own Wc columns
+    if (t < 4 * (p1 - p0)) {
+        constexpr int CWQ = (CW + 3) / 4, CWP = 4 * CWQ;  // columns per lane, padded count
+        const int g = t & 3, tp = t >> 2;
+        const int lp = p0 + tp;
         const int a0 = lp_start[lp] - o0, a1 = lp_start[lp + 1] - o0;
-        double V00 = 0, V01 = 0, V02 = 0, V11 = 0, V12 = 0, V22 = 0, b0 = 0, b1 = 0, b2 = 0;
-        double Wc[CW][3];
+        double V[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // V00 V01 V02 V11 V12 V22 b0 b1 b2
+        double Wc[CWP][3];
 #pragma unroll
-        for (int q = 0; q < CW; ++q) Wc[q][0] = Wc[q][1] = Wc[q][2] = 0.0;
-        for (int i = a0; i < a1; ++i) {
+        for (int q = 0; q < CWP; ++q) Wc[q][0] = Wc[q][1] = Wc[q][2] = 0.0;
+        for (int i = a0 + g; i < a1; i += 4) {
             const double* r = QE + i * ES;
 #pragma unroll
             for (int row = 0; row < 2; ++row) {
                 const double pr = row ? py : px;
                 const double j0 = r[3 * row], j1 = r[3 * row + 1], j2 = r[3 * row + 2], wv = r[6 + row];
                 const double q0 = pr * j0, q1 = pr * j1, q2 = pr * j2;
-                V00 += q0 * j0; V01 += q0 * j1; V02 += q0 * j2;
-                V11 += q1 * j1; V12 += q1 * j2; V22 += q2 * j2;
-                b0 += q0 * wv; b1 += q1 * wv; b2 += q2 * wv;
+                V[0] += q0 * j0; V[1] += q0 * j1; V[2] += q0 * j2;
+                V[3] += q1 * j1; V[4] += q1 * j2; V[5] += q2 * j2;
+                V[6] += q0 * wv; V[7] += q1 * wv; V[8] += q2 * wv;
 #pragma unroll
                 for (int q = 0; q < CW; ++q) {
                     const double jc = r[8 + row * CW + q];
@@ -525,39 +563,66 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
                 }
             }
         }
+#pragma unroll
+        for (int m = 0; m < 9; ++m) {
+            V[m] += dpp_d<0x4E>(V[m]);  // quad_perm [2,3,0,1]
+            V[m] += dpp_d<0xB1>(V[m]);  // quad_perm [1,0,3,2]
+        }
+        const bool hA = (g & 2) != 0, hB = (g & 1) != 0;
+        double W2[2 * CWQ][3], W1[CWQ][3];
+#pragma unroll
+        for (int q = 0; q < 2 * CWQ; ++q)
+#pragma unroll
+            for (int m = 0; m < 3; ++m) {
+                const double keep = hA ? Wc[2 * CWQ + q][m] : Wc[q][m], give = hA ? Wc[q][m] : Wc[2 * CWQ + q][m];
+                W2[q][m] = keep + dpp_d<0x4E>(give);
+            }
+#pragma unroll
+        for (int q = 0; q < CWQ; ++q)
+#pragma unroll
+            for (int m = 0; m < 3; ++m) {
+                const double keep = hB ? W2[CWQ + q][m] : W2[q][m], give = hB ? W2[q][m] : W2[CWQ + q][m];
+                W1[q][m] = keep + dpp_d<0xB1>(give);
+            }
+        const int qb = (hA ? 2 * CWQ : 0) + (hB ? CWQ : 0);  // this lane's first camera column
+        const double V00 = V[0], V01 = V[1], V02 = V[2], V11 = V[3], V12 = V[4], V22 = V[5];
+        const double b0 = V[6], b1 = V[7], b2 = V[8];
         // symmetric 3x3 inverse (adjugate)
         const double c00 = V11 * V22 - V12 * V12, c01 = V02 * V12 - V01 * V22, c02 = V01 * V12 - V02 * V11;
         const double id = 1.0 / (V00 * c00 + V01 * c01 + V02 * c02);
         const double I00 = c00 * id, I01 = c01 * id, I02 = c02 * id;
         const double I11 = (V00 * V22 - V02 * V02) * id, I12 = (V01 * V02 - V00 * V12) * id,
                      I22 = (V00 * V11 - V01 * V01) * id;
-        double* P = PT + (int64_t)lp * PS;
-        P[6] = I00 * b0 + I01 * b1 + I02 * b2;
-        P[7] = I01 * b0 + I11 * b1 + I12 * b2;
-        P[8] = I02 * b0 + I12 * b1 + I22 * b2;
-#pragma unroll
-        for (int q = 0; q < CW; ++q) {
-            P[12 + 3 * CW + 3 * q] = Wc[q][0] * I00 + Wc[q][1] * I01 + Wc[q][2] * I02;
-            P[13 + 3 * CW + 3 * q] = Wc[q][0] * I01 + Wc[q][1] * I11 + Wc[q][2] * I12;
-            P[14 + 3 * CW + 3 * q] = Wc[q][0] * I02 + Wc[q][1] * I12 + Wc[q][2] * I22;
-        }
         // V = L L', R = L^-T (upper): r00 = m00, r01 = m10, r02 = m20, r11 = m11, r12 = m21, r22 = m22
         const double l00 = sqrt(V00), l10 = V01 / l00, l20 = V02 / l00;
         const double l11 = sqrt(V11 - l10 * l10), l21 = (V12 - l20 * l10) / l11;
         const double l22 = sqrt(V22 - l20 * l20 - l21 * l21);
         const double m00 = 1.0 / l00, m11 = 1.0 / l11, m22 = 1.0 / l22;
         const double m10 = -l10 * m00 * m11, m21 = -l21 * m11 * m22, m20 = -(l20 * m00 + l21 * m10) * m22;
-        double* pp = PP + t * PPS;
-        pp[0] = I00; pp[1] = I01; pp[2] = I02; pp[3] = I11; pp[4] = I12; pp[5] = I22;
-        pp[6] = m00; pp[7] = m10; pp[8] = m20; pp[9] = m11; pp[10] = m21; pp[11] = m22;
-        pp[12] = m00 * b0;
-        pp[13] = m10 * b0 + m11 * b1;
-        pp[14] = m20 * b0 + m21 * b1 + m22 * b2;
+        double* P = PT + (int64_t)lp * PS;
+        double* pp = PP + tp * PPS;
+        if (g == 0) {
+            P[6] = I00 * b0 + I01 * b1 + I02 * b2;
+            P[7] = I01 * b0 + I11 * b1 + I12 * b2;
+            P[8] = I02 * b0 + I12 * b1 + I22 * b2;
+            pp[0] = I00; pp[1] = I01; pp[2] = I02; pp[3] = I11; pp[4] = I12; pp[5] = I22;
+            pp[6] = m00; pp[7] = m10; pp[8] = m20; pp[9] = m11; pp[10] = m21; pp[11] = m22;
+            pp[12] = m00 * b0;
+            pp[13] = m10 * b0 + m11 * b1;
+            pp[14] = m20 * b0 + m21 * b1 + m22 * b2;
+        }
 #pragma unroll
-        for (int q = 0; q < CW; ++q) {
-            pp[15 + 3 * q] = Wc[q][0] * m00;
-            pp[16 + 3 * q] = Wc[q][0] * m10 + Wc[q][1] * m11;
-            pp[17 + 3 * q] = Wc[q][0] * m20 + Wc[q][1] * m21 + Wc[q][2] * m22;
+        for (int u = 0; u < CWQ; ++u) {
+            const int q = qb + u;
+            if (q < CW) {
+                const double w0_ = W1[u][0], w1_ = W1[u][1], w2_ = W1[u][2];
+                P[12 + 3 * CW + 3 * q] = w0_ * I00 + w1_ * I01 + w2_ * I02;
+                P[13 + 3 * CW + 3 * q] = w0_ * I01 + w1_ * I11 + w2_ * I12;
+                P[14 + 3 * CW + 3 * q] = w0_ * I02 + w1_ * I12 + w2_ * I22;
+                pp[15 + 3 * q] = w0_ * m00;
+                pp[16 + 3 * q] = w0_ * m10 + w1_ * m11;
+                pp[17 + 3 * q] = w0_ * m20 + w1_ * m21 + w2_ * m22;
+            }
         }
     }
     __syncthreads();
@@ -598,18 +663,8 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     }
     __syncthreads();
     stamp(3);
-    // (D) camera entries first (the longest items), then image keys, then pair keys.  The chunk's
-    // plan lists are staged in LDS first (every inner loop then runs out of LDS); the terms of a
-    // chunk holding one point with more than CHUNK_TERMS of them stay in HBM.
-    const int kp0 = A[plan.ck_pk + c], kp1 = A[plan.ck_pk + c + 1];
-    const int ki0 = A[plan.ck_ik + c], ki1 = A[plan.ck_ik + c + 1];
-    const int tb0 = A[plan.pk_t + kp0], ntm = A[plan.pk_t + kp1] - tb0;
-    const int ob0 = A[plan.ik_o + ki0], nio = A[plan.ik_o + ki1] - ob0;
-    const bool stage_terms = ntm <= CHUNK_TERMS;
-    for (int i = t; i <= kp1 - kp0 && stage_terms; i += LR_THREADS) s_pkt[i] = A[plan.pk_t + kp0 + i] - tb0;
-    for (int i = t; i < ntm && stage_terms; i += LR_THREADS) s_term[i] = A[plan.pk_term + tb0 + i];
-    for (int i = t; i <= ki1 - ki0; i += LR_THREADS) s_iko[i] = A[plan.ik_o + ki0 + i] - ob0;
-    for (int i = t; i < nio; i += LR_THREADS) s_ikobs[i] = A[plan.ik_obs + ob0 + i];
+    // (D) camera entries first (the longest items), then image keys, then pair keys (the plan lists
+    // were staged in LDS before (A)).
     const int nob = o1 - o0, np = p1 - p0;
     // camera entries: CAM_SPLIT observation sub-ranges in parallel
     if (t < CAM_SPLIT * NCAM) {
