@@ -334,10 +334,10 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     c->n_lp_pad = round_up(std::max<int64_t>(c->n_lp, 1), 64);
 
     // chunks (one k_lin_reduce / k_lin_point workgroup each): consecutive whole tie points of one
-    // camera, <= CHUNK_OBS observations and <= CHUNK_PTS points, then control observations of one
+    // camera, <= CHUNK_OBS observations and <= chunk_pts(nK) points, then control observations of one
     // camera, <= CHUNK_OBS at a time
     std::vector<int32_t> chunk_obs{0}, chunk_pt{0};
-    int64_t chunk_terms = 0;
+    int64_t cur_terms = 0;
     for (int64_t lp = 0; lp < c->n_lp; ++lp) {
         if (lp_start[lp + 1] - lp_start[lp] > CHUNK_OBS) {
             set_error("a tie point with more than 256 observations: not implemented in this build");
@@ -347,14 +347,14 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         const int64_t n_lp_obs = lp_start[lp + 1] - lp_start[lp];
         const int64_t lp_terms = n_lp_obs * (n_lp_obs - 1) / 2;
         const bool split = lp > chunk_pt.back() &&
-                           (lp_start[lp + 1] - chunk_obs.back() > CHUNK_OBS || lp - chunk_pt.back() >= CHUNK_PTS ||
-                            lp_cam[lp] != lp_cam[lp - 1] || chunk_terms + lp_terms > CHUNK_TERMS);
+                           (lp_start[lp + 1] - chunk_obs.back() > CHUNK_OBS || lp - chunk_pt.back() >= chunk_pts(L.nk) ||
+                            lp_cam[lp] != lp_cam[lp - 1] || cur_terms + lp_terms > chunk_terms(L.nk));
         if (split) {
             chunk_obs.push_back(lp_start[lp]);
             chunk_pt.push_back((int32_t)lp);
-            chunk_terms = 0;
+            cur_terms = 0;
         }
-        chunk_terms += lp_terms;
+        cur_terms += lp_terms;
     }
     if (c->n_lp > 0) {
         chunk_obs.push_back(lp_start[c->n_lp]);

@@ -19,9 +19,11 @@ namespace fba {
 constexpr int NB = 128;       // Cholesky block size (rows/cols of one panel block, fba_chol.hip)
 constexpr int PTRACE_WG = 2048;  // FBA_PANEL_TRACE: workgroup slots per level
 constexpr int CHUNK_OBS = 256;  // observations per k_lin_reduce / k_lin_point workgroup (chunk)
-constexpr int CHUNK_PTS = 64;   // tie points per chunk
-constexpr int CHUNK_TERMS = 2048;  // co-visibility terms per chunk staged in LDS (a single larger point
-                                   // is read from HBM instead)
+// tie points per chunk and co-visibility terms per chunk staged in LDS (a single larger point's are
+// read from HBM instead): smaller for nK >= 6, whose wider Jacobian rows leave less of the 160 KiB LDS
+// (k_lin_reduce's LR<NK>::LDS, static_assert there); the host chunking uses the same numbers
+constexpr int chunk_pts(int nk) { return nk <= 5 ? 64 : 32; }
+constexpr int chunk_terms(int nk) { return nk <= 5 ? 2048 : 1024; }
 
 // per-image device table (k_params): eop[6], M[9], dM/domega[9], dM/dphi[9], dM/dkappa[9], pad
 constexpr int IMG_TAB = 48;

@@ -402,17 +402,19 @@ __constant__ int c_tri_b[21] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4, 0, 
 template <int NK>
 struct LR {
     static constexpr int CW = 5 + NK;
-    static constexpr int ES = 15 + 2 * CW;          // per-observation staging stride (doubles)
-    static constexpr int US = 19;                   // U row stride
+    static constexpr int ES = 16 + 2 * CW;          // per-observation staging stride (doubles; even: 16-B aligned rows)
+    static constexpr int US = 20;                   // U row stride (16-B aligned rows: ds_read_b128)
     static constexpr int PPS = 15 + 3 * CW;         // per-point: Vinv 6 | R 6 | rb 3 | Uc 3CW
     static constexpr int NIMG = 27 + 6 * CW;        // image partial: 21 lower + 6 RHS + 6CW image-camera
     static constexpr int NCAM = CW * (CW + 1) / 2 + CW;
     // + ints: point of each observation, the chunk's plan (pair-key term offsets, terms, image-key
     // observation offsets, observations)
-    static constexpr int NI = CHUNK_OBS + (CHUNK_TERMS + 1) + CHUNK_TERMS + (CHUNK_OBS + 1) + CHUNK_OBS;
+    static constexpr int CP = chunk_pts(NK), CT = chunk_terms(NK);
+    static constexpr int NI = CHUNK_OBS + (CT + 1) + CT + (CHUNK_OBS + 1) + CHUNK_OBS;
     static constexpr int CAM_SPLIT = 512 / NCAM;   // camera entries: observation sub-ranges in parallel
-    static constexpr size_t LDS = sizeof(double) * (CHUNK_OBS * ES + CHUNK_OBS * US + CHUNK_PTS * PPS + 512) +
+    static constexpr size_t LDS = sizeof(double) * (CHUNK_OBS * ES + CHUNK_OBS * US + CP * PPS + 512) +
                                   sizeof(int) * NI;
+    static_assert(LDS <= 160 * 1024, "k_lin_reduce LDS over the 160 KiB of a CU");
 };
 
 constexpr int LR_THREADS = 512;  // observation phases use the first CHUNK_OBS threads, (D) all of them
@@ -456,12 +458,12 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* QE = lds;                                  // [CHUNK_OBS][ES]
     double* Us = QE + CHUNK_OBS * ES;                  // [CHUNK_OBS][US]
-    double* PP = Us + CHUNK_OBS * US;                  // [CHUNK_PTS][PPS]
-    double* camp = PP + CHUNK_PTS * PPS;                     // [CAM_SPLIT][NCAM] camera sub-range sums
+    double* PP = Us + CHUNK_OBS * US;                  // [CP][PPS]
+    double* camp = PP + R_::CP * PPS;                        // [CAM_SPLIT][NCAM] camera sub-range sums
     int* pl = reinterpret_cast<int*>(camp + 512);            // [CHUNK_OBS] chunk-local point or -1
-    int* s_pkt = pl + CHUNK_OBS;                             // [<= CHUNK_TERMS + 1] term offsets of the pair keys
-    int* s_term = s_pkt + CHUNK_TERMS + 1;                   // [<= CHUNK_TERMS]
-    int* s_iko = s_term + CHUNK_TERMS;                       // [<= CHUNK_OBS + 1] observation offsets of image keys
+    int* s_pkt = pl + CHUNK_OBS;                             // [<= CT + 1] term offsets of the pair keys
+    int* s_term = s_pkt + R_::CT + 1;                        // [<= CT]
+    int* s_iko = s_term + R_::CT;                            // [<= CHUNK_OBS + 1] observation offsets of image keys
     int* s_ikobs = s_iko + CHUNK_OBS + 1;                    // [<= CHUNK_OBS]
     const int t = threadIdx.x;
     const int c = blockIdx.x;
@@ -470,13 +472,13 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     const int o = o0 + t;
     const bool active = t < CHUNK_OBS && o < o1;
     // the chunk's plan lists, staged in LDS for (D) (every inner loop then runs out of LDS; the terms
-    // of a chunk holding one point with more than CHUNK_TERMS of them stay in HBM) by the threads
+    // of a chunk holding one point with more than CT of them stay in HBM) by the threads
     // (A) leaves idle, while (A) runs
     const int kp0 = A[plan.ck_pk + c], kp1 = A[plan.ck_pk + c + 1];
     const int ki0 = A[plan.ck_ik + c], ki1 = A[plan.ck_ik + c + 1];
     const int tb0 = A[plan.pk_t + kp0], ntm = A[plan.pk_t + kp1] - tb0;
     const int ob0 = A[plan.ik_o + ki0], nio = A[plan.ik_o + ki1] - ob0;
-    const bool stage_terms = ntm <= CHUNK_TERMS;
+    const bool stage_terms = ntm <= R_::CT;
     if (t >= CHUNK_OBS) {  // the threads the linearisation leaves idle, 8 loads each in flight
         constexpr int NS = LR_THREADS - CHUNK_OBS;
         const int u = t - CHUNK_OBS;

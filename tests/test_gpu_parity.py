@@ -99,6 +99,25 @@ def test_adjust_synthetic_types(fba, oracle, tmp_path, typ):
     assert res.sigma02 == pytest.approx(ro.sigma02, rel=1e-9)
 
 
+@pytest.mark.parametrize("nk", [1, 3, 6, 7, 8])
+def test_adjust_synthetic_radial_terms(fba, oracle, tmp_path, nk):
+    """Num_Radial_Distortions other than the bundled 5 (BuildAwG.m:18-20, :424-438): nK >= 6 takes the
+    smaller k_lin_reduce chunk capacities (chunk_pts / chunk_terms) that keep its LDS within 160 KiB."""
+    from fba_amd import synth
+    sc = synth.generate(12, 240, seed=23, typ="fisheye")
+    folder = synth.write_folder(sc, str(tmp_path / f"nk{nk}"), nk=nk)
+    ds = fba.load_folder(folder)
+    od = oracle.load_folder(folder)
+    ro = oracle.adjust(od)
+    res = fba.adjust(ds)
+    assert res.iterations == ro.iterations
+    err = group_rel_err(res.xhat, ro.xhat, ro.names, ro.dist_scaling)
+    spread = solver_spread(oracle, od, ro)
+    for g, e in err.items():  # 1e-9, or 20x the restatement's own rounding spread (high K_j are weak)
+        assert e <= max(1e-9, 20 * spread[g]), (g, e, spread[g])
+    assert res.sigma02 == pytest.approx(ro.sigma02, rel=max(1e-9, 20 * spread["sigma02"]))
+
+
 def test_step_is_deterministic(fba, cam0_folders):
     ds = fba.load_folder(cam0_folders["stage3_fisheye"])
     out = []
