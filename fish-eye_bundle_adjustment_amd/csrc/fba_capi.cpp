@@ -568,8 +568,9 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     if (getenv("FBA_LR_PROFILE") && c->n_chunks > 0) FBA_HIP(hipMalloc((void**)&c->d_lrprof, sizeof(uint64_t) * 8 * c->n_chunks));
     if (getenv("FBA_PANEL_TRACE") && c->sched.n_waves > 0)
     {
-        FBA_HIP(hipMalloc((void**)&c->d_ptrace, sizeof(uint64_t) * 8 * PTRACE_WG * c->sched.n_waves));
-        FBA_HIP(hipMemset(c->d_ptrace, 0, sizeof(uint64_t) * 8 * PTRACE_WG * c->sched.n_waves));
+        const size_t nt = std::max<size_t>((size_t)PTRACE_WG * c->sched.n_waves, (size_t)c->sched.flow_n * FTRACE / 8);
+        FBA_HIP(hipMalloc((void**)&c->d_ptrace, sizeof(uint64_t) * 8 * nt));
+        FBA_HIP(hipMemset(c->d_ptrace, 0, sizeof(uint64_t) * 8 * nt));
     }
     FBA_HIP(hipMemset(c->d_delta, 0, sizeof(double) * L.u_full));
     // outside the factor's block pattern S stays zero; the pattern itself is zeroed per accumulation
@@ -708,7 +709,52 @@ static int solve_enqueue(Ctx* c) {
 // FBA_PANEL_TRACE: one line per elimination-tree level, times in us from the first k_panel's start:
 // launch span, the gap after the previous launch, and per workgroup role the last end (diagonal-block
 // updates, potrf start / after its waits / end, panel solves, inverses, other updates)
+// k_chol_flow (FBA_PANEL_TRACE=1): per diagonal-block record, times in us from the launch's first start:
+// start, waits done, fused panel solve + diagonal update done, late partials added, end (potrf done);
+// then per role the record count and the last end
+static void print_flow_trace(Ctx* c) {
+    const Sched& s = c->sched;
+    std::vector<uint64_t> t((size_t)FTRACE * s.flow_n);
+    if (hipMemcpy(t.data(), c->d_ptrace, t.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return;
+    uint64_t t0 = UINT64_MAX;
+    for (int b = 0; b < s.flow_n; ++b)
+        if (t[FTRACE * (size_t)b]) t0 = std::min(t0, t[FTRACE * (size_t)b]);
+    const uint64_t M = (1ull << 63) - 1;
+    auto us = [&](uint64_t v) { return (v & M) ? (double)((v & M) - t0) * 0.01 : -1.0; };
+    uint64_t rend[4] = {0, 0, 0, 0};
+    int rn[4] = {0, 0, 0, 0};
+    const int32_t* recs = s.buf.data() + s.flow_rec;
+    const bool detail = getenv("FBA_PANEL_TRACE")[0] == '2';
+    for (int b = 0; b < s.flow_n; ++b) {
+        const uint64_t* r = &t[FTRACE * (size_t)b];
+        const int32_t* rec = recs + (size_t)Sched::FLOW_REC * b;
+        const int role = rec[0];
+        rend[role] = std::max(rend[role], r[2]);
+        rn[role]++;
+        if (role != 0) continue;
+        fprintf(stderr, "[fba]   diag wg %5d block %3d (fused %3d%s): start %7.1f  waits %7.1f  fused %7.1f  late %7.1f  end %7.1f\n",
+                b, rec[1], rec[2], rec[6] > 0 ? ", late" : "", us(r[0]), us(r[1]), rec[2] >= 0 ? us(r[4]) : -1.0,
+                rec[2] >= 0 ? us(r[5]) : -1.0, us(r[2]));
+        if (!detail || rec[2] < 0) continue;
+        fprintf(stderr, "[fba]       block in LDS / applied:");
+        for (int q = 0; q < 8; ++q) fprintf(stderr, " %.1f/%.1f%s", us(r[8 + q]), us(r[16 + q]), (r[16 + q] >> 63) ? "p" : "");
+        fprintf(stderr, "\n");
+        for (int x = 0; x < s.flow_n; ++x) {  // the panel halves of its fused rows
+            const int32_t* rx = recs + (size_t)Sched::FLOW_REC * x;
+            const uint64_t* q = &t[FTRACE * (size_t)x];
+            if (!(rx[0] == 1 && rx[1] == rec[2] && (rx[2] >> 1) == rec[1])) continue;
+            fprintf(stderr, "[fba]       half %d wg %5d: column in / published:", rx[2] & 1, x);
+            for (int u = 0; u < 8; ++u) fprintf(stderr, " %.1f/%.1f", us(q[8 + u]), us(q[16 + u]));
+            fprintf(stderr, "  end %.1f\n", us(q[2]));
+        }
+    }
+    fprintf(stderr, "[fba] flow: diag %d (last end %.1f), panel halves %d (%.1f), updates %d (%.1f), inverses %d (%.1f)\n", rn[0],
+            us(rend[0]), rn[1], us(rend[1]), rn[2], us(rend[2]), rn[3], us(rend[3]));
+    (void)hipMemset(c->d_ptrace, 0, t.size() * sizeof(uint64_t));
+}
+
 static void print_panel_trace(Ctx* c) {
+    if (c->chol_flow && c->sched.flow_ok && c->sched.flow_n > 0) { print_flow_trace(c); return; }
     const int nw = c->sched.n_waves;
     std::vector<uint64_t> t((size_t)8 * PTRACE_WG * nw);
     if (hipMemcpy(t.data(), c->d_ptrace, t.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return;

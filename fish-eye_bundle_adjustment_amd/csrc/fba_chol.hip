@@ -489,7 +489,8 @@ __device__ __forceinline__ void potrf_body_sync(double* __restrict__ S, int64_t 
 //               and with a flag publishes them
 // Every wait points to work that does not wait for the waiter, so the chain always progresses; the
 // polls are bounded (scal[1] = -1 on timeout, reported by the host).
-template <bool TS>
+// PRE: the block's lower tiles are already in LDS (k_chol_flow's diagonal workgroup updated them there)
+template <bool TS, bool PRE = false>
 __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, int col, double* __restrict__ dinv,
                                            double* __restrict__ scal, unsigned long long* __restrict__ ts,
                                            unsigned* __restrict__ flag, double* __restrict__ smem) {
@@ -537,7 +538,13 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
             Dw[j * 17] = x[j];  // (L^-1)[j][lane]
         });
     };
-    {
+    if constexpr (PRE) {
+        if (wave == 0) {
+#pragma unroll
+            for (int c = 0; c < IB; ++c) a[c] = AT(lr, c);
+            ok = leaf(0);
+        }
+    } else {
         // wave 0 reads the rows of diagonal tile 0 straight into registers and factors leaf 0 while the
         // other 35 lower tiles are on their way into LDS (sc1 loads: in a merged launch the block was
         // just updated by another workgroup); item i -> tile p = 1 + (i >> 7), row (i >> 3) & 15,
@@ -1555,6 +1562,526 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_panel(double* __restrict__ S,
 }
 
 // ------------------------------------------------------------------------------------------------
+// k_chol_flow: the whole block factorisation as ONE persistent launch (schedule: fba_order.cpp
+// build_flow).  One 512-thread workgroup per record; every wait points to an earlier record.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void spin_ge(const unsigned* p, unsigned v, double* __restrict__ scal) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }  // hand-off timeout (host reports it)
+    }
+}
+
+// trsm_flow_body (k_chol_flow role 1): one 64-row half of panel block (r, k), X = A L_kk^-T, RIGHT-looking
+// with each solving wave's 16 rows of A in registers: as block column t of L_kk arrives (waves 4-7
+// load it into LDS as k's potrf publishes it, as in trsm_body), X_t = A_t D_t', then A_s -= X_t L_st' for
+// s > t -- so after the last column only X_7 = A_7 D_7' is left.  Every solved column block is stored
+// write-through; its drain overlaps the next step, after which the last of the four solving waves
+// raises the progress flag (prog = column blocks published).
+constexpr size_t TRSMF_LDS = sizeof(double) * (4 * IB * 17 + (TRSM_NT + CB / IB) * IB * 17) + 16 * sizeof(int);
+__device__ __forceinline__ void trsm_flow_body(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ rec,
+                                               const double* __restrict__ dinv, const unsigned* __restrict__ flag,
+                                               double* __restrict__ scal, double* __restrict__ smem,
+                                               uint64_t* __restrict__ tr, unsigned* __restrict__ prog) {
+    double* T = smem;                       // [4][IB][17]    per-wave transposes
+    double* Lt = T + 4 * IB * 17;           // [28][IB][17]   L_st, p = s(s-1)/2 + t
+    double* Dt = Lt + TRSM_NT * IB * 17;    // [8][IB][17]    D_s
+    int* s_col = reinterpret_cast<int*>(Dt + (CB / IB) * IB * 17);  // [8] column t in LDS
+    int* s_cnt = s_col + CB / IB;                                    // [8] solving waves done with step t
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int lr = lane & 15, lk = lane >> 4;
+    const bool worker = tid < 256;
+    const int64_t k0 = (int64_t)rec[0] * CB;
+    const int rh = rec[1];
+    const int64_t rbase = (int64_t)(rh >> 1) * CB + (rh & 1) * 64 + (wave & 3) * IB;
+    const double* L = S + k0 * ld + k0;
+    const double* Dk = dinv + (k0 / CB) * (CB / IB) * (IB * IB);
+    if (tid < 2 * (CB / IB)) s_col[tid] = 0;
+    const __amdgpu_buffer_rsrc_t rX = block_rsrc(S + rbase * ld + k0, ((int64_t)(IB - 1) * ld + CB) * 8);
+    dbl4 acc[CB / IB];
+    if (worker)  // this wave's 16 rows of A, MFMA output layout: acc[t][r] = A[lk + 4 r][16 t + lr]
+#pragma unroll
+        for (int t = 0; t < CB / IB; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                acc[t][r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                           rX, (int)(((int64_t)(lk + 4 * r) * ld + IB * t + lr) * 8), 0, SC1));
+    __syncthreads();  // the flags are zero
+    if (!worker) {
+        const __amdgpu_buffer_rsrc_t rL = block_rsrc(L, ((int64_t)(CB - 1) * ld + CB) * 8);
+        const __amdgpu_buffer_rsrc_t rD = block_rsrc(Dk, (CB / IB) * IB * IB * 8);
+        for (int t = wave - 4; t < CB / IB; t += 4) {
+            unsigned spins = 0;
+            while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(t + 1)) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins == FLAG_SPINS) {
+                    if (lane == 0) scal[1] = -1.0;  // hand-off timeout (host reports it)
+                    break;
+                }
+            }
+            double2 v[16];
+            double* dst[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {  // items (8 - t) * 128 double2
+                const int i = lane + 64 * q, u = i >> 7, n = (i >> 3) & 15, kc = (i & 7) * 2;
+                dst[q] = nullptr;
+                if (u < CB / IB - 1 - t) {  // tile (r, t), r = t + 1 + u
+                    const int r = t + 1 + u;
+                    v[q] = ld_sc1(rL, ((int64_t)(r * IB + n) * ld + t * IB + kc) * 8);
+                    dst[q] = Lt + ((r * (r - 1) / 2 + t) * IB + n) * 17 + kc;
+                } else if (u == CB / IB - 1 - t) {  // D_t
+                    v[q] = ld_sc1(rD, (int64_t)(t * IB * IB + n * IB + kc) * 8);
+                    dst[q] = Dt + (t * IB + n) * 17 + kc;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if (dst[q]) {
+                    dst[q][0] = v[q].x;
+                    dst[q][1] = v[q].y;
+                }
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's LDS writes done
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) __hip_atomic_store(s_col + t, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (tr && lane == 0) tr[8 + t] = wall_clock64();  // FBA_PANEL_TRACE: column t of L_kk in LDS
+        }
+        return;
+    }
+    double* Tw = T + wave * IB * 17;
+    bool pending = false;  // column block t-1 stored, not yet signalled
+    auto signal = [&](int done) {  // after this wave's drain: the last of the four raises the flag
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0 && __hip_atomic_fetch_add(s_cnt + done - 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 3) {
+            __hip_atomic_store(prog, (unsigned)done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tr) tr[16 + done - 1] = wall_clock64();  // FBA_PANEL_TRACE: column block done-1 published
+        }
+    };
+#pragma unroll
+    for (int t = 0; t < CB / IB; ++t) {
+        unsigned sp = 0;
+        while (__hip_atomic_load(s_col + t, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++sp == FLAG_SPINS) break;  // (the loader reports the timeout)
+        }
+        // X_t = A_t D_t': A_t to the operand layout through Tw
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Tw[(lk + 4 * r) * 17 + lr] = acc[t][r];
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+        double av[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) av[kk] = Tw[lr * 17 + 4 * kk + lk];
+        dbl4 x = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) x = mfma(av[kk], Dt[(t * IB + lr) * 17 + 4 * kk + lk], x);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Tw[(lk + 4 * r) * 17 + lr] = x[r];
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+        double xa[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) xa[kk] = -Tw[lr * 17 + 4 * kk + lk];
+        if (t > 0 && pending) {  // column block t-1's stores drained during this step
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            signal(t);
+        }
+        {
+            const int n = lane >> 2, m = 4 * (lane & 3);
+            double2 v0, v1;
+            v0.x = Tw[n * 17 + m];
+            v0.y = Tw[n * 17 + m + 1];
+            v1.x = Tw[n * 17 + m + 2];
+            v1.y = Tw[n * 17 + m + 3];
+            st_sc1(rX, ((int64_t)n * ld + IB * t + m) * 8, v0);
+            st_sc1(rX, ((int64_t)n * ld + IB * t + m + 2) * 8, v1);
+        }
+        if (t == CB / IB - 1) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            signal(CB / IB);
+            if (tr && tid == 0) tr[6] = wall_clock64();
+        }
+        // right-looking: A_s -= X_t L_st'
+#pragma unroll
+        for (int s = t + 1; s < CB / IB; ++s)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+                acc[s] = mfma(xa[kk], Lt[((s * (s - 1) / 2 + t) * IB + lr) * 17 + 4 * kk + lk], acc[s]);
+        // column block t published now if column t+1 has not arrived (the wave would only wait), else
+        // drained during step t+1
+        pending = true;
+        if (t + 1 < CB / IB && __hip_atomic_load(s_col + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            signal(t + 1);
+            pending = false;
+        }
+    }
+}
+
+// wait until every flag of a list is set, then a workgroup barrier; no acquire fence: every load of
+// the handed-off bytes behind it is an sc1 load of sc1 stores (MI355X guide, hand-off table row 1)
+__device__ __forceinline__ void wait_list_sc1(const int32_t* __restrict__ wl, int n, const unsigned* __restrict__ fl,
+                                              double* __restrict__ scal) {
+    if (n > 0 && threadIdx.x == 0)
+        for (int q = 0; q < n; ++q) spin_ge(fl + wl[q], 1u, scal);
+    __syncthreads();
+}
+
+// LDS of the diagonal-block role: the potrf's lower tiles, leaf inverses and counters, then a second
+// 128 x 17 buffer for the fused source's published column blocks (the first is the leaf-inverse area,
+// free until the potrf starts)
+constexpr size_t FLOWF_LDS = sizeof(double) * (POTRF_NT * IB * 17 + (CB / IB) * IB * 17) + 32 * sizeof(int) +
+                             sizeof(double) * CB * 17;
+static_assert(CB * 17 == (CB / IB) * IB * 17, "a column-block buffer is exactly the leaf-inverse area");
+
+// diag_body (role 0): diagonal block j.  C_jj (its final in-place writers done) is loaded into LDS; with
+// a fused source f (rec[2] >= 0) the block row X = L(j, f) is consumed column block by column block as
+// the two panel-half records of (f, j) publish it (progress flags rec[7], rec[8]): block t + 1's loads
+// are issued before block t's update whenever it is already published, so the update (C_jj -= X_t X_t'
+// in LDS on all eight waves) keeps pace with the panel solves; then the late partials (the other
+// sources of f's level, scratch quarters, slot order); then the potrf on the LDS block.
+__device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ rec,
+                                          const int32_t* __restrict__ lists, double* __restrict__ dinv,
+                                          double* __restrict__ scal, unsigned* __restrict__ colflags,
+                                          unsigned* __restrict__ fl, const double* __restrict__ P,
+                                          double* __restrict__ smem, uint64_t* __restrict__ tr) {
+    const int j = rec[1], f = rec[2];
+    wait_list_sc1(lists + rec[3], rec[4], fl, scal);  // the final in-place writers of C_jj's quarters
+    if (tr && threadIdx.x == 0) tr[1] = wall_clock64();
+    if (f < 0 && rec[6] == 0) {
+        potrf_body<false>(S, ld, j, dinv, scal, nullptr, colflags + j, smem);
+        return;
+    }
+#define AT(r, c) smem[(((r) >> 4) * (((r) >> 4) + 1) / 2 + ((c) >> 4)) * (IB * 17) + ((r) & 15) * 17 + ((c) & 15)]
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int lr = lane & 15, lk = lane >> 4;
+    const int64_t k0 = (int64_t)j * CB;
+    double* Dall = smem + POTRF_NT * IB * 17;
+    int* sy = reinterpret_cast<int*>(Dall + (CB / IB) * IB * 17);
+    double* Xb[2] = {Dall, reinterpret_cast<double*>(sy + 32)};  // [128][17] each
+    {   // C_jj's lower tiles into LDS
+        const __amdgpu_buffer_rsrc_t rC = block_rsrc(S + k0 * ld + k0, ((int64_t)(CB - 1) * ld + CB) * 8);
+        constexpr int NQ = POTRF_NT * 128 / POTRF_THREADS;  // 9
+        double2 v[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int i = tid + POTRF_THREADS * q, p = i >> 7, n = (i >> 3) & 15, m = (i & 7) * 2;
+            int ti = 0, pp = p;
+            while (pp > ti) { pp -= ti + 1; ++ti; }
+            v[q] = ld_sc1(rC, ((int64_t)(ti * IB + n) * ld + pp * IB + m) * 8);
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int i = tid + POTRF_THREADS * q, p = i >> 7, n = (i >> 3) & 15, m = (i & 7) * 2;
+            smem[p * IB * 17 + n * 17 + m] = v[q].x;
+            smem[p * IB * 17 + n * 17 + m + 1] = v[q].y;
+        }
+    }
+    if (f >= 0) {
+        const int64_t f0 = (int64_t)f * CB;
+        const __amdgpu_buffer_rsrc_t rX = block_rsrc(S + k0 * ld + f0, ((int64_t)(CB - 1) * ld + CB) * 8);
+        const unsigned* p0 = fl + rec[7];
+        const unsigned* p1 = rec[8] >= 0 ? fl + rec[8] : nullptr;
+        auto published = [&]() {
+            unsigned v = __hip_atomic_load(p0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (p1) v = std::min(v, __hip_atomic_load(p1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            return v;
+        };
+        // column block t of the 128 rows: thread -> row (tid >> 3) + 64 e, columns 2 (tid & 7), +1
+        double2 xv[2];
+        auto issue = [&](int t) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e)
+                xv[e] = ld_sc1(rX, ((int64_t)((tid >> 3) + 64 * e) * ld + IB * t + 2 * (tid & 7)) * 8);
+        };
+        auto wait_for = [&](int t) {  // column block t published (thread 0 polls), then everyone issues
+            if (tid == 0) {
+                unsigned spins = 0;
+                while (published() <= (unsigned)t) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }
+                }
+            }
+            __syncthreads();
+            issue(t);
+        };
+        wait_for(0);
+        constexpr int NT = (POTRF_NT + POTRF_NW - 1) / POTRF_NW;  // 5 tiles per wave at most
+        int ta[NT], tb[NT];
+        dbl4 c[NT];  // this wave's tiles p = wave + 8 i of C_jj, in registers until the last block
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            int a = 0, b = wave + POTRF_NW * i;
+            while (b > a) { b -= a + 1; ++a; }
+            ta[i] = a;
+            tb[i] = b;
+            if (wave + POTRF_NW * i < POTRF_NT)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) c[i][r] = smem[(wave + POTRF_NW * i) * IB * 17 + (lk + 4 * r) * 17 + lr];
+        }
+#pragma unroll
+        for (int t = 0; t < CB / IB; ++t) {
+            double* X = Xb[t & 1];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                X[((tid >> 3) + 64 * e) * 17 + 2 * (tid & 7)] = xv[e].x;
+                X[((tid >> 3) + 64 * e) * 17 + 2 * (tid & 7) + 1] = xv[e].y;
+            }
+            if (tid == 0) sy[31] = (t + 1 < CB / IB && published() > (unsigned)(t + 1));
+            __syncthreads();  // block t in LDS; the other buffer's readers (block t-1) are done
+            if (tr && tid == 0) tr[8 + t] = wall_clock64();  // FBA_PANEL_TRACE: block t in LDS
+            const bool pre = sy[31] != 0;
+            if (pre) issue(t + 1);  // the next block's loads in flight during this update
+            // C(a, b) -= X_t(a) X_t(b)', tiles p = wave + 8 i of the 36 lower tiles
+            double xa[NT][4], yb[NT][4];
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+                if (wave + POTRF_NW * i < POTRF_NT) {
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) {
+                        xa[i][kk] = -X[(IB * ta[i] + lr) * 17 + 4 * kk + lk];
+                        yb[i][kk] = X[(IB * tb[i] + lr) * 17 + 4 * kk + lk];
+                    }
+                }
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                for (int i = 0; i < NT; ++i)
+                    if (wave + POTRF_NW * i < POTRF_NT) c[i] = mfma(xa[i][kk], yb[i][kk], c[i]);
+            if (t == CB / IB - 1)
+#pragma unroll
+                for (int i = 0; i < NT; ++i)
+                    if (wave + POTRF_NW * i < POTRF_NT) {
+                        const int p = wave + POTRF_NW * i;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) smem[p * IB * 17 + (lk + 4 * r) * 17 + lr] = c[i][r];
+                    }
+            if (tr && tid == 0) tr[16 + t] = wall_clock64() | (pre ? (1ull << 63) : 0);  // block t applied
+            if (!pre && t + 1 < CB / IB) wait_for(t + 1);
+        }
+    }
+    if (tr && threadIdx.x == 0) tr[4] = wall_clock64();
+    // late partials: the other sources of f's level, 64x64 row-major scratch quarters, slot order
+    for (int e = 0; e < rec[6]; ++e) {
+        const int32_t* l3 = lists + rec[5] + 3 * e;
+        const int q = l3[0];
+        __syncthreads();
+        if (tid == 0) spin_ge(fl + l3[2], 1u, scal);
+        __syncthreads();
+        const __amdgpu_buffer_rsrc_t rp = block_rsrc(P + (int64_t)l3[1] * 4096, 4096 * 8);
+        double2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = ld_sc1(rp, (int64_t)(2 * (tid + POTRF_THREADS * u)) * 8);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e2 = 2 * (tid + POTRF_THREADS * u), R = 64 * (q >> 1) + (e2 >> 6), C = 64 * (q & 1) + (e2 & 63);
+            if ((R >> 4) >= (C >> 4)) {
+                AT(R, C) += v[u].x;
+                AT(R, C + 1) += v[u].y;
+            }
+        }
+    }
+    __syncthreads();  // the block final in LDS; the counters and buffers free
+    if (tr && threadIdx.x == 0) tr[5] = wall_clock64();
+    potrf_body<false, true>(S, ld, j, dinv, scal, nullptr, colflags + j, smem);
+#undef AT
+}
+
+// syrk_flow_body (role 2): one update task, C(a, b) quarter q += -sum_k X_ak X_bk' over its sources
+// (one elimination-tree level, ascending), each source's column blocks consumed in batches as they are
+// published (progress flags of the two panel halves), the whole 128-deep panel in one batch when the
+// source is complete.  mode 0: added to C in place after the previous writer of the quarter (rec[9]);
+// 1: a split target's partial to scratch, the last group to arrive adds the groups' partials in slot
+// order; 2: a late partial to scratch for the diagonal workgroup.  rec[8]: the flag it raises.
+__device__ __forceinline__ void syrk_flow_body(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ rec,
+                                               const int32_t* __restrict__ lists, double* __restrict__ P,
+                                               unsigned* __restrict__ fl, unsigned* __restrict__ cnt,
+                                               double* __restrict__ scal, double* __restrict__ smem,
+                                               uint64_t* __restrict__ tr) {
+    double (*As)[LDW] = reinterpret_cast<double (*)[LDW]>(smem);
+    double (*Bs)[LDW] = reinterpret_cast<double (*)[LDW]>(smem + 64 * LDW);
+    int* sv = reinterpret_cast<int*>(smem + 128 * LDW);
+    const int a = rec[1], b = rec[2], q = rec[3], ns = rec[5], slot = rec[6], mode = rec[7];
+    const int32_t* sl = lists + rec[4];
+    const int64_t r0 = (int64_t)a * CB + (q >> 1) * 64, c0 = (int64_t)b * CB + (q & 1) * 64;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int lr = lane & 15, lk = lane >> 4;
+    const int wr = (wave >> 1) * 16, wc = (wave & 1) * 32;
+    const __amdgpu_buffer_rsrc_t rC = block_rsrc(S + r0 * ld + c0, ((int64_t)63 * ld + 64) * 8);
+    auto wait_prev = [&]() {
+        if (rec[9] >= 0 && tid == 0) spin_ge(fl + rec[9], 1u, scal);
+        __syncthreads();
+    };
+    dbl4 acc[2];
+    acc[0] = dbl4{0.0, 0.0, 0.0, 0.0};
+    acc[1] = acc[0];
+    if (mode == 0) {  // in place: the target (after its previous writer) is the accumulators' start
+        wait_prev();
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                acc[bb][r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                            rC, (int)(((int64_t)(wr + lk + 4 * r) * ld + wc + lr + 16 * bb) * 8), 0, SC1));
+    }
+    const __amdgpu_buffer_rsrc_t rA = block_rsrc(S + r0 * ld, ((int64_t)63 * ld + ld) * 8);
+    const __amdgpu_buffer_rsrc_t rB = block_rsrc(S + c0 * ld, ((int64_t)63 * ld + ld) * 8);
+    for (int s = 0; s < ns; ++s) {
+        const int64_t kc = (int64_t)sl[3 * s] * CB;
+        const unsigned* pa = fl + sl[3 * s + 1];
+        const unsigned* pb = fl + sl[3 * s + 2];
+        int t = 0;
+        while (t < CB / IB) {
+            if (tid == 0) {
+                unsigned spins = 0, va, vb;
+                for (;;) {
+                    va = __hip_atomic_load(pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    vb = __hip_atomic_load(pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (va > (unsigned)t && vb > (unsigned)t) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins == FLAG_SPINS) { scal[1] = -1.0; va = vb = CB / IB; break; }
+                }
+                sv[0] = (int)std::min(std::min(va, vb), (unsigned)(CB / IB));
+            }
+            __syncthreads();
+            const int v = sv[0];
+            // columns [16 t, 16 v) of the 64 rows of A and of B: row item / wpr, column pair item % wpr
+            const int wpr = 8 * (v - t), nit = 64 * wpr;
+            double2 xa[8], xb[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = tid + POTRF_THREADS * u;
+                if (i < nit) {
+                    const int row = i / wpr, col = IB * t + 2 * (i % wpr);
+                    xa[u] = ld_sc1(rA, ((int64_t)row * ld + kc + col) * 8);
+                    xb[u] = ld_sc1(rB, ((int64_t)row * ld + kc + col) * 8);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = tid + POTRF_THREADS * u;
+                if (i < nit) {
+                    const int row = i / wpr, col = IB * t + 2 * (i % wpr);
+                    As[row][col] = xa[u].x; As[row][col + 1] = xa[u].y;
+                    Bs[row][col] = xb[u].x; Bs[row][col + 1] = xb[u].y;
+                }
+            }
+            __syncthreads();
+            for (int kb = IB * t; kb < IB * v; kb += IB) {
+                double av[4], b0[4], b1[4];
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    av[kk] = -As[wr + lr][kb + 4 * kk + lk];
+                    b0[kk] = Bs[wc + lr][kb + 4 * kk + lk];
+                    b1[kk] = Bs[wc + 16 + lr][kb + 4 * kk + lk];
+                }
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    acc[0] = mfma(av[kk], b0[kk], acc[0]);
+                    acc[1] = mfma(av[kk], b1[kk], acc[1]);
+                }
+            }
+            t = v;
+        }
+    }
+    if (tr && tid == 0) tr[4] = wall_clock64();
+    auto raise = [&](int32_t flag) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(fl + flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    if (mode == 0) {
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) st_sc1(rC, ((int64_t)(wr + lk + 4 * r) * ld + wc + lr + 16 * bb) * 8, acc[bb][r]);
+        raise(rec[8]);
+        return;
+    }
+    {   // the partial to its scratch quarter (row-major 64 x 64), write-through
+        const __amdgpu_buffer_rsrc_t rP = block_rsrc(P + (int64_t)slot * 4096, 4096 * 8);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                st_sc1(rP, (int64_t)((wr + lk + 4 * r) * 64 + wc + lr + 16 * bb) * 8, acc[bb][r]);
+    }
+    if (mode == 2) {
+        raise(rec[8]);
+        return;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+        sv[1] = __hip_atomic_fetch_add(cnt + rec[10], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(rec[12] - 1);
+    __syncthreads();
+    if (!sv[1]) return;
+    wait_prev();  // (its barrier also orders the partial loads below after the arrival)
+    double2 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int e = 2 * (tid + POTRF_THREADS * u), r = e >> 6, cl = e & 63;
+        v[u] = ld_sc1(rC, ((int64_t)r * ld + cl) * 8);
+    }
+    for (int g = 0; g < rec[12]; ++g) {
+        const __amdgpu_buffer_rsrc_t rg = block_rsrc(P + (int64_t)(rec[11] + g) * 4096, 4096 * 8);
+        double2 pv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) pv[u] = ld_sc1(rg, (int64_t)(2 * (tid + POTRF_THREADS * u)) * 8);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { v[u].x += pv[u].x; v[u].y += pv[u].y; }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int e = 2 * (tid + POTRF_THREADS * u), r = e >> 6, cl = e & 63;
+        st_sc1(rC, ((int64_t)r * ld + cl) * 8, v[u]);
+    }
+    raise(rec[8]);
+}
+
+constexpr size_t FLOW_LDS_A = FLOWF_LDS > TRSMF_LDS ? FLOWF_LDS : TRSMF_LDS;
+constexpr size_t FLOW_LDS_B = SYRKW_LDS > TRTRI_LDS ? SYRKW_LDS : TRTRI_LDS;
+constexpr size_t FLOW_LDS = FLOW_LDS_A > FLOW_LDS_B ? FLOW_LDS_A : FLOW_LDS_B;
+static_assert(FLOW_LDS <= 160 * 1024, "k_chol_flow LDS");
+static_assert(SYRKW_LDS >= sizeof(double) * 128 * LDW + 2 * sizeof(int), "syrk_flow_body broadcast words");
+
+__global__ __launch_bounds__(POTRF_THREADS) void k_chol_flow(double* __restrict__ S, int64_t ld,
+                                                             const int32_t* __restrict__ lists,
+                                                             const int32_t* __restrict__ recs,
+                                                             double* __restrict__ dinv, double* __restrict__ linv,
+                                                             double* __restrict__ scal, unsigned* __restrict__ colflags,
+                                                             unsigned* __restrict__ fl, unsigned* __restrict__ cnt,
+                                                             double* __restrict__ P, uint64_t* __restrict__ trace) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int32_t* rec = recs + Sched::FLOW_REC * (int64_t)blockIdx.x;
+    uint64_t* tr = trace ? trace + FTRACE * (int64_t)blockIdx.x : nullptr;
+    if (tr && threadIdx.x == 0) tr[0] = wall_clock64();
+    const int role = rec[0];
+    if (role == 0) {
+        diag_body(S, ld, rec, lists, dinv, scal, colflags, fl, P, smem, tr);
+    } else if (role == 1) {
+        wait_list_sc1(lists + rec[3], rec[4], fl, scal);  // the final writers of the panel block's quarters
+        if (tr && threadIdx.x == 0) tr[1] = wall_clock64();
+        trsm_flow_body(S, ld, rec + 1, dinv, colflags + rec[1], scal, smem, tr, fl + rec[5]);
+    } else if (role == 2) {
+        syrk_flow_body(S, ld, rec, lists, P, fl, cnt, scal, smem, tr);
+    } else {
+        if (threadIdx.x == 0) spin_ge(colflags + rec[1], (unsigned)(CB / IB), scal);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        trtri_body(S, ld, rec[1], dinv, linv, smem);
+    }
+    if (tr) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            tr[2] = wall_clock64();
+            tr[3] = (uint64_t)role | ((uint64_t)(uint32_t)rec[1] << 8) | ((uint64_t)(uint32_t)rec[2] << 32);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // backward solve L' x = y with the diagonal-block inverses:
 //   k_bwd_first  x_{nb-1} = Linv_{nb-1}^T y_{nb-1}
 //   k_bwd_step   (kb): workgroup 0 (the critical one) y_{kb-1} -= L_{kb,kb-1}^T x_kb and then
@@ -1777,6 +2304,21 @@ __global__ void k_neg_copy(const double* __restrict__ X, double* __restrict__ de
 int launch_cholesky(Ctx& c) {
     const int64_t ld = c.L.ld;
     const Sched& s = c.sched;
+    if (c.chol_flow && s.flow_ok && s.flow_n > 0) {
+        // the whole factorisation + forward solve in one persistent launch (flags zeroed by k_finish_rhs)
+        const bool pp = c.probe == 2 && c.probe_n < (int)c.probe_ev.size() / 2;
+        if (pp) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
+        k_chol_flow<<<(unsigned)s.flow_n, POTRF_THREADS, FLOW_LDS, c.stream>>>(
+            c.d_S, ld, c.d_sched, c.d_sched + s.flow_rec, c.d_dinv, c.d_linv, c.d_scal, c.d_flags, c.d_tflags,
+            c.d_counters, c.d_P, c.d_ptrace);
+        if (pp) {
+            FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], c.stream));
+            c.probe_flops += s.flow_flops;
+            ++c.probe_n;
+        }
+        FBA_HIP(hipGetLastError());
+        return FBA_OK;
+    }
     // the k_panel / k_bwd_flow hand-off flags, the split-target counters and the update flags were
     // zeroed by k_finish_rhs
     int pend = -1;  // a level whose trailing updates run inside the next level's k_panel
@@ -1929,6 +2471,9 @@ int chol_setup(Ctx& c) {
     FBA_HIP(hipFuncSetAttribute((const void*)k_potrf128<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)POTRF_LDS));
     FBA_HIP(hipFuncSetAttribute((const void*)k_trsm128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRSM_LDS));
     FBA_HIP(hipFuncSetAttribute((const void*)k_panel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)PANEL_LDS));
+    FBA_HIP(hipFuncSetAttribute((const void*)k_chol_flow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)FLOW_LDS));
+    // FBA_CHOL_FLOW=0: the level-by-level k_panel launches instead of the persistent dataflow launch
+    c.chol_flow = !(getenv("FBA_CHOL_FLOW") && atoi(getenv("FBA_CHOL_FLOW")) == 0);
     static_assert(TRSM_LDS >= POTRF_LDS, "k_panel LDS");
     hipDeviceProp_t prop;
     FBA_HIP(hipGetDeviceProperties(&prop, c.device));

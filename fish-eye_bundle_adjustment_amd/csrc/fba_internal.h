@@ -18,6 +18,7 @@ namespace fba {
 
 constexpr int NB = 128;       // Cholesky block size (rows/cols of one panel block, fba_chol.hip)
 constexpr int PTRACE_WG = 2048;  // FBA_PANEL_TRACE: workgroup slots per level
+constexpr int FTRACE = 32;       // FBA_PANEL_TRACE: stamps per k_chol_flow record
 constexpr int CHUNK_OBS = 256;  // observations per k_lin_reduce / k_lin_point workgroup (chunk)
 // tie points per chunk and co-visibility terms per chunk staged in LDS (a single larger point's are
 // read from HBM instead): smaller for nK >= 6, whose wider Jacobian rows leave less of the 160 KiB LDS
@@ -80,6 +81,19 @@ struct Sched {
     std::vector<Wave> w;          // factorisation, level 0 up
     std::vector<BWave> b;         // backward solve, indexed by level (run top down)
     std::vector<int32_t> buf;     // host image of the lists (uploaded to Ctx::d_sched)
+
+    // persistent dataflow factorisation (k_chol_flow, fba_order.cpp build_flow): the whole factorisation
+    // in ONE launch, one FLOW_REC record per workgroup in dispatch order; every wait points to an earlier
+    // record.  Roles: 0 = diagonal block j (its fused source's panel solve and diagonal update, then the
+    // potrf), 1 = a panel half solve, 2 = an update task, 3 = a diagonal-block inverse.  Flags live in
+    // the tflags region: progress flags [0, flow_nprog) (column blocks of a panel half solved), then the
+    // update-completion flags
+    static constexpr int FLOW_REC = 16;
+    int64_t flow_rec = 0;
+    int flow_n = 0, flow_nprog = 0, flow_nuflag = 0, flow_ncounter = 0, flow_nscratch = 0;
+    int flow_cnt[4] = {0, 0, 0, 0};  // records per role
+    bool flow_ok = false;
+    double flow_flops = 0.0;
 };
 
 // Accumulation plan (fba_capi.cpp create, run by k_lin_reduce and the k_red_* kernels): offsets
@@ -187,6 +201,8 @@ struct Ctx {
     int merge_max = 1 << 30;        // ... for levels of at most this many update tasks (FBA_MERGE_MAX)
     bool merge_updates = true;      // a level's trailing updates inside the next level's k_panel
                                     // (FBA_MERGE_UPDATES=0: their own k_syrk_multi launch)
+    bool chol_flow = true;          // the factorisation as one persistent k_chol_flow launch (FBA_CHOL_FLOW=0:
+                                    // one k_panel launch per elimination-tree level)
     bool panel_progressive = true;  // k_panel: panel solves step with the potrf's published column blocks
                                     // (FBA_PANEL_PROGRESSIVE=0: wait for the whole factor)         // one-launch backward solve (FBA_BWD_LEVELS=1: one launch per level)
     size_t flags_bytes = 0;

@@ -21,6 +21,7 @@
 #include <deque>
 #include <functional>
 #include <map>
+#include <queue>
 #include <tuple>
 
 #include "fba_internal.h"
@@ -396,6 +397,261 @@ std::vector<int32_t> camera_order(const fba_problem* p) {
     return out;
 }
 
+// Persistent dataflow schedule of the whole block factorisation (k_chol_flow).  Records (one
+// workgroup each):
+//   diagonal block j   waits for the final in-place writers of its diagonal quarters, loads C_jj into
+//                      LDS, then applies its FUSED source f_j (the source of the highest elimination-
+//                      tree level, then the highest index) itself: C_jj -= X X' column block by column
+//                      block as the two panel-half records of (f_j, j) publish X = L(j, f_j) -- so the
+//                      last hand-off before its potrf is panel solve -> diagonal workgroup, with no
+//                      update task and no write-back of C_jj in between; adds the late partials (other
+//                      sources of f_j's level); then the potrf, publishing its column blocks
+//   panel half (k,r,h) solves as k's column blocks are published, publishes each solved column block
+//                      (progress flag = column blocks done)
+//   update task        C(a,b) quarter += -sum X_ak X_bk' over the sources of ONE level (<= SPLIT per
+//                      task), consuming the sources' column blocks as they are published; in place
+//                      after the previous level's writer of the quarter, or via scratch partials
+//                      combined by the last group; diagonal contributions of the fused source's own
+//                      level other than the fused source ("late") go to scratch partials
+//   inverse            of every diagonal block below the top level (k_bwd_flow, covariance)
+// Dispatch order: a topological order of the record dependencies picking, among the ready records,
+// the smallest (level of need, role rank): diagonal blocks first (each placed right after the last
+// record it waits for), then panel halves, the updates feeding the next level, the others, inverses.
+// Every wait points to an earlier record, so in-order dispatch always progresses (checked here).
+static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<std::vector<int32_t>>& R,
+                       const std::vector<int32_t>& level, int64_t nb, const std::function<int64_t(int64_t)>& real_rows,
+                       bool verbose) {
+    constexpr int SPLIT = 2, REC = Sched::FLOW_REC;
+    const int nw = nb > 0 ? 1 + *std::max_element(level.begin(), level.end()) : 0;
+    std::vector<std::vector<int32_t>> srcs(nb);
+    for (int64_t k = 0; k < nb; ++k)
+        for (int32_t i : R[k])
+            if (i < nb) srcs[i].push_back((int32_t)k);
+    std::vector<int32_t> fsrc(nb, -1);
+    // FBA_FLOW_FUSE=0: no fused sources (every diagonal update by update tasks; the potrf loads its block)
+    static const bool fuse = !(getenv("FBA_FLOW_FUSE") && atoi(getenv("FBA_FLOW_FUSE")) == 0);
+    for (int64_t j = 0; j < nb && fuse; ++j)
+        for (int32_t k : srcs[j])
+            if (fsrc[j] < 0 || level[k] > level[fsrc[j]] || (level[k] == level[fsrc[j]] && k > fsrc[j])) fsrc[j] = k;
+    auto halves = [&](int64_t r) { return real_rows(r) > NB / 2 ? 2 : 1; };
+    // progress flags of every panel half (k, r, h), r in R[k] (the RHS block row included)
+    std::map<std::tuple<int32_t, int32_t, int32_t>, int32_t> prog;
+    int np = 0;
+    for (int64_t k = 0; k < nb; ++k)
+        for (int32_t r : R[k])
+            for (int h = 0; h < halves(r); ++h) prog[std::make_tuple((int32_t)k, r, h)] = np++;
+    struct Task {
+        std::array<int32_t, REC> rec;
+        std::array<int, 3> key;  // level of need, role rank, tie-break
+        std::vector<int> deps;   // producer records (flags resolved below)
+    };
+    std::vector<Task> T;
+    std::vector<int> col_task(nb, -1), prog_task(np, -1);
+    std::vector<std::vector<int>> uflag_tasks;  // update flag -> the records that may raise it
+    std::vector<std::vector<int32_t>> flag_deps;  // per record: flags it waits for (resolved to records)
+    auto new_uflag = [&]() { uflag_tasks.emplace_back(); return (int32_t)(np + uflag_tasks.size() - 1); };
+    auto add = [&](std::initializer_list<int32_t> r, std::array<int, 3> key) {
+        Task t;
+        t.rec.fill(0);
+        int q = 0;
+        for (int32_t v : r) t.rec[q++] = v;
+        t.key = key;
+        T.push_back(std::move(t));
+        flag_deps.emplace_back();
+        return (int)T.size() - 1;
+    };
+    // diagonal blocks
+    for (int64_t j = 0; j < nb; ++j) {
+        const int32_t f = fsrc[j];
+        int need = level[j] - 1;
+        col_task[j] = add({0, (int32_t)j, f, 0, 0, 0, 0, f >= 0 ? prog[std::make_tuple(f, (int32_t)j, 0)] : -1,
+                           (f >= 0 && halves(j) > 1) ? prog[std::make_tuple(f, (int32_t)j, 1)] : -1},
+                          {need, 0, (int)j});
+        if (f >= 0) {
+            flag_deps[col_task[j]].push_back(prog[std::make_tuple(f, (int32_t)j, 0)]);
+            if (halves(j) > 1) flag_deps[col_task[j]].push_back(prog[std::make_tuple(f, (int32_t)j, 1)]);
+        }
+        s.flow_flops += (double)NB * NB * NB / 3.0 + (f >= 0 ? (double)NB * NB * NB : 0.0);
+    }
+    // panel-half solves
+    for (int64_t k = 0; k < nb; ++k)
+        for (int32_t r : R[k])
+            for (int h = 0; h < halves(r); ++h) {
+                const int32_t p = prog[std::make_tuple((int32_t)k, r, h)];
+                const int id = add({1, (int32_t)k, 2 * r + h, 0, 0, p}, {level[k], 1, (int)(k * (nb + 1) + r) * 2 + h});
+                T[id].deps.push_back(col_task[k]);
+                prog_task[p] = id;
+                s.flow_flops += 64.0 * NB * NB;
+            }
+    // update tasks, target quarter by target quarter, a chain of writers over the source levels
+    std::map<std::pair<int32_t, int32_t>, std::vector<int32_t>> tg;  // (a, b) -> sources, ascending
+    for (int64_t k = 0; k < nb; ++k)
+        for (size_t bi = 0; bi < R[k].size(); ++bi) {
+            const int32_t b = R[k][bi];
+            if (b == nb) continue;
+            for (size_t ai = bi; ai < R[k].size(); ++ai) {
+                const int32_t a = R[k][ai];
+                if (a == b && fsrc[b] == (int32_t)k) continue;  // the fused diagonal update
+                tg[{a, b}].push_back((int32_t)k);
+            }
+        }
+    std::map<std::tuple<int32_t, int32_t, int32_t>, int32_t> writer;  // final in-place writer flag per quarter
+    std::vector<std::vector<std::array<int32_t, 3>>> late(nb);          // (quarter, slot, flag) per diagonal block
+    int nslot = 0, ncnt = 0;
+    for (auto& t : tg) {
+        const int32_t a = t.first.first, b = t.first.second;
+        std::map<int, std::vector<int32_t>> bylev;
+        for (int32_t k : t.second) bylev[level[k]].push_back(k);
+        for (int q = 0; q < 4; ++q) {
+            const int qr = q >> 1, qc = q & 1;
+            if (a == b && qr == 0 && qc == 1) continue;
+            if ((qr == 1 && halves(a) < 2) || (qc == 1 && halves(b) < 2)) continue;
+            int32_t prev = -1;
+            for (auto& lv : bylev) {
+                const int w = lv.first;
+                const std::vector<int32_t>& S = lv.second;
+                const bool is_late = a == b && fsrc[b] >= 0 && w == level[fsrc[b]];
+                const int ng = (int)((S.size() + SPLIT - 1) / SPLIT);
+                // urgency: the target is read at level level[b] (its column's potrf / panel solves)
+                const int rank = level[b] == w + 1 ? (a == b ? 2 : 3) : 4;
+                const int32_t wflag = is_late ? -1 : new_uflag();
+                const int32_t cidx = (!is_late && ng > 1) ? ncnt++ : -1;
+                const int first = nslot;
+                for (int g = 0; g < ng; ++g) {
+                    const int32_t soff = (int32_t)buf.size();
+                    std::vector<int32_t> fd;
+                    const int g0 = g * SPLIT, g1 = std::min((int)S.size(), g0 + SPLIT);
+                    for (int x = g0; x < g1; ++x) {
+                        const int32_t k = S[x];
+                        const int32_t pa = prog.at(std::make_tuple(k, a, qr)), pb = prog.at(std::make_tuple(k, b, qc));
+                        buf.insert(buf.end(), {k, pa, pb});
+                        fd.push_back(pa);
+                        fd.push_back(pb);
+                        s.flow_flops += 2.0 * 64 * 64 * NB;
+                    }
+                    int32_t mode, flag, slot = -1;
+                    if (is_late) {
+                        mode = 2;
+                        slot = nslot++;
+                        flag = new_uflag();
+                        late[b].push_back({q, slot, flag});
+                    } else if (ng > 1) {
+                        mode = 1;
+                        slot = nslot++;
+                        flag = wflag;
+                    } else {
+                        mode = 0;
+                        flag = wflag;
+                    }
+                    const int id = add({2, a, b, q, soff, g1 - g0, slot, mode, flag, is_late ? -1 : prev, cidx, first, ng},
+                                       {w, is_late ? 2 : rank, (int)(b * (nb + 1) + a) * 4 + q});
+                    flag_deps[id] = fd;
+                    if (!is_late && prev >= 0) flag_deps[id].push_back(prev);
+                    uflag_tasks[flag - np].push_back(id);
+                }
+                if (!is_late) prev = wflag;
+            }
+            writer[std::make_tuple(a, b, q)] = prev;
+        }
+    }
+    // panel halves wait for the final writers of their quarters; diagonal blocks for those of their
+    // diagonal quarters and for their late partials
+    for (int id = 0; id < (int)T.size(); ++id) {
+        Task& X = T[id];
+        if (X.rec[0] == 1) {
+            const int32_t k = X.rec[1], r = X.rec[2] >> 1, h = X.rec[2] & 1;
+            const int32_t woff = (int32_t)buf.size();
+            for (int qc = 0; qc < halves(k); ++qc) {
+                auto it = writer.find(std::make_tuple(r, k, 2 * h + qc));
+                if (it != writer.end() && it->second >= 0) buf.push_back(it->second);
+            }
+            X.rec[3] = woff;
+            X.rec[4] = (int32_t)buf.size() - woff;
+            for (int32_t x = woff; x < (int32_t)buf.size(); ++x) flag_deps[id].push_back(buf[x]);
+        } else if (X.rec[0] == 0) {
+            const int32_t j = X.rec[1];
+            const int32_t woff = (int32_t)buf.size();
+            for (int q : {0, 2, 3}) {
+                if (q > 0 && halves(j) < 2) continue;
+                auto it = writer.find(std::make_tuple(j, j, q));
+                if (it != writer.end() && it->second >= 0) buf.push_back(it->second);
+            }
+            X.rec[3] = woff;
+            X.rec[4] = (int32_t)buf.size() - woff;
+            for (int32_t x = woff; x < (int32_t)buf.size(); ++x) flag_deps[id].push_back(buf[x]);
+            const int32_t loff = (int32_t)buf.size();
+            for (auto& l : late[j]) {
+                buf.insert(buf.end(), l.begin(), l.end());
+                flag_deps[id].push_back(l[2]);
+            }
+            X.rec[5] = loff;
+            X.rec[6] = (int32_t)late[j].size();
+        }
+    }
+    // inverses of the diagonal blocks below the top level
+    for (int64_t j = 0; j < nb; ++j)
+        if (level[j] < nw - 1) {
+            const int id = add({3, (int32_t)j}, {level[j] + 1, 5, (int)j});
+            T[id].deps.push_back(col_task[j]);
+        }
+    // flags -> producer records
+    for (size_t i = 0; i < T.size(); ++i)
+        for (int32_t fg : flag_deps[i]) {
+            if (fg < np) T[i].deps.push_back(prog_task[fg]);
+            else for (int p : uflag_tasks[fg - np]) T[i].deps.push_back(p);
+        }
+    // dispatch order: Kahn's algorithm, the smallest key among the ready records first
+    const int n = (int)T.size();
+    std::vector<int> indeg(n, 0), ord;
+    std::vector<std::vector<int>> succ(n);
+    bool ok = true;
+    for (int i = 0; i < n; ++i) {
+        std::sort(T[i].deps.begin(), T[i].deps.end());
+        T[i].deps.erase(std::unique(T[i].deps.begin(), T[i].deps.end()), T[i].deps.end());
+        for (int d : T[i].deps) {
+            if (d < 0 || d >= n || d == i) { ok = false; continue; }
+            succ[d].push_back(i);
+            indeg[i]++;
+        }
+    }
+    {
+        auto cmp = [&](int x, int y) { return T[x].key != T[y].key ? T[x].key > T[y].key : x > y; };
+        std::priority_queue<int, std::vector<int>, decltype(cmp)> ready(cmp);
+        for (int i = 0; i < n; ++i)
+            if (indeg[i] == 0) ready.push(i);
+        while (!ready.empty()) {
+            const int i = ready.top();
+            ready.pop();
+            ord.push_back(i);
+            for (int x : succ[i])
+                if (--indeg[x] == 0) ready.push(x);
+        }
+    }
+    if ((int)ord.size() != n) ok = false;  // a dependency cycle
+    std::vector<int> pos(n, -1);
+    for (size_t i = 0; i < ord.size(); ++i) pos[ord[i]] = (int)i;
+    for (int i = 0; i < n && ok; ++i)
+        for (int d : T[i].deps)
+            if (pos[d] < 0 || pos[d] >= pos[i]) ok = false;
+    s.flow_ok = ok;
+    s.flow_nprog = np;
+    s.flow_nuflag = (int)uflag_tasks.size();
+    s.flow_ncounter = ncnt;
+    s.flow_nscratch = nslot;
+    s.flow_rec = (int64_t)buf.size();
+    s.flow_n = ok ? n : 0;
+    for (int r = 0; r < 4; ++r) s.flow_cnt[r] = 0;
+    if (ok)
+        for (int i : ord) {
+            buf.insert(buf.end(), T[i].rec.begin(), T[i].rec.end());
+            s.flow_cnt[T[i].rec[0]]++;
+        }
+    if (verbose)
+        fprintf(stderr, "[fba] flow schedule: %d records (%d diagonal, %d panel halves, %d updates, %d inverses), "
+                "%d progress + %d update flags, %d scratch quarters%s\n", n, s.flow_cnt[0], s.flow_cnt[1],
+                s.flow_cnt[2], s.flow_cnt[3], np, s.flow_nuflag, nslot, ok ? "" : " -- ORDER CHECK FAILED, not used");
+}
+
 void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pairs) {
     const Layout& L = c.L;
     const int64_t nb = L.n_pad / NB;
@@ -612,6 +868,10 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
     }
     s.nzero = (int)((at() - s.zero) / 2);
     s.n_tiles = ntile_total;
+    build_flow(s, buf, R, level, nb, real_rows, c.opt.verbose);
+    s.n_tflags = std::max(s.n_tflags, s.flow_nprog + s.flow_nuflag);
+    s.n_counters = std::max(s.n_counters, s.flow_ncounter);
+    s.n_scratch = std::max(s.n_scratch, s.flow_nscratch);
     s.buf = std::move(buf);
     if (c.opt.verbose)
         fprintf(stderr, "[fba] camera system: %ld blocks, %d levels, %ld update tiles, %d images + %d padding slots\n",

@@ -335,8 +335,127 @@ int main(int argc, char** argv) {
         printf("FAIL factor err %.3e solve err %.3e\n", rel, xrel);
         return 1;
     }
+    // -- the persistent dataflow schedule (k_chol_flow): records run to completion in dispatch order
+    // (a valid execution, since every wait points to an earlier record); every flag a record waits for
+    // must already be raised --
+    if (!s.flow_ok) return fail("flow schedule order check");
+    std::vector<double> F = M0;
+    auto Fk = [&](int64_t i, int64_t j) { return &F[(size_t)(i * NB) * n + j * NB]; };
+    std::vector<unsigned> fl((size_t)s.flow_nprog + s.flow_nuflag, 0), colf(nb, 0), cntr(std::max(s.flow_ncounter, 1), 0);
+    std::vector<double> Pf((size_t)std::max(s.flow_nscratch, 1) * 4096, 0.0);
+    std::vector<int> slot_set(std::max(s.flow_nscratch, 1), 0);
+    auto flag_ok = [&](int32_t x, unsigned v) { return x >= 0 && x < (int32_t)fl.size() && fl[x] >= v; };
+    auto solve_rows = [&](int64_t k, int64_t r, int i0, int i1) {  // rows i0..i1 of block (r, k): X = A L_kk^-T
+        const double* Lk = Fk(k, k);
+        double* X = Fk(r, k);
+        for (int i = i0; i < i1; ++i)
+            for (int j = 0; j < NB; ++j) {
+                double v = X[(size_t)i * n + j];
+                for (int t = 0; t < j; ++t) v -= X[(size_t)i * n + t] * Lk[(size_t)j * n + t];
+                X[(size_t)i * n + j] = v / Lk[(size_t)j * n + j];
+            }
+    };
+    if (s.flow_rec + (int64_t)Sched::FLOW_REC * s.flow_n > nbuf) return fail("flow record bounds");
+    for (int b = 0; b < s.flow_n; ++b) {
+        const int32_t* rec = B + s.flow_rec + (int64_t)Sched::FLOW_REC * b;
+        if (rec[0] == 0) {
+            const int64_t j = rec[1], f = rec[2];
+            for (int x = 0; x < rec[4]; ++x)
+                if (!flag_ok(B[rec[3] + x], 1)) return fail("flow: diagonal block waits for an unset flag");
+            double* C = Fk(j, j);
+            if (f >= 0) {
+                if (colf[f] != 8 || f >= j) return fail("flow: fused source not factored");
+                if (!flag_ok(rec[7], 8) || (rec[8] >= 0 && !flag_ok(rec[8], 8))) return fail("flow: fused rows not solved");
+                const double* X = Fk(j, f);
+                for (int a = 0; a < NB; ++a)
+                    for (int c2 = 0; c2 <= a; ++c2) {
+                        double v = 0.0;
+                        for (int t = 0; t < NB; ++t) v += X[(size_t)a * n + t] * X[(size_t)c2 * n + t];
+                        C[(size_t)a * n + c2] -= v;
+                    }
+            }
+            for (int e = 0; e < rec[6]; ++e) {
+                const int32_t* l3 = B + rec[5] + 3 * e;
+                if (!flag_ok(l3[2], 1) || !slot_set[l3[1]]) return fail("flow: late partial not ready");
+                const int qr = l3[0] >> 1, qc = l3[0] & 1;
+                for (int a = 0; a < 64; ++a)
+                    for (int c2 = 0; c2 < 64; ++c2)
+                        if (64 * qr + a >= 64 * qc + c2) C[(size_t)(64 * qr + a) * n + 64 * qc + c2] += Pf[(size_t)l3[1] * 4096 + a * 64 + c2];
+            }
+            for (int jj = 0; jj < NB; ++jj) {  // potrf
+                double d = C[(size_t)jj * n + jj];
+                for (int t = 0; t < jj; ++t) d -= C[(size_t)jj * n + t] * C[(size_t)jj * n + t];
+                if (!(d > 0)) return fail("flow: not SPD in emulation");
+                d = std::sqrt(d);
+                C[(size_t)jj * n + jj] = d;
+                for (int i = jj + 1; i < NB; ++i) {
+                    double v = C[(size_t)i * n + jj];
+                    for (int t = 0; t < jj; ++t) v -= C[(size_t)i * n + t] * C[(size_t)jj * n + t];
+                    C[(size_t)i * n + jj] = v / d;
+                }
+            }
+            colf[j] = 8;
+        } else if (rec[0] == 1) {
+            const int64_t k = rec[1], r = rec[2] >> 1, h = rec[2] & 1;
+            if (colf[k] != 8 || r <= k || r > nb) return fail("flow: panel half before its column");
+            for (int x = 0; x < rec[4]; ++x)
+                if (!flag_ok(B[rec[3] + x], 1)) return fail("flow: panel half waits for an unset flag");
+            solve_rows(k, r, 64 * (int)h, 64 * (int)h + 64);
+            fl[rec[5]] = 8;
+        } else if (rec[0] == 2) {
+            const int64_t a = rec[1], bb = rec[2];
+            const int qr = rec[3] >> 1, qc = rec[3] & 1, mode = rec[7];
+            if (bb >= nb || a < bb || a > nb) return fail("flow: update target");
+            std::vector<double> acc(4096, 0.0);
+            for (int u = 0; u < rec[5]; ++u) {
+                const int32_t* tri = B + rec[4] + 3 * u;
+                if (!flag_ok(tri[1], 8) || !flag_ok(tri[2], 8)) return fail("flow: update source not published");
+                const double* Xa = Fk(a, tri[0]);
+                const double* Xb = Fk(bb, tri[0]);
+                for (int x = 0; x < 64; ++x)
+                    for (int y = 0; y < 64; ++y) {
+                        double v = 0.0;
+                        for (int t = 0; t < NB; ++t) v += Xa[(size_t)(64 * qr + x) * n + t] * Xb[(size_t)(64 * qc + y) * n + t];
+                        acc[x * 64 + y] -= v;
+                    }
+            }
+            double* C = Fk(a, bb);
+            auto add_c = [&](const double* src) {
+                for (int x = 0; x < 64; ++x)
+                    for (int y = 0; y < 64; ++y) C[(size_t)(64 * qr + x) * n + 64 * qc + y] += src[x * 64 + y];
+            };
+            if (mode == 0) {
+                if (rec[9] >= 0 && !flag_ok(rec[9], 1)) return fail("flow: previous writer not done");
+                add_c(acc.data());
+                fl[rec[8]] = 1;
+            } else {
+                if (rec[6] < 0 || rec[6] >= s.flow_nscratch || slot_set[rec[6]]++) return fail("flow: scratch slot");
+                std::copy(acc.begin(), acc.end(), Pf.begin() + (size_t)rec[6] * 4096);
+                if (mode == 2) {
+                    fl[rec[8]] = 1;
+                } else if (++cntr[rec[10]] == (unsigned)rec[12]) {
+                    if (rec[9] >= 0 && !flag_ok(rec[9], 1)) return fail("flow: previous writer not done (combine)");
+                    for (int g = 0; g < rec[12]; ++g) add_c(&Pf[(size_t)(rec[11] + g) * 4096]);
+                    fl[rec[8]] = 1;
+                }
+            }
+        } else if (rec[0] == 3) {
+            if (colf[rec[1]] != 8) return fail("flow: inverse before its factor");
+        } else {
+            return fail("flow: record role");
+        }
+    }
+    double ferr = 0.0;
+    for (int64_t i = 0; i < nr; ++i)
+        for (int64_t j = 0; j < std::min(i + 1, n); ++j) ferr = std::max(ferr, std::fabs(F[(size_t)i * n + j] - rat(i, j)));
+    const double frel = ferr / scale;
+    if (!(frel < 1e-12)) {
+        printf("FAIL flow factor err %.3e\n", frel);
+        return 1;
+    }
     int ncomb = 0;
     for (int w = 0; w < s.n_waves; ++w) ncomb += s.w[w].ncomb;
-    printf("ok levels=%d blocks=%ld slots=%d split=%d err=%.3e xerr=%.3e\n", s.n_waves, (long)nb, L.n_img, ncomb, rel, xrel);
+    printf("ok levels=%d blocks=%ld slots=%d split=%d err=%.3e xerr=%.3e flow_err=%.3e flow_records=%d\n", s.n_waves, (long)nb,
+           L.n_img, ncomb, rel, xrel, frel, s.flow_n);
     return 0;
 }
