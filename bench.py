@@ -161,9 +161,9 @@ def main():
     t, chol_flops, lin_bytes = phase_roofline(ds, ms, n_phase)
 
     # rooflines, outside the timed region: one more step per probed kernel, HIP events around each of
-    # its launches on the stream it runs on.  k_panel (one launch per elimination-tree level: the
-    # level's 128x128 diagonal factorisations, panel solves and the previous level's trailing updates)
-    # has the largest share of GPU time, so it is `roofline`.
+    # its launches on the stream it runs on.  k_chol_flow (the whole block factorisation and forward
+    # solve as one persistent dataflow launch) has the largest share of GPU time, so it is `roofline`
+    # (FBA_CHOL_FLOW=0: k_panel, one launch per elimination-tree level).
     def probe(kind, name, note):
         ctx.set_probe(kind)
         step()
@@ -177,9 +177,14 @@ def main():
              "flops_per_launch": flops_launch, "traffic": pmc_traffic(args.config, name)}
         r["frac"] = r["achieved"] / r["peak"] if r["achieved"] else None
         return r
-    roof = probe(2, "k_panel", "one elimination-tree level: the 128x128 f64 diagonal-block potrf, the panel "
-                               "solves and the previous level's trailing updates as in-launch dataflow; a latency-"
-                               "bound chain, one launch per level")
+    flow = os.environ.get("FBA_CHOL_FLOW", "1") != "0"
+    roof = probe(2, "k_chol_flow", "the whole block Cholesky + forward solve in one persistent dataflow launch: "
+                                   "128x128 f64 diagonal-block potrfs, 64-row panel-half solves, 64x64 trailing-"
+                                   "update quarters, diagonal-block inverses; flops = their algorithmic sum; a "
+                                   "latency-bound chain over the elimination-tree levels") if flow else \
+        probe(2, "k_panel", "one elimination-tree level: the 128x128 f64 diagonal-block potrf, the panel "
+                            "solves and the previous level's trailing updates as in-launch dataflow; a latency-"
+                            "bound chain, one launch per level")
     # k_syrk_multi runs only for levels whose updates are not merged into the next level's k_panel
     # (FBA_MERGE_MAX; by default every level's are)
     roof_bulk = probe(1, "k_syrk_multi", "Cholesky trailing update of a level not merged into the next k_panel "

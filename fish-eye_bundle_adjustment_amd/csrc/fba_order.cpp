@@ -593,6 +593,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
         if (level[j] < nw - 1) {
             const int id = add({3, (int32_t)j}, {level[j] + 1, 5, (int)j});
             T[id].deps.push_back(col_task[j]);
+            s.flow_flops += (double)NB * NB * NB / 3.0;
         }
     // flags -> producer records
     for (size_t i = 0; i < T.size(); ++i)
