@@ -735,7 +735,11 @@ static void print_flow_trace(Ctx* c) {
         fprintf(stderr, "[fba]   diag wg %5d block %3d (fused %3d%s): start %7.1f  waits %7.1f  fused %7.1f  late %7.1f  end %7.1f\n",
                 b, rec[1], rec[2], rec[6] > 0 ? ", late" : "", us(r[0]), us(r[1]), rec[2] >= 0 ? us(r[4]) : -1.0,
                 rec[2] >= 0 ? us(r[5]) : -1.0, us(r[2]));
-        if (!detail || rec[2] < 0) continue;
+        if (!detail) continue;
+        fprintf(stderr, "[fba]       potrf column solved / published:");
+        for (int q = 0; q < 8; ++q) fprintf(stderr, " %.1f/%.1f", us(r[24 + q]), us(r[32 + q]));
+        fprintf(stderr, "\n");
+        if (rec[2] < 0) continue;
         fprintf(stderr, "[fba]       block in LDS / applied:");
         for (int q = 0; q < 8; ++q) fprintf(stderr, " %.1f/%.1f%s", us(r[8 + q]), us(r[16 + q]), (r[16 + q] >> 63) ? "p" : "");
         fprintf(stderr, "\n");
@@ -743,7 +747,8 @@ static void print_flow_trace(Ctx* c) {
             const int32_t* rx = recs + (size_t)Sched::FLOW_REC * x;
             const uint64_t* q = &t[FTRACE * (size_t)x];
             if (!(rx[0] == 1 && rx[1] == rec[2] && (rx[2] >> 1) == rec[1])) continue;
-            fprintf(stderr, "[fba]       half %d wg %5d: column in / published:", rx[2] & 1, x);
+            fprintf(stderr, "[fba]       half %d wg %5d: start %.1f waits %.1f column in / published:", rx[2] & 1, x, us(q[0]),
+                    us(q[1]));
             for (int u = 0; u < 8; ++u) fprintf(stderr, " %.1f/%.1f", us(q[8 + u]), us(q[16 + u]));
             fprintf(stderr, "  end %.1f\n", us(q[2]));
         }

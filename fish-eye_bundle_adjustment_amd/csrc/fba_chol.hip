@@ -493,7 +493,8 @@ __device__ __forceinline__ void potrf_body_sync(double* __restrict__ S, int64_t 
 template <bool TS, bool PRE = false>
 __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, int col, double* __restrict__ dinv,
                                            double* __restrict__ scal, unsigned long long* __restrict__ ts,
-                                           unsigned* __restrict__ flag, double* __restrict__ smem) {
+                                           unsigned* __restrict__ flag, double* __restrict__ smem,
+                                           uint64_t* __restrict__ pubts = nullptr) {
 #define POTRF_TS(i) do { if (TS && threadIdx.x == 0 && blockIdx.x == 0) ts[i] = __builtin_amdgcn_s_memtime(); } while (0)
 #define BULK_TS(i) do { if (TS && threadIdx.x == 64 && blockIdx.x == 0) ts[i] = __builtin_amdgcn_s_memtime(); } while (0)
     POTRF_TS(0);
@@ -715,8 +716,10 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
                 st_sc1(rD, (int64_t)(s * IB * IB + i) * 8, v);
             }
             if (flag) {
+                if (pubts && lane == 0) pubts[8 + s] = wall_clock64();  // FBA_PANEL_TRACE: column s solved
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0) __hip_atomic_store(flag, (unsigned)(s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (pubts && lane == 0) pubts[16 + s] = wall_clock64();  // ... and published
             }
         }
     }
@@ -1609,9 +1612,13 @@ __device__ __forceinline__ void trsm_flow_body(double* __restrict__ S, int64_t l
                                                            rX, (int)(((int64_t)(lk + 4 * r) * ld + IB * t + lr) * 8), 0, SC1));
     __syncthreads();  // the flags are zero
     if (!worker) {
+        // the four loader waves share every column (a single wave reading freshly written-through
+        // data gets only a few GB/s): wave 4 + v takes items v, v + 4, .. of the column's (8 - t) * 128
+        // double2, each raising the column's LDS count once its share is in
         const __amdgpu_buffer_rsrc_t rL = block_rsrc(L, ((int64_t)(CB - 1) * ld + CB) * 8);
         const __amdgpu_buffer_rsrc_t rD = block_rsrc(Dk, (CB / IB) * IB * IB * 8);
-        for (int t = wave - 4; t < CB / IB; t += 4) {
+        const int v4 = wave - 4;
+        for (int t = 0; t < CB / IB; ++t) {
             unsigned spins = 0;
             while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(t + 1)) {
                 __builtin_amdgcn_s_sleep(1);
@@ -1620,11 +1627,11 @@ __device__ __forceinline__ void trsm_flow_body(double* __restrict__ S, int64_t l
                     break;
                 }
             }
-            double2 v[16];
-            double* dst[16];
+            double2 v[4];
+            double* dst[4];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {  // items (8 - t) * 128 double2
-                const int i = lane + 64 * q, u = i >> 7, n = (i >> 3) & 15, kc = (i & 7) * 2;
+            for (int q = 0; q < 4; ++q) {  // items (8 - t) * 128 double2, item i = 256 q + 64 v4 + lane
+                const int i = 256 * q + 64 * v4 + lane, u = i >> 7, n = (i >> 3) & 15, kc = (i & 7) * 2;
                 dst[q] = nullptr;
                 if (u < CB / IB - 1 - t) {  // tile (r, t), r = t + 1 + u
                     const int r = t + 1 + u;
@@ -1636,15 +1643,15 @@ __device__ __forceinline__ void trsm_flow_body(double* __restrict__ S, int64_t l
                 }
             }
 #pragma unroll
-            for (int q = 0; q < 16; ++q)
+            for (int q = 0; q < 4; ++q)
                 if (dst[q]) {
                     dst[q][0] = v[q].x;
                     dst[q][1] = v[q].y;
                 }
             __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's LDS writes done
             __builtin_amdgcn_wave_barrier();
-            if (lane == 0) __hip_atomic_store(s_col + t, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (tr && lane == 0) tr[8 + t] = wall_clock64();  // FBA_PANEL_TRACE: column t of L_kk in LDS
+            if (lane == 0) __hip_atomic_fetch_add(s_col + t, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (tr && lane == 0 && v4 == 0) tr[8 + t] = wall_clock64();  // FBA_PANEL_TRACE: column t of L_kk in LDS
         }
         return;
     }
@@ -1660,7 +1667,7 @@ __device__ __forceinline__ void trsm_flow_body(double* __restrict__ S, int64_t l
 #pragma unroll
     for (int t = 0; t < CB / IB; ++t) {
         unsigned sp = 0;
-        while (__hip_atomic_load(s_col + t, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+        while (__hip_atomic_load(s_col + t, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4) {
             __builtin_amdgcn_s_sleep(1);
             if (++sp == FLAG_SPINS) break;  // (the loader reports the timeout)
         }
@@ -1710,7 +1717,7 @@ __device__ __forceinline__ void trsm_flow_body(double* __restrict__ S, int64_t l
         // column block t published now if column t+1 has not arrived (the wave would only wait), else
         // drained during step t+1
         pending = true;
-        if (t + 1 < CB / IB && __hip_atomic_load(s_col + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+        if (t + 1 < CB / IB && __hip_atomic_load(s_col + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             signal(t + 1);
             pending = false;
@@ -1749,7 +1756,7 @@ __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, co
     wait_list_sc1(lists + rec[3], rec[4], fl, scal);  // the final in-place writers of C_jj's quarters
     if (tr && threadIdx.x == 0) tr[1] = wall_clock64();
     if (f < 0 && rec[6] == 0) {
-        potrf_body<false>(S, ld, j, dinv, scal, nullptr, colflags + j, smem);
+        potrf_body<false>(S, ld, j, dinv, scal, nullptr, colflags + j, smem, tr ? tr + 16 : nullptr);
         return;
     }
 #define AT(r, c) smem[(((r) >> 4) * (((r) >> 4) + 1) / 2 + ((c) >> 4)) * (IB * 17) + ((r) & 15) * 17 + ((c) & 15)]
@@ -1787,25 +1794,28 @@ __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, co
             if (p1) v = std::min(v, __hip_atomic_load(p1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             return v;
         };
-        // column block t of the 128 rows: thread -> row (tid >> 3) + 64 e, columns 2 (tid & 7), +1
-        double2 xv[2];
-        auto issue = [&](int t) {
+        // column block b of the 128 rows: thread -> row (tid >> 3) + 64 e, columns 2 (tid & 7), +1; two
+        // register slots (block parity), so up to two blocks are in flight beyond the one in LDS
+        double2 xv[2][2];
+        auto issue = [&](int b, int sl) {
 #pragma unroll
             for (int e = 0; e < 2; ++e)
-                xv[e] = ld_sc1(rX, ((int64_t)((tid >> 3) + 64 * e) * ld + IB * t + 2 * (tid & 7)) * 8);
+                xv[sl][e] = ld_sc1(rX, ((int64_t)((tid >> 3) + 64 * e) * ld + IB * b + 2 * (tid & 7)) * 8);
         };
-        auto wait_for = [&](int t) {  // column block t published (thread 0 polls), then everyone issues
+        auto wait_pub = [&](int b) {  // column block b published (thread 0 polls), then the barrier
             if (tid == 0) {
                 unsigned spins = 0;
-                while (published() <= (unsigned)t) {
+                while (published() <= (unsigned)b) {
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }
                 }
             }
             __syncthreads();
-            issue(t);
         };
-        wait_for(0);
+        int issued = 0;  // blocks [0, issued) issued (uniform)
+        wait_pub(0);
+        issue(0, 0);
+        issued = 1;
         constexpr int NT = (POTRF_NT + POTRF_NW - 1) / POTRF_NW;  // 5 tiles per wave at most
         int ta[NT], tb[NT];
         dbl4 c[NT];  // this wave's tiles p = wave + 8 i of C_jj, in registers until the last block
@@ -1822,16 +1832,30 @@ __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, co
 #pragma unroll
         for (int t = 0; t < CB / IB; ++t) {
             double* X = Xb[t & 1];
+            if (issued <= t) {  // not in flight yet: wait for it
+                wait_pub(t);
+                issue(t, t & 1);
+                issued = t + 1;
+            }
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
-                X[((tid >> 3) + 64 * e) * 17 + 2 * (tid & 7)] = xv[e].x;
-                X[((tid >> 3) + 64 * e) * 17 + 2 * (tid & 7) + 1] = xv[e].y;
+                X[((tid >> 3) + 64 * e) * 17 + 2 * (tid & 7)] = xv[t & 1][e].x;
+                X[((tid >> 3) + 64 * e) * 17 + 2 * (tid & 7) + 1] = xv[t & 1][e].y;
             }
-            if (tid == 0) sy[31] = (t + 1 < CB / IB && published() > (unsigned)(t + 1));
+            if (tid == 0) sy[31] = (int)published();
             __syncthreads();  // block t in LDS; the other buffer's readers (block t-1) are done
             if (tr && tid == 0) tr[8 + t] = wall_clock64();  // FBA_PANEL_TRACE: block t in LDS
-            const bool pre = sy[31] != 0;
-            if (pre) issue(t + 1);  // the next block's loads in flight during this update
+            const int pub = sy[31];
+            const bool pre = issued > t + 1 || (t + 1 < CB / IB && pub > t + 1);
+            // blocks t+1 (slot of t+1) and t+2 (the slot block t just left) in flight during this update
+            if (issued == t + 1 && t + 1 < CB / IB && pub > t + 1) {
+                issue(t + 1, (t + 1) & 1);
+                issued = t + 2;
+            }
+            if (issued == t + 2 && t + 2 < CB / IB && pub > t + 2) {
+                issue(t + 2, t & 1);
+                issued = t + 3;
+            }
             // C(a, b) -= X_t(a) X_t(b)', tiles p = wave + 8 i of the 36 lower tiles
             double xa[NT][4], yb[NT][4];
 #pragma unroll
@@ -1857,7 +1881,6 @@ __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, co
                         for (int r = 0; r < 4; ++r) smem[p * IB * 17 + (lk + 4 * r) * 17 + lr] = c[i][r];
                     }
             if (tr && tid == 0) tr[16 + t] = wall_clock64() | (pre ? (1ull << 63) : 0);  // block t applied
-            if (!pre && t + 1 < CB / IB) wait_for(t + 1);
         }
     }
     if (tr && threadIdx.x == 0) tr[4] = wall_clock64();
@@ -1883,7 +1906,7 @@ __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, co
     }
     __syncthreads();  // the block final in LDS; the counters and buffers free
     if (tr && threadIdx.x == 0) tr[5] = wall_clock64();
-    potrf_body<false, true>(S, ld, j, dinv, scal, nullptr, colflags + j, smem);
+    potrf_body<false, true>(S, ld, j, dinv, scal, nullptr, colflags + j, smem, tr ? tr + 16 : nullptr);
 #undef AT
 }
 

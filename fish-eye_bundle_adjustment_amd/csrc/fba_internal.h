@@ -18,7 +18,7 @@ namespace fba {
 
 constexpr int NB = 128;       // Cholesky block size (rows/cols of one panel block, fba_chol.hip)
 constexpr int PTRACE_WG = 2048;  // FBA_PANEL_TRACE: workgroup slots per level
-constexpr int FTRACE = 32;       // FBA_PANEL_TRACE: stamps per k_chol_flow record
+constexpr int FTRACE = 40;       // FBA_PANEL_TRACE: stamps per k_chol_flow record
 constexpr int CHUNK_OBS = 256;  // observations per k_lin_reduce / k_lin_point workgroup (chunk)
 // tie points per chunk and co-visibility terms per chunk staged in LDS (a single larger point's are
 // read from HBM instead): smaller for nK >= 6, whose wider Jacobian rows leave less of the 160 KiB LDS
