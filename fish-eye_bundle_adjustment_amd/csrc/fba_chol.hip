@@ -1812,10 +1812,9 @@ __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, co
             }
             __syncthreads();
         };
-        int issued = 0;  // blocks [0, issued) issued (uniform)
-        wait_pub(0);
-        issue(0, 0);
-        issued = 1;
+        const int t0 = rec[11];  // blocks [0, t0) are applied by helper update tasks (late partials)
+        int issued = t0;         // blocks [t0, issued) issued (uniform)
+        if (t0 < CB / IB) wait_pub(t0);  // (its barrier also completes the C_jj load)
         constexpr int NT = (POTRF_NT + POTRF_NW - 1) / POTRF_NW;  // 5 tiles per wave at most
         int ta[NT], tb[NT];
         dbl4 c[NT];  // this wave's tiles p = wave + 8 i of C_jj, in registers until the last block
@@ -1831,6 +1830,7 @@ __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, co
         }
 #pragma unroll
         for (int t = 0; t < CB / IB; ++t) {
+            if (t < t0) continue;
             double* X = Xb[t & 1];
             if (issued <= t) {  // not in flight yet: wait for it
                 wait_pub(t);
@@ -1953,8 +1953,9 @@ __device__ __forceinline__ void syrk_flow_body(double* __restrict__ S, int64_t l
         const int64_t kc = (int64_t)sl[3 * s] * CB;
         const unsigned* pa = fl + sl[3 * s + 1];
         const unsigned* pb = fl + sl[3 * s + 2];
-        int t = 0;
-        while (t < CB / IB) {
+        int t = rec[13];
+        const int t_end = rec[14];
+        while (t < t_end) {
             if (tid == 0) {
                 unsigned spins = 0, va, vb;
                 for (;;) {
@@ -1962,9 +1963,9 @@ __device__ __forceinline__ void syrk_flow_body(double* __restrict__ S, int64_t l
                     vb = __hip_atomic_load(pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (va > (unsigned)t && vb > (unsigned)t) break;
                     __builtin_amdgcn_s_sleep(1);
-                    if (++spins == FLAG_SPINS) { scal[1] = -1.0; va = vb = CB / IB; break; }
+                    if (++spins == FLAG_SPINS) { scal[1] = -1.0; va = vb = (unsigned)t_end; break; }
                 }
-                sv[0] = (int)std::min(std::min(va, vb), (unsigned)(CB / IB));
+                sv[0] = (int)std::min(std::min(va, vb), (unsigned)t_end);
             }
             __syncthreads();
             const int v = sv[0];

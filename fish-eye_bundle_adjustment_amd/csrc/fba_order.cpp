@@ -421,7 +421,7 @@ std::vector<int32_t> camera_order(const fba_problem* p) {
 static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<std::vector<int32_t>>& R,
                        const std::vector<int32_t>& level, int64_t nb, const std::function<int64_t(int64_t)>& real_rows,
                        bool verbose) {
-    constexpr int SPLIT = 2, REC = Sched::FLOW_REC;
+    constexpr int SPLIT = 2, REC = Sched::FLOW_REC, CB_BLOCKS = NB / 16, IB_BLOCK = 16;
     const int nw = nb > 0 ? 1 + *std::max_element(level.begin(), level.end()) : 0;
     std::vector<std::vector<int32_t>> srcs(nb);
     for (int64_t k = 0; k < nb; ++k)
@@ -460,18 +460,24 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
         flag_deps.emplace_back();
         return (int)T.size() - 1;
     };
+    // FBA_FLOW_KSPLIT = K (1..8): the fused update's first K column blocks go to three helper update
+    // tasks (late partials) and the diagonal workgroup applies the rest; measured at config 4 (iter/s):
+    // K = 0 (default, the workgroup applies all eight) 1129, 2: 1078, 4: 1076, 5: 1096, 6: 1091 -- the
+    // helpers' extra hand-off costs more than the diagonal workgroup's arithmetic they take over
+    static const int ksplit = getenv("FBA_FLOW_KSPLIT") ? std::max(0, std::min(8, atoi(getenv("FBA_FLOW_KSPLIT")))) : 0;
     // diagonal blocks
     for (int64_t j = 0; j < nb; ++j) {
         const int32_t f = fsrc[j];
         int need = level[j] - 1;
         col_task[j] = add({0, (int32_t)j, f, 0, 0, 0, 0, f >= 0 ? prog[std::make_tuple(f, (int32_t)j, 0)] : -1,
-                           (f >= 0 && halves(j) > 1) ? prog[std::make_tuple(f, (int32_t)j, 1)] : -1},
+                           (f >= 0 && halves(j) > 1) ? prog[std::make_tuple(f, (int32_t)j, 1)] : -1, -1, -1,
+                           f >= 0 ? ksplit : 0},
                           {need, 0, (int)j});
         if (f >= 0) {
             flag_deps[col_task[j]].push_back(prog[std::make_tuple(f, (int32_t)j, 0)]);
             if (halves(j) > 1) flag_deps[col_task[j]].push_back(prog[std::make_tuple(f, (int32_t)j, 1)]);
         }
-        s.flow_flops += (double)NB * NB * NB / 3.0 + (f >= 0 ? (double)NB * NB * NB : 0.0);
+        s.flow_flops += (double)NB * NB * NB / 3.0 + (f >= 0 ? (double)NB * NB * NB * (8 - ksplit) / 8.0 : 0.0);
     }
     // panel-half solves
     for (int64_t k = 0; k < nb; ++k)
@@ -543,7 +549,8 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
                         mode = 0;
                         flag = wflag;
                     }
-                    const int id = add({2, a, b, q, soff, g1 - g0, slot, mode, flag, is_late ? -1 : prev, cidx, first, ng},
+                    const int id = add({2, a, b, q, soff, g1 - g0, slot, mode, flag, is_late ? -1 : prev, cidx, first, ng, 0,
+                                        CB_BLOCKS},
                                        {w, is_late ? 2 : rank, (int)(b * (nb + 1) + a) * 4 + q});
                     flag_deps[id] = fd;
                     if (!is_late && prev >= 0) flag_deps[id].push_back(prev);
@@ -552,6 +559,25 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
                 if (!is_late) prev = wflag;
             }
             writer[std::make_tuple(a, b, q)] = prev;
+        }
+    }
+    // the helpers of the fused updates: column blocks [0, ksplit) of f_j's panel rows j, per quarter
+    for (int64_t j = 0; j < nb && ksplit > 0; ++j) {
+        const int32_t f = fsrc[j];
+        if (f < 0) continue;
+        for (int q : {0, 2, 3}) {
+            const int qr = q >> 1, qc = q & 1;
+            if (q > 0 && halves(j) < 2) continue;
+            const int32_t pa = prog.at(std::make_tuple(f, (int32_t)j, qr)), pb = prog.at(std::make_tuple(f, (int32_t)j, qc));
+            const int32_t soff = (int32_t)buf.size();
+            buf.insert(buf.end(), {f, pa, pb});
+            const int32_t slot = nslot++, flag = new_uflag();
+            late[j].push_back({q, slot, flag});
+            const int id = add({2, (int32_t)j, (int32_t)j, q, soff, 1, slot, 2, flag, -1, -1, slot, 1, 0, ksplit},
+                               {level[f], 2, (int)(j * (nb + 1) + j) * 4 + q});
+            flag_deps[id] = {pa, pb};
+            uflag_tasks[flag - np].push_back(id);
+            s.flow_flops += 2.0 * 64 * 64 * IB_BLOCK * ksplit;
         }
     }
     // panel halves wait for the final writers of their quarters; diagonal blocks for those of their

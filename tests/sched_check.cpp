@@ -367,10 +367,10 @@ int main(int argc, char** argv) {
                 if (colf[f] != 8 || f >= j) return fail("flow: fused source not factored");
                 if (!flag_ok(rec[7], 8) || (rec[8] >= 0 && !flag_ok(rec[8], 8))) return fail("flow: fused rows not solved");
                 const double* X = Fk(j, f);
-                for (int a = 0; a < NB; ++a)
+                for (int a = 0; a < NB; ++a)  // the column blocks [rec[11], 8); the helpers' partials the rest
                     for (int c2 = 0; c2 <= a; ++c2) {
                         double v = 0.0;
-                        for (int t = 0; t < NB; ++t) v += X[(size_t)a * n + t] * X[(size_t)c2 * n + t];
+                        for (int t = 16 * rec[11]; t < NB; ++t) v += X[(size_t)a * n + t] * X[(size_t)c2 * n + t];
                         C[(size_t)a * n + c2] -= v;
                     }
             }
@@ -412,10 +412,12 @@ int main(int argc, char** argv) {
                 if (!flag_ok(tri[1], 8) || !flag_ok(tri[2], 8)) return fail("flow: update source not published");
                 const double* Xa = Fk(a, tri[0]);
                 const double* Xb = Fk(bb, tri[0]);
+                if (rec[13] < 0 || rec[14] > 8 || rec[13] >= rec[14]) return fail("flow: update column-block range");
                 for (int x = 0; x < 64; ++x)
                     for (int y = 0; y < 64; ++y) {
                         double v = 0.0;
-                        for (int t = 0; t < NB; ++t) v += Xa[(size_t)(64 * qr + x) * n + t] * Xb[(size_t)(64 * qc + y) * n + t];
+                        for (int t = 16 * rec[13]; t < 16 * rec[14]; ++t)
+                            v += Xa[(size_t)(64 * qr + x) * n + t] * Xb[(size_t)(64 * qc + y) * n + t];
                         acc[x * 64 + y] -= v;
                     }
             }
