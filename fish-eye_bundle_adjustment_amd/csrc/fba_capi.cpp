@@ -166,7 +166,7 @@ static void partition(const fba_problem* p, int world, std::vector<int32_t>& tie
 static void destroy(Ctx* c) {
     if (!c) return;
     void* ptrs[] = {c->d_chunk_obs, c->d_chunk_pt, c->d_xy, c->d_img, c->d_cam, c->d_pt, c->d_ctl, c->d_lp_tie, c->d_lp_start, c->d_lp_cam,
-                    c->d_acc, c->d_ppart, c->d_ipart, c->d_cpart, c->d_cseg, c->d_bscr, c->d_lrprof, c->d_ptrace, c->d_gpairs, c->d_red, c->d_xfull, c->d_xlin, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
+                    c->d_acc, c->d_ppart, c->d_ipart, c->d_cpart, c->d_cseg, c->d_bscr, c->d_gblk, c->d_lrprof, c->d_ptrace, c->d_gpairs, c->d_red, c->d_xfull, c->d_xlin, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
                     c->d_pt_tab, c->d_P, c->d_flags, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
                     c->d_active, c->d_counted, c->d_obs_pho, c->d_sched};
     for (void* q : ptrs)
@@ -555,6 +555,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         (rc = dalloc(&c->d_cpart, (size_t)c->n_chunks * npk)) ||
         (rc = dalloc(&c->d_cseg, (size_t)std::max(L.n_cam, 1) * 64 * npk)) ||
         (rc = dalloc(&c->d_bscr, (size_t)(32 * 14 + 16 * 120 + 16))) ||  // k_border_weights / k_border_gram segments, combine coefficients
+        (rc = dalloc(&c->d_gblk, (size_t)(L.n_pad / NB) * 256)) ||
         (rc = dalloc(&c->d_S, (size_t)(L.n_pad + NB) * L.ld)) ||
         (rc = dalloc(&c->d_P, (size_t)std::max(c->sched.n_scratch, 1) * 4096)) || (rc = dalloc(&c->d_X, (size_t)L.n_pad)) ||
         (rc = dalloc(&c->d_dinv, (size_t)(L.n_pad / NB) * 8 * 256)) ||

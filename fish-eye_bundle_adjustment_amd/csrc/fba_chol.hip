@@ -42,6 +42,13 @@ constexpr int CB = 128;   // outer block
 constexpr int IB = 16;    // inner block (MFMA tile)
 constexpr int LDA = 130;  // LDS row stride in doubles for 128-wide tiles: bank = (4r + 2k) mod 64
 
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {  // a DPP-permuted copy of v (all rows, all banks)
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
 __device__ __forceinline__ double readlane_d(double v, int lane) {
     const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
     const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
@@ -1303,8 +1310,11 @@ __global__ __launch_bounds__(256) void k_border_gram(const double* __restrict__ 
 // k_border_combine: every workgroup adds the Gram segments (fixed order), solves
 // [[A'A - I, A'B], [B'A, B'B]] [z; k] = -[A'y; B'y] (14x14, partial pivoting, wave 0 alone) and forms
 // u = y + A z + B k on its 256 entries of the RHS row (derivation in fba_kernels.hip, border section)
+// gblk != nullptr: the Gram comes as nblk per-column-block 16x16 partials (k_chol_flow's RHS panel
+// halves, row-major, rows/columns 15 zero), added in block order instead of the GRAM_SEG segments
 __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, int64_t ld, int64_t n_pad,
-                                                        const double* __restrict__ gpart, double* __restrict__ coef_out) {
+                                                        const double* __restrict__ gpart, double* __restrict__ coef_out,
+                                                        const double* __restrict__ gblk = nullptr, int nblk = 0) {
     __shared__ double g[15][15];
     __shared__ double coef[14];
     const int tid = threadIdx.x;
@@ -1312,19 +1322,33 @@ __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, 
         int a = 0, rem = tid;
         while (rem >= 15 - a) { rem -= 15 - a; ++a; }
         const int b = a + rem;
-        double x[GRAM_SEG];
-#pragma unroll
-        for (int q = 0; q < GRAM_SEG; ++q) x[q] = gpart[q * 120 + tid];
         double v = 0.0;
+        if (gblk) {
+            int q = 0;
+            for (; q + 8 <= nblk; q += 8) {  // 8 loads in flight, the same running sum
+                double x[8];
 #pragma unroll
-        for (int q = 0; q < GRAM_SEG; ++q) v += x[q];
+                for (int u = 0; u < 8; ++u) x[u] = gblk[(int64_t)(q + u) * 256 + a * 16 + b];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v += x[u];
+            }
+            for (; q < nblk; ++q) v += gblk[(int64_t)q * 256 + a * 16 + b];
+        } else {
+            double x[GRAM_SEG];
+#pragma unroll
+            for (int q = 0; q < GRAM_SEG; ++q) x[q] = gpart[q * 120 + tid];
+#pragma unroll
+            for (int q = 0; q < GRAM_SEG; ++q) v += x[q];
+        }
         g[a][b] = g[b][a] = v;
     }
     __syncthreads();
     if (tid < 64) {
-        // wave 0: lane r < 14 holds row r of the augmented H = [H | rhs] in registers; pivot rows move
-        // by cross-lane shuffles (no LDS round trips on the 14-column chain).  The arithmetic and its
-        // order are those of the plain row-by-row elimination and back substitution.
+        // wave 0: lane r < 14 holds row r of the augmented H = [H | rhs] in registers.  The pivot search
+        // is a DPP max-reduction over the 16-lane row (no LDS round trips), the pivot row and row col are
+        // broadcast with v_readlane from their (uniform) lanes, so a step is a few dozen VALU
+        // instructions.  The arithmetic and its order are those of the plain row-by-row elimination
+        // and back substitution.
         double h[15];
         if (tid < 14) {
 #pragma unroll
@@ -1334,24 +1358,24 @@ __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, 
 #pragma unroll
             for (int q = 0; q < 15; ++q) h[q] = 0.0;
         }
+        // v = max |candidate|, ties to the lower row; p its row (lanes outside [col, 14) seed p = col,
+        // so an all-NaN column keeps the pivot at col, as the serial search does)
+        auto take = [](double& v, int& p, double ov, int op) {
+            if (ov > v || (ov == v && op < p)) { v = ov; p = op; }
+        };
 #pragma unroll
         for (int col = 0; col < 14; ++col) {
-            // pivot: the first row of maximal |H[r][col]|, r >= col (wave reduction, ties to the lower row)
-            // lanes outside [col, 14) seed p = col, so an all-NaN column keeps the pivot at col (as the
-            // serial search does) instead of pulling in a finished row
             double v = (tid >= col && tid < 14) ? fabs(h[col]) : -1.0;
             int p = (tid >= col && tid < 14) ? tid : col;
-#pragma unroll
-            for (int w = 1; w < 16; w <<= 1) {
-                const double ov = __shfl_xor(v, w, 64);
-                const int op = __shfl_xor(p, w, 64);
-                if (ov > v || (ov == v && op < p)) { v = ov; p = op; }
-            }
-            p = __shfl(p, 0, 64);
+            take(v, p, dpp_f64<0xB1>(v), __builtin_amdgcn_mov_dpp(p, 0xB1, 0xF, 0xF, false));    // quad_perm [1,0,3,2]
+            take(v, p, dpp_f64<0x4E>(v), __builtin_amdgcn_mov_dpp(p, 0x4E, 0xF, 0xF, false));    // quad_perm [2,3,0,1]
+            take(v, p, dpp_f64<0x141>(v), __builtin_amdgcn_mov_dpp(p, 0x141, 0xF, 0xF, false));  // row_half_mirror
+            take(v, p, dpp_f64<0x140>(v), __builtin_amdgcn_mov_dpp(p, 0x140, 0xF, 0xF, false));  // row_mirror
+            p = __builtin_amdgcn_readfirstlane(p);
             double piv[15];
 #pragma unroll
             for (int q = col; q < 15; ++q) {
-                const double hp = __shfl(h[q], p, 64), hc = __shfl(h[q], col, 64);
+                const double hp = readlane_d(h[q], p), hc = readlane_d(h[q], col);
                 if (tid == p) h[q] = hc;     // row swap (a no-op when p == col)
                 if (tid == col) h[q] = hp;
                 piv[q] = hp;                 // the pivot row after the swap
@@ -1369,7 +1393,7 @@ __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, 
             double v = h[14];
 #pragma unroll
             for (int q = r + 1; q < 14; ++q) v -= h[q] * c[q];
-            c[r] = __shfl(v / h[r], r, 64);
+            c[r] = readlane_d(v / h[r], r);
         }
         if (tid < 14) {
             double mine = c[0];
@@ -1586,7 +1610,8 @@ constexpr size_t TRSMF_LDS = sizeof(double) * (4 * IB * 17 + (TRSM_NT + CB / IB)
 __device__ __forceinline__ void trsm_flow_body(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ rec,
                                                const double* __restrict__ dinv, const unsigned* __restrict__ flag,
                                                double* __restrict__ scal, double* __restrict__ smem,
-                                               uint64_t* __restrict__ tr, unsigned* __restrict__ prog) {
+                                               uint64_t* __restrict__ tr, unsigned* __restrict__ prog,
+                                               double* __restrict__ gram) {
     double* T = smem;                       // [4][IB][17]    per-wave transposes
     double* Lt = T + 4 * IB * 17;           // [28][IB][17]   L_st, p = s(s-1)/2 + t
     double* Dt = Lt + TRSM_NT * IB * 17;    // [8][IB][17]    D_s
@@ -1656,6 +1681,7 @@ __device__ __forceinline__ void trsm_flow_body(double* __restrict__ S, int64_t l
         return;
     }
     double* Tw = T + wave * IB * 17;
+    dbl4 gacc = dbl4{0.0, 0.0, 0.0, 0.0};  // the RHS half (gram != nullptr): the 16 x 16 Gram of wave 0's rows
     bool pending = false;  // column block t-1 stored, not yet signalled
     auto signal = [&](int done) {  // after this wave's drain: the last of the four raises the flag
         __builtin_amdgcn_wave_barrier();
@@ -1689,6 +1715,9 @@ __device__ __forceinline__ void trsm_flow_body(double* __restrict__ S, int64_t l
         double xa[4];
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) xa[kk] = -Tw[lr * 17 + 4 * kk + lk];
+        if (gram && wave == 0)  // the RHS rows (all in wave 0): G += X_t X_t'
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) gacc = mfma(xa[kk], xa[kk], gacc);
         if (t > 0 && pending) {  // column block t-1's stores drained during this step
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             signal(t);
@@ -1723,6 +1752,9 @@ __device__ __forceinline__ void trsm_flow_body(double* __restrict__ S, int64_t l
             pending = false;
         }
     }
+    if (gram && wave == 0)  // consumed by k_border_combine, the next launch
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gram[(lk + 4 * r) * 16 + lr] = gacc[r];
 }
 
 // wait until every flag of a list is set, then a workgroup barrier; no acquire fence: every load of
@@ -2075,7 +2107,8 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_chol_flow(double* __restrict_
                                                              double* __restrict__ dinv, double* __restrict__ linv,
                                                              double* __restrict__ scal, unsigned* __restrict__ colflags,
                                                              unsigned* __restrict__ fl, unsigned* __restrict__ cnt,
-                                                             double* __restrict__ P, uint64_t* __restrict__ trace) {
+                                                             double* __restrict__ P, uint64_t* __restrict__ trace,
+                                                             double* __restrict__ gblk) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int32_t* rec = recs + Sched::FLOW_REC * (int64_t)blockIdx.x;
     uint64_t* tr = trace ? trace + FTRACE * (int64_t)blockIdx.x : nullptr;
@@ -2086,7 +2119,8 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_chol_flow(double* __restrict_
     } else if (role == 1) {
         wait_list_sc1(lists + rec[3], rec[4], fl, scal);  // the final writers of the panel block's quarters
         if (tr && threadIdx.x == 0) tr[1] = wall_clock64();
-        trsm_flow_body(S, ld, rec + 1, dinv, colflags + rec[1], scal, smem, tr, fl + rec[5]);
+        trsm_flow_body(S, ld, rec + 1, dinv, colflags + rec[1], scal, smem, tr, fl + rec[5],
+                       (gblk && rec[7] >= 0) ? gblk + (int64_t)rec[7] * 256 : nullptr);
     } else if (role == 2) {
         syrk_flow_body(S, ld, rec, lists, P, fl, cnt, scal, smem, tr);
     } else {
@@ -2334,7 +2368,7 @@ int launch_cholesky(Ctx& c) {
         if (pp) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
         k_chol_flow<<<(unsigned)s.flow_n, POTRF_THREADS, FLOW_LDS, c.stream>>>(
             c.d_S, ld, c.d_sched, c.d_sched + s.flow_rec, c.d_dinv, c.d_linv, c.d_scal, c.d_flags, c.d_tflags,
-            c.d_counters, c.d_P, c.d_ptrace);
+            c.d_counters, c.d_P, c.d_ptrace, c.set.inner_constraints ? c.d_gblk : nullptr);
         if (pp) {
             FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], c.stream));
             c.probe_flops += s.flow_flops;
@@ -2465,12 +2499,16 @@ int launch_backward(Ctx& c) {
     if (c.set.inner_constraints) {
         // (running k_trtri128 on a forked stream concurrently with these two measured slower: a forked
         // iteration graph adds cross-queue waits to every launch of the Cholesky chain)
-        k_border_gram<<<GRAM_SEG, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_bscr + 32 * 14);
+        // k_chol_flow's RHS panel halves left the Gram as per-block partials (d_gblk); otherwise
+        // k_border_gram forms it from the forward-solved rows
+        const bool gblk = c.chol_flow && s.flow_ok && s.flow_n > 0;
+        if (!gblk) k_border_gram<<<GRAM_SEG, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_bscr + 32 * 14);
         if (flow)  // the 14 coefficients only; k_bwd_flow applies them to its block
-            k_border_combine<<<1, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_bscr + 32 * 14, coef);
+            k_border_combine<<<1, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_bscr + 32 * 14, coef,
+                                                      gblk ? c.d_gblk : nullptr, (int)nb);
         else
             k_border_combine<<<(unsigned)((c.L.n_pad + 255) / 256), 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad,
-                                                                                       c.d_bscr + 32 * 14, nullptr);
+                                                                                       c.d_bscr + 32 * 14, nullptr, gblk ? c.d_gblk : nullptr, (int)nb);
     }
     if (flow) {  // one launch, every workgroup resident; roots solve by substitution
         k_bwd_flow<<<(unsigned)nb, 256, BWD_LDS, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_linv, c.d_dinv, c.d_X, c.d_delta, c.L.u_c,

@@ -186,6 +186,8 @@ struct Ctx {
     int ncomp = 0;
     double* d_cseg = nullptr;    // [n_cam][64][NCAM] camera segment sums (k_red_cam_seg)
     double* d_bscr = nullptr;    // border scratch: [32][14] weight segment sums | [16][120] Gram segments
+    double* d_gblk = nullptr;    // [n_pad / NB][16][16] per-column-block Gram partials of the forward-solved
+                                 // RHS rows (k_chol_flow; inner constraints)
     double* d_WT = nullptr;      // [n_obs_pad][18] per-obs T = W V^-1 (back-substitution)
     double* d_pt_tab = nullptr;  // [n_lp_pad][pt_comp] Vinv(6) vb(3) b(3) Wc(3cw) Tc(3cw)
     int pt_comp = 0;

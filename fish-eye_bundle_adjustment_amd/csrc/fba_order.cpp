@@ -484,7 +484,9 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
         for (int32_t r : R[k])
             for (int h = 0; h < halves(r); ++h) {
                 const int32_t p = prog[std::make_tuple((int32_t)k, r, h)];
-                const int id = add({1, (int32_t)k, 2 * r + h, 0, 0, p}, {level[k], 1, (int)(k * (nb + 1) + r) * 2 + h});
+                // rec[7]: the RHS block row's half 0 accumulates its rows' Gram into partial k
+                const int id = add({1, (int32_t)k, 2 * r + h, 0, 0, p, 0, (r == nb && h == 0) ? (int32_t)k : -1},
+                                   {level[k], 1, (int)(k * (nb + 1) + r) * 2 + h});
                 T[id].deps.push_back(col_task[k]);
                 prog_task[p] = id;
                 s.flow_flops += 64.0 * NB * NB;
