@@ -722,8 +722,8 @@ static void print_flow_trace(Ctx* c) {
         if (t[FTRACE * (size_t)b]) t0 = std::min(t0, t[FTRACE * (size_t)b]);
     const uint64_t M = (1ull << 63) - 1;
     auto us = [&](uint64_t v) { return (v & M) ? (double)((v & M) - t0) * 0.01 : -1.0; };
-    uint64_t rend[4] = {0, 0, 0, 0};
-    int rn[4] = {0, 0, 0, 0};
+    uint64_t rend[5] = {0, 0, 0, 0, 0};
+    int rn[5] = {0, 0, 0, 0, 0};
     const int32_t* recs = s.buf.data() + s.flow_rec;
     const bool detail = getenv("FBA_PANEL_TRACE")[0] == '2';
     for (int b = 0; b < s.flow_n; ++b) {
@@ -737,12 +737,16 @@ static void print_flow_trace(Ctx* c) {
                 b, rec[1], rec[2], rec[6] > 0 ? ", late" : "", us(r[0]), us(r[1]), rec[2] >= 0 ? us(r[4]) : -1.0,
                 rec[2] >= 0 ? us(r[5]) : -1.0, us(r[2]));
         if (!detail) continue;
-        fprintf(stderr, "[fba]       potrf column solved / published:");
+        fprintf(stderr, "[fba]       potrf leaf 0 %.1f, barrier %.1f, panel tile (2, 0) %.1f; column solved / published:",
+                us(r[3]), us(r[6]), us(r[7]));
         for (int q = 0; q < 8; ++q) fprintf(stderr, " %.1f/%.1f", us(r[24 + q]), us(r[32 + q]));
         fprintf(stderr, "\n");
         if (rec[2] < 0) continue;
         fprintf(stderr, "[fba]       block in LDS / applied:");
         for (int q = 0; q < 8; ++q) fprintf(stderr, " %.1f/%.1f%s", us(r[8 + q]), us(r[16 + q]), (r[16 + q] >> 63) ? "p" : "");
+        fprintf(stderr, "\n");
+        fprintf(stderr, "[fba]       loading group's share stored:");
+        for (int q = 0; q < 8; ++q) fprintf(stderr, " %.1f", us(r[40 + q]));
         fprintf(stderr, "\n");
         for (int x = 0; x < s.flow_n; ++x) {  // the panel halves of its fused rows
             const int32_t* rx = recs + (size_t)Sched::FLOW_REC * x;
@@ -753,9 +757,18 @@ static void print_flow_trace(Ctx* c) {
             for (int u = 0; u < 8; ++u) fprintf(stderr, " %.1f/%.1f", us(q[8 + u]), us(q[16 + u]));
             fprintf(stderr, "  end %.1f\n", us(q[2]));
         }
+        for (int x = 0; x < s.flow_n && rec[9] >= 0; ++x) {  // its split helper
+            const int32_t* rx = recs + (size_t)Sched::FLOW_REC * x;
+            const uint64_t* q = &t[FTRACE * (size_t)x];
+            if (!(rx[0] == 4 && rx[1] == rec[1])) continue;
+            fprintf(stderr, "[fba]       split helper wg %5d: start %.1f block in LDS / applied:", x, us(q[0]));
+            for (int u = 0; u < 8; ++u) fprintf(stderr, " %.1f/%.1f", us(q[8 + u]), us(q[16 + u]));
+            fprintf(stderr, "  end %.1f\n", us(q[2]));
+        }
     }
-    fprintf(stderr, "[fba] flow: diag %d (last end %.1f), panel halves %d (%.1f), updates %d (%.1f), inverses %d (%.1f)\n", rn[0],
-            us(rend[0]), rn[1], us(rend[1]), rn[2], us(rend[2]), rn[3], us(rend[3]));
+    fprintf(stderr, "[fba] flow: diag %d (last end %.1f), panel halves %d (%.1f), updates %d (%.1f), inverses %d (%.1f), "
+            "split helpers %d (%.1f)\n", rn[0], us(rend[0]), rn[1], us(rend[1]), rn[2], us(rend[2]), rn[3], us(rend[3]),
+            rn[4], us(rend[4]));
     (void)hipMemset(c->d_ptrace, 0, t.size() * sizeof(uint64_t));
 }
 

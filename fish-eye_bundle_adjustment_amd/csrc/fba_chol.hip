@@ -483,6 +483,34 @@ __device__ __forceinline__ void potrf_body_sync(double* __restrict__ S, int64_t 
 #undef POTRF_TS
 }
 
+__device__ __forceinline__ void spin_ge(const unsigned* p, unsigned v, double* __restrict__ scal) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }  // hand-off timeout (host reports it)
+    }
+}
+
+// tile sets of a fused diagonal update (tiles (a, b), a >= b, in row order): 0 all 36 lower tiles, 1 those
+// of tile columns < FLOW_CSPLIT (the diagonal workgroup's share when split), 2 the others (the helper's)
+__host__ __device__ constexpr bool fset_has(int set, int b) { return set == 0 || (set == 1) == (b < FLOW_CSPLIT); }
+__host__ __device__ constexpr int fset_count(int set) {
+    int n = 0;
+    for (int a = 0; a < CB / IB; ++a)
+        for (int b = 0; b <= a; ++b) n += fset_has(set, b) ? 1 : 0;
+    return n;
+}
+__device__ __forceinline__ void fset_tile(int set, int idx, int& ta, int& tb) {  // (0, 0) past the end
+    ta = tb = 0;
+    int n = 0;
+    for (int a = 0; a < CB / IB; ++a)
+        for (int b = 0; b <= a; ++b)
+            if (fset_has(set, b)) {
+                if (n == idx) { ta = a; tb = b; }
+                ++n;
+            }
+}
+
 // potrf_body (dataflow): factor the 128x128 diagonal block of column col (512 threads); flag != nullptr:
 // publish it column by column (k_panel hand-off).  No workgroup barriers after the load: the waves
 // coordinate through LDS counters (workgroup-scope release / acquire), so wave 0 runs the critical
@@ -497,11 +525,16 @@ __device__ __forceinline__ void potrf_body_sync(double* __restrict__ S, int64_t 
 // Every wait points to work that does not wait for the waiter, so the chain always progresses; the
 // polls are bounded (scal[1] = -1 on timeout, reported by the host).
 // PRE: the block's lower tiles are already in LDS (k_chol_flow's diagonal workgroup updated them there)
+// hpart (flag hflag): the split helper's partial of the tiles of tile columns >= FLOW_CSPLIT (fset 2 order,
+// 16 x 16 row-major each), added by the bulk waves at their step FLOW_CSPLIT - 2, between the trailing
+// updates of the step before (every one done) and their own; nothing reads those tiles earlier (wave 0's
+// step s touches tiles (s+1, s), (s+1, s+1); wave 4 stores block column s after step s)
 template <bool TS, bool PRE = false>
 __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, int col, double* __restrict__ dinv,
                                            double* __restrict__ scal, unsigned long long* __restrict__ ts,
                                            unsigned* __restrict__ flag, double* __restrict__ smem,
-                                           uint64_t* __restrict__ pubts = nullptr) {
+                                           uint64_t* __restrict__ pubts = nullptr, const double* __restrict__ hpart = nullptr,
+                                           const unsigned* __restrict__ hflag = nullptr) {
 #define POTRF_TS(i) do { if (TS && threadIdx.x == 0 && blockIdx.x == 0) ts[i] = __builtin_amdgcn_s_memtime(); } while (0)
 #define BULK_TS(i) do { if (TS && threadIdx.x == 64 && blockIdx.x == 0) ts[i] = __builtin_amdgcn_s_memtime(); } while (0)
     POTRF_TS(0);
@@ -513,6 +546,7 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
     int* s_pc = sy + 1;     // [7] panel tiles of column s solved (complete: 7 - s)
     int* s_bc = sy + 8;     // [6] bulk waves done with the trailing update of step s (complete: 6)
     int* s_cc = sy + 16;    // [6] row s+2 (tiles (s+2, s+1), (s+2, s+2)) updated by column s
+    int* s_add = sy + 14;   // bulk waves done adding the split helper's partial
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int lr = lane & 15, lk = lane >> 4;
     const int64_t dbase = (k0 / CB) * (CB / IB) * (IB * IB);
@@ -551,6 +585,8 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
 #pragma unroll
             for (int c = 0; c < IB; ++c) a[c] = AT(lr, c);
             ok = leaf(0);
+            // FBA_PANEL_TRACE (k_chol_flow's record stamps, pubts = record + 16): leaf 0 factored
+            if (pubts && lane == 0) pubts[-13] = wall_clock64();
         }
     } else {
         // wave 0 reads the rows of diagonal tile 0 straight into registers and factors leaf 0 while the
@@ -594,6 +630,7 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
     }
     __syncthreads();  // all tiles, leaf 0 and the zeroed counters in LDS
     if (tid == 0) __hip_atomic_store(s_leaf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (PRE && pubts && tid == 0) pubts[-10] = wall_clock64();  // FBA_PANEL_TRACE: past the barrier
     POTRF_TS(3);
     if (wave == 0) {
         // the critical chain
@@ -664,6 +701,21 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
             BULK_TS(41 + 3 * s);
             if (s > 0) wait_ge(s_bc + s - 1, NBULK);  // every update of step s-1
             BULK_TS(42 + 3 * s);
+            // the split helper's partial: this wave's tiles h = b + 6 m (15 in all) in flight during the
+            // panel tile, then added; every bulk wave polls the flag itself before its loads
+            constexpr int NH = fset_count(2), HM = (NH + NBULK - 1) / NBULK;
+            static_assert(FLOW_CSPLIT >= 2 && FLOW_CSPLIT < CB / IB, "split step");
+            double2 hv[HM][2];
+            if (hpart && s == FLOW_CSPLIT - 2) {
+                spin_ge(hflag, 1u, scal);
+                const __amdgpu_buffer_rsrc_t rH = block_rsrc(hpart, NH * IB * IB * 8);
+#pragma unroll
+                for (int m = 0; m < HM; ++m)
+                    if (b + NBULK * m < NH)
+#pragma unroll
+                        for (int e = 0; e < 2; ++e)
+                            hv[m][e] = ld_sc1(rH, (int64_t)((b + NBULK * m) * IB * IB + 2 * (lane + 64 * e)) * 8);
+            }
             if (b < CB / IB - 2 - s) {                // panel tile (s+2+b, s)
                 const int r0 = (s + 2 + b) * IB;
                 const double* Dl = Dall + s * IB * 17;
@@ -679,6 +731,23 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
 #pragma unroll
                 for (int r = 0; r < 4; ++r) AT((r0 + lk + 4 * r), c0 + lr) = acc[r];
                 bump(s_pc + s);
+                if (PRE && pubts && s == 0 && b == 0 && lane == 0) pubts[-9] = wall_clock64();  // panel tile (2, 0)
+            }
+            if (hpart && s == FLOW_CSPLIT - 2) {
+#pragma unroll
+                for (int m = 0; m < HM; ++m)
+                    if (b + NBULK * m < NH) {
+                        int ha, hb;
+                        fset_tile(2, b + NBULK * m, ha, hb);
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            const int x = 2 * (lane + 64 * e), hr = IB * ha + (x >> 4), hc = IB * hb + (x & 15);
+                            AT(hr, hc) += hv[m][e].x;
+                            AT(hr, hc + 1) += hv[m][e].y;
+                        }
+                    }
+                bump(s_add);
+                wait_ge(s_add, NBULK);  // every tile final before this step's trailing updates
             }
             wait_ge(s_pc + s, CB / IB - 1 - s);  // column s solved
             // trailing update of rows s+2 .. 7 by column s: row s+2 (wave 0's next panel tile and
@@ -1592,13 +1661,6 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_panel(double* __restrict__ S,
 // k_chol_flow: the whole block factorisation as ONE persistent launch (schedule: fba_order.cpp
 // build_flow).  One 512-thread workgroup per record; every wait points to an earlier record.
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ void spin_ge(const unsigned* p, unsigned v, double* __restrict__ scal) {
-    unsigned spins = 0;
-    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }  // hand-off timeout (host reports it)
-    }
-}
 
 // trsm_flow_body (k_chol_flow role 1): one 64-row half of panel block (r, k), X = A L_kk^-T, RIGHT-looking
 // with each solving wave's 16 rows of A in registers: as block column t of L_kk arrives (waves 4-7
@@ -1773,12 +1835,154 @@ constexpr size_t FLOWF_LDS = sizeof(double) * (POTRF_NT * IB * 17 + (CB / IB) * 
                              sizeof(double) * CB * 17;
 static_assert(CB * 17 == (CB / IB) * IB * 17, "a column-block buffer is exactly the leaf-inverse area");
 
+// fused_apply<SET>: C -= X X' on the tiles of SET, X = L(j, f) consumed column block by column block as
+// the two panel-half records of (f, j) publish it (progress flags p0, p1): block t + 1's loads are issued
+// before block t's update whenever it is already published, so the update (in registers, tiles spread
+// over all eight waves) keeps pace with the panel solves.  SET 0/1: C from and back to the LDS block
+// (smem, the potrf's tile layout); SET 2: from zero, to out (the helper's scratch partial).  X's column
+// blocks [t0, 8) (blocks [0, t0): helper update tasks).  X0, X1: two [128][17] LDS buffers; sy[31] a word.
+template <int SET>
+__device__ __forceinline__ void fused_apply(const __amdgpu_buffer_rsrc_t rX, int64_t ld, const unsigned* __restrict__ p0,
+                                            const unsigned* __restrict__ p1, int t0, double* __restrict__ X0,
+                                            double* __restrict__ X1, int* __restrict__ sy, double* __restrict__ smem,
+                                            double* __restrict__ out, double* __restrict__ scal, uint64_t* __restrict__ tr) {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int lr = lane & 15, lk = lane >> 4;
+    double* Xb[2] = {X0, X1};
+    auto published = [&]() {
+        unsigned v = __hip_atomic_load(p0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (p1) v = std::min(v, __hip_atomic_load(p1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        return v;
+    };
+    // column block b (128 rows x 16) is loaded by ONE group of waves, block parity: waves 1-3 (even, six
+    // 16-B items per lane) or waves 4-7 (odd, four), item i -> row i >> 3, columns 2 (i & 7), +1; wave 0
+    // loads nothing and thread 0 reads the progress flags.  So every wave has at most one block's loads
+    // in flight and the compiler's wait before storing a block into LDS waits for that block alone,
+    // while the other group's block (t + 2) stays in flight across the barrier (with both slots in
+    // every wave, the wait for block t + 1 also waited for t + 2's loads)
+    const int grp = wave == 0 ? -1 : (wave < 4 ? 0 : 1);
+    const int gl = grp == 0 ? tid - 64 : tid - 256;
+    constexpr int GM = 6;  // items per lane, group 0 (group 1: 4)
+    double2 xl[GM];
+    auto issue = [&](int b) {
+        if (grp != (b & 1)) return;
+#pragma unroll
+        for (int m = 0; m < GM; ++m) {
+            const int i = gl + (grp == 0 ? 192 : 256) * m;
+            if ((grp == 0 || m < 4) && i < 1024)
+                xl[m] = ld_sc1(rX, ((int64_t)(i >> 3) * ld + IB * b + 2 * (i & 7)) * 8);
+        }
+    };
+    auto store = [&](int b, double* X) {
+        if (grp != (b & 1)) return;
+#pragma unroll
+        for (int m = 0; m < GM; ++m) {
+            const int i = gl + (grp == 0 ? 192 : 256) * m;
+            if ((grp == 0 || m < 4) && i < 1024) {
+                X[(i >> 3) * 17 + 2 * (i & 7)] = xl[m].x;
+                X[(i >> 3) * 17 + 2 * (i & 7) + 1] = xl[m].y;
+            }
+        }
+    };
+    // thread 0: the progress values last read (issued after a barrier, their min taken at the next, so
+    // wave 0 does not wait for the loads before its update)
+    unsigned fv, fv0 = 0, fv1 = ~0u;
+    auto wait_pub = [&](int b) {  // column block b published (thread 0 polls), then the barrier
+        if (tid == 0) {
+            unsigned spins = 0;
+            while ((fv = published()) <= (unsigned)b) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }
+            }
+            fv0 = fv;
+            fv1 = ~0u;
+        }
+        __syncthreads();
+    };
+    int issued = t0;         // blocks [t0, issued) issued (uniform)
+    if (t0 < CB / IB) wait_pub(t0);  // (its barrier also completes the C_jj load)
+    constexpr int NS = fset_count(SET), NT = (NS + POTRF_NW - 1) / POTRF_NW;  // tiles of the set, per wave at most
+    int ta[NT], tb[NT];
+    dbl4 c[NT];  // this wave's tiles wave + 8 i of the set, in registers until the last block
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+        fset_tile(SET, wave + POTRF_NW * i, ta[i], tb[i]);
+        if (wave + POTRF_NW * i < NS)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                c[i][r] = SET == 2 ? 0.0 : smem[(ta[i] * (ta[i] + 1) / 2 + tb[i]) * IB * 17 + (lk + 4 * r) * 17 + lr];
+    }
+#pragma unroll
+    for (int t = 0; t < CB / IB; ++t) {
+        if (t < t0) continue;
+        double* X = Xb[t & 1];
+        if (issued <= t) {  // not in flight yet: wait for it
+            wait_pub(t);
+            issue(t);
+            issued = t + 1;
+        }
+        store(t, X);
+        if (tr && tid == ((t & 1) ? 256 : 64)) tr[40 + t] = wall_clock64();  // FBA_PANEL_TRACE: group's share stored
+        // (block t + 1 not in flight yet: read the flags now rather than use the values read during the
+        // last update, which would issue it one update later)
+        if (tid == 0) sy[31] = (int)(issued == t + 1 && t + 1 < CB / IB ? published() : std::min(fv0, fv1));
+        __syncthreads();  // block t in LDS; the other buffer's readers (block t-1) are done
+        if (tr && tid == 0) tr[8 + t] = wall_clock64();  // FBA_PANEL_TRACE: block t in LDS
+        const int pub = sy[31];
+        const bool pre = issued > t + 1 || (t + 1 < CB / IB && pub > t + 1);
+        // blocks t+1 (the other group, idle since it stored t-1) and t+2 (this block's group) in flight
+        // during this update
+        if (issued == t + 1 && t + 1 < CB / IB && pub > t + 1) {
+            issue(t + 1);
+            issued = t + 2;
+        }
+        if (issued == t + 2 && t + 2 < CB / IB && pub > t + 2) {
+            issue(t + 2);
+            issued = t + 3;
+        }
+        if (tid == 0) {  // consumed before the next barrier, after this update
+            fv0 = __hip_atomic_load(p0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            fv1 = p1 ? __hip_atomic_load(p1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
+        }
+        // C(a, b) -= X_t(a) X_t(b)' on this wave's tiles of the set
+        double xa[NT][4], yb[NT][4];
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+            if (wave + POTRF_NW * i < NS) {
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    xa[i][kk] = -X[(IB * ta[i] + lr) * 17 + 4 * kk + lk];
+                    yb[i][kk] = X[(IB * tb[i] + lr) * 17 + 4 * kk + lk];
+                }
+            }
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+                if (wave + POTRF_NW * i < NS) c[i] = mfma(xa[i][kk], yb[i][kk], c[i]);
+        if (t == CB / IB - 1)
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+                if (wave + POTRF_NW * i < NS) {
+                    if (SET == 2)  // the helper: its tiles to the scratch partial, 16 x 16 row-major each
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            __hip_atomic_store(out + (wave + POTRF_NW * i) * IB * IB + (lk + 4 * r) * IB + lr, c[i][r],
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    else
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            smem[(ta[i] * (ta[i] + 1) / 2 + tb[i]) * IB * 17 + (lk + 4 * r) * 17 + lr] = c[i][r];
+                }
+        if (tr && tid == 0) tr[16 + t] = wall_clock64() | (pre ? (1ull << 63) : 0);  // block t applied
+    }
+}
+
 // diag_body (role 0): diagonal block j.  C_jj (its final in-place writers done) is loaded into LDS; with
-// a fused source f (rec[2] >= 0) the block row X = L(j, f) is consumed column block by column block as
-// the two panel-half records of (f, j) publish it (progress flags rec[7], rec[8]): block t + 1's loads
-// are issued before block t's update whenever it is already published, so the update (C_jj -= X_t X_t'
-// in LDS on all eight waves) keeps pace with the panel solves; then the late partials (the other
-// sources of f's level, scratch quarters, slot order); then the potrf on the LDS block.
+// a fused source f (rec[2] >= 0) C_jj -= X X', X = L(j, f), as the panel halves of (f, j) publish X
+// (fused_apply: all tiles, or with a split helper, rec[9] >= 0, those of tile columns < FLOW_CSPLIT);
+// then the late partials (the other sources of f's level, scratch quarters, slot order); then the potrf
+// on the LDS block, whose bulk waves add the helper's partial (scratch slot rec[10], flag rec[9]).
 __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ rec,
                                           const int32_t* __restrict__ lists, double* __restrict__ dinv,
                                           double* __restrict__ scal, unsigned* __restrict__ colflags,
@@ -1792,8 +1996,7 @@ __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, co
         return;
     }
 #define AT(r, c) smem[(((r) >> 4) * (((r) >> 4) + 1) / 2 + ((c) >> 4)) * (IB * 17) + ((r) & 15) * 17 + ((c) & 15)]
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int lr = lane & 15, lk = lane >> 4;
+    const int tid = threadIdx.x;
     const int64_t k0 = (int64_t)j * CB;
     double* Dall = smem + POTRF_NT * IB * 17;
     int* sy = reinterpret_cast<int*>(Dall + (CB / IB) * IB * 17);
@@ -1821,99 +2024,10 @@ __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, co
         const __amdgpu_buffer_rsrc_t rX = block_rsrc(S + k0 * ld + f0, ((int64_t)(CB - 1) * ld + CB) * 8);
         const unsigned* p0 = fl + rec[7];
         const unsigned* p1 = rec[8] >= 0 ? fl + rec[8] : nullptr;
-        auto published = [&]() {
-            unsigned v = __hip_atomic_load(p0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (p1) v = std::min(v, __hip_atomic_load(p1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            return v;
-        };
-        // column block b of the 128 rows: thread -> row (tid >> 3) + 64 e, columns 2 (tid & 7), +1; two
-        // register slots (block parity), so up to two blocks are in flight beyond the one in LDS
-        double2 xv[2][2];
-        auto issue = [&](int b, int sl) {
-#pragma unroll
-            for (int e = 0; e < 2; ++e)
-                xv[sl][e] = ld_sc1(rX, ((int64_t)((tid >> 3) + 64 * e) * ld + IB * b + 2 * (tid & 7)) * 8);
-        };
-        auto wait_pub = [&](int b) {  // column block b published (thread 0 polls), then the barrier
-            if (tid == 0) {
-                unsigned spins = 0;
-                while (published() <= (unsigned)b) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }
-                }
-            }
-            __syncthreads();
-        };
-        const int t0 = rec[11];  // blocks [0, t0) are applied by helper update tasks (late partials)
-        int issued = t0;         // blocks [t0, issued) issued (uniform)
-        if (t0 < CB / IB) wait_pub(t0);  // (its barrier also completes the C_jj load)
-        constexpr int NT = (POTRF_NT + POTRF_NW - 1) / POTRF_NW;  // 5 tiles per wave at most
-        int ta[NT], tb[NT];
-        dbl4 c[NT];  // this wave's tiles p = wave + 8 i of C_jj, in registers until the last block
-#pragma unroll
-        for (int i = 0; i < NT; ++i) {
-            int a = 0, b = wave + POTRF_NW * i;
-            while (b > a) { b -= a + 1; ++a; }
-            ta[i] = a;
-            tb[i] = b;
-            if (wave + POTRF_NW * i < POTRF_NT)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) c[i][r] = smem[(wave + POTRF_NW * i) * IB * 17 + (lk + 4 * r) * 17 + lr];
-        }
-#pragma unroll
-        for (int t = 0; t < CB / IB; ++t) {
-            if (t < t0) continue;
-            double* X = Xb[t & 1];
-            if (issued <= t) {  // not in flight yet: wait for it
-                wait_pub(t);
-                issue(t, t & 1);
-                issued = t + 1;
-            }
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                X[((tid >> 3) + 64 * e) * 17 + 2 * (tid & 7)] = xv[t & 1][e].x;
-                X[((tid >> 3) + 64 * e) * 17 + 2 * (tid & 7) + 1] = xv[t & 1][e].y;
-            }
-            if (tid == 0) sy[31] = (int)published();
-            __syncthreads();  // block t in LDS; the other buffer's readers (block t-1) are done
-            if (tr && tid == 0) tr[8 + t] = wall_clock64();  // FBA_PANEL_TRACE: block t in LDS
-            const int pub = sy[31];
-            const bool pre = issued > t + 1 || (t + 1 < CB / IB && pub > t + 1);
-            // blocks t+1 (slot of t+1) and t+2 (the slot block t just left) in flight during this update
-            if (issued == t + 1 && t + 1 < CB / IB && pub > t + 1) {
-                issue(t + 1, (t + 1) & 1);
-                issued = t + 2;
-            }
-            if (issued == t + 2 && t + 2 < CB / IB && pub > t + 2) {
-                issue(t + 2, t & 1);
-                issued = t + 3;
-            }
-            // C(a, b) -= X_t(a) X_t(b)', tiles p = wave + 8 i of the 36 lower tiles
-            double xa[NT][4], yb[NT][4];
-#pragma unroll
-            for (int i = 0; i < NT; ++i)
-                if (wave + POTRF_NW * i < POTRF_NT) {
-#pragma unroll
-                    for (int kk = 0; kk < 4; ++kk) {
-                        xa[i][kk] = -X[(IB * ta[i] + lr) * 17 + 4 * kk + lk];
-                        yb[i][kk] = X[(IB * tb[i] + lr) * 17 + 4 * kk + lk];
-                    }
-                }
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-                for (int i = 0; i < NT; ++i)
-                    if (wave + POTRF_NW * i < POTRF_NT) c[i] = mfma(xa[i][kk], yb[i][kk], c[i]);
-            if (t == CB / IB - 1)
-#pragma unroll
-                for (int i = 0; i < NT; ++i)
-                    if (wave + POTRF_NW * i < POTRF_NT) {
-                        const int p = wave + POTRF_NW * i;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) smem[p * IB * 17 + (lk + 4 * r) * 17 + lr] = c[i][r];
-                    }
-            if (tr && tid == 0) tr[16 + t] = wall_clock64() | (pre ? (1ull << 63) : 0);  // block t applied
-        }
+        if (rec[9] >= 0)  // split: the tiles of tile columns >= FLOW_CSPLIT come from the helper record
+            fused_apply<1>(rX, ld, p0, p1, rec[11], Xb[0], Xb[1], sy, smem, nullptr, scal, tr);
+        else
+            fused_apply<0>(rX, ld, p0, p1, rec[11], Xb[0], Xb[1], sy, smem, nullptr, scal, tr);
     }
     if (tr && threadIdx.x == 0) tr[4] = wall_clock64();
     // late partials: the other sources of f's level, 64x64 row-major scratch quarters, slot order
@@ -1938,8 +2052,29 @@ __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, co
     }
     __syncthreads();  // the block final in LDS; the counters and buffers free
     if (tr && threadIdx.x == 0) tr[5] = wall_clock64();
-    potrf_body<false, true>(S, ld, j, dinv, scal, nullptr, colflags + j, smem, tr ? tr + 16 : nullptr);
+    potrf_body<false, true>(S, ld, j, dinv, scal, nullptr, colflags + j, smem, tr ? tr + 16 : nullptr,
+                            rec[9] >= 0 ? P + (int64_t)rec[10] * 4096 : nullptr, rec[9] >= 0 ? fl + rec[9] : nullptr);
 #undef AT
+}
+
+// split_helper_body (role 4): the tiles of tile columns >= FLOW_CSPLIT of diagonal block j's fused update
+// (rec: j, f, -, -, -, -, -, progress flags of the two panel halves of (f, j), flag, scratch slot), from
+// the same published rows as the diagonal workgroup, to a scratch partial; then every wave's stores
+// drained, a barrier, and one flag (MI355X guide hand-off table row 1)
+__device__ __forceinline__ void split_helper_body(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ rec,
+                                                  unsigned* __restrict__ fl, double* __restrict__ P,
+                                                  double* __restrict__ scal, double* __restrict__ smem,
+                                                  uint64_t* __restrict__ tr) {
+    const int64_t k0 = (int64_t)rec[1] * CB, f0 = (int64_t)rec[2] * CB;
+    const __amdgpu_buffer_rsrc_t rX = block_rsrc(S + k0 * ld + f0, ((int64_t)(CB - 1) * ld + CB) * 8);
+    double* Dall = smem + POTRF_NT * IB * 17;
+    int* sy = reinterpret_cast<int*>(Dall + (CB / IB) * IB * 17);
+    fused_apply<2>(rX, ld, fl + rec[7], fl + rec[8], 0, Dall, reinterpret_cast<double*>(sy + 32), sy, smem,
+                   P + (int64_t)rec[10] * 4096, scal, tr);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(fl + rec[9], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tr && threadIdx.x == 0) tr[2] = wall_clock64();
 }
 
 // syrk_flow_body (role 2): one update task, C(a, b) quarter q += -sum_k X_ak X_bk' over its sources
@@ -2123,6 +2258,8 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_chol_flow(double* __restrict_
                        (gblk && rec[7] >= 0) ? gblk + (int64_t)rec[7] * 256 : nullptr);
     } else if (role == 2) {
         syrk_flow_body(S, ld, rec, lists, P, fl, cnt, scal, smem, tr);
+    } else if (role == 4) {
+        split_helper_body(S, ld, rec, fl, P, scal, smem, tr);
     } else {
         if (threadIdx.x == 0) spin_ge(colflags + rec[1], (unsigned)(CB / IB), scal);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");

@@ -18,7 +18,10 @@ namespace fba {
 
 constexpr int NB = 128;       // Cholesky block size (rows/cols of one panel block, fba_chol.hip)
 constexpr int PTRACE_WG = 2048;  // FBA_PANEL_TRACE: workgroup slots per level
-constexpr int FTRACE = 40;       // FBA_PANEL_TRACE: stamps per k_chol_flow record
+constexpr int FTRACE = 48;       // FBA_PANEL_TRACE: stamps per k_chol_flow record
+// k_chol_flow: a fused diagonal update's tiles of tile columns >= FLOW_CSPLIT go to a helper record,
+// added into the potrf's LDS block during its bulk step FLOW_CSPLIT - 2 (fba_order.cpp build_flow)
+constexpr int FLOW_CSPLIT = 3;
 constexpr int CHUNK_OBS = 256;  // observations per k_lin_reduce / k_lin_point workgroup (chunk)
 // tie points per chunk and co-visibility terms per chunk staged in LDS (a single larger point's are
 // read from HBM instead): smaller for nK >= 6, whose wider Jacobian rows leave less of the 160 KiB LDS
@@ -91,7 +94,7 @@ struct Sched {
     static constexpr int FLOW_REC = 16;
     int64_t flow_rec = 0;
     int flow_n = 0, flow_nprog = 0, flow_nuflag = 0, flow_ncounter = 0, flow_nscratch = 0;
-    int flow_cnt[4] = {0, 0, 0, 0};  // records per role
+    int flow_cnt[5] = {0, 0, 0, 0, 0};  // records per role
     bool flow_ok = false;
     double flow_flops = 0.0;
 };

@@ -465,17 +465,32 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     // K = 0 (default, the workgroup applies all eight) 1129, 2: 1078, 4: 1076, 5: 1096, 6: 1091 -- the
     // helpers' extra hand-off costs more than the diagonal workgroup's arithmetic they take over
     static const int ksplit = getenv("FBA_FLOW_KSPLIT") ? std::max(0, std::min(8, atoi(getenv("FBA_FLOW_KSPLIT")))) : 0;
+    // FBA_FLOW_CSPLIT=0 disables the tile-column split of the fused updates (helper records, role 4): the
+    // diagonal workgroup applies the tiles of tile columns < FLOW_CSPLIT, a helper workgroup the others
+    // (consuming the same published rows) into a scratch partial that the potrf's bulk waves add at
+    // their step FLOW_CSPLIT - 2, well after the potrf has started -- so the update's arithmetic no
+    // longer trails the panel solves (the diagonal workgroup alone is MFMA-bound at ~1.5 us per
+    // column block, behind panel halves that publish one every ~1-2 us)
+    static const bool csplit = !(getenv("FBA_FLOW_CSPLIT") && atoi(getenv("FBA_FLOW_CSPLIT")) == 0);
+    int nslot = 0, ncnt = 0;
     // diagonal blocks
     for (int64_t j = 0; j < nb; ++j) {
         const int32_t f = fsrc[j];
         int need = level[j] - 1;
-        col_task[j] = add({0, (int32_t)j, f, 0, 0, 0, 0, f >= 0 ? prog[std::make_tuple(f, (int32_t)j, 0)] : -1,
-                           (f >= 0 && halves(j) > 1) ? prog[std::make_tuple(f, (int32_t)j, 1)] : -1, -1, -1,
-                           f >= 0 ? ksplit : 0},
-                          {need, 0, (int)j});
+        const int32_t p0 = f >= 0 ? prog[std::make_tuple(f, (int32_t)j, 0)] : -1;
+        const int32_t p1 = (f >= 0 && halves(j) > 1) ? prog[std::make_tuple(f, (int32_t)j, 1)] : -1;
+        const bool split = csplit && f >= 0 && p1 >= 0 && ksplit == 0;
+        const int32_t hflag = split ? new_uflag() : -1, hslot = split ? nslot++ : -1;
+        col_task[j] = add({0, (int32_t)j, f, 0, 0, 0, 0, p0, p1, hflag, hslot, f >= 0 ? ksplit : 0}, {need, 0, (int)j});
         if (f >= 0) {
-            flag_deps[col_task[j]].push_back(prog[std::make_tuple(f, (int32_t)j, 0)]);
-            if (halves(j) > 1) flag_deps[col_task[j]].push_back(prog[std::make_tuple(f, (int32_t)j, 1)]);
+            flag_deps[col_task[j]].push_back(p0);
+            if (p1 >= 0) flag_deps[col_task[j]].push_back(p1);
+        }
+        if (split) {
+            const int hid = add({4, (int32_t)j, f, 0, 0, 0, 0, p0, p1, hflag, hslot}, {need, 0, (int)j});
+            flag_deps[hid] = {p0, p1};
+            uflag_tasks[hflag - np].push_back(hid);
+            flag_deps[col_task[j]].push_back(hflag);
         }
         s.flow_flops += (double)NB * NB * NB / 3.0 + (f >= 0 ? (double)NB * NB * NB * (8 - ksplit) / 8.0 : 0.0);
     }
@@ -505,7 +520,6 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
         }
     std::map<std::tuple<int32_t, int32_t, int32_t>, int32_t> writer;  // final in-place writer flag per quarter
     std::vector<std::vector<std::array<int32_t, 3>>> late(nb);          // (quarter, slot, flag) per diagonal block
-    int nslot = 0, ncnt = 0;
     for (auto& t : tg) {
         const int32_t a = t.first.first, b = t.first.second;
         std::map<int, std::vector<int32_t>> bylev;
@@ -669,16 +683,17 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     s.flow_nscratch = nslot;
     s.flow_rec = (int64_t)buf.size();
     s.flow_n = ok ? n : 0;
-    for (int r = 0; r < 4; ++r) s.flow_cnt[r] = 0;
+    for (int r = 0; r < 5; ++r) s.flow_cnt[r] = 0;
     if (ok)
         for (int i : ord) {
             buf.insert(buf.end(), T[i].rec.begin(), T[i].rec.end());
             s.flow_cnt[T[i].rec[0]]++;
         }
     if (verbose)
-        fprintf(stderr, "[fba] flow schedule: %d records (%d diagonal, %d panel halves, %d updates, %d inverses), "
-                "%d progress + %d update flags, %d scratch quarters%s\n", n, s.flow_cnt[0], s.flow_cnt[1],
-                s.flow_cnt[2], s.flow_cnt[3], np, s.flow_nuflag, nslot, ok ? "" : " -- ORDER CHECK FAILED, not used");
+        fprintf(stderr, "[fba] flow schedule: %d records (%d diagonal, %d panel halves, %d updates, %d inverses, "
+                "%d split helpers), %d progress + %d update flags, %d scratch quarters%s\n", n, s.flow_cnt[0],
+                s.flow_cnt[1], s.flow_cnt[2], s.flow_cnt[3], s.flow_cnt[4], np, s.flow_nuflag, nslot,
+                ok ? "" : " -- ORDER CHECK FAILED, not used");
 }
 
 void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pairs) {

@@ -367,8 +367,11 @@ int main(int argc, char** argv) {
                 if (colf[f] != 8 || f >= j) return fail("flow: fused source not factored");
                 if (!flag_ok(rec[7], 8) || (rec[8] >= 0 && !flag_ok(rec[8], 8))) return fail("flow: fused rows not solved");
                 const double* X = Fk(j, f);
-                for (int a = 0; a < NB; ++a)  // the column blocks [rec[11], 8); the helpers' partials the rest
-                    for (int c2 = 0; c2 <= a; ++c2) {
+                // the column blocks [rec[11], 8) (the helpers' partials the rest); with a split helper
+                // (rec[9] >= 0) only the tile columns < FLOW_CSPLIT
+                const int cmax = rec[9] >= 0 ? 16 * FLOW_CSPLIT : NB;
+                for (int a = 0; a < NB; ++a)
+                    for (int c2 = 0; c2 <= a && c2 < cmax; ++c2) {
                         double v = 0.0;
                         for (int t = 16 * rec[11]; t < NB; ++t) v += X[(size_t)a * n + t] * X[(size_t)c2 * n + t];
                         C[(size_t)a * n + c2] -= v;
@@ -381,6 +384,17 @@ int main(int argc, char** argv) {
                 for (int a = 0; a < 64; ++a)
                     for (int c2 = 0; c2 < 64; ++c2)
                         if (64 * qr + a >= 64 * qc + c2) C[(size_t)(64 * qr + a) * n + 64 * qc + c2] += Pf[(size_t)l3[1] * 4096 + a * 64 + c2];
+            }
+            if (rec[9] >= 0) {  // the split helper's partial (the potrf's bulk waves add it)
+                if (!flag_ok(rec[9], 1) || rec[10] < 0 || rec[10] >= s.flow_nscratch || !slot_set[rec[10]])
+                    return fail("flow: split helper partial not ready");
+                int h = 0;
+                for (int ta = 0; ta < NB / 16; ++ta)
+                    for (int tb = FLOW_CSPLIT; tb <= ta; ++tb, ++h)
+                        for (int r = 0; r < 16; ++r)
+                            for (int c2 = 0; c2 < 16; ++c2)
+                                if (16 * ta + r >= 16 * tb + c2)
+                                    C[(size_t)(16 * ta + r) * n + 16 * tb + c2] += Pf[(size_t)rec[10] * 4096 + h * 256 + r * 16 + c2];
             }
             for (int jj = 0; jj < NB; ++jj) {  // potrf
                 double d = C[(size_t)jj * n + jj];
@@ -443,6 +457,22 @@ int main(int argc, char** argv) {
             }
         } else if (rec[0] == 3) {
             if (colf[rec[1]] != 8) return fail("flow: inverse before its factor");
+        } else if (rec[0] == 4) {  // split helper: tiles (ta, tb), tb >= FLOW_CSPLIT, of C_jj -= X X', X = L(j, f)
+            const int64_t j = rec[1], f = rec[2];
+            if (colf[f] != 8 || f >= j) return fail("flow: split helper before its source");
+            if (!flag_ok(rec[7], 8) || !flag_ok(rec[8], 8)) return fail("flow: split helper rows not solved");
+            if (rec[10] < 0 || rec[10] >= s.flow_nscratch || slot_set[rec[10]]++) return fail("flow: split helper slot");
+            const double* X = Fk(j, f);
+            int h = 0;
+            for (int ta = 0; ta < NB / 16; ++ta)
+                for (int tb = FLOW_CSPLIT; tb <= ta; ++tb, ++h)
+                    for (int r = 0; r < 16; ++r)
+                        for (int c2 = 0; c2 < 16; ++c2) {
+                            double v = 0.0;
+                            for (int t = 0; t < NB; ++t) v += X[(size_t)(16 * ta + r) * n + t] * X[(size_t)(16 * tb + c2) * n + t];
+                            Pf[(size_t)rec[10] * 4096 + h * 256 + r * 16 + c2] = -v;
+                        }
+            fl[rec[9]] = 1;
         } else {
             return fail("flow: record role");
         }
