@@ -726,6 +726,13 @@ static void print_flow_trace(Ctx* c) {
     int rn[5] = {0, 0, 0, 0, 0};
     const int32_t* recs = s.buf.data() + s.flow_rec;
     const bool detail = getenv("FBA_PANEL_TRACE")[0] == '2';
+    if (getenv("FBA_PANEL_TRACE")[0] == '3')  // every record in dispatch order: role, ids, start, waits done, end
+        for (int b = 0; b < s.flow_n; ++b) {
+            const uint64_t* r = &t[FTRACE * (size_t)b];
+            const int32_t* rec = recs + (size_t)Sched::FLOW_REC * b;
+            fprintf(stderr, "[fba] rec %d %d %d %d %d %.2f %.2f %.2f\n", b, rec[0], rec[1], rec[2], rec[3], us(r[0]),
+                    us(r[1]), us(r[2]));
+        }
     for (int b = 0; b < s.flow_n; ++b) {
         const uint64_t* r = &t[FTRACE * (size_t)b];
         const int32_t* rec = recs + (size_t)Sched::FLOW_REC * b;

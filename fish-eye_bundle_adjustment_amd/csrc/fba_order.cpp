@@ -472,6 +472,10 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     // longer trails the panel solves (the diagonal workgroup alone is MFMA-bound at ~1.5 us per
     // column block, behind panel halves that publish one every ~1-2 us)
     static const bool csplit = !(getenv("FBA_FLOW_CSPLIT") && atoi(getenv("FBA_FLOW_CSPLIT")) == 0);
+    // FBA_FLOW_LOOKAHEAD = D: an update task is dispatched among the records of level
+    // max(source level, level of need - D) (a large D: at its source level)
+    static const int promote_mode = getenv("FBA_FLOW_PROMOTE") ? atoi(getenv("FBA_FLOW_PROMOTE")) : 0;
+    static const int lookahead = getenv("FBA_FLOW_LOOKAHEAD") ? atoi(getenv("FBA_FLOW_LOOKAHEAD")) : 1000;
     int nslot = 0, ncnt = 0;
     // diagonal blocks
     for (int64_t j = 0; j < nb; ++j) {
@@ -500,8 +504,11 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
             for (int h = 0; h < halves(r); ++h) {
                 const int32_t p = prog[std::make_tuple((int32_t)k, r, h)];
                 // rec[7]: the RHS block row's half 0 accumulates its rows' Gram into partial k
+                // FBA_FLOW_PROMOTE: 1 = the panel halves feeding a fused diagonal update (the critical
+                // chain) are dispatched among the previous level's records, 2 = every panel half
+                const bool promote = promote_mode == 2 || (promote_mode == 1 && r < nb && fsrc[r] == (int32_t)k);
                 const int id = add({1, (int32_t)k, 2 * r + h, 0, 0, p, 0, (r == nb && h == 0) ? (int32_t)k : -1},
-                                   {level[k], 1, (int)(k * (nb + 1) + r) * 2 + h});
+                                   {level[k] - (promote ? 1 : 0), 1, (int)(k * (nb + 1) + r) * 2 + h});
                 T[id].deps.push_back(col_task[k]);
                 prog_task[p] = id;
                 s.flow_flops += 64.0 * NB * NB;
@@ -565,9 +572,14 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
                         mode = 0;
                         flag = wflag;
                     }
+                    // dispatch level: the source level, deferred to `lookahead` levels before the
+                    // target is read (its diagonal workgroup at level[b] - 1, its panel halves at
+                    // level[b]), so updates of far-away targets do not hold CUs ahead of the next
+                    // levels' panel halves
+                    const int need = a == b ? level[b] - 1 : level[b];
                     const int id = add({2, a, b, q, soff, g1 - g0, slot, mode, flag, is_late ? -1 : prev, cidx, first, ng, 0,
                                         CB_BLOCKS},
-                                       {w, is_late ? 2 : rank, (int)(b * (nb + 1) + a) * 4 + q});
+                                       {std::max(w, need - lookahead), is_late ? 2 : rank, (int)(b * (nb + 1) + a) * 4 + q});
                     flag_deps[id] = fd;
                     if (!is_late && prev >= 0) flag_deps[id].push_back(prev);
                     uflag_tasks[flag - np].push_back(id);
