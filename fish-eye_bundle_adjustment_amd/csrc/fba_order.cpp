@@ -472,8 +472,12 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     // longer trails the panel solves (the diagonal workgroup alone is MFMA-bound at ~1.5 us per
     // column block, behind panel halves that publish one every ~1-2 us)
     static const bool csplit = !(getenv("FBA_FLOW_CSPLIT") && atoi(getenv("FBA_FLOW_CSPLIT")) == 0);
-    // FBA_FLOW_LOOKAHEAD = D: an update task is dispatched among the records of level
-    // max(source level, level of need - D) (a large D: at its source level)
+    // FBA_FLOW_PROMOTE (panel halves) and FBA_FLOW_LOOKAHEAD = D (an update task dispatched among the
+    // records of level max(source level, level of need - D); default: at its source level) reorder the
+    // dispatch; measured at config 4 (iter/s): default 1125-1130, PROMOTE=1 1126, PROMOTE=2 1102, D = 0 /
+    // 1 / 2 / 3 / 5: 724 / 760 / 828 / 916 / 1035 -- an update deferred towards its need lands on the
+    // critical path.  (FBA_PANEL_TRACE=3: the mid levels' panel halves start late because the CUs are
+    // held by update tasks that wait for progressively published source columns, ~20 us each.)
     static const int promote_mode = getenv("FBA_FLOW_PROMOTE") ? atoi(getenv("FBA_FLOW_PROMOTE")) : 0;
     static const int lookahead = getenv("FBA_FLOW_LOOKAHEAD") ? atoi(getenv("FBA_FLOW_LOOKAHEAD")) : 1000;
     int nslot = 0, ncnt = 0;
