@@ -2500,7 +2500,7 @@ int launch_cholesky(Ctx& c) {
     const int64_t ld = c.L.ld;
     const Sched& s = c.sched;
     if (c.chol_flow && s.flow_ok && s.flow_n > 0) {
-        // the whole factorisation + forward solve in one persistent launch (flags zeroed by k_finish_rhs)
+        // the whole factorisation + forward solve in one persistent launch (flags zeroed by k_border_rhs)
         const bool pp = c.probe == 2 && c.probe_n < (int)c.probe_ev.size() / 2;
         if (pp) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
         k_chol_flow<<<(unsigned)s.flow_n, POTRF_THREADS, FLOW_LDS, c.stream>>>(
@@ -2515,7 +2515,7 @@ int launch_cholesky(Ctx& c) {
         return FBA_OK;
     }
     // the k_panel / k_bwd_flow hand-off flags, the split-target counters and the update flags were
-    // zeroed by k_finish_rhs
+    // zeroed by k_border_rhs
     int pend = -1;  // a level whose trailing updates run inside the next level's k_panel
     auto updates = [&](int v) -> int {  // a level's trailing updates as their own launch
         const Sched::Wave& V = s.w[v];

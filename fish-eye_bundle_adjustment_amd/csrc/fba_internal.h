@@ -201,7 +201,7 @@ struct Ctx {
     unsigned* d_counters = nullptr; // [Sched::n_counters] split-target arrival counters
     unsigned* d_tflags = nullptr;   // [Sched::n_tflags] update-target completion flags (merged k_panel)
     int64_t n_sync = 0;           // unsigned words of flags + bflags + counters (one allocation at d_flags,
-                                  // zeroed by k_finish_rhs ahead of every factorisation)
+                                  // zeroed by k_border_rhs ahead of every factorisation)
     bool bwd_flow = true;
     int merge_max = 1 << 30;        // ... for levels of at most this many update tasks (FBA_MERGE_MAX)
     bool merge_updates = true;      // a level's trailing updates inside the next level's k_panel

@@ -12,7 +12,7 @@
 //   k_red_*         the partials of each reduced block added in chunk order: image-pair blocks,
 //                   image diagonal blocks + RHS + image-camera blocks, camera blocks
 //   k_lin_point     the same linearisation writing the Jacobian rows out (residuals, dense AwG)
-//   k_border        inner-constraint bordering M = S + G W G' (reference: NG = [N G; G' 0],
+//   k_border_rhs    inner-constraint bordering M = S + G W G' (reference: NG = [N G; G' 0],
 //                   main.m:428-432), unit diagonal for fixed parameters, RHS rows
 //   k_backsub       tie-point corrections from the camera-side solution
 //   k_update        de-scaling of distortion corrections (main.m:460-482), xhat += delta
@@ -70,14 +70,15 @@ __device__ __forceinline__ void params_body(int t, int nthreads, const double* _
         Mk[6] = 0.0;      Mk[7] = 0.0;                      Mk[8] = 0.0;
         if (ic) {  // BuildAwG.m:516-523, rows Xc Yc Zc w p k, 7 columns
             double* g = G + (int64_t)t * 42;
-            double tp = tan(p), secp = 1.0 / cos(p);
+            // tan(phi), sec(phi) from the sincos above (equal to tan() / 1 / cos() to rounding)
+            const double secp = 1.0 / cp, tp = sp * secp;
             const double rows[42] = {
                 1, 0, 0, 0, -Zc, Yc, Xc,
                 0, 1, 0, Zc, 0, -Xc, Yc,
                 0, 0, 1, -Yc, Xc, 0, Zc,
-                0, 0, 0, -1, -sin(w) * tp, cos(w) * tp, 0,
-                0, 0, 0, 0, -cos(w), -sin(w), 0,
-                0, 0, 0, 0, sin(w) * secp, -cos(w) * secp, 0};
+                0, 0, 0, -1, -sw * tp, cw_ * tp, 0,
+                0, 0, 0, 0, -cw_, -sw, 0,
+                0, 0, 0, 0, sw * secp, -cw_ * secp, 0};
             const bool slot = active[6 * (int64_t)t];  // padding slots (fba_order.cpp) carry no constraint
 #pragma unroll
             for (int i = 0; i < 42; ++i) g[i] = slot ? rows[i] : 0.0;
@@ -981,7 +982,7 @@ __global__ __launch_bounds__(128) void k_red_cam(const double* __restrict__ cseg
 // in k_border_combine.  scal: [1] Cholesky failure flag, [2] sumabs, [8..14] W_l, [16..22] D^2.
 // ------------------------------------------------------------------------------------------------
 // k_border_weights: BW_SEG workgroups, each the 14 weight sums over a contiguous range of the 6 n_img
-// EOP rows -> part[seg][14]; the consumers (k_border, k_finish_rhs) add the segments in order
+// EOP rows -> part[seg][14]; the consumer (k_border_rhs) adds the segments in order
 constexpr int BW_SEG = 32;
 
 __global__ __launch_bounds__(256) void k_border_weights(const double* __restrict__ S, const double* __restrict__ G,
@@ -1035,34 +1036,39 @@ __device__ __forceinline__ void border_weights_lds(const double* __restrict__ pa
     __syncthreads();
 }
 
-// M += G_l W_l G_l' on the 6 n_loc x 6 n_loc block (lower part)
-__global__ __launch_bounds__(256) void k_border(double* __restrict__ S, const double* __restrict__ G,
-                                                const double* __restrict__ part, int64_t ld, int n_loc) {
-    __shared__ double w[14];
-    border_weights_lds(part, w);
-    const int64_t n = 6 * (int64_t)n_loc;
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n * n; q += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = q / n, j = q % n;
-        if (j > i) continue;
-        const double* gi = G + (i / 6) * 42 + (i % 6) * 7;
-        const double* gj = G + (j / 6) * 42 + (j % 6) * 7;
-        double acc = 0.0;
-        for (int m = 0; m < 7; ++m) acc += gi[m] * w[m] * gj[m];
-        S[i * ld + j] += acc;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_finish_rhs(double* __restrict__ S, const double* __restrict__ G,
+// One launch, two roles by workgroup (both need the 14 weights first):
+//   workgroups [0, nbr): row i = blockIdx of the local border, M(i, j) += G_i W_l G_j' for j <= i (lower
+//                        part); padding slots have zero G rows and are left alone (their unit diagonal
+//                        is written by the other role, so the two never touch the same entry)
+//   workgroups [nbr, ..): one thread per row i of S: unit row for fixed parameters and padding, the
+//                        border's RHS rows A = G_l W_l^1/2 and B = G D; the hand-off flags and counters
+//                        of the factorisation / backward solve zeroed
+__global__ __launch_bounds__(256) void k_border_rhs(double* __restrict__ S, const double* __restrict__ G,
                                                     double* __restrict__ scal, const double* __restrict__ part,
                                                     const uint8_t* __restrict__ active, int64_t ld, int64_t n_pad,
-                                                    int64_t u_c, int n_img, int n_loc, int ic,
+                                                    int64_t u_c, int n_img, int n_loc, int ic, int nbr,
                                                     unsigned* __restrict__ sync, int64_t n_sync) {
     __shared__ double w[14];
     if (ic) border_weights_lds(part, w);
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    // the hand-off flags and split-target counters of the factorisation / backward solve that follow
-    for (int64_t q = i; q < n_sync; q += (int64_t)gridDim.x * blockDim.x) sync[q] = 0u;
-    if (ic && blockIdx.x == 0 && threadIdx.x < 14) scal[8 + (threadIdx.x / 7) * 8 + threadIdx.x % 7] = w[threadIdx.x];
+    if ((int)blockIdx.x < nbr) {
+        const int64_t i = blockIdx.x;
+        const double* gi = G + (i / 6) * 42 + (i % 6) * 7;
+        double gw[7];
+#pragma unroll
+        for (int m = 0; m < 7; ++m) gw[m] = gi[m] * w[m];
+        for (int64_t j = threadIdx.x; j <= i; j += 256) {
+            const double* gj = G + (j / 6) * 42 + (j % 6) * 7;
+            double acc = 0.0;
+#pragma unroll
+            for (int m = 0; m < 7; ++m) acc += gw[m] * gj[m];
+            if (acc != 0.0) S[i * ld + j] += acc;
+        }
+        return;
+    }
+    const int64_t nthr = ((int64_t)gridDim.x - nbr) * blockDim.x;
+    const int64_t i = ((int64_t)blockIdx.x - nbr) * blockDim.x + threadIdx.x;
+    for (int64_t q = i; q < n_sync; q += nthr) sync[q] = 0u;
+    if (ic && blockIdx.x == nbr && threadIdx.x < 14) scal[8 + (threadIdx.x / 7) * 8 + threadIdx.x % 7] = w[threadIdx.x];
     if (i >= n_pad) return;
     if (i >= u_c || !active[i]) {
         // fixed parameter or padding: decoupled unit row, zero RHS
@@ -1404,14 +1410,10 @@ int launch_border(Ctx& c) {
     const int ic = c.set.inner_constraints;
     k_border_weights<<<BW_SEG, 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, c.d_bscr, L.ld, L.n_img, c.n_loc, ic);
     FBA_HIP(hipGetLastError());
-    if (ic && c.n_loc > 0) {
-        const int64_t n = 6 * (int64_t)c.n_loc;
-        k_border<<<(unsigned)((n * n + 255) / 256), 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_bscr, L.ld, c.n_loc);
-        FBA_HIP(hipGetLastError());
-    }
-    k_finish_rhs<<<(unsigned)((L.n_pad + 255) / 256), 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, c.d_bscr, c.d_active,
-                                                                           L.ld, L.n_pad, L.u_c, L.n_img, c.n_loc, ic,
-                                                                           c.d_flags, c.n_sync);
+    const int nbr = (ic && c.n_loc > 0) ? 6 * c.n_loc : 0;
+    k_border_rhs<<<(unsigned)(nbr + (L.n_pad + 255) / 256), 256, 0, c.stream>>>(
+        c.d_S, c.d_G, c.d_scal, c.d_bscr, c.d_active, L.ld, L.n_pad, L.u_c, L.n_img, c.n_loc, ic, nbr, c.d_flags,
+        c.n_sync);
     FBA_HIP(hipGetLastError());
     return FBA_OK;
 }

@@ -421,7 +421,12 @@ std::vector<int32_t> camera_order(const fba_problem* p) {
 static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<std::vector<int32_t>>& R,
                        const std::vector<int32_t>& level, int64_t nb, const std::function<int64_t(int64_t)>& real_rows,
                        bool verbose) {
-    constexpr int SPLIT = 2, REC = Sched::FLOW_REC, CB_BLOCKS = NB / 16, IB_BLOCK = 16;
+    constexpr int REC = Sched::FLOW_REC, CB_BLOCKS = NB / 16, IB_BLOCK = 16;
+    // sources per update task (FBA_FLOW_SPLIT; a target quarter's sources of one level are split into
+    // groups of at most SPLIT, summed through scratch partials when there are several groups); config 4
+    // (iter/s, two runs each): 1: 1050, 2: 1120 / 1137, 3: 1153 / 1143, 4: 1152 / 1147, all in one: 1087
+    // -- fewer update records hold fewer CUs while waiting for their sources' columns
+    static const int SPLIT = getenv("FBA_FLOW_SPLIT") ? std::max(1, atoi(getenv("FBA_FLOW_SPLIT"))) : 4;
     const int nw = nb > 0 ? 1 + *std::max_element(level.begin(), level.end()) : 0;
     std::vector<std::vector<int32_t>> srcs(nb);
     for (int64_t k = 0; k < nb; ++k)
