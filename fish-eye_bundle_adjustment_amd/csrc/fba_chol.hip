@@ -1393,15 +1393,14 @@ __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, 
         const int b = a + rem;
         double v = 0.0;
         if (gblk) {
-            int q = 0;
-            for (; q + 8 <= nblk; q += 8) {  // 8 loads in flight, the same running sum
-                double x[8];
+            for (int q = 0; q < nblk; q += 32) {  // 32 loads in flight, the same running sum
+                double x[32];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) x[u] = gblk[(int64_t)(q + u) * 256 + a * 16 + b];
+                for (int u = 0; u < 32; ++u) x[u] = q + u < nblk ? gblk[(int64_t)(q + u) * 256 + a * 16 + b] : 0.0;
 #pragma unroll
-                for (int u = 0; u < 8; ++u) v += x[u];
+                for (int u = 0; u < 32; ++u)
+                    if (q + u < nblk) v += x[u];
             }
-            for (; q < nblk; ++q) v += gblk[(int64_t)q * 256 + a * 16 + b];
         } else {
             double x[GRAM_SEG];
 #pragma unroll

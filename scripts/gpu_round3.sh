@@ -1,0 +1,11 @@
+#!/bin/bash
+# GPU-box round check: parity tests, smoke, bench with the CPU baseline, kernel trace, PMC traffic
+# passes, configs 3 and 5
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+bash scripts/gpu_check.sh tests smoke bench prof pmc || exit $?
+for cfg in 3 5; do
+  timeout -k 10 400 python bench.py --config $cfg --steps 10 --warmup 2 --no-cpu > gpurun_out/bench_c$cfg.log 2>&1
+  rc=$?; echo "== config $cfg rc=$rc"; tail -1 gpurun_out/bench_c$cfg.log | cut -c1-300
+  [ $rc -ne 0 ] && exit $rc
+done
+exit 0
