@@ -1381,11 +1381,9 @@ __global__ __launch_bounds__(256) void k_border_gram(const double* __restrict__ 
 // u = y + A z + B k on its 256 entries of the RHS row (derivation in fba_kernels.hip, border section)
 // gblk != nullptr: the Gram comes as nblk per-column-block 16x16 partials (k_chol_flow's RHS panel
 // halves, row-major, rows/columns 15 zero), added in block order instead of the GRAM_SEG segments
-__global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, int64_t ld, int64_t n_pad,
-                                                        const double* __restrict__ gpart, double* __restrict__ coef_out,
-                                                        const double* __restrict__ gblk = nullptr, int nblk = 0) {
-    __shared__ double g[15][15];
-    __shared__ double coef[14];
+// the 14 coefficients into coef[] (LDS, 256 threads; g: 15 x 15 LDS scratch); ends with a barrier
+__device__ __forceinline__ void border_combine_body(const double* __restrict__ gpart, const double* __restrict__ gblk,
+                                                    int nblk, double (*g)[15], double* coef) {
     const int tid = threadIdx.x;
     if (tid < 120) {
         int a = 0, rem = tid;
@@ -1471,6 +1469,15 @@ __global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, 
         }
     }
     __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_border_combine(double* __restrict__ S, int64_t ld, int64_t n_pad,
+                                                        const double* __restrict__ gpart, double* __restrict__ coef_out,
+                                                        const double* __restrict__ gblk = nullptr, int nblk = 0) {
+    __shared__ double g[15][15];
+    __shared__ double coef[14];
+    const int tid = threadIdx.x;
+    border_combine_body(gpart, gblk, nblk, g, coef);
     if (coef_out) {  // one workgroup: the 14 coefficients only (k_bwd_flow applies them)
         if (tid < 14) coef_out[tid] = coef[tid];
         return;
@@ -2349,7 +2356,10 @@ __global__ __launch_bounds__(256) void k_bwd_wave(double* __restrict__ S, int64_
 // with an agent-scope flag, and delta_c = -x_j stored (k_neg_copy fused).  Waits only point to higher
 // blocks and every workgroup is resident (nb <= CUs, checked by the host), so they end; polls are
 // bounded (scal[1] = -1 on timeout, reported by the host).
-constexpr size_t BWD_LDS = sizeof(double) * (CB * CB + (CB / IB) * IB * IB + 2 * CB + 512);
+// With inner constraints and `combine`, one more workgroup (blockIdx nb) solves the border's 14x14
+// system (border_combine_body) meanwhile, publishes the coefficients write-through and raises flags[nb];
+// the block workgroups wait for it only where they form u_j (after staging and their sources).
+constexpr size_t BWD_LDS = sizeof(double) * (CB * CB + (CB / IB) * IB * IB + 2 * CB + 512 + 16);
 
 __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, int64_t ld, int64_t n_pad,
                                                   const double* __restrict__ linv, const double* __restrict__ dinv,
@@ -2357,15 +2367,28 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
                                                   double* __restrict__ delta, int64_t u_c,
                                                   const int32_t* __restrict__ src_start, const int32_t* __restrict__ src,
                                                   unsigned* __restrict__ flags, double* __restrict__ scal,
-                                                  const double* __restrict__ coef) {
+                                                  double* __restrict__ coef, int combine,
+                                                  const double* __restrict__ gpart, const double* __restrict__ gblk, int nblk) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* Li = smem;              // [128][128] Linv_j, or L_jj for a root column
     double* Dt = Li + CB * CB;      // [8][16][16] the leaf inverses of a root column
     double* xs = Dt + (CB / IB) * IB * IB;  // [128] x_i of the current source
     double* ys = xs + CB;           // [128]
     double* red = ys + CB;          // [512]
+    double* cs = red + 512;         // [16] the border coefficients
     const int tid = threadIdx.x;
     const int nb = (int)(n_pad / CB);
+    if (combine && (int)blockIdx.x == nb) {  // the border combine workgroup
+        border_combine_body(gpart, gblk, nblk, reinterpret_cast<double (*)[15]>(Li), cs);
+        if (tid < 14) {
+            const __amdgpu_buffer_rsrc_t rc = block_rsrc(coef, 16 * 8);
+            st_sc1(rc, (int64_t)tid * 8, cs[tid]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(flags + nb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     const int j = nb - 1 - (int)blockIdx.x;
     const int c2 = tid & 63, h = tid >> 6;  // gemv_t128's thread map: columns 2 c2 + {0,1}, rows 32 h ..
     // a root of the elimination tree (no source blocks: the top level) is solved by substitution with
@@ -2414,14 +2437,29 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
     }
     red[h * 128 + 2 * c2] = a0;
     red[h * 128 + 2 * c2 + 1] = a1;
+    if (coef) {  // the border coefficients: from the combine workgroup (its flag), or a previous launch
+        if (combine && tid == 0) {
+            unsigned spins = 0;
+            while (__hip_atomic_load(flags + nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1u) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }
+            }
+        }
+        __syncthreads();
+        if (tid < 7) {
+            const double2 v = ld_sc1(block_rsrc(coef, 16 * 8), (int64_t)(2 * tid) * 8);
+            cs[2 * tid] = v.x;
+            cs[2 * tid + 1] = v.y;
+        }
+    }
     __syncthreads();
     if (tid < CB) {
         const double s = (red[tid] + red[128 + tid]) + (red[256 + tid] + red[384 + tid]);
-        // u_j = y_j + F_j c (the inner-constraint combine, coefficients from k_border_combine), then - s
+        // u_j = y_j + F_j c (the inner-constraint combine, coefficients cs), then - s
         double u = S[n_pad * ld + (int64_t)j * CB + tid];
         if (coef)
 #pragma unroll
-            for (int m = 0; m < 14; ++m) u += S[(n_pad + 1 + m) * ld + (int64_t)j * CB + tid] * coef[m];
+            for (int m = 0; m < 14; ++m) u += S[(n_pad + 1 + m) * ld + (int64_t)j * CB + tid] * cs[m];
         ys[tid] = u - s;
     }
     __syncthreads();
@@ -2630,14 +2668,16 @@ int launch_backward(Ctx& c) {
     const int64_t ld = c.L.ld;
     const Sched& s = c.sched;
     const int64_t nb = c.L.n_pad / CB;
-    const bool flow = c.bwd_flow && nb <= c.n_cu;
+    const bool flow = c.bwd_flow && nb + 1 <= c.n_cu;
     double* coef = c.d_bscr + 32 * 14 + 16 * 120;
-    if (c.set.inner_constraints) {
+    const bool gblk = c.chol_flow && s.flow_ok && s.flow_n > 0;
+    // the combine inside k_bwd_flow (one more workgroup) when the Gram comes from k_chol_flow
+    const int combine = (c.set.inner_constraints && flow && gblk) ? 1 : 0;
+    if (c.set.inner_constraints && !combine) {
         // (running k_trtri128 on a forked stream concurrently with these two measured slower: a forked
         // iteration graph adds cross-queue waits to every launch of the Cholesky chain)
         // k_chol_flow's RHS panel halves left the Gram as per-block partials (d_gblk); otherwise
         // k_border_gram forms it from the forward-solved rows
-        const bool gblk = c.chol_flow && s.flow_ok && s.flow_n > 0;
         if (!gblk) k_border_gram<<<GRAM_SEG, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_bscr + 32 * 14);
         if (flow)  // the 14 coefficients only; k_bwd_flow applies them to its block
             k_border_combine<<<1, 256, 0, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_bscr + 32 * 14, coef,
@@ -2647,9 +2687,10 @@ int launch_backward(Ctx& c) {
                                                                                        c.d_bscr + 32 * 14, nullptr, gblk ? c.d_gblk : nullptr, (int)nb);
     }
     if (flow) {  // one launch, every workgroup resident; roots solve by substitution
-        k_bwd_flow<<<(unsigned)nb, 256, BWD_LDS, c.stream>>>(c.d_S, ld, c.L.n_pad, c.d_linv, c.d_dinv, c.d_X, c.d_delta, c.L.u_c,
-                                                           c.d_sched + s.bf_start, c.d_sched + s.bf_src, c.d_bflags,
-                                                           c.d_scal, c.set.inner_constraints ? coef : nullptr);
+        k_bwd_flow<<<(unsigned)(nb + combine), 256, BWD_LDS, c.stream>>>(
+            c.d_S, ld, c.L.n_pad, c.d_linv, c.d_dinv, c.d_X, c.d_delta, c.L.u_c, c.d_sched + s.bf_start,
+            c.d_sched + s.bf_src, c.d_bflags, c.d_scal, c.set.inner_constraints ? coef : nullptr, combine,
+            c.d_bscr + 32 * 14, c.d_gblk, (int)nb);
         FBA_HIP(hipGetLastError());
         return FBA_OK;
     }
@@ -2676,7 +2717,8 @@ int chol_setup(Ctx& c) {
     hipDeviceProp_t prop;
     FBA_HIP(hipGetDeviceProperties(&prop, c.device));
     c.n_cu = prop.multiProcessorCount;
-    c.flags_bytes = (size_t)((c.L.n_pad / CB + 3) / 4 * 4) * sizeof(unsigned);  // multiple of 16 bytes
+    // (one more than the blocks: k_bwd_flow's border-combine flag; a multiple of 16 bytes)
+    c.flags_bytes = (size_t)((c.L.n_pad / CB + 1 + 3) / 4 * 4) * sizeof(unsigned);
     const size_t nf = c.flags_bytes / sizeof(unsigned);
     c.n_sync = (int64_t)(2 * nf + std::max(c.sched.n_counters, 1) + std::max(c.sched.n_tflags, 1));
     FBA_HIP(hipMalloc((void**)&c.d_flags, sizeof(unsigned) * c.n_sync));
