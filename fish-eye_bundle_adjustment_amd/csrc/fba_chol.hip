@@ -2351,9 +2351,9 @@ __global__ __launch_bounds__(256) void k_bwd_wave(double* __restrict__ S, int64_
 
 // k_bwd_flow: the whole backward solve L' x = y in ONE launch, dataflow-ordered: workgroup b owns
 // block column j = nb-1-b; it stages Linv_j in LDS, then for each source block row i of column j
-// (descending: the order the x_i are published in) streams L(i,j) into registers, waits for x_i's
-// flag, reads x_i (sc1) and adds L(i,j)' x_i; then x_j = Linv_j' (y_j - sum), published write-through
-// with an agent-scope flag, and delta_c = -x_j stored (k_neg_copy fused).  Waits only point to higher
+// (descending: the order the x_i are published in) streams L(i,j) into registers, polls x_i itself
+// (sc1 loads until no value is X_SENTINEL, which k_border_rhs wrote) and adds L(i,j)' x_i; then
+// x_j = Linv_j' (y_j - sum), published write-through, and delta_c = -x_j stored (k_neg_copy fused).  Waits only point to higher
 // blocks and every workgroup is resident (nb <= CUs, checked by the host), so they end; polls are
 // bounded (scal[1] = -1 on timeout, reported by the host).
 // With inner constraints and `combine`, one more workgroup (blockIdx nb) solves the border's 14x14
@@ -2412,17 +2412,20 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
         double2 m[32];
 #pragma unroll
         for (int r = 0; r < 32; ++r) m[r] = *reinterpret_cast<const double2*>(M + (int64_t)(h * 32 + r) * ld + 2 * c2);
-        if (tid == 0) {
+        if (tid < CB / 2) {  // wave 0 polls x_i itself (sc1) until none of its 128 values is the sentinel
             unsigned spins = 0;
-            while (__hip_atomic_load(flags + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1u) {
+            double2 v;
+            for (;;) {
+                asm volatile("" ::: "memory");  // the load is re-issued every spin (not hoisted)
+                v = ld_sc1(rX, ((int64_t)i * CB + 2 * tid) * 8);
+                const bool ok = __builtin_bit_cast(uint64_t, v.x) != X_SENTINEL && __builtin_bit_cast(uint64_t, v.y) != X_SENTINEL;
+                if (__all(ok)) break;
                 __builtin_amdgcn_s_sleep(1);
-                if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }
+                if (++spins == FLAG_SPINS) {
+                    if (tid == 0) scal[1] = -1.0;
+                    break;
+                }
             }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        __syncthreads();
-        if (tid < CB / 2) {
-            const double2 v = ld_sc1(rX, ((int64_t)i * CB + 2 * tid) * 8);
             xs[2 * tid] = v.x;
             xs[2 * tid + 1] = v.y;
         }
@@ -2495,9 +2498,6 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
             const int64_t g = (int64_t)j * CB + tid;
             if (g < u_c) delta[g] = -x;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) __hip_atomic_store(flags + j, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
     // x_j = Linv_j' y_j from LDS
@@ -2518,9 +2518,6 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
         const int64_t g = (int64_t)j * CB + tid;
         if (g < u_c) delta[g] = -x;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(flags + j, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void k_neg_copy(const double* __restrict__ X, double* __restrict__ delta, int64_t u_c) {

@@ -22,6 +22,9 @@ constexpr int FTRACE = 48;       // FBA_PANEL_TRACE: stamps per k_chol_flow reco
 // k_chol_flow: a fused diagonal update's tiles of tile columns >= FLOW_CSPLIT go to a helper record,
 // added into the potrf's LDS block during its bulk step FLOW_CSPLIT - 2 (fba_order.cpp build_flow)
 constexpr int FLOW_CSPLIT = 3;
+// k_bwd_flow's "not yet published" value of the solution blocks X (a signalling NaN with a payload no
+// arithmetic produces): the consumers poll the data itself, k_border_rhs resets it every solve
+constexpr uint64_t X_SENTINEL = 0x7FF4DEADBEEF5A5Aull;
 constexpr int CHUNK_OBS = 256;  // observations per k_lin_reduce / k_lin_point workgroup (chunk)
 // tie points per chunk and co-visibility terms per chunk staged in LDS (a single larger point's are
 // read from HBM instead): smaller for nK >= 6, whose wider Jacobian rows leave less of the 160 KiB LDS

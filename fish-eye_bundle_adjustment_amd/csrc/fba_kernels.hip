@@ -1047,7 +1047,7 @@ __global__ __launch_bounds__(256) void k_border_rhs(double* __restrict__ S, cons
                                                     double* __restrict__ scal, const double* __restrict__ part,
                                                     const uint8_t* __restrict__ active, int64_t ld, int64_t n_pad,
                                                     int64_t u_c, int n_img, int n_loc, int ic, int nbr,
-                                                    unsigned* __restrict__ sync, int64_t n_sync) {
+                                                    unsigned* __restrict__ sync, int64_t n_sync, double* __restrict__ X) {
     __shared__ double w[14];
     if (ic) border_weights_lds(part, w);
     if ((int)blockIdx.x < nbr) {
@@ -1070,6 +1070,7 @@ __global__ __launch_bounds__(256) void k_border_rhs(double* __restrict__ S, cons
     for (int64_t q = i; q < n_sync; q += nthr) sync[q] = 0u;
     if (ic && blockIdx.x == nbr && threadIdx.x < 14) scal[8 + (threadIdx.x / 7) * 8 + threadIdx.x % 7] = w[threadIdx.x];
     if (i >= n_pad) return;
+    X[i] = __builtin_bit_cast(double, X_SENTINEL);  // k_bwd_flow's solution blocks: not yet published
     if (i >= u_c || !active[i]) {
         // fixed parameter or padding: decoupled unit row, zero RHS
         S[i * ld + i] = 1.0;
@@ -1413,7 +1414,7 @@ int launch_border(Ctx& c) {
     const int nbr = (ic && c.n_loc > 0) ? 6 * c.n_loc : 0;
     k_border_rhs<<<(unsigned)(nbr + (L.n_pad + 255) / 256), 256, 0, c.stream>>>(
         c.d_S, c.d_G, c.d_scal, c.d_bscr, c.d_active, L.ld, L.n_pad, L.u_c, L.n_img, c.n_loc, ic, nbr, c.d_flags,
-        c.n_sync);
+        c.n_sync, c.d_X);
     FBA_HIP(hipGetLastError());
     return FBA_OK;
 }
