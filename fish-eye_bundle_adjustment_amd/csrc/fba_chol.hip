@@ -2036,25 +2036,37 @@ __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, co
             fused_apply<0>(rX, ld, p0, p1, rec[11], Xb[0], Xb[1], sy, smem, nullptr, scal, tr);
     }
     if (tr && threadIdx.x == 0) tr[4] = wall_clock64();
-    // late partials: the other sources of f's level, 64x64 row-major scratch quarters, slot order
-    for (int e = 0; e < rec[6]; ++e) {
-        const int32_t* l3 = lists + rec[5] + 3 * e;
-        const int q = l3[0];
+    // late partials: the other sources of f's level, 64x64 row-major scratch quarters, added in slot
+    // order; every flag checked first, then up to four partials' loads in flight together
+    if (rec[6] > 0) {
         __syncthreads();
-        if (tid == 0) spin_ge(fl + l3[2], 1u, scal);
+        if (tid == 0)
+            for (int e = 0; e < rec[6]; ++e) spin_ge(fl + lists[rec[5] + 3 * e + 2], 1u, scal);
         __syncthreads();
-        const __amdgpu_buffer_rsrc_t rp = block_rsrc(P + (int64_t)l3[1] * 4096, 4096 * 8);
-        double2 v[4];
+    }
+    for (int e0 = 0; e0 < rec[6]; e0 += 4) {
+        const int ne = rec[6] - e0 < 4 ? rec[6] - e0 : 4;
+        double2 v[4][4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = ld_sc1(rp, (int64_t)(2 * (tid + POTRF_THREADS * u)) * 8);
+        for (int e = 0; e < 4; ++e)
+            if (e < ne) {
+                const __amdgpu_buffer_rsrc_t rp = block_rsrc(P + (int64_t)lists[rec[5] + 3 * (e0 + e) + 1] * 4096, 4096 * 8);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int e2 = 2 * (tid + POTRF_THREADS * u), R = 64 * (q >> 1) + (e2 >> 6), C = 64 * (q & 1) + (e2 & 63);
-            if ((R >> 4) >= (C >> 4)) {
-                AT(R, C) += v[u].x;
-                AT(R, C + 1) += v[u].y;
+                for (int u = 0; u < 4; ++u) v[e][u] = ld_sc1(rp, (int64_t)(2 * (tid + POTRF_THREADS * u)) * 8);
             }
-        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (e < ne) {
+                const int q = lists[rec[5] + 3 * (e0 + e)];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int e2 = 2 * (tid + POTRF_THREADS * u), R = 64 * (q >> 1) + (e2 >> 6), C = 64 * (q & 1) + (e2 & 63);
+                    if ((R >> 4) >= (C >> 4)) {
+                        AT(R, C) += v[e][u].x;
+                        AT(R, C + 1) += v[e][u].y;
+                    }
+                }
+            }
     }
     __syncthreads();  // the block final in LDS; the counters and buffers free
     if (tr && threadIdx.x == 0) tr[5] = wall_clock64();
