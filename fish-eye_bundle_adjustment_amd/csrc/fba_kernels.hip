@@ -412,7 +412,9 @@ struct LR {
     // observation offsets, observations)
     static constexpr int CP = chunk_pts(NK), CT = chunk_terms(NK);
     static constexpr int NI = CHUNK_OBS + (CT + 1) + CT + (CHUNK_OBS + 1) + CHUNK_OBS;
-    static constexpr int CAM_SPLIT = 512 / NCAM;   // camera entries: observation sub-ranges in parallel
+    // camera entries: CAM_SPLIT - 1 observation sub-ranges and the points' Schur terms in parallel
+    static constexpr int CAM_SPLIT = 512 / NCAM;
+    static_assert(CAM_SPLIT >= 2, "camera entries: at least one observation part and the points' part");
     static constexpr size_t LDS = sizeof(double) * (CHUNK_OBS * ES + CHUNK_OBS * US + CP * PPS + 512) +
                                   sizeof(int) * NI;
     static_assert(LDS <= 160 * 1024, "k_lin_reduce LDS over the 160 KiB of a CU");
@@ -669,7 +671,8 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     // (D) camera entries first (the longest items), then image keys, then pair keys (the plan lists
     // were staged in LDS before (A)).
     const int nob = o1 - o0, np = p1 - p0;
-    // camera entries: CAM_SPLIT observation sub-ranges in parallel
+    // camera entries: parts 0 .. CAM_SPLIT - 2 sum observation sub-ranges, part CAM_SPLIT - 1 the points'
+    // Schur terms (so no thread runs both loops)
     if (t < CAM_SPLIT * NCAM) {
         constexpr int NPK = CW * (CW + 1) / 2;
         const int it = t % NCAM, part = t / NCAM;
@@ -681,15 +684,18 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
         } else {
             c1 = it - NPK;
         }
-        const int l0 = nob * part / CAM_SPLIT, l1 = nob * (part + 1) / CAM_SPLIT;
+        constexpr int NO = CAM_SPLIT - 1;
+        const int l0 = part < NO ? nob * part / NO : 0, l1 = part < NO ? nob * (part + 1) / NO : 0;
         double s = 0.0;
+#pragma unroll 4
         for (int l = l0; l < l1; ++l) {
             const double* r = QE + l * ES;
             const double s0 = (c2 >= 0) ? r[14 + c2] : r[12];
             const double s1 = (c2 >= 0) ? r[14 + CW + c2] : r[13];
             s += r[14 + c1] * s0 + r[14 + CW + c1] * s1;
         }
-        if (part == CAM_SPLIT - 1)  // the points' Schur terms with the last sub-range
+        if (part == CAM_SPLIT - 1)  // the points' Schur terms
+#pragma unroll 4
             for (int q = 0; q < np; ++q) {
                 const double* pp = PP + q * PPS;
                 const double* u1 = pp + 15 + 3 * c1;
