@@ -483,6 +483,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     // 1 / 2 / 3 / 5: 724 / 760 / 828 / 916 / 1035 -- an update deferred towards its need lands on the
     // critical path.  (FBA_PANEL_TRACE=3: the mid levels' panel halves start late because the CUs are
     // held by update tasks that wait for progressively published source columns, ~20 us each.)
+    static const int defer = getenv("FBA_FLOW_DEFER") ? atoi(getenv("FBA_FLOW_DEFER")) : 0;
     static const int promote_mode = getenv("FBA_FLOW_PROMOTE") ? atoi(getenv("FBA_FLOW_PROMOTE")) : 0;
     static const int lookahead = getenv("FBA_FLOW_LOOKAHEAD") ? atoi(getenv("FBA_FLOW_LOOKAHEAD")) : 1000;
     int nslot = 0, ncnt = 0;
@@ -586,9 +587,12 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
                     // level[b]), so updates of far-away targets do not hold CUs ahead of the next
                     // levels' panel halves
                     const int need = a == b ? level[b] - 1 : level[b];
+                    // FBA_FLOW_DEFER = N: among the records of level min(source level + N, need - 1)
+                    const int lev = defer > 0 && !is_late ? std::max(w, std::min(w + defer, need - 1))
+                                                          : std::max(w, need - lookahead);
                     const int id = add({2, a, b, q, soff, g1 - g0, slot, mode, flag, is_late ? -1 : prev, cidx, first, ng, 0,
                                         CB_BLOCKS},
-                                       {std::max(w, need - lookahead), is_late ? 2 : rank, (int)(b * (nb + 1) + a) * 4 + q});
+                                       {lev, is_late ? 2 : rank, (int)(b * (nb + 1) + a) * 4 + q});
                     flag_deps[id] = fd;
                     if (!is_late && prev >= 0) flag_deps[id].push_back(prev);
                     uflag_tasks[flag - np].push_back(id);
