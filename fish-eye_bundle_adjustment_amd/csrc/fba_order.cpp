@@ -483,6 +483,8 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     // 1 / 2 / 3 / 5: 724 / 760 / 828 / 916 / 1035 -- an update deferred towards its need lands on the
     // critical path.  (FBA_PANEL_TRACE=3: the mid levels' panel halves start late because the CUs are
     // held by update tasks that wait for progressively published source columns, ~20 us each.)
+    // FBA_FLOW_DEFER = N (updates among the records of level min(source level + N, need - 1)): config 4
+    // 1172-1180 iter/s at N = 0, 1135-1140 at 1, 1058-1063 at 2
     static const int defer = getenv("FBA_FLOW_DEFER") ? atoi(getenv("FBA_FLOW_DEFER")) : 0;
     static const int promote_mode = getenv("FBA_FLOW_PROMOTE") ? atoi(getenv("FBA_FLOW_PROMOTE")) : 0;
     static const int lookahead = getenv("FBA_FLOW_LOOKAHEAD") ? atoi(getenv("FBA_FLOW_LOOKAHEAD")) : 1000;
