@@ -578,7 +578,8 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     FBA_HIP(hipMemsetAsync(c->d_S, 0, sizeof(double) * (size_t)(L.n_pad + NB) * L.ld, c->stream));
     FBA_HIP(hipStreamSynchronize(c->stream));
     FBA_HIP(hipMemset(c->d_scal, 0, sizeof(double) * 16));
-    FBA_HIP(hipHostMalloc((void**)&c->h_pinned, sizeof(double) * 64));
+    FBA_HIP(hipHostMalloc((void**)&c->h_pinned, sizeof(double) * 64, hipHostMallocMapped | hipHostMallocCoherent));
+    FBA_HIP(hipHostGetDevicePointer((void**)&c->d_hpinned, c->h_pinned, 0));
     for (auto& e : c->ev) FBA_HIP(hipEventCreate(&e));
     if (opt.verbose)
         fprintf(stderr, "[fba] rank %d/%d: n_obs %ld (tie %ld), points %ld, pairs %ld (%ld terms), u_c %ld, n_pad %ld; "
@@ -696,7 +697,7 @@ static int solve_body(Ctx* c) {
     mark(c, 6);
     if ((rc = launch_backsub_update(*c))) return rc;
     mark(c, 7);
-    FBA_HIP(hipMemcpyAsync(c->h_pinned, c->d_scal, sizeof(double) * 4, hipMemcpyDeviceToHost, c->stream));
+    // scal[0..3] reach h_pinned from k_sum_parts itself (host-mapped stores, no copy node)
     return FBA_OK;
 }
 

@@ -227,7 +227,8 @@ struct Ctx {
     uint8_t* d_active = nullptr; // [n_pad] 1 = estimated camera-side parameter
     uint8_t* d_counted = nullptr;// [u_full] 1 = counted in this rank's sumabs share
     int64_t* d_obs_pho = nullptr;// [n_obs] PHO row of each local observation
-    double* h_pinned = nullptr;  // pinned host scratch
+    double* h_pinned = nullptr;  // pinned host scratch (coherent, mapped: k_sum_parts writes scal[0..3] here)
+    double* d_hpinned = nullptr; // its device address
 
     // state
     bool have_lin = false;       // d_J holds a linearisation

@@ -1178,7 +1178,8 @@ __global__ __launch_bounds__(256) void k_update(double* __restrict__ xfull, doub
     if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
 
-__global__ void k_sum_parts(const double* __restrict__ part, int n, double* __restrict__ out) {
+// deltasum into scal[2]; scal[0..3] also to the host-mapped scratch `host` (read after the stream sync)
+__global__ void k_sum_parts(const double* __restrict__ part, int n, double* __restrict__ scal, double* __restrict__ host) {
     __shared__ double red[256];
     double a = 0.0;
     // each thread sums a contiguous range (fixed order), then a fixed tree
@@ -1190,7 +1191,15 @@ __global__ void k_sum_parts(const double* __restrict__ part, int n, double* __re
         if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) *out = red[0];
+    if (threadIdx.x == 0) {
+        scal[2] = red[0];
+        if (host) {
+            host[0] = scal[0];
+            host[1] = scal[1];
+            host[2] = red[0];
+            host[3] = scal[3];
+        }
+    }
 }
 
 
@@ -1441,7 +1450,7 @@ int launch_backsub_update(Ctx& c) {
     k_update<<<nblk, 256, 0, c.stream>>>(c.d_xfull, c.d_delta, c.d_cam_tab, c.d_counted, c.d_part, L.u_full,
                                          L.n_img, L.n_cam, L.nk, L.cw, c.cam_tab_stride);
     FBA_HIP(hipGetLastError());
-    k_sum_parts<<<1, 256, 0, c.stream>>>(c.d_part, nblk, c.d_scal + 2);
+    k_sum_parts<<<1, 256, 0, c.stream>>>(c.d_part, nblk, c.d_scal, c.d_hpinned);
     FBA_HIP(hipGetLastError());
     return FBA_OK;
 }
