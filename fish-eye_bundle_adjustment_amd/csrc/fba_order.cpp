@@ -657,10 +657,12 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
             X.rec[6] = (int32_t)late[j].size();
         }
     }
-    // inverses of the diagonal blocks below the top level
+    // inverses of the diagonal blocks below the top level (FBA_FLOW_INV_LAST=1: all after the last level's
+    // records, so they hold no CU while the middle levels run; config 4: 1160-1167 vs 1162-1170 iter/s)
+    static const bool inv_last = getenv("FBA_FLOW_INV_LAST") && atoi(getenv("FBA_FLOW_INV_LAST")) != 0;
     for (int64_t j = 0; j < nb; ++j)
         if (level[j] < nw - 1) {
-            const int id = add({3, (int32_t)j}, {level[j] + 1, 5, (int)j});
+            const int id = add({3, (int32_t)j}, {inv_last ? nw : level[j] + 1, 5, (int)j});
             T[id].deps.push_back(col_task[j]);
             s.flow_flops += (double)NB * NB * NB / 3.0;
         }
