@@ -8,7 +8,4 @@ for cfg in 3 5; do
   rc=$?; echo "== config $cfg rc=$rc"; tail -1 gpurun_out/bench_c$cfg.log | cut -c1-300
   [ $rc -ne 0 ] && exit $rc
 done
-FBA_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-  --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 1 > gpurun_out/gloo2.log 2>&1
-rc=$?; echo "== gloo 2-rank rc=$rc"; grep '"metric"' gpurun_out/gloo2.log | cut -c1-300
-exit $rc
+bash scripts/gpu_gloo2.sh  # per-level launches: two ranks' persistent kernels cannot share the one GPU
