@@ -105,12 +105,30 @@ __device__ __forceinline__ void params_body(int t, int nthreads, const double* _
     }
 }
 
-__global__ void k_params(const double* __restrict__ xfull, const double* __restrict__ caminfo,
-                         double* __restrict__ img_tab, double* __restrict__ cam_tab, double* __restrict__ G,
-                         const uint8_t* __restrict__ active, int n_img, int n_cam, int nk, int cw, int cam_stride,
-                         int ic, double* __restrict__ xcopy, int64_t n_copy) {
-    params_body(blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x, xfull, caminfo, img_tab, cam_tab, G,
-                active, n_img, n_cam, nk, cw, cam_stride, ic, xcopy, n_copy);
+// 64-thread workgroups: [0, nb) the image and camera tables, [nb, grid) the copy of the linearisation
+// point with four independent loads in flight per thread, so the table waves do not first wait out
+// serial copy iterations (kernel time = max of the two instead of their sum)
+constexpr int PARAMS_WG = 64;
+__global__ __launch_bounds__(PARAMS_WG) void k_params(const double* __restrict__ xfull, const double* __restrict__ caminfo,
+                                                      double* __restrict__ img_tab, double* __restrict__ cam_tab,
+                                                      double* __restrict__ G, const uint8_t* __restrict__ active, int n_img,
+                                                      int n_cam, int nk, int cw, int cam_stride, int ic,
+                                                      double* __restrict__ xcopy, int64_t n_copy) {
+    const int nb = (n_img + n_cam + PARAMS_WG - 1) / PARAMS_WG;
+    if ((int)blockIdx.x < nb) {
+        params_body(blockIdx.x * PARAMS_WG + threadIdx.x, nb * PARAMS_WG, xfull, caminfo, img_tab, cam_tab, G, active,
+                    n_img, n_cam, nk, cw, cam_stride, ic, nullptr, 0);
+        return;
+    }
+    if (!xcopy) return;
+    const int64_t t = (int64_t)(blockIdx.x - nb) * PARAMS_WG + threadIdx.x, st = (int64_t)(gridDim.x - nb) * PARAMS_WG;
+    double v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = t + j * st < n_copy ? xfull[t + j * st] : 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (t + j * st < n_copy) xcopy[t + j * st] = v[j];
+    for (int64_t i = t + 4 * st; i < n_copy; i += st) xcopy[i] = xfull[i];
 }
 
 // the per-iteration head of the accumulation in one launch: workgroups < npb build the parameter
@@ -1348,9 +1366,9 @@ int launch_params_zero(Ctx& c, double* copy_to) {
 
 int launch_params(Ctx& c, const double* x, double* copy_to) {
     const int n = c.L.n_img + c.L.n_cam;
-    const int64_t blocks = copy_to ? std::max<int64_t>((n + 63) / 64, std::min<int64_t>(1024, (c.L.u_full + 255) / 256))
-                                   : (n + 63) / 64;
-    k_params<<<(unsigned)blocks, 64, 0, c.stream>>>(x ? x : c.d_xfull, c.d_caminfo, c.d_img_tab, c.d_cam_tab, c.d_G,
+    const int64_t nb = (n + PARAMS_WG - 1) / PARAMS_WG;
+    const int64_t blocks = copy_to ? nb + std::min<int64_t>(2048, (c.L.u_full + 4 * PARAMS_WG - 1) / (4 * PARAMS_WG)) : nb;
+    k_params<<<(unsigned)blocks, PARAMS_WG, 0, c.stream>>>(x ? x : c.d_xfull, c.d_caminfo, c.d_img_tab, c.d_cam_tab, c.d_G,
                                                     c.d_active, c.L.n_img, c.L.n_cam, c.L.nk, c.L.cw, c.cam_tab_stride,
                                                     c.set.inner_constraints, copy_to, c.L.u_full);
     FBA_HIP(hipGetLastError());
