@@ -1622,7 +1622,8 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_panel(double* __restrict__ S,
     const int b = blockIdx.x;
     const int e1 = ndiag, e2 = e1 + ncol, e3 = e2 + npanel, e4 = e3 + ntrsm, e5 = e4 + nprev;
     // FBA_PANEL_TRACE: [start, after the waits, end, role, phase stamps] per workgroup (100 MHz wall clock)
-    uint64_t* tr = trace ? trace + 8 * (int64_t)b : nullptr;
+    // (PTRACE_WG slots per level: a larger grid leaves its extra workgroups untraced)
+    uint64_t* tr = (trace && b < PTRACE_WG) ? trace + 8 * (int64_t)b : nullptr;
     if (tr && threadIdx.x == 0) tr[0] = wall_clock64();
     int role;
     if (b < e1) {
@@ -2251,7 +2252,7 @@ __device__ __forceinline__ void syrk_flow_body(double* __restrict__ S, int64_t l
 constexpr size_t FLOW_LDS_A = FLOWF_LDS > TRSMF_LDS ? FLOWF_LDS : TRSMF_LDS;
 constexpr size_t FLOW_LDS_B = SYRKW_LDS > TRTRI_LDS ? SYRKW_LDS : TRTRI_LDS;
 constexpr size_t FLOW_LDS = FLOW_LDS_A > FLOW_LDS_B ? FLOW_LDS_A : FLOW_LDS_B;
-static_assert(FLOW_LDS <= 160 * 1024, "k_chol_flow LDS");
+static_assert(FLOW_LDS + 16 <= 160 * 1024, "k_chol_flow LDS (+ the static ticket word)");
 static_assert(SYRKW_LDS >= sizeof(double) * 128 * LDW + 2 * sizeof(int), "syrk_flow_body broadcast words");
 
 __global__ __launch_bounds__(POTRF_THREADS) void k_chol_flow(double* __restrict__ S, int64_t ld,
@@ -2261,10 +2262,19 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_chol_flow(double* __restrict_
                                                              double* __restrict__ scal, unsigned* __restrict__ colflags,
                                                              unsigned* __restrict__ fl, unsigned* __restrict__ cnt,
                                                              double* __restrict__ P, uint64_t* __restrict__ trace,
-                                                             double* __restrict__ gblk) {
+                                                             double* __restrict__ gblk, unsigned* __restrict__ ticket) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int32_t* rec = recs + Sched::FLOW_REC * (int64_t)blockIdx.x;
-    uint64_t* tr = trace ? trace + FTRACE * (int64_t)blockIdx.x : nullptr;
+    // the record comes from an atomic ticket, not from blockIdx: tickets follow the order in which the
+    // workgroups really start, and every record waits only for records of smaller index (build_flow's
+    // order check), so each wait points to a workgroup that has already started and is resident (or
+    // done) -- progress does not depend on the hardware dispatching blockIdx in order, nor on every
+    // record being co-resident (a second process on the GPU only slows it down)
+    __shared__ int s_ticket;
+    if (threadIdx.x == 0) s_ticket = (int)__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int rid = s_ticket;
+    const int32_t* rec = recs + Sched::FLOW_REC * (int64_t)rid;
+    uint64_t* tr = trace ? trace + FTRACE * (int64_t)rid : nullptr;
     if (tr && threadIdx.x == 0) tr[0] = wall_clock64();
     const int role = rec[0];
     if (role == 0) {
@@ -2365,13 +2375,15 @@ __global__ __launch_bounds__(256) void k_bwd_wave(double* __restrict__ S, int64_
 // block column j = nb-1-b; it stages Linv_j in LDS, then for each source block row i of column j
 // (descending: the order the x_i are published in) streams L(i,j) into registers, polls x_i itself
 // (sc1 loads until no value is X_SENTINEL, which k_border_rhs wrote) and adds L(i,j)' x_i; then
-// x_j = Linv_j' (y_j - sum), published write-through, and delta_c = -x_j stored (k_neg_copy fused).  Waits only point to higher
-// blocks and every workgroup is resident (nb <= CUs, checked by the host), so they end; polls are
+// x_j = Linv_j' (y_j - sum), published write-through, and delta_c = -x_j stored (k_neg_copy fused).  Roles
+// come from an atomic ticket in start order and waits only point to higher blocks (earlier tickets), so
+// they end whether or not the whole grid is co-resident; polls are
 // bounded (scal[1] = -1 on timeout, reported by the host).
-// With inner constraints and `combine`, one more workgroup (blockIdx nb) solves the border's 14x14
+// With inner constraints and `combine`, one more workgroup (ticket 0) solves the border's 14x14
 // system (border_combine_body) meanwhile, publishes the coefficients write-through and raises flags[nb];
 // the block workgroups wait for it only where they form u_j (after staging and their sources).
 constexpr size_t BWD_LDS = sizeof(double) * (CB * CB + (CB / IB) * IB * IB + 2 * CB + 512 + 16);
+static_assert(BWD_LDS + 16 <= 160 * 1024, "k_bwd_flow LDS (+ the static ticket word)");
 
 __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, int64_t ld, int64_t n_pad,
                                                   const double* __restrict__ linv, const double* __restrict__ dinv,
@@ -2380,7 +2392,8 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
                                                   const int32_t* __restrict__ src_start, const int32_t* __restrict__ src,
                                                   unsigned* __restrict__ flags, double* __restrict__ scal,
                                                   double* __restrict__ coef, int combine,
-                                                  const double* __restrict__ gpart, const double* __restrict__ gblk, int nblk) {
+                                                  const double* __restrict__ gpart, const double* __restrict__ gblk, int nblk,
+                                                  unsigned* __restrict__ ticket) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* Li = smem;              // [128][128] Linv_j, or L_jj for a root column
     double* Dt = Li + CB * CB;      // [8][16][16] the leaf inverses of a root column
@@ -2390,7 +2403,14 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
     double* cs = red + 512;         // [16] the border coefficients
     const int tid = threadIdx.x;
     const int nb = (int)(n_pad / CB);
-    if (combine && (int)blockIdx.x == nb) {  // the border combine workgroup
+    // roles by atomic ticket (real start order): ticket 0 is the border combine (when present), then
+    // the block columns top down -- every wait (a higher block's x, the combine's coefficients) points
+    // to a workgroup that started earlier, so progress needs neither in-order dispatch nor co-residency
+    __shared__ int s_ticket;
+    if (tid == 0) s_ticket = (int)__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int tk = s_ticket;
+    if (combine && tk == 0) {  // the border combine workgroup
         border_combine_body(gpart, gblk, nblk, reinterpret_cast<double (*)[15]>(Li), cs);
         if (tid < 14) {
             const __amdgpu_buffer_rsrc_t rc = block_rsrc(coef, 16 * 8);
@@ -2401,7 +2421,7 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
         if (tid == 0) __hip_atomic_store(flags + nb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
-    const int j = nb - 1 - (int)blockIdx.x;
+    const int j = nb - 1 - (tk - combine);
     const int c2 = tid & 63, h = tid >> 6;  // gemv_t128's thread map: columns 2 c2 + {0,1}, rows 32 h ..
     // a root of the elimination tree (no source blocks: the top level) is solved by substitution with
     // its factor and leaf inverses, so its Linv (k_trtri128, 30 us) is off the critical path
@@ -2551,7 +2571,7 @@ int launch_cholesky(Ctx& c) {
         if (pp) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
         k_chol_flow<<<(unsigned)s.flow_n, POTRF_THREADS, FLOW_LDS, c.stream>>>(
             c.d_S, ld, c.d_sched, c.d_sched + s.flow_rec, c.d_dinv, c.d_linv, c.d_scal, c.d_flags, c.d_tflags,
-            c.d_counters, c.d_P, c.d_ptrace, c.set.inner_constraints ? c.d_gblk : nullptr);
+            c.d_counters, c.d_P, c.d_ptrace, c.set.inner_constraints ? c.d_gblk : nullptr, c.d_tickets);
         if (pp) {
             FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], c.stream));
             c.probe_flops += s.flow_flops;
@@ -2677,7 +2697,7 @@ int launch_backward(Ctx& c) {
     const int64_t ld = c.L.ld;
     const Sched& s = c.sched;
     const int64_t nb = c.L.n_pad / CB;
-    const bool flow = c.bwd_flow && nb + 1 <= c.n_cu;
+    const bool flow = c.bwd_flow;  // (ticket-ordered roles: no co-residency requirement)
     double* coef = c.d_bscr + 32 * 14 + 16 * 120;
     const bool gblk = c.chol_flow && s.flow_ok && s.flow_n > 0;
     // the combine inside k_bwd_flow (one more workgroup) when the Gram comes from k_chol_flow
@@ -2699,7 +2719,7 @@ int launch_backward(Ctx& c) {
         k_bwd_flow<<<(unsigned)(nb + combine), 256, BWD_LDS, c.stream>>>(
             c.d_S, ld, c.L.n_pad, c.d_linv, c.d_dinv, c.d_X, c.d_delta, c.L.u_c, c.d_sched + s.bf_start,
             c.d_sched + s.bf_src, c.d_bflags, c.d_scal, c.set.inner_constraints ? coef : nullptr, combine,
-            c.d_bscr + 32 * 14, c.d_gblk, (int)nb);
+            c.d_bscr + 32 * 14, c.d_gblk, (int)nb, c.d_tickets + 1);
         FBA_HIP(hipGetLastError());
         return FBA_OK;
     }
@@ -2729,12 +2749,14 @@ int chol_setup(Ctx& c) {
     // (one more than the blocks: k_bwd_flow's border-combine flag; a multiple of 16 bytes)
     c.flags_bytes = (size_t)((c.L.n_pad / CB + 1 + 3) / 4 * 4) * sizeof(unsigned);
     const size_t nf = c.flags_bytes / sizeof(unsigned);
-    c.n_sync = (int64_t)(2 * nf + std::max(c.sched.n_counters, 1) + std::max(c.sched.n_tflags, 1));
+    // [flags][bflags][split-target counters][update flags][2 tickets: k_chol_flow, k_bwd_flow]
+    c.n_sync = (int64_t)(2 * nf + std::max(c.sched.n_counters, 1) + std::max(c.sched.n_tflags, 1) + 2);
     FBA_HIP(hipMalloc((void**)&c.d_flags, sizeof(unsigned) * c.n_sync));
     FBA_HIP(hipMemset(c.d_flags, 0, sizeof(unsigned) * c.n_sync));
     c.d_bflags = c.d_flags + nf;
     c.d_counters = c.d_bflags + nf;
     c.d_tflags = c.d_counters + std::max(c.sched.n_counters, 1);
+    c.d_tickets = c.d_tflags + std::max(c.sched.n_tflags, 1);
     FBA_HIP(hipFuncSetAttribute((const void*)k_bwd_flow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)BWD_LDS));
     c.bwd_flow = !(getenv("FBA_BWD_LEVELS") && atoi(getenv("FBA_BWD_LEVELS")) != 0);
     c.panel_progressive = !(getenv("FBA_PANEL_PROGRESSIVE") && atoi(getenv("FBA_PANEL_PROGRESSIVE")) == 0);

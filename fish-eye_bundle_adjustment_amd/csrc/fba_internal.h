@@ -203,6 +203,7 @@ struct Ctx {
     unsigned* d_bflags = nullptr; // [nb] k_bwd_flow hand-off flags (zeroed before each backward solve)
     unsigned* d_counters = nullptr; // [Sched::n_counters] split-target arrival counters
     unsigned* d_tflags = nullptr;   // [Sched::n_tflags] update-target completion flags (merged k_panel)
+    unsigned* d_tickets = nullptr;  // [2] start-order tickets of k_chol_flow / k_bwd_flow records
     int64_t n_sync = 0;           // unsigned words of flags + bflags + counters (one allocation at d_flags,
                                   // zeroed by k_border_rhs ahead of every factorisation)
     bool bwd_flow = true;

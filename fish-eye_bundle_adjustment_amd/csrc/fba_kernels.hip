@@ -1085,7 +1085,9 @@ __global__ __launch_bounds__(256) void k_border_rhs(double* __restrict__ S, cons
             double acc = 0.0;
 #pragma unroll
             for (int m = 0; m < 7; ++m) acc += gw[m] * gj[m];
-            if (acc != 0.0) S[i * ld + j] += acc;
+            // an inactive row's diagonal is the unit written by the other role (inner constraints need all
+            // six EOPs, so such rows have zero G rows today; the guard keeps the two roles disjoint)
+            if (acc != 0.0 && (j != i || active[i])) S[i * ld + j] += acc;
         }
         return;
     }

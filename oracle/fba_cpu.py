@@ -202,16 +202,40 @@ def time_iterations(folder, seconds=20.0, threads=None, data=None):
     if data is None:
         data = fba_oracle.load_folder(folder)
     threads = threads or default_threads()
+    ph = {"linearize_reduce": 0.0, "solve": 0.0, "update": 0.0}
     with threadpool_limits(limits=threads):
         adj = CpuAdjustment(data, threads=threads, solver="chol")
         t0 = time.perf_counter()
         n = 0
         while True:
-            adj.step()
+            # one pass of main.m:413-488 (= adj.step()), timed per phase
+            ta = time.perf_counter()
+            adj.accumulate()
+            tb = time.perf_counter()
+            dc = np.ascontiguousarray(adj._solve())
+            tc = time.perf_counter()
+            adj.deltasum.append(lib().fbo_update(adj.h, _p(dc), _p(adj.xhat)))
+            td = time.perf_counter()
+            ph["linearize_reduce"] += tb - ta
+            ph["solve"] += tc - tb
+            ph["update"] += td - tc
             n += 1
             el = time.perf_counter() - t0
             if el >= seconds or n >= 1000:
                 break
         adj.close()
     return {"value": n / el, "iterations": n, "seconds": el, "cores": threads,
-            "n_pts": len(data.x), "u": adj.u, "u_c": adj.u_c}
+            "n_pts": len(data.x), "u": adj.u, "u_c": adj.u_c, "cpu_model": cpu_model(),
+            "phase_ms": {k: 1e3 * v / n for k, v in ph.items()}}
+
+
+def cpu_model():
+    """The host CPU's model string (/proc/cpuinfo), for the cpu_baseline record."""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for ln in fh:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"

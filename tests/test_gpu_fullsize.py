@@ -4,12 +4,13 @@
   adjustment (main.m:407-494) against the C restatement oracle/fba_cpu.c solving the reference's
   bordered system directly ("kkt") -- same iteration count, xhat <= 1e-9 relative per parameter
   group (distortion terms in scaled units), sigma0^2 <= 1e-9.
-* config 4 (1,000 x 50,000, the bench workload): the first two Gauss-Newton passes against the
-  same oracle -- deltasum <= 1e-9 of the first correction, xhat <= 1e-9 per group.
-* config 5 (4,000 x 200,000, 2M image points; too large for a CPU oracle within a test): size-
-  independent properties -- bit-identical repeat runs, monotone convergence below Threshold_Value
-  within Iteration_Cap, and sigma0^2 = 1 +- 5% (the generator's noise equals Meas_std, so the a
-  posteriori variance factor of a correct adjustment is ~1).
+* config 4 (1,000 x 50,000, the bench workload): the whole adjustment against the same oracle --
+  iteration count, deltasum history, xhat, sigma0^2, RMS and v.
+* config 5 (4,000 x 200,000, 2M image points): the first two Gauss-Newton passes against the C
+  oracle's dense regularised-border Cholesky; then size-independent properties of the converged
+  run -- bit-identical repeat runs, monotone convergence below Threshold_Value within
+  Iteration_Cap, and sigma0^2 = 1 +- 5% (the generator's noise equals Meas_std, so the a posteriori
+  variance factor of a correct adjustment is ~1).
 """
 import os
 
@@ -65,6 +66,19 @@ def test_config3_adjust_matches_oracle(fba, fbo, oracle, scenes):
     _check_adjust(fba, fbo, oracle, _scene(3, scenes))
 
 
+@pytest.mark.parametrize("env", [{"FBA_CHOL_FLOW": "0"}, {"FBA_BWD_LEVELS": "1"},
+                                 {"FBA_CHOL_FLOW": "0", "FBA_BWD_LEVELS": "1"}],
+                         ids=["per-level-factor", "per-level-backward", "both"])
+def test_config3_fallback_paths_match_oracle(fba, fbo, oracle, scenes, env, monkeypatch):
+    """The non-default solve paths (read per context in chol_setup): the per-level k_panel launches
+    instead of the persistent k_chol_flow (with k_border_gram -> k_border_combine), and the per-level
+    k_bwd_wave backward solve instead of k_bwd_flow -- the paths build_flow's order check falls back
+    to, and the one the 2-rank rehearsal used."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    _check_adjust(fba, fbo, oracle, _scene(3, scenes))
+
+
 def test_control_points_adjust_matches_oracle(fba, fbo, oracle, tmp_path):
     """No inner constraints: 40 control points fix the datum (the cam0 configuration, at scale)."""
     from fba_amd import synth
@@ -103,23 +117,49 @@ def test_config3_covariance_matches_oracle(fba, fbo, oracle, scenes):
     assert np.isfinite(tie).all() and (tie > 0).all()
 
 
-def test_config4_first_iterations_match_oracle(fba, fbo, oracle, scenes):
+def test_config4_adjust_matches_oracle(fba, fbo, oracle, scenes):
+    """The bench workload, converged: the whole adjustment (main.m:407-494) against the C oracle
+    solving the reference's bordered system [S G; G' 0] directly -- same iteration count, the whole
+    deltasum history, xhat <= 1e-9 relative per parameter group (distortion terms in the scaled
+    units), sigma0^2 <= 1e-9 (main.m:601) and RMSx / RMSy (main.m:594-598) <= 1e-9."""
     folder = _scene(4, scenes)
     ds = fba.load_folder(folder)
     od = oracle.load_folder(folder)
     ref = fbo.CpuAdjustment(od, solver="kkt")
+    it = ref.adjust()
+    v_ref, s02 = ref.residuals()
+    res = fba.adjust(ds, covariance=False)
+    assert res.iterations == it
+    np.testing.assert_allclose(res.deltasum, ref.deltasum, rtol=0, atol=1e-9 * ref.deltasum[0])
+    err = group_rel_err(res.xhat, ref.xhat, ref.names, dist_scaling_of(od))
+    assert max(err.values()) <= 1e-9, err
+    assert abs(res.sigma02 - s02) <= 1e-9 * s02
+    rms_ref = (np.sqrt(np.mean(v_ref[0::2] ** 2)), np.sqrt(np.mean(v_ref[1::2] ** 2)))
+    assert abs(res.rms[0] - rms_ref[0]) <= 1e-9 * rms_ref[0] and abs(res.rms[1] - rms_ref[1]) <= 1e-9 * rms_ref[1]
+    # per observation: v = A delta + w of the last linearisation (main.m:569)
+    assert np.max(np.abs(res.v - v_ref)) <= 1e-7 * np.max(np.abs(v_ref))
+
+
+def test_config5_first_iterations_match_oracle(fba, fbo, oracle, scenes):
+    """config 5 (4,000 images x 200,000 tie points, u_c = 24,010): the first two Gauss-Newton passes
+    against the C oracle with the regularised-border Cholesky of the dense reduced system (4.6 GB)
+    -- deltasum and xhat after each pass <= 1e-9 relative per parameter group."""
+    folder = _scene(5, scenes)
+    ds = fba.load_folder(folder)
+    od = oracle.load_folder(folder)
+    ref = fbo.CpuAdjustment(od, solver="chol")
     ctx = _ctx(fba, ds)
+    dsc = dist_scaling_of(od)
     try:
         for _ in range(2):
             d_ref = ref.step()
             d = ctx.step()
-            assert abs(d - d_ref) <= 1e-9 * ref.deltasum[0]
-        x = ctx.get_xhat()
+            assert abs(d - d_ref) <= 1e-9 * ref.deltasum[0], (d, d_ref)
+            err = group_rel_err(ctx.get_xhat(), ref.xhat, ref.names, dsc)
+            assert max(err.values()) <= 1e-9, err
     finally:
         ctx.close()
-    dsc = dist_scaling_of(od)
-    err = group_rel_err(x, ref.xhat, ref.names, dsc)
-    assert max(err.values()) <= 1e-9, err
+        ref.close()
 
 
 def test_config5_properties(fba, scenes):
