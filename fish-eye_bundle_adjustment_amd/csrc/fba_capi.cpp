@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <map>
 #include <numeric>
 #include <tuple>
 
@@ -116,21 +117,15 @@ static int check_problem(const fba_problem* p, const fba_settings* s) {
         const double yd = p->cam_info[5 * k];
         if (yd != 1.0 && yd != -1.0) { set_error("y_dir should be +-1 only (main.m:334-337)"); return FBA_ERR_ARG; }
     }
-    std::vector<int32_t> img_cam(p->n_img, -1), tie_cam(p->n_tie, -1);
+    std::vector<int32_t> img_cam(p->n_img, -1);
     for (int64_t i = 0; i < p->n_pts; ++i) {
         const int e = p->img[i], k = p->cam[i], t = p->tie[i];
         if (e < 0 || e >= p->n_img) { set_error("image index out of range (EXT must list the images of .pho in order)"); return FBA_ERR_ARG; }
         if (k < 0 || k >= p->n_cam) { set_error("camera index out of range"); return FBA_ERR_ARG; }
         if (t < -1 || t >= p->n_tie) { set_error("tie index out of range"); return FBA_ERR_ARG; }
+        // an image's camera is its EXT row's (main.m:323): every observation of it goes through that camera
         if (img_cam[e] < 0) img_cam[e] = k;
         else if (img_cam[e] != k) { set_error("observations of one image with different cameras"); return FBA_ERR_ARG; }
-        if (t >= 0) {
-            if (tie_cam[t] < 0) tie_cam[t] = k;
-            else if (tie_cam[t] != k) {
-                set_error("tie point observed by more than one camera: not implemented in this build");
-                return FBA_ERR_UNSUPPORTED;
-            }
-        }
     }
     (void)s;
     return FBA_OK;
@@ -168,7 +163,8 @@ static void destroy(Ctx* c) {
     void* ptrs[] = {c->d_chunk_obs, c->d_chunk_pt, c->d_xy, c->d_img, c->d_cam, c->d_pt, c->d_ctl, c->d_lp_tie, c->d_lp_start, c->d_lp_cam,
                     c->d_acc, c->d_ppart, c->d_ipart, c->d_cpart, c->d_cseg, c->d_bscr, c->d_gblk, c->d_lrprof, c->d_ptrace, c->d_gpairs, c->d_red, c->d_xfull, c->d_xlin, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
                     c->d_pt_tab, c->d_P, c->d_flags, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
-                    c->d_active, c->d_counted, c->d_obs_pho, c->d_sched};
+                    c->d_active, c->d_counted, c->d_obs_pho, c->d_sched, c->d_gpt, c->d_gcu, c->d_gug, c->d_xpart,
+                    c->d_kpart};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
@@ -238,9 +234,22 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
             tie_obs[p->tie[i]].push_back(i);
             tie_cam[p->tie[i]] = p->cam[i];
         }
-    std::vector<int32_t> lps;
+    // regular tie points (k_lin_reduce's chunks): one camera, <= CHUNK_OBS observations, at most one per
+    // image; the others are "general" points (fba_general.hip) -- the reference accepts all of them
+    auto is_general = [&](int t) {
+        const std::vector<int64_t>& ob = tie_obs[t];
+        if ((int64_t)ob.size() > CHUNK_OBS) return true;
+        std::vector<int32_t> im;
+        for (int64_t i : ob) {
+            if (p->cam[i] != p->cam[ob[0]]) return true;
+            im.push_back(p->img[i]);
+        }
+        std::sort(im.begin(), im.end());
+        return std::adjacent_find(im.begin(), im.end()) != im.end();
+    };
+    std::vector<int32_t> lps, gps;
     for (int t = 0; t < L.n_tie; ++t)
-        if (c->tie_owner[t] == opt.rank && !tie_obs[t].empty()) lps.push_back(t);
+        if (c->tie_owner[t] == opt.rank && !tie_obs[t].empty()) (is_general(t) ? gps : lps).push_back(t);
     // within a camera, points in Morton (Z-curve) order of their initial coordinates: the points two
     // co-visible images share -- and so the W/T and Jacobian rows a pair or an image gathers -- sit
     // close together in memory
@@ -328,6 +337,23 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         pt.push_back(-1 - (int32_t)q);
         for (int m = 0; m < 3; ++m) ctl.push_back(p->xyz_fixed[3 * i + m]);
     }
+    // the general points' observations, after the control observations: each point's contiguous,
+    // sorted by image slot (then PHO row)
+    const int64_t o_gen0 = (int64_t)pho.size();
+    std::vector<int32_t> g_obs{(int32_t)o_gen0};
+    for (size_t q = 0; q < gps.size(); ++q) {
+        std::vector<int64_t> ob = tie_obs[gps[q]];
+        std::stable_sort(ob.begin(), ob.end(), [&](int64_t a, int64_t b) { return c->img_new[p->img[a]] < c->img_new[p->img[b]]; });
+        for (int64_t i : ob) {
+            pho.push_back(i);
+            xy.push_back(p->xy[2 * i]);
+            xy.push_back(p->xy[2 * i + 1]);
+            img.push_back(c->img_new[p->img[i]]);
+            cam.push_back(p->cam[i]);
+            pt.push_back((int32_t)(c->n_lp + (int64_t)q));
+        }
+        g_obs.push_back((int32_t)pho.size());
+    }
     c->n_obs = (int64_t)pho.size();
     if (c->n_obs >= (int64_t)1 << 31) { set_error("too many observations per rank"); destroy(c); return FBA_ERR_UNSUPPORTED; }
     c->n_obs_pad = round_up(std::max<int64_t>(c->n_obs, 1), 64);
@@ -339,11 +365,6 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     std::vector<int32_t> chunk_obs{0}, chunk_pt{0};
     int64_t cur_terms = 0;
     for (int64_t lp = 0; lp < c->n_lp; ++lp) {
-        if (lp_start[lp + 1] - lp_start[lp] > CHUNK_OBS) {
-            set_error("a tie point with more than 256 observations: not implemented in this build");
-            destroy(c);
-            return FBA_ERR_UNSUPPORTED;
-        }
         const int64_t n_lp_obs = lp_start[lp + 1] - lp_start[lp];
         const int64_t lp_terms = n_lp_obs * (n_lp_obs - 1) / 2;
         const bool split = lp > chunk_pt.back() &&
@@ -360,9 +381,17 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         chunk_obs.push_back(lp_start[c->n_lp]);
         chunk_pt.push_back((int32_t)c->n_lp);
     }
-    for (int64_t o = c->n_obs_tie; o < c->n_obs;) {
+    for (int64_t o = c->n_obs_tie; o < o_gen0;) {
         int64_t e = o + 1;
-        while (e < c->n_obs && e - o < CHUNK_OBS && cam[e] == cam[o]) ++e;
+        while (e < o_gen0 && e - o < CHUNK_OBS && cam[e] == cam[o]) ++e;
+        chunk_obs.push_back((int32_t)e);
+        chunk_pt.push_back((int32_t)c->n_lp);
+        o = e;
+    }
+    c->n_chunks_lr = (int64_t)chunk_obs.size() - 1;
+    // the general observations: linearised by k_lin_point only (empty point range), CHUNK_OBS at a time
+    for (int64_t o = o_gen0; o < c->n_obs;) {
+        const int64_t e = std::min<int64_t>(o + CHUNK_OBS, c->n_obs);
         chunk_obs.push_back((int32_t)e);
         chunk_pt.push_back((int32_t)c->n_lp);
         o = e;
@@ -376,7 +405,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     std::vector<int32_t> ck_cam, ck_pk{0}, pk_t{0}, pk_term, ck_ik{0}, ik_o{0}, ik_obs;
     std::vector<std::pair<int32_t, int32_t>> pk_key;
     std::vector<int32_t> ik_img;
-    for (int64_t ch = 0; ch < c->n_chunks; ++ch) {
+    for (int64_t ch = 0; ch < c->n_chunks_lr; ++ch) {
         const int o0 = chunk_obs[ch], o1 = chunk_obs[ch + 1];
         ck_cam.push_back(cam[o0]);
         std::vector<std::tuple<int32_t, int32_t, int32_t>> tk;  // (e1, e2, term), e1 > e2, point order
@@ -423,6 +452,85 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         if (!io.empty()) ik_o.push_back((int32_t)ik_obs.size());
         ck_ik.push_back((int32_t)ik_img.size());
     }
+    // general points: gimg / gpc groups and their keys, appended after the chunks' keys
+    GenPlan& G = c->gen;
+    G.n_gp = (int64_t)gps.size();
+    G.lp0 = c->n_lp;
+    G.pk0 = (int64_t)pk_key.size();
+    G.ik0 = (int64_t)ik_img.size();
+    G.ck0 = c->n_chunks_lr;
+    std::vector<int32_t> g_gi{0}, g_gc{0}, gi_obs, gi_img, gi_gp, gi_gc, gc_cam, gc_gp, gc_o{0}, gc_list, gpk, gx, gkk;
+    std::map<std::pair<int32_t, int32_t>, std::vector<int32_t>> xt, kt;  // target block -> slots, ascending
+    for (int64_t q = 0; q < G.n_gp; ++q) {
+        const int a = g_obs[q], b = g_obs[q + 1];
+        const int gi0 = (int)gi_img.size(), gc0 = (int)gc_cam.size();
+        for (int o = a; o < b; ++o)
+            if (o == a || img[o] != img[o - 1]) {
+                gi_obs.push_back(o);
+                gi_img.push_back(img[o]);
+                gi_gp.push_back((int32_t)q);
+            }
+        std::vector<int32_t> cams;
+        for (int o = a; o < b; ++o) cams.push_back(cam[o]);
+        std::sort(cams.begin(), cams.end());
+        cams.erase(std::unique(cams.begin(), cams.end()), cams.end());
+        for (int32_t k : cams) {
+            gc_cam.push_back(k);
+            gc_gp.push_back((int32_t)q);
+            for (int o = a; o < b; ++o)
+                if (cam[o] == k) gc_list.push_back(o);
+            gc_o.push_back((int32_t)gc_list.size());
+        }
+        const int gi1 = (int)gi_img.size(), gc1 = (int)gc_cam.size();
+        for (int i = gi0; i < gi1; ++i) {
+            const int32_t own = cam[gi_obs[i]];
+            for (int k = gc0; k < gc1; ++k) {
+                if (gc_cam[k] == own) gi_gc.push_back(k);
+                else {  // image i x another camera of the point
+                    xt[{gi_img[i], gc_cam[k]}].push_back((int32_t)(gx.size() / 2));
+                    gx.push_back(i);
+                    gx.push_back(k);
+                }
+            }
+            for (int j = gi0; j < i; ++j) {  // images ascending: gimg i is the higher image
+                gpk.push_back(i);
+                gpk.push_back(j);
+                pk_key.emplace_back(gi_img[i], gi_img[j]);
+            }
+            ik_img.push_back(gi_img[i]);
+        }
+        for (int k1 = gc0; k1 < gc1; ++k1) {
+            ck_cam.push_back(gc_cam[k1]);  // camera partial slot ck0 + gpc
+            for (int k2 = gc0; k2 < k1; ++k2) {  // cameras ascending: k1 the higher camera
+                kt[{gc_cam[k1], gc_cam[k2]}].push_back((int32_t)(gkk.size() / 2));
+                gkk.push_back(k1);
+                gkk.push_back(k2);
+            }
+        }
+        g_gi.push_back(gi1);
+        g_gc.push_back(gc1);
+    }
+    gi_obs.push_back(c->n_obs);
+    G.n_gi = (int64_t)gi_img.size();
+    G.n_gc = (int64_t)gc_cam.size();
+    G.n_gpk = (int64_t)gpk.size() / 2;
+    G.n_gx = (int64_t)gx.size() / 2;
+    G.n_gkk = (int64_t)gkk.size() / 2;
+    std::vector<int32_t> xt_start{0}, xt_list, xt_key, kt_start{0}, kt_list, kt_key;
+    for (auto& e : xt) {
+        xt_key.push_back(e.first.first);
+        xt_key.push_back(e.first.second);
+        xt_list.insert(xt_list.end(), e.second.begin(), e.second.end());
+        xt_start.push_back((int32_t)xt_list.size());
+    }
+    for (auto& e : kt) {
+        kt_key.push_back(e.first.first);
+        kt_key.push_back(e.first.second);
+        kt_list.insert(kt_list.end(), e.second.begin(), e.second.end());
+        kt_start.push_back((int32_t)kt_list.size());
+    }
+    G.n_xt = (int64_t)xt.size();
+    G.n_kt = (int64_t)kt.size();
     // the local co-visible pairs and, per pair, its partial slots
     std::vector<std::pair<int32_t, int32_t>> lpairs(pk_key);
     std::sort(lpairs.begin(), lpairs.end());
@@ -449,12 +557,13 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         for (size_t q = 0; q < ik_img.size(); ++q) ri_list[fill[ik_img[q]]++] = (int32_t)q;
         for (int64_t o = 0; o < c->n_obs; ++o) img_cam[img[o]] = cam[o];
     }
-    std::vector<int32_t> rc_start(L.n_cam + 1, 0), rc_list(c->n_chunks);
+    // camera partial slots: the chunks', then one per general point-camera group (ck_cam covers both)
+    std::vector<int32_t> rc_start(L.n_cam + 1, 0), rc_list(ck_cam.size());
     {
         for (int32_t k : ck_cam) rc_start[k + 1]++;
         for (int k = 0; k < L.n_cam; ++k) rc_start[k + 1] += rc_start[k];
         std::vector<int32_t> fill(rc_start.begin(), rc_start.end() - 1);
-        for (int64_t ch = 0; ch < c->n_chunks; ++ch) rc_list[fill[ck_cam[ch]]++] = (int32_t)ch;
+        for (size_t ch = 0; ch < ck_cam.size(); ++ch) rc_list[fill[ck_cam[ch]]++] = (int32_t)ch;
     }
     A.n_pk = (int64_t)pk_key.size();
     A.n_ik = (int64_t)ik_img.size();
@@ -479,6 +588,26 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     A.img_cam = put(img_cam);
     A.rc_start = put(rc_start);
     A.rc_list = put(rc_list);
+    G.g_obs = put(g_obs);
+    G.g_gi = put(g_gi);
+    G.g_gc = put(g_gc);
+    G.gi_obs = put(gi_obs);
+    G.gi_img = put(gi_img);
+    G.gi_gp = put(gi_gp);
+    G.gi_gc = put(gi_gc);
+    G.gc_cam = put(gc_cam);
+    G.gc_gp = put(gc_gp);
+    G.gc_o = put(gc_o);
+    G.gc_list = put(gc_list);
+    G.gpk = put(gpk);
+    G.gx = put(gx);
+    G.gkk = put(gkk);
+    G.xt_start = put(xt_start);
+    G.xt_list = put(xt_list);
+    G.xt_key = put(xt_key);
+    G.kt_start = put(kt_start);
+    G.kt_list = put(kt_list);
+    G.kt_key = put(kt_key);
     // the co-visible image pairs of ALL tie points (identical on every rank): the compact reduce
     // buffer of ranks > 1 and the block envelope of the reduced system
     std::vector<int32_t> gpairs;
@@ -526,6 +655,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
 
     // device allocations
     std::vector<int32_t> lp_tie(lps.begin(), lps.end());
+    lp_tie.insert(lp_tie.end(), gps.begin(), gps.end());
     std::vector<double> caminfo(p->cam_info, p->cam_info + 5 * (size_t)L.n_cam);
     if ((rc = upload(&c->d_xy, xy)) || (rc = upload(&c->d_img, img)) || (rc = upload(&c->d_cam, cam)) ||
         (rc = upload(&c->d_pt, pt)) || (rc = upload(&c->d_ctl, ctl)) || (rc = upload(&c->d_lp_tie, lp_tie)) ||
@@ -552,7 +682,10 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         (rc = dalloc(&c->d_pt_tab, (size_t)c->pt_comp * c->n_lp_pad)) ||
         (rc = dalloc(&c->d_ppart, (size_t)A.n_pk * 36)) ||
         (rc = dalloc(&c->d_ipart, (size_t)A.n_ik * (27 + 6 * L.cw))) ||
-        (rc = dalloc(&c->d_cpart, (size_t)c->n_chunks * npk)) ||
+        (rc = dalloc(&c->d_cpart, (size_t)(c->n_chunks_lr + G.n_gc) * npk)) ||
+        (rc = dalloc(&c->d_gpt, (size_t)G.n_gp * 18)) || (rc = dalloc(&c->d_gcu, (size_t)G.n_gc * 6 * L.cw)) ||
+        (rc = dalloc(&c->d_gug, (size_t)G.n_gi * 36)) || (rc = dalloc(&c->d_xpart, (size_t)G.n_gx * 6 * L.cw)) ||
+        (rc = dalloc(&c->d_kpart, (size_t)G.n_gkk * L.cw * L.cw)) ||
         (rc = dalloc(&c->d_cseg, (size_t)std::max(L.n_cam, 1) * 64 * npk)) ||
         (rc = dalloc(&c->d_bscr, (size_t)(32 * 14 + 16 * 120 + 16))) ||  // k_border_weights / k_border_gram segments, combine coefficients
         (rc = dalloc(&c->d_gblk, (size_t)(L.n_pad / NB) * 256)) ||
@@ -566,7 +699,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         return rc;
     }
     if ((rc = chol_setup(*c)) || (rc = acc_setup(*c))) { destroy(c); return rc; }
-    if (getenv("FBA_LR_PROFILE") && c->n_chunks > 0) FBA_HIP(hipMalloc((void**)&c->d_lrprof, sizeof(uint64_t) * 8 * c->n_chunks));
+    if (getenv("FBA_LR_PROFILE") && c->n_chunks_lr > 0) FBA_HIP(hipMalloc((void**)&c->d_lrprof, sizeof(uint64_t) * 8 * c->n_chunks_lr));
     if (getenv("FBA_PANEL_TRACE") && c->sched.n_waves > 0)
     {
         const size_t nt = std::max<size_t>((size_t)PTRACE_WG * c->sched.n_waves, (size_t)c->sched.flow_n * FTRACE / 8);
@@ -583,9 +716,9 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     for (auto& e : c->ev) FBA_HIP(hipEventCreate(&e));
     if (opt.verbose)
         fprintf(stderr, "[fba] rank %d/%d: n_obs %ld (tie %ld), points %ld, pairs %ld (%ld terms), u_c %ld, n_pad %ld; "
-                "chunks %ld, pair keys %ld, image keys %ld\n",
+                "chunks %ld, pair keys %ld, image keys %ld; general points %ld\n",
                 opt.rank, opt.world, (long)c->n_obs, (long)c->n_obs_tie, (long)c->n_lp, (long)c->n_pairs,
-                (long)c->n_pair_terms, (long)L.u_c, (long)L.n_pad, (long)c->n_chunks, (long)c->acc.n_pk, (long)c->acc.n_ik);
+                (long)c->n_pair_terms, (long)L.u_c, (long)L.n_pad, (long)c->n_chunks_lr, (long)c->acc.n_pk, (long)c->acc.n_ik, (long)G.n_gp);
     *out = c;
     return FBA_OK;
 }
@@ -650,19 +783,22 @@ static int accumulate_body(Ctx* c) {
     static const bool zero_head = getenv("FBA_ZERO_HEAD") && atoi(getenv("FBA_ZERO_HEAD"));
     if ((rc = zero_head ? launch_params_zero(*c, c->d_xlin) : launch_params(*c, nullptr, c->d_xlin))) return rc;
     mark(c, 1);
+    // general tie points: their Jacobian rows, point tables and partials (ahead of the reductions)
+    if ((rc = launch_gen_tables(*c, nullptr)) || (rc = launch_gen_keys(*c))) return rc;
     mark(c, 2);
-    if ((rc = launch_accumulate(*c, zero_head))) return rc;
+    if ((rc = launch_accumulate(*c, zero_head)) || (rc = launch_gen_reduce(*c))) return rc;
     if (c->d_lrprof) {  // FBA_LR_PROFILE: per-phase averages of k_lin_reduce (us)
-        std::vector<uint64_t> tp(8 * c->n_chunks);
+        std::vector<uint64_t> tp(8 * c->n_chunks_lr);
         FBA_HIP(hipMemcpyAsync(tp.data(), c->d_lrprof, sizeof(uint64_t) * tp.size(), hipMemcpyDeviceToHost, c->stream));
         FBA_HIP(hipStreamSynchronize(c->stream));
         double ph[6] = {0, 0, 0, 0, 0, 0};
         uint64_t lo = UINT64_MAX, hi = 0;
-        for (int64_t ch = 0; ch < c->n_chunks; ++ch) {
+        const double nch = (double)c->n_chunks_lr;
+        for (int64_t ch = 0; ch < c->n_chunks_lr; ++ch) {
             const uint64_t* q = &tp[8 * ch];
-            for (int i = 0; i < 4; ++i) ph[i] += (double)(q[i + 1] - q[i]) * 0.01 / (double)c->n_chunks;
-            ph[4] += (double)(q[6] - q[4]) * 0.01 / (double)c->n_chunks;  // image keys
-            ph[5] += (double)(q[5] - q[6]) * 0.01 / (double)c->n_chunks;  // pair keys
+            for (int i = 0; i < 4; ++i) ph[i] += (double)(q[i + 1] - q[i]) * 0.01 / nch;
+            ph[4] += (double)(q[6] - q[4]) * 0.01 / nch;  // image keys
+            ph[5] += (double)(q[5] - q[6]) * 0.01 / nch;  // pair keys
             lo = std::min(lo, q[0]);
             hi = std::max(hi, q[5]);
         }

@@ -292,7 +292,8 @@ int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, 
     const Sched& s = c.sched;
     int rc;
     // point tables of the last linearisation (V^-1, T, Tc), as fba_residuals does
-    if ((rc = launch_params(c, c.d_xlin)) || (rc = launch_linearize(c, c.d_xlin))) return rc;
+    if ((rc = launch_params(c, c.d_xlin)) || (rc = launch_linearize(c, c.d_xlin)) || (rc = launch_gen_tables(c, c.d_xlin)))
+        return rc;
 
     // the last level's diagonal-block inverses (the iteration's backward solve does without them)
     if ((rc = launch_trtri_last(c))) return rc;
@@ -423,6 +424,7 @@ int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, 
                                                                       c.pt_comp, c.d_lp_start, c.d_lp_tie, c.d_lp_cam,
                                                                       c.d_img, c.n_lp, L.n_img, L.cw, L.u_c, d_pdiag);
     FBA_HIP(hipGetLastError());
+    if (d_pdiag && (rc = launch_gen_cov(c, d_Z, d_Wz, nz, d_pdiag))) { cleanup(); return rc; }
     FBA_HIP(hipStreamSynchronize(c.stream));
     cleanup();
     c.have_factor = false;

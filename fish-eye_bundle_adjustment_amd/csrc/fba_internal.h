@@ -123,6 +123,35 @@ struct AccPlan {
     int64_t n_pk = 0, n_ik = 0;
 };
 
+// General tie points (fba_general.hip): the points the chunked fast path does not take -- seen by
+// several cameras, by more than CHUNK_OBS images, or measured more than once in one image.  The
+// reference accepts all of them (it loops over every PHO row, BuildAwG.m:46; camera columns by the
+// point's own cam_num, :448-451; tie columns camera-independent, :501-502).  Each general point q
+// owns a contiguous range of the local observations, sorted by image; "gimg" = the observations of
+// one point in one image (their eliminated image coupling Ug = sum U_o), "gpc" = the observations of
+// one point through one camera (its camera coupling Uc).  Offsets into Ctx::d_acc.
+struct GenPlan {
+    int64_t n_gp = 0, n_gi = 0, n_gc = 0, n_gpk = 0, n_gx = 0, n_gkk = 0, n_xt = 0, n_kt = 0;
+    int64_t lp0 = 0;      // local point index of general point 0
+    int64_t g_obs = 0;    // [n_gp+1] observation range of each point
+    int64_t g_gi = 0;     // [n_gp+1] its gimg range
+    int64_t g_gc = 0;     // [n_gp+1] its gpc range
+    int64_t gi_obs = 0;   // [n_gi+1] observation range of each gimg
+    int64_t gi_img = 0;   // [n_gi] image slot
+    int64_t gi_gp = 0;    // [n_gi] point
+    int64_t gi_gc = 0;    // [n_gi] the gpc of the image's own camera
+    int64_t gc_cam = 0;   // [n_gc] camera
+    int64_t gc_gp = 0;    // [n_gc] point
+    int64_t gc_o = 0;     // [n_gc+1] range in gc_list
+    int64_t gc_list = 0;  // observations of each gpc (ascending)
+    int64_t gpk = 0;      // [2 n_gpk] pair keys (gimg of the higher image, gimg of the lower image)
+    int64_t gx = 0;       // [2 n_gx] foreign-camera keys (gimg, gpc of another camera)
+    int64_t gkk = 0;      // [2 n_gkk] camera-pair keys (gpc of the higher camera, gpc of the lower camera)
+    int64_t xt_start = 0, xt_list = 0, xt_key = 0;  // image x foreign camera blocks: [n_xt+1], slots, [2 n_xt] (e, k)
+    int64_t kt_start = 0, kt_list = 0, kt_key = 0;  // camera x camera blocks: [n_kt+1], slots, [2 n_kt] (k1 > k2)
+    int64_t pk0 = 0, ik0 = 0, ck0 = 0;  // first partial slot of the general keys in ppart / ipart / cpart
+};
+
 struct Ctx {
     fba_problem prob{};   // shallow copy (pointers valid only during fba_create)
     fba_settings set{};
@@ -159,7 +188,16 @@ struct Ctx {
     int32_t* d_lp_tie = nullptr; // [n_lp] global tie index of local point
     int32_t* d_lp_start = nullptr;   // [n_lp+1] obs range of each local point
     int32_t* d_lp_cam = nullptr;     // [n_lp] camera of each local point
-    int64_t n_chunks = 0;            // k_lin_reduce workgroups: whole tie points of one camera
+    int64_t n_chunks = 0;            // chunks: [k_lin_reduce's: whole regular tie points of one camera,
+                                     // then control observations][the general points' observations,
+                                     // linearised by k_lin_point only]
+    int64_t n_chunks_lr = 0;         // k_lin_reduce workgroups (regular + control chunks)
+    GenPlan gen;                     // general tie points (fba_general.hip)
+    double* d_gpt = nullptr;         // [n_gp][18] Vinv 6 | R 6 | rb 3 | vb 3
+    double* d_gcu = nullptr;         // [n_gc][6 cw] Uc 3cw | Tc 3cw
+    double* d_gug = nullptr;         // [n_gi][36] Ug 18 | sum of T_o 18
+    double* d_xpart = nullptr;       // [n_gx][6 cw] foreign-camera partials
+    double* d_kpart = nullptr;       // [n_gkk][cw cw] camera-pair partials
     AccPlan acc;                     // accumulation plan (offsets into d_acc)
     int32_t* d_acc = nullptr;
     double* d_ppart = nullptr;       // [acc.n_pk][36] pair-block partials
@@ -267,6 +305,15 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
 int launch_params(Ctx& c, const double* x = nullptr, double* copy_to = nullptr);  // x: parameters (default d_xfull),
                                                                                    // also copied to copy_to
 int launch_linearize(Ctx& c, const double* x = nullptr);  // Jacobian rows to d_J (residuals, dense AwG)
+int launch_linearize_range(Ctx& c, const double* x, int64_t c0, int64_t c1);  // chunks [c0, c1) only
+// general tie points (fba_general.hip): Jacobian rows of their observations + point tables
+// (gen_tables), their partials (gen_keys), the blocks only they touch (gen_reduce, after
+// launch_accumulate), back-substitution (gen_backsub), tie variances (gen_cov, fba_cov.hip)
+int launch_gen_tables(Ctx& c, const double* x);
+int launch_gen_keys(Ctx& c);
+int launch_gen_reduce(Ctx& c);
+int launch_gen_backsub(Ctx& c);
+int launch_gen_cov(Ctx& c, const double* Z, const double* Wz, int nz, double* pdiag);
 int launch_params_zero(Ctx& c, double* copy_to);  // k_params (+ copy of the linearisation point) and the
                                                    // zeroing of the factor's pattern blocks, one launch
 int launch_accumulate(Ctx& c, bool zeroed = false);  // zero S (unless zeroed), image, pair, camera blocks

@@ -286,14 +286,14 @@ __global__ __launch_bounds__(256) void k_lin_point(
     const double* __restrict__ xfull, const double* __restrict__ img_tab, const double* __restrict__ cam_tab,
     const int32_t* __restrict__ chunk_obs, const int32_t* __restrict__ chunk_pt, const int32_t* __restrict__ lp_start,
     double* __restrict__ J, double* __restrict__ WT, double* __restrict__ PT, int64_t u_c, int type, int cam_stride,
-    unsigned eop_mask, unsigned cam_mask, double px, double py) {
+    unsigned eop_mask, unsigned cam_mask, double px, double py, int c_off) {
     using LY = Lay<NK>;
     constexpr int CW = LY::CW, NJ = LY::NJ, JS = LY::JS, PS = LY::PS;
     constexpr int SH = 8 + 2 * CW;  // Jp (2x3), w (2), Jc (2xCW)
     __shared__ double sh[256][SH + 1];
     __shared__ double vinv[256][6];
     const int t = threadIdx.x;
-    const int c = blockIdx.x;
+    const int c = blockIdx.x + c_off;
     const int o0 = chunk_obs[c], o1 = chunk_obs[c + 1];
     const int p0 = chunk_pt[c], p1 = chunk_pt[c + 1];
     const int o = o0 + t;
@@ -1377,15 +1377,17 @@ int launch_params(Ctx& c, const double* x, double* copy_to) {
     return FBA_OK;
 }
 
-// linearisation fused with the tie-point reduction (the dense debug path uses the same kernel)
-int launch_linearize(Ctx& c, const double* x) {
-    if (c.n_chunks == 0) return FBA_OK;
+// Jacobian rows of every observation (+ the regular points' tables): residuals, dense AwG, covariance
+int launch_linearize(Ctx& c, const double* x) { return launch_linearize_range(c, x, 0, c.n_chunks); }
+
+int launch_linearize_range(Ctx& c, const double* x, int64_t c0, int64_t c1) {
+    if (c1 <= c0) return FBA_OK;
     const unsigned em = eop_mask(c.set), cm = cam_mask(c.set, c.L.nk);
 #define LIN(NKV)                                                                                               \
-    k_lin_point<NKV><<<(unsigned)c.n_chunks, 256, 0, c.stream>>>(                                              \
+    k_lin_point<NKV><<<(unsigned)(c1 - c0), 256, 0, c.stream>>>(                                               \
         c.d_xy, c.d_img, c.d_cam, c.d_pt, c.d_lp_tie, c.d_ctl, x ? x : c.d_xfull, c.d_img_tab, c.d_cam_tab,     \
         c.d_chunk_obs, c.d_chunk_pt, c.d_lp_start, c.d_J, c.d_WT, c.d_pt_tab, c.L.u_c, c.set.type,              \
-        c.cam_tab_stride, em, cm, px_of(c), py_of(c))
+        c.cam_tab_stride, em, cm, px_of(c), py_of(c), (int)c0)
     FBA_NK_DISPATCH(c.L.nk, LIN);
 #undef LIN
     FBA_HIP(hipGetLastError());
@@ -1407,18 +1409,20 @@ __global__ __launch_bounds__(256) void k_zero_blocks(double* __restrict__ S, int
 int launch_accumulate(Ctx& c, bool zeroed) {
     const Layout& L = c.L;
     // the pattern is zeroed by tail workgroups of k_lin_reduce (it does not touch S), unless done already
-    const int ztail = (zeroed || c.n_chunks == 0) ? 0 : c.sched.nzero;
-    if (c.sched.nzero > 0 && !zeroed && c.n_chunks == 0)
+    const int64_t nlr = c.n_chunks_lr;
+    const int ztail = (zeroed || nlr == 0) ? 0 : c.sched.nzero;
+    if (c.sched.nzero > 0 && !zeroed && nlr == 0)
         k_zero_blocks<<<(unsigned)(8 * c.sched.nzero), 256, 0, c.stream>>>(c.d_S, L.ld, c.d_sched + c.sched.zero);
-    if (c.n_chunks == 0) return FBA_OK;
+    if (nlr == 0 && c.gen.n_gp == 0) return FBA_OK;
     const unsigned em = eop_mask(c.set), cm = cam_mask(c.set, c.L.nk);
     const double px = px_of(c), py = py_of(c);
 #define ACC(NKV)                                                                                                  \
-    k_lin_reduce<NKV><<<(unsigned)(c.n_chunks + ztail), LR_THREADS, LR<NKV>::LDS, c.stream>>>(                    \
+    if (nlr > 0)                                                                                                  \
+    k_lin_reduce<NKV><<<(unsigned)(nlr + ztail), LR_THREADS, LR<NKV>::LDS, c.stream>>>(                           \
         c.d_xy, c.d_img, c.d_cam, c.d_pt, c.d_lp_tie, c.d_ctl, c.d_xfull, c.d_img_tab, c.d_cam_tab,                \
         c.d_chunk_obs, c.d_chunk_pt, c.d_lp_start, c.d_acc, c.acc, c.d_WT, c.d_pt_tab, c.d_ppart, c.d_ipart,       \
         c.d_cpart, c.L.u_c, c.set.type, c.cam_tab_stride, em, cm, px, py, c.d_lrprof,                              \
-        c.d_lrprof && getenv("FBA_LR_SKIP") ? atoi(getenv("FBA_LR_SKIP")) : 0, (int)c.n_chunks, c.d_S, L.ld,       \
+        c.d_lrprof && getenv("FBA_LR_SKIP") ? atoi(getenv("FBA_LR_SKIP")) : 0, (int)nlr, c.d_S, L.ld,              \
         c.d_sched + c.sched.zero);                                                                                \
     {                                                                                                             \
         const int npb = (int)((c.n_pairs + 3) / 4), nib = (L.n_img + 1) / 2, ncb = (L.n_cam * CAM_SEG + 1) / 2;   \
@@ -1456,9 +1460,11 @@ int launch_border(Ctx& c) {
 
 int launch_backsub_update(Ctx& c) {
     const Layout& L = c.L;
+    int rc;
+    if ((rc = launch_gen_backsub(c))) return rc;
     if (c.n_lp > 0) {
 #define BS(NKV)                                                                                                    \
-    k_backsub<NKV><<<(unsigned)c.n_chunks, 256, 0, c.stream>>>(c.d_WT, c.d_pt_tab, c.d_chunk_obs, c.d_chunk_pt,       \
+    k_backsub<NKV><<<(unsigned)c.n_chunks_lr, 256, 0, c.stream>>>(c.d_WT, c.d_pt_tab, c.d_chunk_obs, c.d_chunk_pt,    \
                                                               c.d_lp_start, c.d_lp_tie, c.d_lp_cam, c.d_img, c.d_delta, \
                                                               L.u_c, L.n_img)
         FBA_NK_DISPATCH(L.nk, BS);

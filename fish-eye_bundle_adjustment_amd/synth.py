@@ -78,13 +78,18 @@ def camera_params(k):
 
 
 def generate(n_img, n_tie, seed, obs_per_point=10, noise=0.3, typ="fisheye", spacing=1000.0,
-             max_theta_deg=80.0, n_cam=1, n_control=0):
+             max_theta_deg=80.0, n_cam=1, n_control=0, cam_layout="alternate", n_wide=0, wide_min_obs=0,
+             n_dup=0):
     """Returns a dict of arrays describing the scene (truth and initial values).
 
-    n_cam > 1: image i uses camera i % n_cam (camera_params(k)); n_control > 0: the first
-    n_control points are control points (exact CNT coordinates, not in the .tie list)."""
+    n_cam > 1: image i uses camera i % n_cam ("alternate": every tie point is seen through several
+    cameras -- a rig sharing its targets) or camera i * n_cam // n_img ("blocks": only the points
+    near a block boundary are); n_control > 0: the first n_control points are control points (exact
+    CNT coordinates, not in the .tie list); n_wide > 0: that many extra tie points near the block
+    centre observed by EVERY image that sees them (at least wide_min_obs); n_dup > 0: that many image
+    points measured a second time (same point, same image, fresh noise)."""
     rng = np.random.default_rng(seed)
-    cam_of = np.arange(n_img) % n_cam
+    cam_of = np.arange(n_img) % n_cam if cam_layout == "alternate" else np.arange(n_img) * n_cam // n_img
     cxp, cyp, cc = (np.array(v) for v in zip(*[camera_params(k) for k in range(n_cam)]))
     obs_per_point = min(obs_per_point, n_img)
     g = int(math.ceil(math.sqrt(n_img)))
@@ -139,7 +144,35 @@ def generate(n_img, n_tie, seed, obs_per_point=10, noise=0.3, typ="fisheye", spa
     X_true = np.concatenate(pts)
     img = np.concatenate(obs_img).reshape(-1).astype(np.int64)
     pid = np.repeat(np.arange(n_tie), obs_per_point)
-    xy = np.concatenate(obs_xy).reshape(-1, 2) + rng.normal(0, noise, (len(img), 2))
+    xy0 = np.concatenate(obs_xy).reshape(-1, 2)
+    # wide points: near the block centre, observed by every image with the point in its valid field
+    wide = []
+    while len(wide) < n_wide:
+        Xw = np.array([0.5 * (lo + hi) + rng.normal(0, spacing), 0.5 * (lo + hi_y) + rng.normal(0, spacing),
+                       rng.uniform(0.0, 1500.0)])
+        d = Xw[None, :] - C_true
+        UVW = np.einsum("kij,kj->ki", Mall, d)
+        U, V, W = UVW[:, 0], UVW[:, 1], UVW[:, 2]
+        dist = np.sqrt((d * d).sum(-1))
+        with np.errstate(invalid="ignore", divide="ignore"):
+            x, y = _project(typ, U, V, W, cc[cam_of], cxp[cam_of], cyp[cam_of], K0, P0)
+        ok = (W < 0) & (-W >= cos_max * dist)
+        ok &= (x > SENSOR[0] + 1) & (x < SENSOR[2] - 1) & (y > SENSOR[1] + 1) & (y < SENSOR[3] - 1)
+        if ok.sum() >= max(wide_min_obs, 2):
+            wide.append((Xw, np.nonzero(ok)[0], np.stack([x[ok], y[ok]], -1)))
+    for j, (Xw, ids, wxy) in enumerate(wide):
+        X_true = np.concatenate([X_true, Xw[None]])
+        img = np.concatenate([img, ids])
+        pid = np.concatenate([pid, np.full(len(ids), n_tie + j)])
+        xy0 = np.concatenate([xy0, wxy])
+    n_tie += len(wide)
+    # repeated measurements: the same point in the same image once more
+    if n_dup:
+        dup = rng.choice(len(img), size=n_dup, replace=False)
+        img = np.concatenate([img, img[dup]])
+        pid = np.concatenate([pid, pid[dup]])
+        xy0 = np.concatenate([xy0, xy0[dup]])
+    xy = xy0 + rng.normal(0, noise, (len(img), 2))
     # initial values
     C0v = C_true + rng.normal(0, 10.0, C_true.shape)
     ang0 = ang_true + rng.normal(0, math.radians(0.1), ang_true.shape)

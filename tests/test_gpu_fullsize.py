@@ -140,23 +140,34 @@ def test_config4_adjust_matches_oracle(fba, fbo, oracle, scenes):
     assert np.max(np.abs(res.v - v_ref)) <= 1e-7 * np.max(np.abs(v_ref))
 
 
+DISTORTION = ("k1", "k2", "k3", "k4", "k5", "p1", "p2")
+
+
 def test_config5_first_iterations_match_oracle(fba, fbo, oracle, scenes):
     """config 5 (4,000 images x 200,000 tie points, u_c = 24,010): the first two Gauss-Newton passes
-    against the C oracle with the regularised-border Cholesky of the dense reduced system (4.6 GB)
-    -- deltasum and xhat after each pass <= 1e-9 relative per parameter group."""
+    against the C oracle solving the dense bordered system [S G; G' 0] (4.6 GB) directly.
+
+    deltasum <= 1e-9 relative after each pass; xhat <= 1e-9 per parameter group after each pass,
+    except the distortion groups after the FIRST pass (the linearisation at the start values): there
+    the pass is sensitive to the association of the reduced system's sums at the 1e-7 level -- the C
+    oracle itself moves k1 by 1.2e-7 / 2.1e-7 (k2..p2 ~1e-8) when only its OpenMP thread count
+    changes (scripts/order_spread.py, profiles/r03_order_spread_c5.log) -- so that pass is held to
+    5e-8 (measured: 1.06e-8 for k1, profiles/r03_c5_solver_spread.log).  The second pass damps the
+    first's rounding (Gauss-Newton contraction): 1e-9 for every group (measured: 7e-11)."""
     folder = _scene(5, scenes)
     ds = fba.load_folder(folder)
     od = oracle.load_folder(folder)
-    ref = fbo.CpuAdjustment(od, solver="chol")
+    ref = fbo.CpuAdjustment(od, solver="kkt")
     ctx = _ctx(fba, ds)
     dsc = dist_scaling_of(od)
     try:
-        for _ in range(2):
+        for it in range(2):
             d_ref = ref.step()
             d = ctx.step()
             assert abs(d - d_ref) <= 1e-9 * ref.deltasum[0], (d, d_ref)
             err = group_rel_err(ctx.get_xhat(), ref.xhat, ref.names, dsc)
-            assert max(err.values()) <= 1e-9, err
+            for g, e in err.items():
+                assert e <= (5e-8 if it == 0 and g in DISTORTION else 1e-9), (it, g, e)
     finally:
         ctx.close()
         ref.close()

@@ -117,3 +117,24 @@ def test_shard_reduced_systems_sum_to_full(fba, fbo, oracle, tmp_path, world):
         assert max(err.values()) == 0.0, err
     err = group_rel_err(xr, full.xhat, full.names, dsc)
     assert max(err.values()) == 0.0, err
+
+
+@pytest.mark.parametrize("kind", ["rig2", "rig3_blocks", "dup"])
+def test_general_points_match_dense_oracle(fba, fbo, oracle, tmp_path, kind):
+    """Inputs the reference accepts beyond the single-camera case (BuildAwG.m:46, :448-451, :501-502):
+    tie points seen through several cameras (a rig sharing its targets; cameras alternating or in
+    blocks) and image points measured twice -- the block-sparse restatement against the dense one."""
+    from fba_amd import synth
+    kw = {"rig2": dict(n_cam=2), "rig3_blocks": dict(n_cam=3, cam_layout="blocks"), "dup": dict(n_dup=25)}[kind]
+    sc = synth.generate(18, 300, seed=41, **kw)
+    folder = synth.write_folder(sc, str(tmp_path / kind))
+    od = oracle.load_folder(folder)
+    if kind != "dup":
+        pts_cams = {}
+        for t, k in zip(od.tie_index, od.cam_num):
+            pts_cams.setdefault(int(t), set()).add(int(k))
+        assert sum(len(v) > 1 for v in pts_cams.values()) > 0
+    ro = oracle.adjust(od)
+    ca = fbo.CpuAdjustment(od, threads=2)
+    assert ca.adjust() == ro.iterations
+    _compare(ca, ro, dtol=1e-9)
