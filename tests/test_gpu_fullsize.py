@@ -7,7 +7,7 @@
 * config 4 (1,000 x 50,000, the bench workload): the whole adjustment against the same oracle --
   iteration count, deltasum history, xhat, sigma0^2, RMS and v.
 * config 5 (4,000 x 200,000, 2M image points): the first two Gauss-Newton passes against the C
-  oracle's dense regularised-border Cholesky; then size-independent properties of the converged
+  oracle's direct solve of the dense bordered system; then size-independent properties of the converged
   run -- bit-identical repeat runs, monotone convergence below Threshold_Value within
   Iteration_Cap, and sigma0^2 = 1 +- 5% (the generator's noise equals Meas_std, so the a posteriori
   variance factor of a correct adjustment is ~1).
