@@ -59,34 +59,10 @@ def BuildAwG(data: Dataset, xhat):
 
 
 def BuildRSD(v, data: Dataset, xhat):
-    """BuildRSD.m:1-43: rows [targetID, imageID, x, y, r, vx, vy, vr, vt].
-
-    Radial/tangential split of given residuals with xp, yp taken from xhat when estimated.  (Inside
-    the GPU loop the same rows are produced by the device residual kernel; this host form serves
-    callers that hold a v of their own.)"""
-    s = data.settings
-    u_img = sum(int(s[k]) for k in ("Estimate_Xc", "Estimate_Yc", "Estimate_Zc", "Estimate_w", "Estimate_p",
-                                      "Estimate_k"))
-    u_cam = int(s["Estimate_c"]) + int(s["Estimate_xp"]) + int(s["Estimate_yp"]) + \
-        int(s["Estimate_radial"]) * int(s["Num_Radial_Distortions"]) + int(s["Estimate_decent"]) * 2
-    v = np.asarray(v, dtype=np.float64)
-    base = u_img * data.numImg + data.cam * u_cam
-    cnt = 0
-    iop = np.array([c[6][:2] for c in data.INT[: data.numCam]])
-    if s["Estimate_xp"]:
-        xp = np.asarray(xhat)[base]
-        cnt = 1
-    else:
-        xp = iop[data.cam, 0]
-    yp = np.asarray(xhat)[base + cnt] if s["Estimate_yp"] else iop[data.cam, 1]
-    vx, vy = v[0::2], v[1::2]
-    xb = data.xy[:, 0] - xp
-    yb = data.xy[:, 1] - yp
-    theta = np.arctan2(yb, xb)
-    phi = np.arctan2(vy, vx)
-    vd = np.sqrt(vx ** 2 + vy ** 2)
-    num = np.stack([np.sqrt(xb ** 2 + yb ** 2), vx, vy, vd * np.cos(theta - phi), vd * np.sin(theta - phi)], 1)
-    return [[data.pho_target[i], data.pho_image[i], data.xy[i, 0], data.xy[i, 1], *num[i]] for i in range(len(num))]
+    """BuildRSD.m:1-43: rows [targetID, imageID, x, y, r, vx, vy, vr, vt] -- the radial / tangential
+    split of a given v, with xp, yp from xhat where estimated (fba_build_rsd on the device)."""
+    rsd = _ctx(data).build_rsd(v, xhat)
+    return [[data.pho_target[i], data.pho_image[i], data.xy[i, 0], data.xy[i, 1], *rsd[i]] for i in range(len(rsd))]
 
 
 @dataclass

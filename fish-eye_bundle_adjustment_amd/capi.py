@@ -23,7 +23,7 @@ EXPORTS = (
     "fba_destroy", "fba_buildxhat", "fba_set_xhat", "fba_get_xhat", "fba_build_awg",
     "fba_accumulate", "fba_reduce_buffer", "fba_synchronize", "fba_solve_update", "fba_solve_update_async",
     "fba_deltasum_device", "fba_solve_finish", "fba_step", "fba_adjust",
-    "fba_residuals", "fba_finish_stats", "fba_covariance", "fba_last_timings", "fba_set_timing", "fba_set_probe",
+    "fba_residuals", "fba_build_rsd", "fba_finish_stats", "fba_covariance", "fba_last_timings", "fba_set_timing", "fba_set_probe",
     "fba_probe_stats", "fba_test_border_solve",
 )
 
@@ -78,6 +78,7 @@ def _load():
         "fba_deltasum_device": ([P, P], C.c_int),
         "fba_solve_finish": ([P, P], C.c_int),
         "fba_step": ([P, P], C.c_int),
+        "fba_build_rsd": ([P, P, P, P], C.c_int),
         "fba_adjust": ([P, P, P], C.c_int),
         "fba_residuals": ([P, P, P, P], C.c_int),
         "fba_finish_stats": ([P, P, P, D, P], C.c_int),
@@ -249,6 +250,17 @@ class Context:
         st = np.zeros(6)
         check(lib.fba_residuals(self.h, ptr(v), ptr(rsd), ptr(st)))
         return v, rsd, st
+
+    def build_rsd(self, v, xhat):
+        """fba_build_rsd: BuildRSD.m rows [r, vx, vy, vr, vt] for a given v (PHO order) and xhat."""
+        n = self.packed.n_pts
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        x = np.ascontiguousarray(xhat, dtype=np.float64)
+        if v.size != 2 * n or x.size != int(self.u):
+            raise ValueError("BuildRSD: v must have 2*n_pts entries and xhat u entries")
+        rsd = np.zeros((n, 5))
+        check(lib.fba_build_rsd(self.h, ptr(v), ptr(x), ptr(rsd)))
+        return rsd
 
     def covariance(self, sigma02, corr=True):
         """fba_covariance: diag of the reference's final Cx (main.m:428-482, :602) in xhat order, and

@@ -1255,6 +1255,32 @@ int fba_residuals(fba_ctx* ctx, double* v, double* rsd, double* stats) {
     return FBA_OK;
 }
 
+int fba_build_rsd(fba_ctx* ctx, const double* v, const double* xhat, double* rsd) {
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    if (!c || !v || !xhat || !rsd) { set_error("NULL argument"); return FBA_ERR_ARG; }
+    const Layout& L = c->L;
+    // xp, yp per camera: from xhat when estimated, else the INT values (BuildRSD.m:12-26)
+    std::vector<double> xpyp(2 * (size_t)std::max(L.n_cam, 1));
+    for (int k = 0; k < L.n_cam; ++k)
+        for (int a = 0; a < 2; ++a) {
+            const int64_t f = 6 * (int64_t)L.n_img + (int64_t)k * L.cw + a;
+            xpyp[2 * k + a] = c->full_to_ref[f] >= 0 ? xhat[c->full_to_ref[f]] : c->xfull0[f];
+        }
+    const int64_t n = c->n_pts;
+    double *dv = nullptr, *dx = nullptr, *dr = nullptr;
+    int rc;
+    auto release = [&]() { for (void* q : {(void*)dv, (void*)dx, (void*)dr}) if (q) (void)hipFree(q); };
+    if ((rc = dalloc(&dv, 2 * (size_t)n)) || (rc = upload(&dx, xpyp)) || (rc = dalloc(&dr, 5 * (size_t)n))) { release(); return rc; }
+    hipError_t e = hipMemcpyAsync(dv, v, sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(dr, 0, sizeof(double) * 5 * n, c->stream);
+    if (e == hipSuccess && (rc = launch_build_rsd(*c, dv, dx, dr))) { release(); return rc; }
+    if (e == hipSuccess) e = hipMemcpyAsync(rsd, dr, sizeof(double) * 5 * n, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    release();
+    if (e != hipSuccess) { set_error(std::string("HIP error in fba_build_rsd: ") + hipGetErrorString(e)); return FBA_ERR_HIP; }
+    return FBA_OK;
+}
+
 int fba_covariance(fba_ctx* ctx, double sigma02, double* cx_diag, double* corr) {
     Ctx* c = reinterpret_cast<Ctx*>(ctx);
     if (!c) { set_error("NULL context"); return FBA_ERR_ARG; }

@@ -325,6 +325,7 @@ int launch_cholesky(Ctx& c);     // factor + forward solve of RHS rows
 int launch_backward(Ctx& c);     // border combine + backward solve -> delta_c
 int launch_backsub_update(Ctx& c);
 int launch_residuals(Ctx& c);    // v per obs, partial sums
+int launch_build_rsd(Ctx& c, const double* d_v, const double* d_xpyp, double* d_rsd);  // BuildRSD for a given v
 int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, const int32_t* d_islot,
                       const int32_t* d_icam, int n_iblk);  // post-fit covariance (fba_cov.hip)
 int launch_dense_awg(Ctx& c, double* dA, double* dG, const int64_t* d_map, int64_t n_rows, int64_t u_ref);

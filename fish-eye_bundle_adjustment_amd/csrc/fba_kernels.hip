@@ -1288,6 +1288,35 @@ __global__ __launch_bounds__(256) void k_residuals(const double* __restrict__ J,
         for (int m = 0; m < 3; ++m) part[3 * blockIdx.x + m] = red[m][0];
 }
 
+// BuildRSD.m:29-40 for a given v (PHO order): one thread per local observation, xp / yp of its camera
+// from `xpyp` (BuildRSD.m:12-26 gathered on the host), rows written at the observation's PHO row
+__global__ __launch_bounds__(256) void k_build_rsd(const double* __restrict__ xy, const int32_t* __restrict__ cam,
+                                                   const int64_t* __restrict__ obs_pho, const double* __restrict__ v,
+                                                   const double* __restrict__ xpyp, double* __restrict__ rsd,
+                                                   int64_t n_obs) {
+    const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= n_obs) return;
+    const int64_t i = obs_pho[o];
+    const double vx = v[2 * i], vy = v[2 * i + 1];
+    const double xb = xy[2 * o] - xpyp[2 * cam[o]], yb = xy[2 * o + 1] - xpyp[2 * cam[o] + 1];
+    const double theta = atan2(yb, xb), phi = atan2(vy, vx);
+    const double vd = sqrt(vx * vx + vy * vy);
+    double* r = rsd + 5 * i;
+    r[0] = sqrt(xb * xb + yb * yb);
+    r[1] = vx;
+    r[2] = vy;
+    r[3] = vd * cos(theta - phi);
+    r[4] = vd * sin(theta - phi);
+}
+
+int launch_build_rsd(Ctx& c, const double* d_v, const double* d_xpyp, double* d_rsd) {
+    if (c.n_obs == 0) return FBA_OK;
+    k_build_rsd<<<(unsigned)((c.n_obs + 255) / 256), 256, 0, c.stream>>>(c.d_xy, c.d_cam, c.d_obs_pho, d_v, d_xpyp, d_rsd,
+                                                                      c.n_obs);
+    FBA_HIP(hipGetLastError());
+    return FBA_OK;
+}
+
 // ------------------------------------------------------------------------------------------------
 // dense debug A (BuildAwG's A, column-major n x u_ref, PHO row order)
 // ------------------------------------------------------------------------------------------------

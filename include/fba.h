@@ -14,6 +14,7 @@
  *                               multi-GPU caller all-reduces the normal equations
  *   fba_step          = fba_accumulate + fba_solve_update (single GPU)
  *   fba_adjust        replaces  the whole loop main.m:407-494 (while deltasum > threshold, cap)
+ *   fba_build_rsd     replaces  RSD = BuildRSD(v, data, xhat) (functions/BuildRSD.m:1) for a given v
  *   fba_residuals     replaces  v = A*delta + w (main.m:569), RSD = BuildRSD(v, data, xhat)
  *                               (functions/BuildRSD.m:1, main.m:571), RMSx/RMSy/RMS (main.m:594-598),
  *                               sigma02 = v'Pv/(n-u) (main.m:601)
@@ -171,6 +172,12 @@ int fba_adjust(fba_ctx* ctx, int32_t* iterations, double* deltasum_hist);
  * fills only its observations (others 0) and stats hold this rank's partial sums
  * (sum vx^2, sum vy^2, 0, 0, vTPv, n-u); fba_finish_stats turns reduced sums into RMS / sigma02. */
 int fba_residuals(fba_ctx* ctx, double* v, double* rsd, double* stats);
+
+/* BuildRSD.m:1 for a caller-given v (e.g. the reference's v = A*delta + w, main.m:569-571): per PHO
+ * row [r, vx, vy, vr, vt] (BuildRSD.m:29-40) with xp, yp from xhat where estimated, else the INT
+ * values (BuildRSD.m:12-26).  v [2*n_pts] x y interleaved (PHO order), xhat [u] the reference layout,
+ * rsd [5*n_pts] row-major.  With world > 1 only this rank's rows are written (others 0). */
+int fba_build_rsd(fba_ctx* ctx, const double* v, const double* xhat, double* rsd);
 int fba_finish_stats(const fba_problem* p, const fba_settings* s, const double* sums /*[2]: sum vx^2, sum vy^2*/,
                      double vtpv, double* stats /*[6]*/);
 

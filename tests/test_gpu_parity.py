@@ -340,3 +340,16 @@ def test_border_solve_nan_column_stays_local(fba):
     coef = np.zeros(14)
     fba.capi.check(fba.capi.lib.fba_test_border_solve(0, fba.capi.ptr(np.ascontiguousarray(g)), fba.capi.ptr(coef)))
     assert not np.isfinite(coef).all()
+
+
+def test_buildrsd_matches_oracle(fba, oracle, cam0_folders):
+    """fba.BuildRSD(v, data, xhat) (BuildRSD.m:1, fba_build_rsd on the device) for a given v."""
+    for variant in ("stage3_pinhole", "stage1_pinhole"):
+        ds = fba.load_folder(cam0_folders[variant])
+        od = oracle.load_folder(cam0_folders[variant])
+        ro = oracle.adjust(od)
+        rows = fba.BuildRSD(ro.v, ds, ro.xhat)
+        assert [r[0] for r in rows] == od.target and [r[1] for r in rows] == od.image
+        num = np.array([r[4:] for r in rows], dtype=np.float64)
+        ref = oracle.build_rsd(od, ro.v, ro.xhat)
+        assert np.abs(num - ref).max() <= 1e-12 * np.abs(ref).max()

@@ -122,25 +122,3 @@ def test_synthetic_scene_files_roundtrip(fba, oracle, tmp_path):
     A, w, G, dsc = oracle.build_awg(od, oracle.buildxhat(od)[0])
     # initial misclosure is small (model-consistent observations, perturbed start)
     assert np.sqrt(np.mean(w ** 2)) < 50
-
-
-MEX_DECLS = """#include <stddef.h>
-typedef struct mxArray_tag mxArray; typedef size_t mwSize; typedef enum { mxREAL } mxComplexity;
-typedef enum { mxDOUBLE_CLASS } mxClassID; typedef int mxInt32;
-double* mxGetDoubles(const mxArray*); mxInt32* mxGetInt32s(const mxArray*); size_t mxGetN(const mxArray*);
-int mxIsInt32(const mxArray*); mxArray* mxCreateDoubleMatrix(mwSize, mwSize, mxComplexity);
-mxArray* mxCreateDoubleScalar(double); mxArray* mxCreateNumericArray(mwSize, const mwSize*, mxClassID, mxComplexity);
-void mxDestroyArray(mxArray*); void* mxMalloc(size_t); void mxFree(void*);
-void mexErrMsgIdAndTxt(const char*, const char*, ...);
-"""
-
-
-def test_mex_gateway_compiles(tmp_path):
-    """mex/fba_mex.c (source-only: no MATLAB here) against the MEX API declarations it uses and the
-    real include/fba.h: a syntax/type check, nothing is linked or run."""
-    import subprocess
-    (tmp_path / "mex.h").write_text(MEX_DECLS)
-    r = subprocess.run(["gcc", "-fsyntax-only", "-Wall", "-Werror", "-I", str(tmp_path), "-I",
-                        os.path.join(ROOT, "include"), os.path.join(ROOT, "mex", "fba_mex.c")],
-                       capture_output=True, text=True)
-    assert r.returncode == 0, r.stderr
