@@ -5,6 +5,11 @@ Run in the build container (the only place /root/reference exists):
 
 `functions/BuildAwG.m` carries its forward model (lines 163-207) and its Jacobian as
 machine-generated symbolic text (EOP partials :223-348, d/dc :401-414, tie partials :457-495),
+and hand-written arithmetic (distortion model :167-181, xp / yp partials :373-398, rmax and the
+scaled K / P columns :419-445, the inner-constraint block :516-523).  Both are evaluated here: the
+generated expressions at zero distortion ("values") and, with the hand-written statements
+(translated from the text: 1-based K(j) / P(1) / dist_scaling(cam, 2 + j) indexing, MATLAB row and
+matrix literals), everything at nonzero distortion ("distortion"),
 one assignment per line, branched on `typeint` (0 fisheye, 1 pinhole, 2 equisolid,
 3 orthographic, 4 stereographic).  This script reads that file at generation time, evaluates each
 assignment's right-hand side at 40 significant digits (mpmath) on seeded sample points and on the
@@ -94,6 +99,187 @@ def samples(rng, n):
     return out
 
 
+# ---- the hand-written arithmetic of BuildAwG.m (distortion model :167-181, xp / yp partials
+# :373-398, rmax and the scaled K / P columns :419-445, the inner-constraint block :516-523) ----
+def statements(path):
+    """The file as statements: comments stripped, continuation lines joined until brackets balance."""
+    out, cur, depth = [], "", 0
+    with open(path) as fh:
+        for line in fh:
+            code = line.split("%", 1)[0]
+            cur += " " + code.strip()
+            depth += code.count("[") + code.count("(") - code.count("]") - code.count(")")
+            if depth <= 0 and cur.strip():
+                out.append(cur.strip())
+                cur, depth = "", 0
+    return out
+
+
+def split_elems(body):
+    """Elements of a MATLAB row / matrix literal body: rows by ';', elements by whitespace where
+    MATLAB splits them (an operand follows, or a unary +/- glued to its operand)."""
+    rows, elems, cur, depth = [], [], "", 0
+    i = 0
+    while i < len(body):
+        ch = body[i]
+        if ch in "([":
+            depth += 1
+        elif ch in ")]":
+            depth -= 1
+        if depth == 0 and ch == ";":
+            if cur.strip():
+                elems.append(cur.strip())
+            if elems:
+                rows.append(elems)
+            elems, cur = [], ""
+        elif depth == 0 and ch == " " and cur.strip():
+            j = i
+            while j < len(body) and body[j] == " ":
+                j += 1
+            nxt = body[j] if j < len(body) else ""
+            prev = cur.rstrip()[-1]
+            unary = nxt in "+-" and j + 1 < len(body) and body[j + 1] != " "
+            operand = nxt and (nxt.isalnum() or nxt in "(._")
+            if prev not in "+-*/^,(" and (operand or unary):
+                elems.append(cur.strip())
+                cur = ""
+            else:
+                cur += " "
+            i = j - 1
+        else:
+            cur += ch
+        i += 1
+    if cur.strip():
+        elems.append(cur.strip())
+    if elems:
+        rows.append(elems)
+    return rows
+
+
+class MVec:
+    """a MATLAB vector / matrix indexed from 1 (K(j), P(1), dist_scaling(cam, 2 + j))"""
+
+    def __init__(self, f):
+        self.f = f
+
+    def __call__(self, *idx):
+        return self.f(*[int(i) for i in idx])
+
+
+def handwritten(path):
+    st = statements(path)
+    py = lambda e: to_python(e.replace("data.points(i).", "pt_"))  # noqa: E731
+
+    def first(pat, after=0):
+        for q in range(after, len(st)):
+            if re.match(pat, st[q]):
+                return q
+        raise KeyError(pat)
+    q_model = first(r"R = sqrt\(U\^2")
+    h = {}
+    for nm in ("x_bar", "y_bar", "r", "decentering_x", "decentering_y"):
+        q = first(rf"{nm} = ", q_model)
+        h[nm] = py(st[q].split("=", 1)[1])
+    q = first(r"for j = 1:length\(K\)", q_model)
+    h["delta_r_term"] = py(st[q + 1].split("=", 1)[1].replace("delta_r +", "", 1))
+    assert st[q + 1].startswith("delta_r = delta_r +") and st[q + 2] == "end"
+    for par in ("xp", "yp"):
+        q0 = first(rf"if data\.settings\.Estimate_{par}", q_model)
+        qa = first(r"dxp_rad = dxp_rad", q0)
+        qb = first(r"dyp_rad = dyp_rad", q0)
+        h[f"d{par}_xrad"] = py(st[qa].split("=", 1)[1].replace("dxp_rad", "0", 1))
+        h[f"d{par}_yrad"] = py(st[qb].split("=", 1)[1].replace("dyp_rad", "0", 1))
+        qc = first(r"Ablock_IOPs\(:,count_A\) = \[", q0)
+        body = st[qc].split("=", 1)[1].strip()
+        rows = split_elems(body[1:body.rindex("]")])
+        assert len(rows) == 2 and all(len(r) == 1 for r in rows), rows
+        h[f"A_{par}"] = [py(r[0]) for r in rows]
+    h["rmax"] = py(st[first(r"rmax = ")].split("=", 1)[1])
+    q = first(r"dist_scaling\(data\.points\(i\)\.cam_num,2\+j\) = ")
+    h["scale"] = py(st[q].split("=", 1)[1])
+    for nm in ("Ax_K", "Ay_K"):
+        h[nm] = py(st[first(rf"{nm}\(1,j\) = ")].split("=", 1)[1])
+    for nm in ("Ax_P", "Ay_P"):
+        rhs = st[first(rf"{nm} = \[")].split("=", 1)[1].strip()
+        close = rhs.index("]")
+        rows = split_elems(rhs[1:close])
+        assert len(rows) == 1 and len(rows[0]) == 2, rows
+        div = rhs[close + 1:].strip()
+        assert div.startswith("./")
+        h[nm] = [py(e) for e in rows[0]]
+        h[nm + "_div"] = py(div[2:])
+    rhs = st[first(r"Gblock = \[")].split("=", 1)[1].strip()
+    rows = split_elems(rhs[1:rhs.rindex("]")])
+    assert len(rows) == 6 and all(len(r) == 7 for r in rows), rows
+    h["G"] = [[py(e) for e in r] for r in rows]
+    return h
+
+
+def dist_samples(rng, n, nk):
+    """EOP / XYZ / c as samples(); plus observed x, y on a 2048 px sensor, K and P of realistic size
+    (each radial term up to ~10 px at the sensor corner), sensor bounds"""
+    out = []
+    for pt in samples(rng, n):
+        xmin, ymin = rng.uniform(-10, 10, 2)
+        xmax, ymax = xmin + rng.uniform(1500, 2500), ymin + rng.uniform(1500, 2500)
+        rmax = math.hypot((xmax - xmin) / 2, (ymax - ymin) / 2)
+        pt.update(x=rng.uniform(xmin, xmax), y=rng.uniform(ymin, ymax), xmin=xmin, ymin=ymin, xmax=xmax,
+                  ymax=ymax, K=[float(rng.uniform(-10, 10) / rmax ** (2 * j + 1)) for j in range(1, nk + 1)],
+                  P=[float(rng.uniform(-1e-6, 1e-6)) for _ in range(2)])
+        pt["xp"] += 0.5 * (xmin + xmax)
+        pt["yp"] += 0.5 * (ymin + ymax)
+        out.append(pt)
+    return out
+
+
+def eval_handwritten(h, model, fxfy, branches, pt, t, nk):
+    env = ns({k: v for k, v in pt.items() if not isinstance(v, list)})
+    env["K"] = MVec(lambda j: mp.mpf(pt["K"][j - 1]))
+    env["P"] = MVec(lambda j: mp.mpf(pt["P"][j - 1]))
+    for k in ("xmin", "ymin", "xmax", "ymax"):
+        env["pt_" + k] = mp.mpf(pt[k])
+    env["pt_cam_num"] = 1
+    ev = lambda e: eval(e, {"__builtins__": {}}, env)  # noqa: E731
+    for nm in MODEL:
+        env[nm] = ev(model[nm])
+    for nm in ("x_bar", "y_bar", "r", "decentering_x", "decentering_y"):
+        env[nm] = ev(h[nm])
+    env["delta_r"] = mp.mpf(0)
+    for j in range(1, nk + 1):
+        env["j"] = j
+        env["delta_r"] = env["delta_r"] + ev(h["delta_r_term"])
+    vals = {nm: float(ev(fxfy[t][nm])) for nm in ("fx", "fy")}
+    for nm in TARGETS:
+        vals[nm] = float(ev(branches[t][nm]))
+    for par in ("xp", "yp"):
+        dx = dy = mp.mpf(0)
+        for j in range(1, nk + 1):
+            env["j"] = j
+            dx += ev(h[f"d{par}_xrad"])
+            dy += ev(h[f"d{par}_yrad"])
+        env["dxp_rad"], env["dyp_rad"] = dx, dy
+        vals[f"A_{par}"] = [float(ev(e)) for e in h[f"A_{par}"]]
+    rmax = ev(h["rmax"])
+    env["rmax"] = rmax
+    scale = {}
+    for j in range(1, nk + 1):
+        env["j"] = j
+        scale[j] = ev(h["scale"])
+    env["dist_scaling"] = MVec(lambda cam, col: scale[col - 2])
+    vals["rmax"] = float(rmax)
+    vals["scale"] = [float(scale[j]) for j in range(1, nk + 1)]
+    for nm in ("Ax_K", "Ay_K"):
+        vals[nm] = []
+        for j in range(1, nk + 1):
+            env["j"] = j
+            vals[nm].append(float(ev(h[nm])))
+    for nm in ("Ax_P", "Ay_P"):
+        d = ev(h[nm + "_div"])
+        vals[nm] = [float(ev(e) / d) for e in h[nm]]
+    vals["G"] = [[float(ev(e)) for e in row] for row in h["G"]]
+    return vals
+
+
 def main(ref_root):
     path = os.path.join(ref_root, "functions", "BuildAwG.m")
     model, fxfy, branches = extract(path)
@@ -123,6 +309,12 @@ def main(ref_root):
                 vals[nm] = float(eval(branches[t][nm], {"__builtins__": {}}, env))
             rows.append(vals)
         out["values"][out["types"][t]] = rows
+    # the hand-written terms at nonzero distortion (nK = 5, config.cfg:33)
+    h = handwritten(path)
+    nk = 5
+    dpts = dist_samples(np.random.default_rng(20201017), 24, nk)
+    out["distortion"] = {"nk": nk, "points": dpts, "values": {
+        out["types"][t]: [eval_handwritten(h, model, fxfy, branches, pt, t, nk) for pt in dpts] for t in range(5)}}
     dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), "jac_golden.json")
     with open(dst, "w") as fh:
         json.dump(out, fh, indent=1)

@@ -353,3 +353,62 @@ def test_buildrsd_matches_oracle(fba, oracle, cam0_folders):
         num = np.array([r[4:] for r in rows], dtype=np.float64)
         ref = oracle.build_rsd(od, ro.v, ro.xhat)
         assert np.abs(num - ref).max() <= 1e-12 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("t", range(5))
+def test_buildawg_matches_reference_text(fba, t):
+    """The device BuildAwG (fba_build_awg) against the reference's own BuildAwG.m text evaluated at
+    40 digits (tests/golden/jac_golden.json "distortion": generated EOP / tie / c partials and the
+    hand-written distortion model, xp / yp partials, scaled K / P columns, dist_scaling and G at
+    nonzero distortion), one image and one camera per sample point: <= 1e-12 relative per entry."""
+    import json
+    import os
+    from conftest import GOLDEN
+    from test_oracle import EOP_NAMES, TIE_NAMES
+    with open(os.path.join(GOLDEN, "jac_golden.json")) as fh:
+        g = json.load(fh)["distortion"]
+    typ = ["fisheye", "pinhole", "equisolid", "orthographic", "stereographic"][t]
+    nk, pts = g["nk"], g["points"]
+    n, cw = len(pts), 5 + g["nk"]
+    eop = np.array([[p["Xc"], p["Yc"], p["Zc"], p["w"], p["p"], p["k"]] for p in pts])
+    iop = np.array([[p["xp"], p["yp"], p["c"], *p["K"], *p["P"]] for p in pts])
+    xyz = np.array([[p["X"], p["Y"], p["Z"]] for p in pts])
+    cam_info = np.array([[p["y_dir"], p["xmin"], p["ymin"], p["xmax"], p["ymax"]] for p in pts])
+    xy = np.array([[p["x"], p["y"]] for p in pts])
+    idx = np.arange(n)
+    packed = fba.capi.PackedProblem(xy, idx, idx, idx, xyz, eop, iop, cam_info, xyz, n, n, n)
+    s = {"type": typ, "Num_Radial_Distortions": nk, "Inner_Constraints": 1, "Iteration_Cap": 1, "threshold": 1e-6,
+         "Meas_std": 1.0, "Meas_std_y": 1.0}
+    for k in ("Xc", "Yc", "Zc", "w", "p", "k", "c", "xp", "yp", "radial", "decent"):
+        s["Estimate_" + k] = 1
+    ctx = fba.capi.Context(packed, fba.capi.make_settings(s))
+    try:
+        xhat = np.concatenate([eop.reshape(-1), iop.reshape(-1), xyz.reshape(-1)])
+        A, w, G, ds = ctx.build_awg(xhat)
+    finally:
+        ctx.close()
+
+    def close(a, b, what):
+        assert abs(a - b) <= 1e-12 * max(abs(b), 1e-300), (typ, what, a, b)
+    for i, v in enumerate(g["values"][typ]):
+        rx, ry, base, tb = 2 * i, 2 * i + 1, 6 * n + cw * i, 6 * n + cw * n + 3 * i
+        close(w[rx] + xy[i, 0], v["fx"], (i, "fx"))
+        close(w[ry] + xy[i, 1], v["fy"], (i, "fy"))
+        for nm, (r, col) in EOP_NAMES.items():
+            close(A[2 * i + r, 6 * i + col], v[nm], (i, nm))
+        for nm, (r, col) in TIE_NAMES.items():
+            close(A[2 * i + r, tb + col], v[nm], (i, nm))
+        for q, par in enumerate(("A_xp", "A_yp")):
+            close(A[rx, base + q], v[par][0], (i, par))
+            close(A[ry, base + q], v[par][1], (i, par))
+        close(A[rx, base + 2], v["Ax_c"], (i, "Ax_c"))
+        close(A[ry, base + 2], v["Ay_c"], (i, "Ay_c"))
+        for j in range(nk):
+            close(A[rx, base + 3 + j], v["Ax_K"][j], (i, "Ax_K", j))
+            close(A[ry, base + 3 + j], v["Ay_K"][j], (i, "Ay_K", j))
+            close(ds[i, 2 + j], v["scale"][j], (i, "dist_scaling", j))
+        for j in range(2):
+            close(A[rx, base + 3 + nk + j], v["Ax_P"][j], (i, "Ax_P", j))
+            close(A[ry, base + 3 + nk + j], v["Ay_P"][j], (i, "Ay_P", j))
+        gv = np.array(v["G"])
+        assert np.abs(G[6 * i:6 * i + 6] - gv).max() <= 1e-14 * np.abs(gv).max(), (typ, i, "G")

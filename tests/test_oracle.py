@@ -1,8 +1,10 @@
 """CPU: pin the oracle (oracle/fba_oracle.py) before trusting it.
 
 * The Jacobian and forward model against tests/golden/jac_golden.json: numbers obtained by
-  evaluating the reference's OWN generated expression text (functions/BuildAwG.m:163-207,
-  :223-348, :401-414, :457-495) at 40 digits (tests/golden/make_jac_golden.py), all 5 types.
+  evaluating the reference's OWN text (functions/BuildAwG.m: generated expressions :163-207,
+  :223-348, :401-414, :457-495, and the hand-written distortion / IOP / scaling / G statements
+  :167-181, :373-398, :419-445, :516-523) at 40 digits (tests/golden/make_jac_golden.py), all 5
+  types, at zero and at nonzero distortion.
 * The cam0 runs against the committed fixtures (tests/golden/cam0_*.npz, written by
   tests/golden/make_cam0_golden.py) -- a regression pin of the restatement itself.
 * The block-sparse (Schur) restatement against the explicit bordered inverse of main.m:432.
@@ -49,6 +51,61 @@ def test_jacobian_matches_reference_expressions(oracle, jac, t):
         assert m["J_c"][i, 1] == pytest.approx(row["Ay_c"], rel=tol)
         assert m["f"][i, 0] == pytest.approx(row["fx"], rel=tol)
         assert m["f"][i, 1] == pytest.approx(row["fy"], rel=tol)
+
+
+@pytest.mark.parametrize("t", range(5))
+def test_handwritten_terms_match_reference_text(oracle, jac, t):
+    """BuildAwG's hand-written arithmetic pinned to the reference text at NONZERO distortion: the
+    distortion model and misclosure (BuildAwG.m:167-187, :505-512), the xp / yp partials with their
+    radial and decentering terms (:373-398), d/dc (:401-414), rmax and dist_scaling (:419-426), the
+    scaled K / P columns (:428-445), the inner-constraint block (:516-523) and the EOP / tie partials,
+    for every Type -- tests/golden/make_jac_golden.py evaluates those statements from the .m text at
+    40 digits.  The oracle's build_awg (one image and one camera per sample point) must agree to
+    1e-12 relative, entry by entry."""
+    from fba_oracle import Data
+    g = jac["distortion"]
+    typ, nk, pts = jac["types"][t], g["nk"], g["points"]
+    n, cw = len(pts), 5 + g["nk"]
+    s = {"type": typ, "Num_Radial_Distortions": nk, "Inner_Constraints": 1}
+    for k in ("Xc", "Yc", "Zc", "w", "p", "k", "c", "xp", "yp", "radial", "decent"):
+        s["Estimate_" + k] = 1
+    eop = np.array([[p["Xc"], p["Yc"], p["Zc"], p["w"], p["p"], p["k"]] for p in pts])
+    iop = np.array([[p["xp"], p["yp"], p["c"], *p["K"], *p["P"]] for p in pts])
+    xyz = np.array([[p["X"], p["Y"], p["Z"]] for p in pts])
+    bounds = np.array([[p["y_dir"], p["xmin"], p["ymin"], p["xmax"], p["ymax"]] for p in pts])
+    idx = np.arange(n)
+    od = Data(settings=s, x=np.array([p["x"] for p in pts]), y=np.array([p["y"] for p in pts]),
+              target=[f"T{i}" for i in idx], image=[f"I{i}" for i in idx], ext_index=idx, cam_num=idx,
+              tie_index=idx, eop_fixed=eop, iop_fixed=iop, bounds=bounds, xyz_fixed=xyz, numImg=n, numCam=n,
+              n=2 * n, numGCP=n, numtie=n)
+    xhat = np.concatenate([eop.reshape(-1), iop.reshape(-1), xyz.reshape(-1)])
+    A, w, G, ds = oracle.build_awg(od, xhat)
+
+    def close(a, b, what):
+        assert abs(a - b) <= 1e-12 * max(abs(b), 1e-300), (typ, what, a, b)
+    for i, v in enumerate(g["values"][typ]):
+        rx, ry, base, tb = 2 * i, 2 * i + 1, 6 * n + cw * i, 6 * n + cw * n + 3 * i
+        close(w[rx] + od.x[i], v["fx"], (i, "fx"))
+        close(w[ry] + od.y[i], v["fy"], (i, "fy"))
+        for nm, (r, col) in EOP_NAMES.items():
+            close(A[2 * i + r, 6 * i + col], v[nm], (i, nm))
+        for nm, (r, col) in TIE_NAMES.items():
+            close(A[2 * i + r, tb + col], v[nm], (i, nm))
+        for q, par in enumerate(("A_xp", "A_yp")):
+            close(A[rx, base + q], v[par][0], (i, par, "x"))
+            close(A[ry, base + q], v[par][1], (i, par, "y"))
+        close(A[rx, base + 2], v["Ax_c"], (i, "Ax_c"))
+        close(A[ry, base + 2], v["Ay_c"], (i, "Ay_c"))
+        for j in range(nk):
+            close(A[rx, base + 3 + j], v["Ax_K"][j], (i, "Ax_K", j))
+            close(A[ry, base + 3 + j], v["Ay_K"][j], (i, "Ay_K", j))
+            close(ds[i, 2 + j], v["scale"][j], (i, "dist_scaling", j))
+        for j in range(2):
+            close(A[rx, base + 3 + nk + j], v["Ax_P"][j], (i, "Ax_P", j))
+            close(A[ry, base + 3 + nk + j], v["Ay_P"][j], (i, "Ay_P", j))
+        gv = np.array(v["G"])
+        gmax = np.abs(gv).max()
+        assert np.abs(G[6 * i:6 * i + 6] - gv).max() <= 1e-14 * gmax, (typ, i, "G")
 
 
 def test_jacobian_distortion_terms_by_finite_differences(oracle):
