@@ -26,12 +26,13 @@ HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 matrix (AMD public spec; survey section 8(d))
 
 
-def scene_folder(config, rank, world):
+def scene_folder(config, rank, world, network="grid"):
     from fba_amd import synth
-    folder = os.path.join(os.environ.get("FBA_BENCH_DIR", "/tmp/fba_bench"), f"c{config}")
+    tag = f"c{config}" + ("" if network == "grid" else f"_{network}")
+    folder = os.path.join(os.environ.get("FBA_BENCH_DIR", "/tmp/fba_bench"), tag)
     marker = os.path.join(folder, ".done")
     if rank == 0 and not os.path.exists(marker):
-        synth.make_config(config, folder)
+        synth.make_config(config, folder, network=network)
         open(marker, "w").close()
     if world > 1:
         import torch.distributed as dist
@@ -52,12 +53,13 @@ def phase_roofline(ds, ms_phase, n_steps):
     return t, chol_flops, lin_bytes
 
 
-def pmc_traffic(config, kernel):
+def pmc_traffic(config, kernel, network="grid"):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this workload
     (profiles/*pmc_config<N>.json, made by scripts/pmc_summary.py: FETCH_SIZE x2 per the gfx950
     correction + WRITE_SIZE), or None."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_config{config}.json")), reverse=True):
+    tag = f"{config}" + ("" if network == "grid" else f"_{network}")
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_config{tag}.json")), reverse=True):
         with open(f) as fh:
             d = json.load(fh)
         k = d.get("kernels", {}).get(kernel)
@@ -93,6 +95,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=4)
+    # "convergent": the same counts as a convergent (close-range) network, dense reduced system
+    # (synth.generate_convergent) -- a measurement scene, not the headline workload
+    ap.add_argument("--network", default="grid", choices=("grid", "convergent"))
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verbose", action="store_true")
@@ -118,7 +123,7 @@ def main():
     import fba_import
     fba = fba_import.load()
 
-    folder = scene_folder(args.config, rank, world)
+    folder = scene_folder(args.config, rank, world, args.network)
     ds = fba.load_folder(folder)
     if world > 1:  # a dedicated stream (capturable: the iteration replays as HIP graphs), RCCL on it too
         torch.cuda.set_stream(torch.cuda.Stream(dev))
@@ -181,7 +186,7 @@ def main():
         r = {"bound": "mfma", "kernel": f"{name} ({note})",
              "achieved": flops_launch / avg_s / 1e12 if avg_s > 0 else None, "peak": FP64_PEAK_TFLOPS,
              "unit": "TFLOP/s", "launches": pr["launches"], "avg_launch_us": avg_s * 1e6,
-             "flops_per_launch": flops_launch, "traffic": pmc_traffic(args.config, name)}
+             "flops_per_launch": flops_launch, "traffic": pmc_traffic(args.config, name, args.network)}
         r["frac"] = r["achieved"] / r["peak"] if r["achieved"] else None
         return r
     flow = os.environ.get("FBA_CHOL_FLOW", "1") != "0"
@@ -206,8 +211,9 @@ def main():
         "value": value, "unit": "iter/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": f"synthetic fish-eye config {args.config}: {ds.numImg} images x {ds.numtie} tie "
-                               f"points, {ds.n_pts} image points, inner constraints, nK=5",
+        "config": {"workload": f"synthetic fish-eye config {args.config}"
+                               f"{'' if args.network == 'grid' else ' (' + args.network + ' network)'}: {ds.numImg} "
+                               f"images x {ds.numtie} tie points, {ds.n_pts} image points, inner constraints, nK=5",
                    "n_pts": ds.n_pts, "n_img": ds.numImg, "n_tie": ds.numtie, "u": int(ctx.u),
                    "parallelism": f"obs-shard{world}"},
         "obs_per_s": ds.n_pts * value,

@@ -32,72 +32,87 @@ namespace fba {
 constexpr int CB = NB;  // 128
 
 // ------------------------------------------------------------------------------------------------
-// k_blk_gemm: one workgroup per task, C(128x128) = sum_t sign_t op(A_t) op(B_t), terms in list order.
-// Operand/output bases: 0 = S (leading dimension ld), 1 = linv, 2 = Y scratch (both 128).
-// Thread (ty, tx) of a 16x16 grid owns rows ty + 16 a, columns tx + 16 b (a, b < 8); K in slices of
-// 16 staged through LDS.
+// k_blk_gemm: one workgroup per task, C(128x128) = sum_t sign_t op(A_t) op(B_t), terms in list order,
+// on v_mfma_f64_16x16x4_f64.  Operand/output bases: 0 = S (leading dimension ld), 1 = linv, 2 = Y
+// scratch (both 128).  Four waves, each a 64x64 quarter of C as 4x4 MFMA tiles (64 accumulators per
+// lane); K in slices of 16 staged through LDS (rows padded to 17 doubles: the 16 lanes of an MFMA
+// operand read hit distinct banks), the next slice's global loads in flight during the current
+// slice's MFMAs.  Fixed order: terms in list order, K ascending -- bitwise reproducible.
 // task record (int64): out offset, out base, first term, end term
 // term record (int64): A offset, B offset, flags = baseA | baseB << 2 | tA << 4 | tB << 5 | neg << 6
 // ------------------------------------------------------------------------------------------------
 constexpr int KS = 16;
-constexpr int LP = CB + 4;
+constexpr int LK = KS + 1;
+typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(256) void k_blk_gemm(const int64_t* __restrict__ tasks, const int64_t* __restrict__ terms,
                                                   double* __restrict__ S, int64_t ld, const double* __restrict__ linv,
                                                   double* __restrict__ Y) {
-    __shared__ double As[KS][LP];
-    __shared__ double Bs[KS][LP];
-    const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+    __shared__ double As[CB * LK];  // op(A)[i][k0 + kk] at i * LK + kk (sign applied)
+    __shared__ double Bs[CB * LK];  // op(B)[k0 + kk][j] at j * LK + kk
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lk = lane >> 4;
+    const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
     const int64_t* tk = tasks + 4 * (int64_t)blockIdx.x;
-    double acc[8][8];
+    dbl4 acc[4][4];
 #pragma unroll
-    for (int a = 0; a < 8; ++a)
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 8; ++b) acc[a][b] = 0.0;
-    for (int64_t t = tk[2]; t < tk[3]; ++t) {
-        const int64_t* tr = terms + 3 * t;
+        for (int b = 0; b < 4; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+    const int64_t t0 = tk[2], t1 = tk[3];
+    const int nsl = (int)(t1 - t0) * (CB / KS);
+    // slice s = (term t0 + s / 8, k0 = 16 (s % 8)): 8 elements of each operand per thread
+    double va[8], vb[8];
+    auto fetch = [&](int sl) {
+        const int64_t* tr = terms + 3 * (t0 + sl / (CB / KS));
+        const int k0 = (sl % (CB / KS)) * KS;
         const int fl = (int)tr[2];
         const int ba = fl & 3, bb = (fl >> 2) & 3, ta = (fl >> 4) & 1, tb = (fl >> 5) & 1;
         const double sg = (fl >> 6) & 1 ? -1.0 : 1.0;
         const double* A = (ba == 0 ? S : ba == 1 ? linv : Y) + tr[0];
         const double* B = (bb == 0 ? S : bb == 1 ? linv : Y) + tr[1];
         const int64_t lda = ba == 0 ? ld : CB, ldb = bb == 0 ? ld : CB;
-        for (int k0 = 0; k0 < CB; k0 += KS) {
-            __syncthreads();
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int idx = tid + 256 * q;
-                int r, kk;
-                double v;
-                if (!ta) { r = idx >> 4; kk = idx & 15; v = A[(int64_t)r * lda + k0 + kk]; }
-                else { kk = idx >> 7; r = idx & 127; v = A[(int64_t)(k0 + kk) * lda + r]; }
-                As[kk][r] = sg * v;
-                int c;
-                if (!tb) { kk = idx >> 7; c = idx & 127; v = B[(int64_t)(k0 + kk) * ldb + c]; }
-                else { c = idx >> 4; kk = idx & 15; v = B[(int64_t)c * ldb + k0 + kk]; }
-                Bs[kk][c] = v;
-            }
-            __syncthreads();
-#pragma unroll 4
-            for (int kk = 0; kk < KS; ++kk) {
-                double av[8], bv[8];
+        for (int q = 0; q < 8; ++q) {
+            const int idx = tid + 256 * q;
+            va[q] = sg * (!ta ? A[(int64_t)(idx >> 4) * lda + k0 + (idx & 15)] : A[(int64_t)(k0 + (idx >> 7)) * lda + (idx & 127)]);
+            vb[q] = !tb ? B[(int64_t)(k0 + (idx >> 7)) * ldb + (idx & 127)] : B[(int64_t)(idx >> 4) * ldb + k0 + (idx & 15)];
+        }
+        return (ta ? 1 : 0) | (tb ? 2 : 0);
+    };
+    int tt = nsl > 0 ? fetch(0) : 0;
+    for (int sl = 0; sl < nsl; ++sl) {
+        __syncthreads();  // the previous slice's MFMA reads are done
 #pragma unroll
-                for (int a = 0; a < 8; ++a) av[a] = As[kk][ty + 16 * a];
+        for (int q = 0; q < 8; ++q) {
+            const int idx = tid + 256 * q;
+            if (!(tt & 1)) As[(idx >> 4) * LK + (idx & 15)] = va[q];
+            else As[(idx & 127) * LK + (idx >> 7)] = va[q];
+            if (!(tt & 2)) Bs[(idx & 127) * LK + (idx >> 7)] = vb[q];
+            else Bs[(idx >> 4) * LK + (idx & 15)] = vb[q];
+        }
+        __syncthreads();
+        if (sl + 1 < nsl) tt = fetch(sl + 1);
 #pragma unroll
-                for (int b = 0; b < 8; ++b) bv[b] = Bs[kk][tx + 16 * b];
+        for (int kk = 0; kk < KS; kk += 4) {
+            double av[4], bv[4];
 #pragma unroll
-                for (int a = 0; a < 8; ++a)
+            for (int a = 0; a < 4; ++a) av[a] = As[(wr + 16 * a + lr) * LK + kk + lk];
 #pragma unroll
-                    for (int b = 0; b < 8; ++b) acc[a][b] += av[a] * bv[b];
-            }
+            for (int b = 0; b < 4; ++b) bv[b] = Bs[(wc + 16 * b + lr) * LK + kk + lk];
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
         }
     }
     double* C = (tk[1] == 0 ? S : Y) + tk[0];
     const int64_t ldc = tk[1] == 0 ? ld : CB;
 #pragma unroll
-    for (int a = 0; a < 8; ++a)
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 8; ++b) C[(int64_t)(ty + 16 * a) * ldc + tx + 16 * b] = acc[a][b];
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) C[(int64_t)(wr + 16 * a + lk + 4 * r) * ldc + wc + 16 * b + lr] = acc[a][b][r];
 }
 
 // H^-1 of the 14x14 border system (k_border_combine's H = [[A'A - I, A'B], [B'A, B'B]] from the Gram of
@@ -334,40 +349,17 @@ int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, 
     double* d_Y = nullptr;
     int64_t *d_tasks = nullptr, *d_terms = nullptr;
     if ((rc = alloc(&d_Y, ymax * CB * CB))) { cleanup(); return rc; }
-    // generous task/term buffers: sized by the largest level
-    size_t tmax = 1, rmax = 1;
-    for (int w = 0; w < s.n_waves; ++w) {
-        size_t nt = 0, nr = 0;
-        const int32_t* cols = s.buf.data() + s.w[w].cols;
-        for (int q = 0; q < s.w[w].ncol; ++q) {
-            const size_t r = R[cols[q]].size();
-            nt += 2 * r + 1;
-            nr += r + r * r + 1 + r;
-        }
-        tmax = std::max(tmax, nt);
-        rmax = std::max(rmax, nr);
-    }
-    if ((rc = alloc((double**)&d_tasks, 4 * tmax)) || (rc = alloc((double**)&d_terms, 3 * rmax))) { cleanup(); return rc; }
-
+    // every phase's task / term lists built up front and uploaded once; the phases (three per level,
+    // top level first) then run back to back on the stream, no host round trip in between
     auto blk = [&](int64_t i, int64_t j) { return i * CB * ld + j * CB; };
     std::vector<int64_t> tasks, terms;
-    auto launch = [&]() -> int {
-        if (tasks.empty()) return FBA_OK;
-        FBA_HIP(hipMemcpyAsync(d_tasks, tasks.data(), sizeof(int64_t) * tasks.size(), hipMemcpyHostToDevice, c.stream));
-        FBA_HIP(hipMemcpyAsync(d_terms, terms.data(), sizeof(int64_t) * std::max<size_t>(terms.size(), 1),
-                               hipMemcpyHostToDevice, c.stream));
-        k_blk_gemm<<<(unsigned)(tasks.size() / 4), 256, 0, c.stream>>>(d_tasks, d_terms, c.d_S, ld, c.d_linv, d_Y);
-        FBA_HIP(hipGetLastError());
-        FBA_HIP(hipStreamSynchronize(c.stream));  // host lists are rebuilt for the next launch
-        tasks.clear();
-        terms.clear();
-        return FBA_OK;
-    };
+    std::vector<std::pair<int64_t, int64_t>> phases;  // [first task, end task)
     auto task = [&](int64_t out, int base) {
         tasks.insert(tasks.end(), {out, (int64_t)base, (int64_t)terms.size() / 3, 0});
     };
     auto term = [&](int64_t a, int64_t b, int fl) { terms.insert(terms.end(), {a, b, (int64_t)fl}); };
     auto close_task = [&]() { tasks.back() = (int64_t)terms.size() / 3; };
+    auto phase = [&](int64_t first) { if ((int64_t)tasks.size() / 4 > first) phases.emplace_back(first, (int64_t)tasks.size() / 4); };
     enum { BS = 0, BL = 1, BY = 2 };
     for (int w = s.n_waves - 1; w >= 0; --w) {
         const int32_t* cols = s.buf.data() + s.w[w].cols;
@@ -376,6 +368,7 @@ int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, 
         size_t ny = 0;
         for (int q = 0; q < ncol; ++q) { ybase[q] = ny; ny += R[cols[q]].size(); }
         // (1) Y_i = L_ik Linv_k
+        int64_t first = (int64_t)tasks.size() / 4;
         for (int q = 0; q < ncol; ++q) {
             const int64_t k = cols[q];
             for (size_t a = 0; a < R[k].size(); ++a) {
@@ -384,8 +377,9 @@ int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, 
                 close_task();
             }
         }
-        if ((rc = launch())) { cleanup(); return rc; }
+        phase(first);
         // (2) Q_ik = -sum_j Q_ij Y_j
+        first = (int64_t)tasks.size() / 4;
         for (int q = 0; q < ncol; ++q) {
             const int64_t k = cols[q];
             for (size_t a = 0; a < R[k].size(); ++a) {
@@ -400,8 +394,9 @@ int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, 
                 close_task();
             }
         }
-        if ((rc = launch())) { cleanup(); return rc; }
+        phase(first);
         // (3) Q_kk = Linv_k' Linv_k - sum_i Y_i' Q_ik
+        first = (int64_t)tasks.size() / 4;
         for (int q = 0; q < ncol; ++q) {
             const int64_t k = cols[q];
             task(blk(k, k), BS);
@@ -410,8 +405,18 @@ int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, 
                 term((int64_t)(ybase[q] + a) * CB * CB, blk(R[k][a], k), BY | BS << 2 | 1 << 4 | 1 << 6);
             close_task();
         }
-        if ((rc = launch())) { cleanup(); return rc; }
+        phase(first);
     }
+    if ((rc = alloc((double**)&d_tasks, std::max<size_t>(tasks.size(), 1))) ||
+        (rc = alloc((double**)&d_terms, std::max<size_t>(terms.size(), 1)))) { cleanup(); return rc; }
+    if (!tasks.empty()) {
+        FBA_HIP(hipMemcpyAsync(d_tasks, tasks.data(), sizeof(int64_t) * tasks.size(), hipMemcpyHostToDevice, c.stream));
+        FBA_HIP(hipMemcpyAsync(d_terms, terms.data(), sizeof(int64_t) * terms.size(), hipMemcpyHostToDevice, c.stream));
+    }
+    for (auto& ph : phases)
+        k_blk_gemm<<<(unsigned)(ph.second - ph.first), 256, 0, c.stream>>>(d_tasks + 4 * ph.first, d_terms, c.d_S, ld,
+                                                                           c.d_linv, d_Y);
+    FBA_HIP(hipGetLastError());
 
     if (d_cdiag)
         k_cov_cam<<<(unsigned)((L.u_c + 255) / 256), 256, 0, c.stream>>>(c.d_S, ld, d_Z, d_Wz, nz, n_pad, L.u_c, L.n_img,

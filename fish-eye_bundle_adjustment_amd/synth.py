@@ -62,7 +62,7 @@ def _project(typ, U, V, W, c, xp, yp, K, P):
     px = -c * U * s + xp
     py = -c * YDIR * V * s + yp
     x, y = px.copy(), py.copy()
-    for _ in range(30):  # observed-coordinate distortion: fixed point
+    for _ in range(30 if (np.any(K) or np.any(P)) else 0):  # observed-coordinate distortion: fixed point
         xb, yb = x - xp, y - yp
         r2 = xb * xb + yb * yb
         dr = sum(K[j] * r2 ** (j + 1) for j in range(len(K)))
@@ -184,6 +184,70 @@ def generate(n_img, n_tie, seed, obs_per_point=10, noise=0.3, typ="fisheye", spa
                 xy=xy, typ=typ, cam=cam_of, control=control)
 
 
+def generate_convergent(n_img, n_tie, seed, obs_per_point=10, noise=0.3, typ="fisheye", radius=3000.0,
+                        distance=4500.0, max_theta_deg=80.0):
+    """A convergent (close-range) network -- the reference's own calibration setting: cam0's 42 images
+    all look at one target field (main.m:424-444 forms the dense N).  Cameras on a hemisphere of
+    radius `distance` around a ball of tie points of radius `radius`, each looking at its centre
+    (random kappa); each tie point observed by `obs_per_point` cameras drawn at random from ALL the
+    cameras that see it (W < 0, off-axis angle <= max_theta_deg, inside the sensor), so almost every
+    pair of images shares points and the reduced camera system is dense (no nested-dissection
+    sparsity: the Cholesky is throughput-, not latency-bound).  Same camera, noise and start-value
+    recipe as generate()."""
+    rng = np.random.default_rng(seed)
+    obs_per_point = min(obs_per_point, n_img)
+    az = rng.uniform(-math.pi, math.pi, n_img)
+    el = np.radians(rng.uniform(25.0, 85.0, n_img))
+    dirs = np.stack([np.cos(el) * np.cos(az), np.cos(el) * np.sin(az), np.sin(el)], 1)  # centre -> camera
+    C_true = distance * dirs + rng.normal(0, 50.0, (n_img, 3))
+    # the third row of M(omega, phi, kappa) is (sin phi, -cos phi sin omega, cos phi cos omega): make it
+    # the viewing direction so the ball's centre lies on the optical axis (W = -distance)
+    phi = np.arcsin(np.clip(dirs[:, 0], -1, 1))
+    omega = np.arctan2(-dirs[:, 1], dirs[:, 2])
+    ang_true = np.stack([omega + rng.normal(0, math.radians(2), n_img), phi + rng.normal(0, math.radians(2), n_img),
+                         rng.uniform(-math.pi, math.pi, n_img)], 1)
+    Mall = _rot(ang_true[:, 0], ang_true[:, 1], ang_true[:, 2])
+    cos_max = math.cos(math.radians(max_theta_deg))
+    pts, obs_img, obs_xy = [], [], []
+    n_have = 0
+    while n_have < n_tie:
+        m = int(min(4096, n_tie - n_have + 64))
+        v = rng.normal(0, 1, (m, 3))
+        X = radius * (v / np.linalg.norm(v, axis=1, keepdims=True)) * rng.uniform(0, 1, (m, 1)) ** (1 / 3)
+        d = X[:, None, :] - C_true[None, :, :]                        # (m, n_img, 3)
+        UVW = np.einsum("kij,mkj->mki", Mall, d)
+        U, V, W = UVW[..., 0], UVW[..., 1], UVW[..., 2]
+        dist = np.sqrt((d * d).sum(-1))
+        # validity from the distortion-free projection with a 5 px margin (distortion moves a point by
+        # < 4 px on this sensor), the distorted coordinates for the chosen observations only
+        with np.errstate(invalid="ignore", divide="ignore"):
+            x, y = _project(typ, U, V, W, C0, XP, YP, [0.0], [0.0, 0.0])
+        ok = (W < 0) & (-W >= cos_max * dist)
+        ok &= (x > SENSOR[0] + 5) & (x < SENSOR[2] - 5) & (y > SENSOR[1] + 5) & (y < SENSOR[3] - 5)
+        # a uniformly random subset of the valid cameras: the obs_per_point smallest random keys
+        key = np.where(ok, rng.random(ok.shape), np.inf)
+        sel = np.sort(np.argpartition(key, obs_per_point - 1, axis=1)[:, :obs_per_point], axis=1)
+        good = np.isfinite(np.take_along_axis(key, sel, 1)).all(1)
+        take = np.nonzero(good)[0][: n_tie - n_have]
+        sel = sel[take]
+        with np.errstate(invalid="ignore", divide="ignore"):
+            xs, ys = _project(typ, np.take_along_axis(U[take], sel, 1), np.take_along_axis(V[take], sel, 1),
+                              np.take_along_axis(W[take], sel, 1), C0, XP, YP, K0, P0)
+        pts.append(X[take])
+        obs_img.append(sel)
+        obs_xy.append(np.stack([xs, ys], -1))
+        n_have += len(take)
+    X_true = np.concatenate(pts)
+    img = np.concatenate(obs_img).reshape(-1).astype(np.int64)
+    pid = np.repeat(np.arange(n_tie), obs_per_point)
+    xy = np.concatenate(obs_xy).reshape(-1, 2) + rng.normal(0, noise, (len(img), 2))
+    C0v = C_true + rng.normal(0, 10.0, C_true.shape)
+    ang0 = ang_true + rng.normal(0, math.radians(0.1), ang_true.shape)
+    X0 = X_true + rng.normal(0, 10.0, X_true.shape)
+    return dict(C_true=C_true, ang_true=ang_true, X_true=X_true, C0=C0v, ang0=ang0, X0=X0, img=img, pid=pid,
+                xy=xy, typ=typ, cam=np.zeros(n_img, np.int64), control=np.zeros(n_tie, bool))
+
+
 def write_folder(scene, folder, name="synth", nk=5, cfg_overrides=None):
     """Write .pho/.ext/.int/.cnt/.tie/.cfg (the reference's formats, Appendix A of SURVEY.md)."""
     os.makedirs(folder, exist_ok=True)
@@ -231,7 +295,12 @@ def write_folder(scene, folder, name="synth", nk=5, cfg_overrides=None):
     return folder
 
 
-def make_config(config, folder, **kw):
+def make_config(config, folder, network="grid", **kw):
+    """BASELINE.json configs 3-5; network="convergent": the same image / tie-point counts as a
+    convergent network (generate_convergent, seed 2000 + config)."""
     n_img, n_tie = CONFIGS[config]
-    scene = generate(n_img, n_tie, seed=1000 + config, **kw)
+    if network == "convergent":
+        scene = generate_convergent(n_img, n_tie, seed=2000 + config, **kw)
+    else:
+        scene = generate(n_img, n_tie, seed=1000 + config, **kw)
     return write_folder(scene, folder)

@@ -79,6 +79,19 @@ def test_config3_fallback_paths_match_oracle(fba, fbo, oracle, scenes, env, monk
     _check_adjust(fba, fbo, oracle, _scene(3, scenes))
 
 
+def test_convergent_config3_adjust_matches_oracle(fba, fbo, oracle, scenes):
+    """config 3's counts (200 images x 5,000 tie points) as a convergent network (synth.
+    generate_convergent: every tie point seen by 10 images drawn from the whole block, the reference's
+    close-range setting): a dense reduced camera system, so the factorisation takes its dense-chain,
+    MFMA-throughput form.  Whole adjustment against the C oracle's direct bordered solve."""
+    from fba_amd import synth
+    folder = os.path.join(scenes, "c3_convergent")
+    if not os.path.exists(os.path.join(folder, ".done")):
+        synth.make_config(3, folder, network="convergent")
+        open(os.path.join(folder, ".done"), "w").close()
+    _check_adjust(fba, fbo, oracle, folder)
+
+
 def test_control_points_adjust_matches_oracle(fba, fbo, oracle, tmp_path):
     """No inner constraints: 40 control points fix the datum (the cam0 configuration, at scale)."""
     from fba_amd import synth
@@ -191,3 +204,47 @@ def test_config5_properties(fba, scenes):
     assert abs(res.sigma02 - 1.0) <= 0.05, res.sigma02
     assert np.isfinite(res.xhat).all()
     assert np.isfinite(res.cx_diag).all() and (res.cx_diag > 0).all()  # fba_covariance at 2M image points
+
+
+def test_config4_two_rank_shards_match_single_context(fba, scenes):
+    """The multi-GPU split at the bench scene: two rank contexts (fba_partition's tie-point shards) on
+    one GPU, their compact reduce buffers (~6 MB: co-visible image-pair blocks, diagonal blocks,
+    camera rows, RHS row) summed on the host as the RCCL all-reduce would, reproduce the single
+    context's iterates to 1e-10 over two Gauss-Newton passes; the deltasum shares add up to the
+    single context's deltasum."""
+    import ctypes
+    folder = _scene(4, scenes)
+    ds = fba.load_folder(folder)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    mk = lambda **kw: fba.capi.Context(ds.pack(), fba.capi.make_settings(ds.settings), **kw)  # noqa: E731
+    single = mk()
+    ranks = [mk(rank=r, world=2) for r in range(2)]
+    try:
+        d_first = None
+        for _ in range(2):
+            d1 = single.step()
+            d_first = d_first or d1
+            for c in ranks:
+                c.accumulate()
+                c.synchronize()
+            bufs = [c.reduce_buffer() for c in ranks]
+            assert bufs[0][1] == bufs[1][1] and bufs[0][1] * 8 < 16e6
+            total = np.zeros(bufs[0][1])
+            for p, n in bufs:
+                a = np.empty(n)
+                assert hip.hipMemcpy(a.ctypes.data, p, n * 8, 2) == 0
+                total += a
+            for p, n in bufs:
+                assert hip.hipMemcpy(p, total.ctypes.data, n * 8, 1) == 0
+            parts = [c.solve_update() for c in ranks]
+            assert abs(sum(parts) - d1) <= 1e-9 * d_first
+        xs = single.get_xhat()
+        xr = sum(c.get_xhat(owned_only=True) for c in ranks)
+        od_dsc = dist_scaling_of(__import__("fba_oracle").load_folder(folder))
+        err = group_rel_err(xr, xs, fba.xhat_names(ds), od_dsc)
+        assert max(err.values()) <= 1e-10, err
+    finally:
+        single.close()
+        for c in ranks:
+            c.close()
