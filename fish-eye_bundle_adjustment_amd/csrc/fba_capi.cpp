@@ -160,7 +160,7 @@ static void partition(const fba_problem* p, int world, std::vector<int32_t>& tie
 
 static void destroy(Ctx* c) {
     if (!c) return;
-    void* ptrs[] = {c->d_chunk_obs, c->d_chunk_pt, c->d_xy, c->d_img, c->d_cam, c->d_pt, c->d_ctl, c->d_lp_tie, c->d_lp_start, c->d_lp_cam,
+    void* ptrs[] = {c->d_chunk_obs, c->d_chunk_pt, c->d_xy, c->d_img, c->d_cam, c->d_pt, c->d_ctl, c->d_lp_tie, c->d_xoff, c->d_lrt, c->d_lp_start, c->d_lp_cam,
                     c->d_acc, c->d_ppart, c->d_ipart, c->d_cpart, c->d_cseg, c->d_bscr, c->d_gblk, c->d_lrprof, c->d_ptrace, c->d_gpairs, c->d_red, c->d_xfull, c->d_xlin, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
                     c->d_pt_tab, c->d_P, c->d_flags, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
                     c->d_active, c->d_counted, c->d_obs_pho, c->d_sched, c->d_gpt, c->d_gcu, c->d_gug, c->d_xpart,
@@ -657,6 +657,16 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     std::vector<int32_t> lp_tie(lps.begin(), lps.end());
     lp_tie.insert(lp_tie.end(), gps.begin(), gps.end());
     std::vector<double> caminfo(p->cam_info, p->cam_info + 5 * (size_t)L.n_cam);
+    // k_lin_reduce reads the observation's point coordinates at xfull[xoff] (one gather level fewer than
+    // pt -> lp_tie -> xfull, so the next chunk's inputs can be in flight behind the current chunk)
+    std::vector<int32_t> xoff(pt.size(), 0);
+    for (size_t o = 0; o < pt.size(); ++o)
+        if (pt[o] >= 0) xoff[o] = (int32_t)(L.u_c + 3 * (int64_t)lp_tie[pt[o]]);
+    if ((rc = upload(&c->d_xoff, xoff)) || (rc = dalloc(&c->d_lrt, 2)) ||
+        hipMemset(c->d_lrt, 0, 2 * sizeof(unsigned)) != hipSuccess) {
+        destroy(c);
+        return rc ? rc : FBA_ERR_HIP;
+    }
     if ((rc = upload(&c->d_xy, xy)) || (rc = upload(&c->d_img, img)) || (rc = upload(&c->d_cam, cam)) ||
         (rc = upload(&c->d_pt, pt)) || (rc = upload(&c->d_ctl, ctl)) || (rc = upload(&c->d_lp_tie, lp_tie)) ||
         (rc = upload(&c->d_lp_start, lp_start)) || (rc = upload(&c->d_lp_cam, lp_cam)) ||

@@ -186,6 +186,8 @@ struct Ctx {
     int32_t* d_pt = nullptr;     // [n_obs] local point (>=0) or -1-ctl
     double* d_ctl = nullptr;     // [3*n_ctl] fixed XYZ of control observations
     int32_t* d_lp_tie = nullptr; // [n_lp] global tie index of local point
+    int32_t* d_xoff = nullptr;   // [n_obs] offset of the observation's tie point in xfull (u_c + 3 tie; 0: control)
+    unsigned* d_lrt = nullptr;   // k_lin_reduce's work tickets [2]: next item, workgroups out (reset by the last out)
     int32_t* d_lp_start = nullptr;   // [n_lp+1] obs range of each local point
     int32_t* d_lp_cam = nullptr;     // [n_lp] camera of each local point
     int64_t n_chunks = 0;            // chunks: [k_lin_reduce's: whole regular tie points of one camera,

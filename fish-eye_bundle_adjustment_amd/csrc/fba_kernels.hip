@@ -449,7 +449,8 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     const int32_t* __restrict__ A, const AccPlan plan, double* __restrict__ WT, double* __restrict__ PT,
     double* __restrict__ ppart, double* __restrict__ ipart, double* __restrict__ cpart, int64_t u_c, int type,
     int cam_stride, unsigned eop_mask, unsigned cam_mask, double px, double py, uint64_t* __restrict__ tprof, int dbg,
-    int n_chunks, double* __restrict__ S, int64_t ld, const int32_t* __restrict__ zblk) {
+    int n_chunks, double* __restrict__ S, int64_t ld, const int32_t* __restrict__ zblk,
+    const int32_t* __restrict__ xoff) {
     using LY = Lay<NK>;
     using R_ = LR<NK>;
     if ((int)blockIdx.x >= n_chunks) {  // tail workgroups: zero one 128x128 block of the factor's pattern
@@ -530,19 +531,14 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     int p = -1;
     // (A)
     if (active) {
-        const double x = xy[2 * (int64_t)o], y = xy[2 * (int64_t)o + 1];
-        const int e = img[o], k = cam[o];
+        // (the point's coordinates at xfull[xoff[o]]: one gather level fewer than pt -> lp_tie -> xfull)
+        const double2 xyv = *reinterpret_cast<const double2*>(xy + 2 * (int64_t)o);
+        const int e = img[o], k = cam[o], xo = xoff[o];
         p = pt[o];
-        double X, Y, Z;
-        if (p >= 0) {
-            const double* q = xfull + u_c + 3 * (int64_t)lp_tie[p];
-            X = q[0]; Y = q[1]; Z = q[2];
-        } else {
-            const double* q = ctl + 3 * (int64_t)(-1 - p);
-            X = q[0]; Y = q[1]; Z = q[2];
-        }
-        obs_model<NK>(x, y, img_tab + (int64_t)e * IMG_TAB, cam_tab + (int64_t)k * cam_stride, X, Y, Z, p >= 0, type,
-                      eop_mask, cam_mask, jr, w0, w1);
+        const double* q = p >= 0 ? xfull + xo : ctl + 3 * (int64_t)(-1 - p);
+        const double X = q[0], Y = q[1], Z = q[2];
+        obs_model<NK>(xyv.x, xyv.y, img_tab + (int64_t)e * IMG_TAB, cam_tab + (int64_t)k * cam_stride, X, Y, Z, p >= 0,
+                      type, eop_mask, cam_mask, jr, w0, w1);
         if (p >= 0) {
             double* q = QE + t * ES;  // Jp (2x3) | w (2) | Jc (2xCW), raw
 #pragma unroll
@@ -1452,7 +1448,7 @@ int launch_accumulate(Ctx& c, bool zeroed) {
         c.d_chunk_obs, c.d_chunk_pt, c.d_lp_start, c.d_acc, c.acc, c.d_WT, c.d_pt_tab, c.d_ppart, c.d_ipart,       \
         c.d_cpart, c.L.u_c, c.set.type, c.cam_tab_stride, em, cm, px, py, c.d_lrprof,                              \
         c.d_lrprof && getenv("FBA_LR_SKIP") ? atoi(getenv("FBA_LR_SKIP")) : 0, (int)nlr, c.d_S, L.ld,              \
-        c.d_sched + c.sched.zero);                                                                                \
+        c.d_sched + c.sched.zero, c.d_xoff);                                                                      \
     {                                                                                                             \
         const int npb = (int)((c.n_pairs + 3) / 4), nib = (L.n_img + 1) / 2, ncb = (L.n_cam * CAM_SEG + 1) / 2;   \
         k_red_blocks<NKV><<<(unsigned)(npb + nib + ncb), 256, 0, c.stream>>>(                                     \

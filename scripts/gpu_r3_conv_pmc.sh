@@ -11,3 +11,6 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$PWD/gpur
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$PWD/gpurun_out/conv_write" -o run -- $B > gpurun_out/conv_write.log 2>&1 || exit $?
 timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$PWD/gpurun_out/conv_mfma" -o run -- $B > gpurun_out/conv_mfma.log 2>&1 || exit $?
 echo done
+# k_chol_flow per-record timeline at config 4 (FBA_PANEL_TRACE=2: eager launches, one step traced)
+FBA_PANEL_TRACE=2 timeout -k 10 200 python bench.py --steps 1 --warmup 1 --no-cpu > gpurun_out/flow_trace_c4.log 2>&1 || exit $?
+echo traced
