@@ -22,5 +22,12 @@ for step in "$@"; do
     pmc) cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
           run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$PWD/gpurun_out/pmc_fetch" -o run -- python bench.py --steps 2 --warmup 1 --no-cpu
           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$PWD/gpurun_out/pmc_write" -o run -- python bench.py --steps 2 --warmup 1 --no-cpu ;;
+    conv) run conv 600 python bench.py --network convergent --steps 5 --warmup 1 --no-cpu --verbose ;;
+    convprof) cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+          run convprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/convprof" -o run -- python bench.py --network convergent --steps 3 --warmup 1 --no-cpu ;;
+    covprof) cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+          run covprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/covprof" -o run -- python scripts/cov_time.py 4 ;;
+    c3) run bench_c3 400 python bench.py --config 3 --steps 10 --warmup 2 --no-cpu ;;
+    c5) run bench_c5 400 python bench.py --config 5 --steps 10 --warmup 2 --no-cpu ;;
   esac
 done
