@@ -164,7 +164,7 @@ static void destroy(Ctx* c) {
                     c->d_acc, c->d_ppart, c->d_ipart, c->d_cpart, c->d_cseg, c->d_bscr, c->d_gblk, c->d_lrprof, c->d_ptrace, c->d_gpairs, c->d_red, c->d_xfull, c->d_xlin, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
                     c->d_pt_tab, c->d_P, c->d_flags, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
                     c->d_active, c->d_counted, c->d_obs_pho, c->d_sched, c->d_gpt, c->d_gcu, c->d_gug, c->d_xpart,
-                    c->d_kpart};
+                    c->d_kpart, c->d_dynargs};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
@@ -877,8 +877,8 @@ static void print_flow_trace(Ctx* c) {
         for (int b = 0; b < s.flow_n; ++b) {
             const uint64_t* r = &t[FTRACE * (size_t)b];
             const int32_t* rec = recs + (size_t)Sched::FLOW_REC * b;
-            fprintf(stderr, "[fba] rec %d %d %d %d %d %.2f %.2f %.2f\n", b, rec[0], rec[1], rec[2], rec[3], us(r[0]),
-                    us(r[1]), us(r[2]));
+            fprintf(stderr, "[fba] rec %d %d %d %d %d %.2f %.2f %.2f %.2f %.2f\n", b, rec[0], rec[1], rec[2], rec[3], us(r[0]),
+                    us(r[1]), us(r[2]), us(r[48]), us(r[49]));
         }
     for (int b = 0; b < s.flow_n; ++b) {
         const uint64_t* r = &t[FTRACE * (size_t)b];
@@ -918,6 +918,19 @@ static void print_flow_trace(Ctx* c) {
             fprintf(stderr, "[fba]       split helper wg %5d: start %.1f block in LDS / applied:", x, us(q[0]));
             for (int u = 0; u < 8; ++u) fprintf(stderr, " %.1f/%.1f", us(q[8 + u]), us(q[16 + u]));
             fprintf(stderr, "  end %.1f\n", us(q[2]));
+        }
+    }
+    if (c->flow_dyn) {  // the dynamic dispatch's final state: every trigger received, every slot taken
+        const int n = s.flow_dyn_n;
+        std::vector<unsigned> st(2 * (size_t)n + 2);
+        if (hipMemcpy(st.data(), c->d_dyn, st.size() * sizeof(unsigned), hipMemcpyDeviceToHost) == hipSuccess) {
+            const int32_t* info = s.buf.data() + s.flow_dyn_info;
+            int bad = 0;
+            for (int r = 0; r < n; ++r)
+                if (st[r] != (unsigned)info[8 * r] && bad++ < 10)
+                    fprintf(stderr, "[fba] dyn: record %d triggers %u of %d\n", r, st[r], info[8 * r]);
+            fprintf(stderr, "[fba] dyn: slots taken %u, records appended %u + %d at launch, of %d; %d incomplete\n",
+                    st[2 * n], st[2 * n + 1], s.flow_dyn_ninit, n, bad);
         }
     }
     fprintf(stderr, "[fba] flow: diag %d (last end %.1f), panel halves %d (%.1f), updates %d (%.1f), inverses %d (%.1f), "

@@ -1990,15 +1990,19 @@ __device__ __forceinline__ void fused_apply(const __amdgpu_buffer_rsrc_t rX, int
 // (fused_apply: all tiles, or with a split helper, rec[9] >= 0, those of tile columns < FLOW_CSPLIT);
 // then the late partials (the other sources of f's level, scratch quarters, slot order); then the potrf
 // on the LDS block, whose bulk waves add the helper's partial (scratch slot rec[10], flag rec[9]).
+// (at_potrf: called by every thread right before the potrf starts -- the dynamic dispatch's trigger of
+// the records that consume the block's published columns, FlowDyn)
+template <class AtPotrf>
 __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ rec,
                                           const int32_t* __restrict__ lists, double* __restrict__ dinv,
                                           double* __restrict__ scal, unsigned* __restrict__ colflags,
                                           unsigned* __restrict__ fl, const double* __restrict__ P,
-                                          double* __restrict__ smem, uint64_t* __restrict__ tr) {
+                                          double* __restrict__ smem, uint64_t* __restrict__ tr, AtPotrf&& at_potrf) {
     const int j = rec[1], f = rec[2];
     wait_list_sc1(lists + rec[3], rec[4], fl, scal);  // the final in-place writers of C_jj's quarters
     if (tr && threadIdx.x == 0) tr[1] = wall_clock64();
     if (f < 0 && rec[6] == 0) {
+        at_potrf();
         potrf_body<false>(S, ld, j, dinv, scal, nullptr, colflags + j, smem, tr ? tr + 16 : nullptr);
         return;
     }
@@ -2071,6 +2075,7 @@ __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, co
     }
     __syncthreads();  // the block final in LDS; the counters and buffers free
     if (tr && threadIdx.x == 0) tr[5] = wall_clock64();
+    at_potrf();
     potrf_body<false, true>(S, ld, j, dinv, scal, nullptr, colflags + j, smem, tr ? tr + 16 : nullptr,
                             rec[9] >= 0 ? P + (int64_t)rec[10] * 4096 : nullptr, rec[9] >= 0 ? fl + rec[9] : nullptr);
 #undef AT
@@ -2255,30 +2260,79 @@ constexpr size_t FLOW_LDS = FLOW_LDS_A > FLOW_LDS_B ? FLOW_LDS_A : FLOW_LDS_B;
 static_assert(FLOW_LDS + 16 <= 160 * 1024, "k_chol_flow LDS (+ the static ticket word)");
 static_assert(SYRKW_LDS >= sizeof(double) * 128 * LDW + 2 * sizeof(int), "syrk_flow_body broadcast words");
 
-__global__ __launch_bounds__(POTRF_THREADS) void k_chol_flow(double* __restrict__ S, int64_t ld,
-                                                             const int32_t* __restrict__ lists,
-                                                             const int32_t* __restrict__ recs,
-                                                             double* __restrict__ dinv, double* __restrict__ linv,
-                                                             double* __restrict__ scal, unsigned* __restrict__ colflags,
-                                                             unsigned* __restrict__ fl, unsigned* __restrict__ cnt,
-                                                             double* __restrict__ P, uint64_t* __restrict__ trace,
-                                                             double* __restrict__ gblk, unsigned* __restrict__ ticket) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    // the record comes from an atomic ticket, not from blockIdx: tickets follow the order in which the
-    // workgroups really start, and every record waits only for records of smaller index (build_flow's
-    // order check), so each wait points to a workgroup that has already started and is resident (or
-    // done) -- progress does not depend on the hardware dispatching blockIdx in order, nor on every
-    // record being co-resident (a second process on the GPU only slows it down)
-    __shared__ int s_ticket;
-    if (threadIdx.x == 0) s_ticket = (int)__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const int rid = s_ticket;
+// Dynamic dispatch of k_chol_flow's records (FlowDyn, fba_order.cpp build_flow): one workgroup per record;
+// when it starts, a workgroup takes the next slot of a FIFO of READY records (one atomic add, then a poll of
+// that slot, written once -- the flag hand-off of every other wait in this file).  A record becomes ready
+// when every producer has triggered it: a "start" producer at its own claim (a diagonal block: when its
+// potrf starts), a "done" producer at its end; the trigger that completes the count appends the record to
+// the FIFO.  Records consume their producers' output progressively (flags), so a start trigger only means
+// the producer is running -- resident and progressing -- and every wait of a claimed record points to a
+// running or finished record: the earliest unfinished record in any topological order has only finished
+// producers, so the launch always progresses whatever the number of resident workgroups (as many
+// workgroups as records, and every record is appended exactly once, so each slot is filled).  The
+// records ready at launch come first, in priority order (the longest remaining path, host estimate).
+// (FBA_FLOW_DYN=0: the static order -- one record per workgroup in ticket order, each holding its CU from
+// dispatch to end; update tasks of later levels dispatched early then hold most CUs while the middle
+// levels' diagonal blocks wait for one.)  A bitmap of ready records scanned by the starting workgroups
+// was measured unusable: polled words that many workgroups keep changing by atomics read stale for up to
+// ~0.5 s, and the workgroups racing for the same bit serialise.
+struct FlowDyn {
+    const int32_t* info;    // [n][8]: need, -, consumer offset, start consumers, done consumers
+    const int32_t* cons;    // consumer record ids (start consumers first)
+    const int32_t* init;    // [n_init] the records ready at launch (no producer), priority order
+    unsigned* cnt;          // [n] triggers received        } zeroed by k_border_rhs
+    unsigned* ring;         // [n] FIFO slots: record + 1   } ahead of every
+    unsigned* head;         // [1] slots taken              } factorisation
+    unsigned* tail;         // [1] records appended         }
+    int n, n_init;
+};
+
+// the consumers [first, first + count) of record r's list: one thread each, any thread count
+__device__ __forceinline__ void dyn_trigger(const FlowDyn& d, int r, int first, int count, uint64_t* __restrict__ trace) {
+    const int off = d.info[8 * r + 2] + first;
+    for (int i = threadIdx.x; i < count; i += blockDim.x) {
+        const int c = d.cons[off + i];
+        const unsigned old = __hip_atomic_fetch_add(d.cnt + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old + 1 == (unsigned)d.info[8 * c]) {
+            const unsigned slot = d.n_init + __hip_atomic_fetch_add(d.tail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(d.ring + slot, (unsigned)c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (trace) trace[FTRACE * (int64_t)c + 49] = wall_clock64();  // FBA_PANEL_TRACE: ready
+        }
+    }
+}
+
+// thread 0: the record of this workgroup's FIFO slot (-1: the slot stayed empty within the bounded wait)
+__device__ __forceinline__ int dyn_claim(const FlowDyn& d, double* __restrict__ scal) {
+    const unsigned s = __hip_atomic_fetch_add(d.head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (s < (unsigned)d.n_init) return d.init[s];
+    if (s >= (unsigned)d.n) return -1;
+    unsigned spins = 0, v;
+    while ((v = __hip_atomic_load(d.ring + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins == FLAG_SPINS) { scal[1] = -1.0; return -1; }
+    }
+    return (int)v - 1;
+}
+
+__device__ __forceinline__ void flow_record(int rid, double* __restrict__ S, int64_t ld, const int32_t* __restrict__ lists,
+                                            const int32_t* __restrict__ recs, double* __restrict__ dinv,
+                                            double* __restrict__ linv, double* __restrict__ scal,
+                                            unsigned* __restrict__ colflags, unsigned* __restrict__ fl,
+                                            unsigned* __restrict__ cnt, double* __restrict__ P,
+                                            uint64_t* __restrict__ trace, double* __restrict__ gblk,
+                                            const FlowDyn* __restrict__ dyp, double* __restrict__ smem) {
     const int32_t* rec = recs + Sched::FLOW_REC * (int64_t)rid;
     uint64_t* tr = trace ? trace + FTRACE * (int64_t)rid : nullptr;
     if (tr && threadIdx.x == 0) tr[0] = wall_clock64();
     const int role = rec[0];
+    // (dyp: the dynamic dispatch's state, read from memory where needed so it holds no registers across
+    // the record bodies)
+    // start triggers: at the claim, except a diagonal block's (when its potrf starts)
+    if (dyp && role != 0) dyn_trigger(*dyp, rid, 0, dyp->info[8 * rid + 3], trace);
     if (role == 0) {
-        diag_body(S, ld, rec, lists, dinv, scal, colflags, fl, P, smem, tr);
+        diag_body(S, ld, rec, lists, dinv, scal, colflags, fl, P, smem, tr, [&]() {
+            if (dyp) dyn_trigger(*dyp, rid, 0, dyp->info[8 * rid + 3], trace);
+        });
     } else if (role == 1) {
         wait_list_sc1(lists + rec[3], rec[4], fl, scal);  // the final writers of the panel block's quarters
         if (tr && threadIdx.x == 0) tr[1] = wall_clock64();
@@ -2295,6 +2349,10 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_chol_flow(double* __restrict_
         __syncthreads();
         trtri_body(S, ld, rec[1], dinv, linv, smem);
     }
+    if (dyp) {  // done triggers (after every wave's part of the record)
+        __syncthreads();
+        dyn_trigger(*dyp, rid, dyp->info[8 * rid + 3], dyp->info[8 * rid + 4], trace);
+    }
     if (tr) {
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -2302,6 +2360,35 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_chol_flow(double* __restrict_
             tr[3] = (uint64_t)role | ((uint64_t)(uint32_t)rec[1] << 8) | ((uint64_t)(uint32_t)rec[2] << 32);
         }
     }
+}
+
+__global__ __launch_bounds__(POTRF_THREADS) void k_chol_flow(double* __restrict__ S, int64_t ld,
+                                                             const int32_t* __restrict__ lists,
+                                                             const int32_t* __restrict__ recs,
+                                                             double* __restrict__ dinv, double* __restrict__ linv,
+                                                             double* __restrict__ scal, unsigned* __restrict__ colflags,
+                                                             unsigned* __restrict__ fl, unsigned* __restrict__ cnt,
+                                                             double* __restrict__ P, uint64_t* __restrict__ trace,
+                                                             double* __restrict__ gblk, unsigned* __restrict__ ticket,
+                                                             const FlowDyn* __restrict__ dyp) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    __shared__ int s_ticket;
+    const uint64_t t_wg = trace ? wall_clock64() : 0;
+    if (dyp) {  // dynamic dispatch: this workgroup runs the record of its FIFO slot
+        if (threadIdx.x == 0) s_ticket = dyn_claim(*dyp, scal);
+    } else if (threadIdx.x == 0) {
+        // static order: the record comes from an atomic ticket, not from blockIdx: tickets follow the
+        // order in which the workgroups really start, and every record waits only for records of smaller
+        // index (build_flow's order check), so each wait points to a workgroup that has already started
+        // and is resident (or done) -- progress does not depend on the hardware dispatching blockIdx in
+        // order, nor on every record being co-resident
+        s_ticket = (int)__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const int rid = s_ticket;
+    if (rid < 0) return;
+    if (trace && threadIdx.x == 0) trace[FTRACE * (int64_t)rid + 48] = t_wg;
+    flow_record(rid, S, ld, lists, recs, dinv, linv, scal, colflags, fl, cnt, P, trace, gblk, dyp, smem);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2571,7 +2658,8 @@ int launch_cholesky(Ctx& c) {
         if (pp) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
         k_chol_flow<<<(unsigned)s.flow_n, POTRF_THREADS, FLOW_LDS, c.stream>>>(
             c.d_S, ld, c.d_sched, c.d_sched + s.flow_rec, c.d_dinv, c.d_linv, c.d_scal, c.d_flags, c.d_tflags,
-            c.d_counters, c.d_P, c.d_ptrace, c.set.inner_constraints ? c.d_gblk : nullptr, c.d_tickets);
+            c.d_counters, c.d_P, c.d_ptrace, c.set.inner_constraints ? c.d_gblk : nullptr, c.d_tickets,
+            c.flow_dyn ? reinterpret_cast<const FlowDyn*>(c.d_dynargs) : nullptr);
         if (pp) {
             FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], c.stream));
             c.probe_flops += s.flow_flops;
@@ -2750,13 +2838,35 @@ int chol_setup(Ctx& c) {
     c.flags_bytes = (size_t)((c.L.n_pad / CB + 1 + 3) / 4 * 4) * sizeof(unsigned);
     const size_t nf = c.flags_bytes / sizeof(unsigned);
     // [flags][bflags][split-target counters][update flags][2 tickets: k_chol_flow, k_bwd_flow]
-    c.n_sync = (int64_t)(2 * nf + std::max(c.sched.n_counters, 1) + std::max(c.sched.n_tflags, 1) + 2);
+    // [flags][bflags][split-target counters][update flags][2 tickets: k_chol_flow, k_bwd_flow]
+    // [dynamic dispatch: triggers per record, FIFO slots, head, tail]
+    // FBA_FLOW_DYN=1: k_chol_flow's records by dynamic dispatch (FlowDyn) instead of the static ticket
+    // order; measured at config 4 (k_chol_flow per launch, FBA_DYN_EAGER = 0 / 1 / 2 / 4 / all): 661 / 545 /
+    // 519 / 515 / 559 us vs 466 us static -- the static order's level priorities beat FIFO-of-ready dispatch
+    c.flow_dyn = getenv("FBA_FLOW_DYN") && atoi(getenv("FBA_FLOW_DYN")) != 0 && c.sched.flow_dyn_n > 0;
+    const int64_t ndyn = c.flow_dyn ? 2 * (int64_t)c.sched.flow_dyn_n + 2 : 0;
+    c.n_sync = (int64_t)(2 * nf + std::max(c.sched.n_counters, 1) + std::max(c.sched.n_tflags, 1) + 2) + ndyn;
     FBA_HIP(hipMalloc((void**)&c.d_flags, sizeof(unsigned) * c.n_sync));
     FBA_HIP(hipMemset(c.d_flags, 0, sizeof(unsigned) * c.n_sync));
     c.d_bflags = c.d_flags + nf;
     c.d_counters = c.d_bflags + nf;
     c.d_tflags = c.d_counters + std::max(c.sched.n_counters, 1);
     c.d_tickets = c.d_tflags + std::max(c.sched.n_tflags, 1);
+    c.d_dyn = c.flow_dyn ? c.d_tickets + 2 : nullptr;
+    if (c.flow_dyn) {  // the dispatch state's addresses, uploaded once
+        FlowDyn dy{};
+        dy.info = c.d_sched + c.sched.flow_dyn_info;
+        dy.cons = c.d_sched + c.sched.flow_dyn_cons;
+        dy.init = c.d_sched + c.sched.flow_dyn_init;
+        dy.cnt = c.d_dyn;
+        dy.ring = dy.cnt + c.sched.flow_dyn_n;
+        dy.head = dy.ring + c.sched.flow_dyn_n;
+        dy.tail = dy.head + 1;
+        dy.n = c.sched.flow_dyn_n;
+        dy.n_init = c.sched.flow_dyn_ninit;
+        FBA_HIP(hipMalloc(&c.d_dynargs, sizeof(FlowDyn)));
+        FBA_HIP(hipMemcpy(c.d_dynargs, &dy, sizeof(FlowDyn), hipMemcpyHostToDevice));
+    }
     FBA_HIP(hipFuncSetAttribute((const void*)k_bwd_flow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)BWD_LDS));
     c.bwd_flow = !(getenv("FBA_BWD_LEVELS") && atoi(getenv("FBA_BWD_LEVELS")) != 0);
     c.panel_progressive = !(getenv("FBA_PANEL_PROGRESSIVE") && atoi(getenv("FBA_PANEL_PROGRESSIVE")) == 0);

@@ -18,7 +18,7 @@ namespace fba {
 
 constexpr int NB = 128;       // Cholesky block size (rows/cols of one panel block, fba_chol.hip)
 constexpr int PTRACE_WG = 2048;  // FBA_PANEL_TRACE: workgroup slots per level
-constexpr int FTRACE = 48;       // FBA_PANEL_TRACE: stamps per k_chol_flow record
+constexpr int FTRACE = 56;       // FBA_PANEL_TRACE: stamps per k_chol_flow record ([48]: its workgroup's start)
 // k_chol_flow: a fused diagonal update's tiles of tile columns >= FLOW_CSPLIT go to a helper record,
 // added into the potrf's LDS block during its bulk step FLOW_CSPLIT - 2 (fba_order.cpp build_flow)
 constexpr int FLOW_CSPLIT = 3;
@@ -100,6 +100,10 @@ struct Sched {
     int flow_cnt[5] = {0, 0, 0, 0, 0};  // records per role
     bool flow_ok = false;
     double flow_flops = 0.0;
+    // dynamic dispatch of the records (k_chol_flow FlowDyn): per record [need, 0, consumer offset,
+    // start consumers, done consumers, 0, 0, 0], the consumer lists, the records ready at launch
+    int flow_dyn_n = 0, flow_dyn_ninit = 0;
+    int64_t flow_dyn_info = 0, flow_dyn_cons = 0, flow_dyn_init = 0;
 };
 
 // Accumulation plan (fba_capi.cpp create, run by k_lin_reduce and the k_red_* kernels): offsets
@@ -244,6 +248,9 @@ struct Ctx {
     unsigned* d_counters = nullptr; // [Sched::n_counters] split-target arrival counters
     unsigned* d_tflags = nullptr;   // [Sched::n_tflags] update-target completion flags (merged k_panel)
     unsigned* d_tickets = nullptr;  // [2] start-order tickets of k_chol_flow / k_bwd_flow records
+    unsigned* d_dyn = nullptr;      // k_chol_flow dynamic dispatch state (FlowDyn; zeroed with the flags)
+    void* d_dynargs = nullptr;      // the FlowDyn struct itself (device copy: its addresses)
+    bool flow_dyn = true;           // k_chol_flow records dispatched dynamically (FBA_FLOW_DYN=0: static order)
     int64_t n_sync = 0;           // unsigned words of flags + bflags + counters (one allocation at d_flags,
                                   // zeroed by k_border_rhs ahead of every factorisation)
     bool bwd_flow = true;

@@ -718,6 +718,81 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
             buf.insert(buf.end(), T[i].rec.begin(), T[i].rec.end());
             s.flow_cnt[T[i].rec[0]]++;
         }
+    // dynamic dispatch tables (k_chol_flow FlowDyn, record ids = positions in the static order).  Eager
+    // records (diagonal blocks, split helpers, panel halves feeding the next level or the RHS rows, update
+    // tasks whose target is read at the next level, late partials) become ready while their producers
+    // run: a panel half when its diagonal block's potrf starts, a diagonal block / update / helper when
+    // the panel halves it consumes are claimed, a diagonal block when its late partials are claimed.
+    // Everything else -- the in-place writer a record waits for at its start, and every producer of a
+    // lazy record (updates of later levels' targets, inverses) -- triggers at its end, so a lazy record
+    // holds no CU while it could only wait.  Priority: the longest path to the end (estimated us).
+    s.flow_dyn_n = 0;
+    if (ok && n > 0) {
+        auto B0 = [&](int i) { return buf[T[i].rec[4]]; };  // an update's first source column
+        // FBA_DYN_EAGER = D: a panel half (k, r) / an update of sources at level w is eager when its block
+        // row / target is read within D levels of its source's (the RHS rows: always)
+        static const int D = getenv("FBA_DYN_EAGER") ? atoi(getenv("FBA_DYN_EAGER")) : 1;
+        auto eager = [&](int i) {
+            const auto& r = T[i].rec;
+            switch (r[0]) {
+                case 0: case 4: return true;
+                case 1: { const int k = r[1], rr = r[2] >> 1; return rr == nb || level[rr] <= level[k] + D; }
+                case 2: {
+                    if (r[7] == 2) return true;  // a late partial
+                    const int a = r[1], b = r[2], w = level[B0(i)];
+                    return (a == b ? level[b] - 1 : (b == nb ? w : level[b])) - w <= D;
+                }
+                default: return false;
+            }
+        };
+        auto start_edge = [&](int d, int i) {
+            if (!eager(i)) return false;
+            if (T[d].rec[0] == 0) return T[i].rec[0] == 1;  // a panel half of the block: at its potrf's start
+            return true;  // consumed progressively, or waited for by a running record
+        };
+        auto dur = [&](int i) {
+            const auto& r = T[i].rec;
+            switch (r[0]) {
+                case 0: return r[2] >= 0 ? 28.0 : 18.0;
+                case 1: return 8.0;
+                case 2: return 2.0 + 4.0 * r[5];
+                case 4: return 10.0;
+                default: return 10.0;
+            }
+        };
+        std::vector<double> up(n, 0.0);
+        for (int q = n - 1; q >= 0; --q) {  // reverse topological order
+            const int i = ord[q];
+            double m = 0.0;
+            for (int x : succ[i]) m = std::max(m, up[x]);
+            up[i] = dur(i) + m;
+        }
+        std::vector<int> byprio(ord);  // descending priority, ties in the static order
+        std::stable_sort(byprio.begin(), byprio.end(), [&](int a, int b) { return up[a] > up[b]; });
+        const int64_t info = (int64_t)buf.size();
+        buf.resize(buf.size() + 8 * (size_t)n, 0);
+        std::vector<int32_t> cons;
+        for (int q = 0; q < n; ++q) {  // record q = ord[q]
+            const int i = ord[q];
+            std::vector<int32_t> st, dn;
+            for (int x : succ[i]) (start_edge(i, x) ? st : dn).push_back(pos[x]);
+            int32_t* e = &buf[info + 8 * (int64_t)q];
+            e[0] = (int32_t)T[i].deps.size();
+            e[2] = (int32_t)cons.size();
+            e[3] = (int32_t)st.size();
+            e[4] = (int32_t)dn.size();
+            cons.insert(cons.end(), st.begin(), st.end());
+            cons.insert(cons.end(), dn.begin(), dn.end());
+        }
+        s.flow_dyn_info = info;
+        s.flow_dyn_cons = (int64_t)buf.size();
+        buf.insert(buf.end(), cons.begin(), cons.end());
+        s.flow_dyn_init = (int64_t)buf.size();
+        s.flow_dyn_ninit = 0;
+        for (int i : byprio)
+            if (T[i].deps.empty()) { buf.push_back(pos[i]); s.flow_dyn_ninit++; }
+        s.flow_dyn_n = n;
+    }
     if (verbose)
         fprintf(stderr, "[fba] flow schedule: %d records (%d diagonal, %d panel halves, %d updates, %d inverses, "
                 "%d split helpers), %d progress + %d update flags, %d scratch quarters%s\n", n, s.flow_cnt[0],

@@ -335,9 +335,8 @@ int main(int argc, char** argv) {
         printf("FAIL factor err %.3e solve err %.3e\n", rel, xrel);
         return 1;
     }
-    // -- the persistent dataflow schedule (k_chol_flow): records run to completion in dispatch order
-    // (a valid execution, since every wait points to an earlier record); every flag a record waits for
-    // must already be raised --
+    // -- the persistent dataflow schedule (k_chol_flow): records run to completion in an order the
+    // dispatch can produce; every flag a record waits for must already be raised --
     if (!s.flow_ok) return fail("flow schedule order check");
     std::vector<double> F = M0;
     auto Fk = [&](int64_t i, int64_t j) { return &F[(size_t)(i * NB) * n + j * NB]; };
@@ -356,7 +355,70 @@ int main(int argc, char** argv) {
             }
     };
     if (s.flow_rec + (int64_t)Sched::FLOW_REC * s.flow_n > nbuf) return fail("flow record bounds");
-    for (int b = 0; b < s.flow_n; ++b) {
+    // -- the dynamic dispatch (k_chol_flow FlowDyn): W workers take FIFO slots of ready records (the
+    // records ready at launch first); a claimed record completes once every producer has completed (a
+    // diagonal block's start triggers fire then: its potrf start); no state may be stuck.  The completion
+    // order is a valid execution of the records and is emulated below like the static order --
+    std::vector<int> order;
+    if (s.flow_dyn_n > 0) {
+        const int nd = s.flow_dyn_n, W = 3 + seed % 29;
+        const int32_t* info = B + s.flow_dyn_info;
+        const int32_t* cons = B + s.flow_dyn_cons;
+        const int32_t* init = B + s.flow_dyn_init;
+        if (nd != s.flow_n) return fail("dyn: record count");
+        std::vector<int> cnt(nd, 0), pdone(nd, 0), started(nd, 0), fifo;
+        for (int q = 0; q < s.flow_dyn_ninit; ++q) {
+            if (init[q] < 0 || init[q] >= nd || info[8 * init[q]] != 0) return fail("dyn: initial ready list");
+            fifo.push_back(init[q]);
+        }
+        int nzero = 0;
+        for (int r = 0; r < nd; ++r) nzero += info[8 * r] == 0;
+        if (nzero != s.flow_dyn_ninit) return fail("dyn: initial ready count");
+        auto trig = [&](int r, int first, int count, bool completion) {
+            for (int i = 0; i < count; ++i) {
+                const int c = cons[info[8 * r + 2] + first + i];
+                if (++cnt[c] == info[8 * c]) fifo.push_back(c);
+                if (cnt[c] > info[8 * c]) return false;
+            }
+            if (completion)
+                for (int i = 0; i < info[8 * r + 3] + info[8 * r + 4]; ++i) pdone[cons[info[8 * r + 2] + i]]++;
+            return true;
+        };
+        std::vector<int> running;
+        size_t head = 0;
+        std::mt19937 pick(seed);
+        while ((int)order.size() < nd) {
+            bool prog = false;
+            while (head < fifo.size() && (int)running.size() < W) {
+                const int r = fifo[head++];
+                running.push_back(r);
+                if (B[s.flow_rec + (int64_t)Sched::FLOW_REC * r] != 0 && !trig(r, 0, info[8 * r + 3], false))
+                    return fail("dyn: trigger count");
+                prog = true;
+            }
+            for (int r : running)  // diagonal blocks whose producers are all complete start their potrf
+                if (!started[r] && B[s.flow_rec + (int64_t)Sched::FLOW_REC * r] == 0 && pdone[r] == info[8 * r]) {
+                    started[r] = 1;
+                    if (!trig(r, 0, info[8 * r + 3], false)) return fail("dyn: trigger count");
+                    prog = true;
+                }
+            std::vector<int> can;
+            for (size_t q = 0; q < running.size(); ++q)
+                if (pdone[running[q]] == info[8 * running[q]]) can.push_back((int)q);
+            if (!can.empty()) {
+                const int q = can[pick() % can.size()], r = running[q];
+                running.erase(running.begin() + q);
+                if (!trig(r, info[8 * r + 3], info[8 * r + 4], true)) return fail("dyn: trigger count");
+                order.push_back(r);
+                prog = true;
+            }
+            if (!prog) return fail("dyn: dispatch stuck (no ready record, no completable running record)");
+        }
+        if (fifo.size() != (size_t)nd) return fail("dyn: a record appended twice or never");
+    } else {
+        for (int b = 0; b < s.flow_n; ++b) order.push_back(b);
+    }
+    for (int b : order) {
         const int32_t* rec = B + s.flow_rec + (int64_t)Sched::FLOW_REC * b;
         if (rec[0] == 0) {
             const int64_t j = rec[1], f = rec[2];
