@@ -167,6 +167,8 @@ static void destroy(Ctx* c) {
                     c->d_kpart, c->d_dynargs};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
+    for (auto& w : c->ws)
+        if (w.first) (void)hipFree(w.first);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -1320,16 +1322,19 @@ int fba_covariance(fba_ctx* ctx, double sigma02, double* cx_diag, double* corr) 
         islot[e] = c->img_new[e];
         icam[e] = std::max(c->ref_img_cam[e], 0);
     }
-    auto release = [&]() {
-        for (void* q : {(void*)d_cdiag, (void*)d_pdiag, (void*)d_iblk, (void*)d_islot, (void*)d_icam})
-            if (q) (void)hipFree(q);
-    };
+    auto release = [&]() {};  // (the context's workspace slots 64..68, kept for the next call)
     int rc;
-    if ((rc = dalloc(&d_cdiag, (size_t)L.u_c)) || (rc = dalloc(&d_pdiag, 3 * (size_t)std::max(L.n_tie, 1))) ||
-        (corr && (rc = dalloc(&d_iblk, (size_t)std::max(L.n_img_ref, 1) * m * m))) || (rc = upload(&d_islot, islot)) ||
-        (rc = upload(&d_icam, icam))) {
-        release();
+    if ((rc = ws_get(*c, 64, sizeof(double) * std::max<int64_t>(L.u_c, 1), (void**)&d_cdiag)) ||
+        (rc = ws_get(*c, 65, sizeof(double) * 3 * (size_t)std::max(L.n_tie, 1), (void**)&d_pdiag)) ||
+        (corr && (rc = ws_get(*c, 66, sizeof(double) * (size_t)std::max(L.n_img_ref, 1) * m * m, (void**)&d_iblk))) ||
+        (rc = ws_get(*c, 67, sizeof(int32_t) * islot.size(), (void**)&d_islot)) ||
+        (rc = ws_get(*c, 68, sizeof(int32_t) * icam.size(), (void**)&d_icam))) {
         return rc;
+    }
+    if (hipMemcpyAsync(d_islot, islot.data(), sizeof(int32_t) * islot.size(), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemcpyAsync(d_icam, icam.data(), sizeof(int32_t) * icam.size(), hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+        set_error("hipMemcpyAsync failed");
+        return FBA_ERR_HIP;
     }
     if (hipMemsetAsync(d_pdiag, 0, sizeof(double) * 3 * std::max(L.n_tie, 1), c->stream) != hipSuccess) {
         release();

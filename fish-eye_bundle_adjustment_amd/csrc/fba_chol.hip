@@ -2425,16 +2425,18 @@ __device__ __forceinline__ double gemv_t128(const double* __restrict__ M, int64_
 // i = srcs[b] of the level, x_i = Linv_i' y_i (y_i is final: its contributions came from higher
 // levels).  Workgroup nsrc + t: target column j = tgts[t], y_j -= sum_i L(i,j)' x_i over its sources
 // (ascending; x_i recomputed locally from y_i, one 128x128 GEMV, instead of a second launch).
+// (blockIdx.y = r: right-hand-side row yrow + r, solution X + r xstride -- several rows per launch)
 __global__ __launch_bounds__(256) void k_bwd_wave(double* __restrict__ S, int64_t ld, int64_t yrow,
                                                   const double* __restrict__ linv, double* __restrict__ X,
                                                   const int32_t* __restrict__ srcs, int nsrc,
                                                   const int32_t* __restrict__ tgts, const int32_t* __restrict__ tstart,
-                                                  const int32_t* __restrict__ tsrc) {
+                                                  const int32_t* __restrict__ tsrc, int64_t xstride = 0) {
     __shared__ double ys[CB];
     __shared__ double xs[CB];
     __shared__ double red[512];
     const int tid = threadIdx.x;
-    double* y = S + yrow * ld;  // the right-hand-side row (n_pad: the solve; n_pad + a: border column a)
+    X += (int64_t)blockIdx.y * xstride;
+    double* y = S + (yrow + blockIdx.y) * ld;  // the right-hand-side row (n_pad: the solve; n_pad + a: border column a)
     if ((int)blockIdx.x < nsrc) {
         const int64_t i = srcs[blockIdx.x];
         if (tid < CB) ys[tid] = y[i * CB + tid];
@@ -2730,13 +2732,12 @@ int launch_cholesky(Ctx& c) {
 int launch_backward_rows(Ctx& c, int row0, int nrows, double* X) {
     const int64_t ld = c.L.ld;
     const Sched& s = c.sched;
-    for (int r = 0; r < nrows; ++r)
-        for (int w = s.n_waves - 1; w >= 0; --w) {
-            const Sched::BWave& B = s.b[w];
-            k_bwd_wave<<<(unsigned)(B.nsrc + B.ntgt), 256, 0, c.stream>>>(
-                c.d_S, ld, c.L.n_pad + row0 + r, c.d_linv, X + (int64_t)r * c.L.n_pad, c.d_sched + B.srcs, B.nsrc,
-                c.d_sched + B.tgts, c.d_sched + B.src_start, c.d_sched + B.src);
-        }
+    for (int w = s.n_waves - 1; w >= 0; --w) {  // all rows of a level in one launch
+        const Sched::BWave& B = s.b[w];
+        k_bwd_wave<<<dim3((unsigned)(B.nsrc + B.ntgt), (unsigned)nrows), 256, 0, c.stream>>>(
+            c.d_S, ld, c.L.n_pad + row0, c.d_linv, X, c.d_sched + B.srcs, B.nsrc, c.d_sched + B.tgts,
+            c.d_sched + B.src_start, c.d_sched + B.src, c.L.n_pad);
+    }
     FBA_HIP(hipGetLastError());
     return FBA_OK;
 }

@@ -25,6 +25,7 @@
 #include "fba_internal.h"
 
 #include <algorithm>
+#include <array>
 #include <vector>
 
 namespace fba {
@@ -32,37 +33,46 @@ namespace fba {
 constexpr int CB = NB;  // 128
 
 // ------------------------------------------------------------------------------------------------
-// k_blk_gemm: one workgroup per task, C(128x128) = sum_t sign_t op(A_t) op(B_t), terms in list order,
-// on v_mfma_f64_16x16x4_f64.  Operand/output bases: 0 = S (leading dimension ld), 1 = linv, 2 = Y
+// k_blk_gemm: one workgroup per PART of a task, C(128x128) = sum_t sign_t op(A_t) op(B_t), terms in list
+// order, on v_mfma_f64_16x16x4_f64.  Operand/output bases: 0 = S (leading dimension ld), 1 = linv, 2 = Y
 // scratch (both 128).  Four waves, each a 64x64 quarter of C as 4x4 MFMA tiles (64 accumulators per
 // lane); K in slices of 16 staged through LDS (rows padded to 17 doubles: the 16 lanes of an MFMA
 // operand read hit distinct banks), the next slice's global loads in flight during the current
-// slice's MFMAs.  Fixed order: terms in list order, K ascending -- bitwise reproducible.
+// slice's MFMAs.  A phase of the selected inversion has few tasks at the top levels (one per block row
+// of a separator column), each with many terms, so a task's slices are split into parts (split K) that
+// run on workgroups of their own: a part writes C directly (one part) or its partial to a scratch
+// block, and k_blk_combine adds a task's partials in part order.  Fixed order throughout -- bitwise
+// reproducible.
 // task record (int64): out offset, out base, first term, end term
 // term record (int64): A offset, B offset, flags = baseA | baseB << 2 | tA << 4 | tB << 5 | neg << 6
+// part record (int64): task, first slice, end slice (slice = term * 8 + K block), scratch slot (-1: C)
+// combine record (int64): task, first slot, slots
 // ------------------------------------------------------------------------------------------------
 constexpr int KS = 16;
 constexpr int LK = KS + 1;
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(256) void k_blk_gemm(const int64_t* __restrict__ tasks, const int64_t* __restrict__ terms,
-                                                  double* __restrict__ S, int64_t ld, const double* __restrict__ linv,
-                                                  double* __restrict__ Y) {
+__global__ __launch_bounds__(256) void k_blk_gemm(const int64_t* __restrict__ parts, const int64_t* __restrict__ tasks,
+                                                  const int64_t* __restrict__ terms, double* __restrict__ S, int64_t ld,
+                                                  const double* __restrict__ linv, double* __restrict__ Y,
+                                                  double* __restrict__ P) {
     __shared__ double As[CB * LK];  // op(A)[i][k0 + kk] at i * LK + kk (sign applied)
     __shared__ double Bs[CB * LK];  // op(B)[k0 + kk][j] at j * LK + kk
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lk = lane >> 4;
     const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
-    const int64_t* tk = tasks + 4 * (int64_t)blockIdx.x;
+    const int64_t* pk = parts + 4 * (int64_t)blockIdx.x;
+    const int64_t* tk = tasks + 4 * pk[0];
     dbl4 acc[4][4];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
-    const int64_t t0 = tk[2], t1 = tk[3];
-    const int nsl = (int)(t1 - t0) * (CB / KS);
-    // slice s = (term t0 + s / 8, k0 = 16 (s % 8)): 8 elements of each operand per thread
+    const int64_t t0 = tk[2];
+    const int sl0 = (int)pk[1], nsl = (int)(pk[2] - pk[1]);
+    // slice sl0 + s = (term t0 + (sl0 + s) / 8, k0 = 16 ((sl0 + s) % 8)): 8 elements of each operand per thread
     double va[8], vb[8];
     auto fetch = [&](int sl) {
+        sl += sl0;
         const int64_t* tr = terms + 3 * (t0 + sl / (CB / KS));
         const int k0 = (sl % (CB / KS)) * KS;
         const int fl = (int)tr[2];
@@ -105,14 +115,42 @@ __global__ __launch_bounds__(256) void k_blk_gemm(const int64_t* __restrict__ ta
                 for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
         }
     }
-    double* C = (tk[1] == 0 ? S : Y) + tk[0];
-    const int64_t ldc = tk[1] == 0 ? ld : CB;
+    double* C = pk[3] >= 0 ? P + pk[3] * CB * CB : (tk[1] == 0 ? S : Y) + tk[0];
+    const int64_t ldc = pk[3] < 0 && tk[1] == 0 ? ld : CB;
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) C[(int64_t)(wr + 16 * a + lk + 4 * r) * ldc + wc + 16 * b + lr] = acc[a][b][r];
+}
+
+// k_blk_combine: one workgroup per split task, C = P[first] + P[first + 1] + ... (part order)
+__global__ __launch_bounds__(256) void k_blk_combine(const int64_t* __restrict__ combs, const int64_t* __restrict__ tasks,
+                                                     double* __restrict__ S, int64_t ld, double* __restrict__ Y,
+                                                     const double* __restrict__ P) {
+    const int64_t* cb = combs + 3 * (int64_t)blockIdx.x;
+    const int64_t* tk = tasks + 4 * cb[0];
+    double* C = (tk[1] == 0 ? S : Y) + tk[0];
+    const int64_t ldc = tk[1] == 0 ? ld : CB;
+    const double2* Pp = reinterpret_cast<const double2*>(P + cb[1] * CB * CB);
+    constexpr int NQ = CB * CB / 2 / 256;
+    double2 acc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc[q] = Pp[threadIdx.x + 256 * q];
+    for (int64_t p = 1; p < cb[2]; ++p) {
+        const double2* Pq = Pp + p * CB * CB / 2;
+        double2 v[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) v[q] = Pq[threadIdx.x + 256 * q];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) { acc[q].x += v[q].x; acc[q].y += v[q].y; }
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int e = 2 * (threadIdx.x + 256 * q), r = e / CB, cc = e % CB;
+        *reinterpret_cast<double2*>(C + (int64_t)r * ldc + cc) = acc[q];
+    }
 }
 
 // H^-1 of the 14x14 border system (k_border_combine's H = [[A'A - I, A'B], [B'A, B'B]] from the Gram of
@@ -220,8 +258,8 @@ __global__ __launch_bounds__(256) void k_cov_img(const double* __restrict__ S, i
 }
 
 // tie points: one wave per local point.  Row groups g = 0..m-1 (observation g: 6 rows of its image,
-// T = WT[o]), g = m (the camera: cw rows, Tc).  Lane pairs (g, h) of groups add sum T_g' C_gh T_h
-// (diagonal of the 3x3 only); lanes a < nz add the border term (Z_a' T)(Wz_a' T).  Fixed-order
+// T = WT[o]), g = m (the camera: cw rows, Tc).  Lane pairs (g >= h) of groups add sum T_g' C_gh T_h
+// (diagonal of the 3x3 only, twice for g > h); lanes a < nz add the border term (Z_a' T)(Wz_a' T).  Fixed-order
 // wave reduction.
 __global__ __launch_bounds__(256) void k_cov_pts(const double* __restrict__ S, int64_t ld, const double* __restrict__ Z,
                                                  const double* __restrict__ Wz, int nz, int64_t n_pad,
@@ -242,8 +280,11 @@ __global__ __launch_bounds__(256) void k_cov_pts(const double* __restrict__ S, i
     };
     double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
     const int ng = m + 1;
-    for (int pr = lane; pr < ng * ng; pr += 64) {
-        const int g = pr / ng, h = pr % ng;
+    // pairs g >= h only: diag(T_g' C_gh T_h) = diag(T_h' C_hg T_g), so an off-diagonal pair counts twice
+    for (int pr = lane; pr < ng * (ng + 1) / 2; pr += 64) {
+        int g = 0, h = pr;
+        while (h > g) { h -= g + 1; ++g; }
+        const double wgt = g == h ? 1.0 : 2.0;
         int64_t r0, c0;
         int nr, nc;
         const double *Tg, *Th;
@@ -257,7 +298,7 @@ __global__ __launch_bounds__(256) void k_cov_pts(const double* __restrict__ S, i
                 const double q = S[rr * ld + cc];
                 s0 += q * Th[3 * b]; s1 += q * Th[3 * b + 1]; s2 += q * Th[3 * b + 2];
             }
-            acc0 += Tg[3 * a] * s0; acc1 += Tg[3 * a + 1] * s1; acc2 += Tg[3 * a + 2] * s2;
+            acc0 += wgt * Tg[3 * a] * s0; acc1 += wgt * Tg[3 * a + 1] * s1; acc2 += wgt * Tg[3 * a + 2] * s2;
         }
     }
     if (lane < nz) {
@@ -314,13 +355,10 @@ int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, 
     if ((rc = launch_trtri_last(c))) return rc;
     const int nz = L.nrhs > 1 ? 14 : 0;
     double *d_Z = nullptr, *d_Wz = nullptr, *d_h = nullptr, *d_g = nullptr;
-    std::vector<void*> tmp;
-    auto alloc = [&](double** p, size_t n) -> int {
-        FBA_HIP(hipMalloc((void**)p, sizeof(double) * std::max<size_t>(n, 1)));
-        tmp.push_back(*p);
-        return FBA_OK;
-    };
-    auto cleanup = [&]() { for (void* q : tmp) (void)hipFree(q); tmp.clear(); };
+    // scratch from the context's covariance workspace (kept across calls: no allocation per call)
+    int next_slot = 0;
+    auto alloc = [&](double** p, size_t n) -> int { return ws_get(c, next_slot++, sizeof(double) * std::max<size_t>(n, 1), (void**)p); };
+    auto cleanup = [&]() {};
     if (nz) {
         if ((rc = alloc(&d_Z, 14 * (size_t)n_pad)) || (rc = alloc(&d_Wz, 14 * (size_t)n_pad)) ||
             (rc = alloc(&d_h, 196)) || (rc = alloc(&d_g, 64 * 120))) { cleanup(); return rc; }
@@ -407,15 +445,49 @@ int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, 
         }
         phase(first);
     }
+    // split K: a phase's tasks split into parts of >= 4 slices so that the phase fills the chip (about
+    // one part per CU), the partials of a split task in scratch slots (reused by every phase)
+    std::vector<int64_t> parts, combs;
+    std::vector<std::array<int64_t, 4>> pph;  // per phase: first part, end part, first combine, end combine
+    int64_t max_slots = 0;
+    const int64_t target = (int64_t)std::max(c.n_cu, 1);
+    for (auto& ph : phases) {
+        const int64_t ntask = ph.second - ph.first;
+        const int64_t p0 = (int64_t)parts.size() / 4, c0 = (int64_t)combs.size() / 3;
+        int64_t slot = 0;
+        for (int64_t t = ph.first; t < ph.second; ++t) {
+            const int64_t nsl = (tasks[4 * t + 3] - tasks[4 * t + 2]) * (CB / KS);
+            const int64_t np = std::max<int64_t>(1, std::min<int64_t>((target + ntask - 1) / ntask, nsl / 4));
+            if (np == 1) {
+                parts.insert(parts.end(), {t, 0, nsl, -1});
+                continue;
+            }
+            combs.insert(combs.end(), {t, slot, np});
+            for (int64_t q = 0; q < np; ++q) parts.insert(parts.end(), {t, nsl * q / np, nsl * (q + 1) / np, slot++});
+        }
+        max_slots = std::max(max_slots, slot);
+        pph.push_back({p0, (int64_t)parts.size() / 4, c0, (int64_t)combs.size() / 3});
+    }
+    double* d_P = nullptr;
+    int64_t *d_parts = nullptr, *d_combs = nullptr;
     if ((rc = alloc((double**)&d_tasks, std::max<size_t>(tasks.size(), 1))) ||
-        (rc = alloc((double**)&d_terms, std::max<size_t>(terms.size(), 1)))) { cleanup(); return rc; }
+        (rc = alloc((double**)&d_terms, std::max<size_t>(terms.size(), 1))) ||
+        (rc = alloc((double**)&d_parts, std::max<size_t>(parts.size(), 1))) ||
+        (rc = alloc((double**)&d_combs, std::max<size_t>(combs.size(), 1))) ||
+        (rc = alloc(&d_P, (size_t)std::max<int64_t>(max_slots, 1) * CB * CB))) { cleanup(); return rc; }
     if (!tasks.empty()) {
         FBA_HIP(hipMemcpyAsync(d_tasks, tasks.data(), sizeof(int64_t) * tasks.size(), hipMemcpyHostToDevice, c.stream));
         FBA_HIP(hipMemcpyAsync(d_terms, terms.data(), sizeof(int64_t) * terms.size(), hipMemcpyHostToDevice, c.stream));
+        FBA_HIP(hipMemcpyAsync(d_parts, parts.data(), sizeof(int64_t) * parts.size(), hipMemcpyHostToDevice, c.stream));
+        if (!combs.empty())
+            FBA_HIP(hipMemcpyAsync(d_combs, combs.data(), sizeof(int64_t) * combs.size(), hipMemcpyHostToDevice, c.stream));
     }
-    for (auto& ph : phases)
-        k_blk_gemm<<<(unsigned)(ph.second - ph.first), 256, 0, c.stream>>>(d_tasks + 4 * ph.first, d_terms, c.d_S, ld,
-                                                                           c.d_linv, d_Y);
+    for (auto& ph : pph) {
+        k_blk_gemm<<<(unsigned)(ph[1] - ph[0]), 256, 0, c.stream>>>(d_parts + 4 * ph[0], d_tasks, d_terms, c.d_S, ld,
+                                                                   c.d_linv, d_Y, d_P);
+        if (ph[3] > ph[2])
+            k_blk_combine<<<(unsigned)(ph[3] - ph[2]), 256, 0, c.stream>>>(d_combs + 3 * ph[2], d_tasks, c.d_S, ld, d_Y, d_P);
+    }
     FBA_HIP(hipGetLastError());
 
     if (d_cdiag)

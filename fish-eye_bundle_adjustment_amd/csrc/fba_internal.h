@@ -294,7 +294,9 @@ struct Ctx {
     double probe_flops = 0.0;
     hipEvent_t ev[9] = {};
     double last_ms[8] = {0};
+    std::vector<std::pair<void*, size_t>> ws;  // reusable device scratch (fba_covariance), by slot
 };
+
 
 // error helpers
 void set_error(const std::string& msg);
@@ -307,6 +309,20 @@ void set_error(const std::string& msg);
             return FBA_ERR_HIP;                                                        \
         }                                                                              \
     } while (0)
+
+// device scratch slot `slot` of at least `bytes` (grown when needed, kept until fba_destroy)
+inline int ws_get(Ctx& c, int slot, size_t bytes, void** p) {
+    if ((int)c.ws.size() <= slot) c.ws.resize(slot + 1, {nullptr, 0});
+    auto& e = c.ws[slot];
+    if (e.second < bytes) {
+        if (e.first) (void)hipFree(e.first);
+        e = {nullptr, 0};
+        if (hipMalloc(&e.first, bytes) != hipSuccess) { set_error("hipMalloc failed (workspace)"); return FBA_ERR_HIP; }
+        e.second = bytes;
+    }
+    *p = e.first;
+    return FBA_OK;
+}
 
 // kernel launchers (fba_kernels.hip / fba_chol.hip)
 std::vector<int32_t> camera_order(const fba_problem* p);  // internal image slot -> EXT row or -1 (fba_order.cpp)
