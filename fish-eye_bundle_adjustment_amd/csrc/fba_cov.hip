@@ -69,27 +69,29 @@ __global__ __launch_bounds__(256) void k_blk_gemm(const int64_t* __restrict__ pa
         for (int b = 0; b < 4; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
     const int64_t t0 = tk[2];
     const int sl0 = (int)pk[1], nsl = (int)(pk[2] - pk[1]);
-    // slice sl0 + s = (term t0 + (sl0 + s) / 8, k0 = 16 ((sl0 + s) % 8)): 8 elements of each operand per thread
+    // slice sl0 + s = (term t0 + (sl0 + s) / 8, k0 = 16 ((sl0 + s) % 8)): 8 elements of each operand per
+    // thread, loaded one slice ahead (plain code, no lambda: captured register arrays went to scratch)
     double va[8], vb[8];
-    auto fetch = [&](int sl) {
-        sl += sl0;
-        const int64_t* tr = terms + 3 * (t0 + sl / (CB / KS));
-        const int k0 = (sl % (CB / KS)) * KS;
-        const int fl = (int)tr[2];
-        const int ba = fl & 3, bb = (fl >> 2) & 3, ta = (fl >> 4) & 1, tb = (fl >> 5) & 1;
-        const double sg = (fl >> 6) & 1 ? -1.0 : 1.0;
-        const double* A = (ba == 0 ? S : ba == 1 ? linv : Y) + tr[0];
-        const double* B = (bb == 0 ? S : bb == 1 ? linv : Y) + tr[1];
-        const int64_t lda = ba == 0 ? ld : CB, ldb = bb == 0 ? ld : CB;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int idx = tid + 256 * q;
-            va[q] = sg * (!ta ? A[(int64_t)(idx >> 4) * lda + k0 + (idx & 15)] : A[(int64_t)(k0 + (idx >> 7)) * lda + (idx & 127)]);
-            vb[q] = !tb ? B[(int64_t)(k0 + (idx >> 7)) * ldb + (idx & 127)] : B[(int64_t)(idx >> 4) * ldb + k0 + (idx & 15)];
-        }
-        return (ta ? 1 : 0) | (tb ? 2 : 0);
-    };
-    int tt = nsl > 0 ? fetch(0) : 0;
+    int tt = 0;
+#define BLK_FETCH(SL)                                                                                              \
+    do {                                                                                                           \
+        const int sl_ = (SL) + sl0;                                                                                \
+        const int64_t* tr = terms + 3 * (t0 + sl_ / (CB / KS));                                                    \
+        const int k0 = (sl_ % (CB / KS)) * KS;                                                                     \
+        const int fl = (int)tr[2];                                                                                 \
+        const int ba = fl & 3, bb = (fl >> 2) & 3, ta = (fl >> 4) & 1, tb = (fl >> 5) & 1;                         \
+        const double sg = (fl >> 6) & 1 ? -1.0 : 1.0;                                                              \
+        const double* A = (ba == 0 ? S : ba == 1 ? linv : Y) + tr[0];                                              \
+        const double* B = (bb == 0 ? S : bb == 1 ? linv : Y) + tr[1];                                              \
+        const int64_t lda = ba == 0 ? ld : CB, ldb = bb == 0 ? ld : CB;                                            \
+        _Pragma("unroll") for (int q = 0; q < 8; ++q) {                                                            \
+            const int idx = tid + 256 * q;                                                                         \
+            va[q] = sg * (!ta ? A[(int64_t)(idx >> 4) * lda + k0 + (idx & 15)] : A[(int64_t)(k0 + (idx >> 7)) * lda + (idx & 127)]); \
+            vb[q] = !tb ? B[(int64_t)(k0 + (idx >> 7)) * ldb + (idx & 127)] : B[(int64_t)(idx >> 4) * ldb + k0 + (idx & 15)]; \
+        }                                                                                                          \
+        tt = (ta ? 1 : 0) | (tb ? 2 : 0);                                                                          \
+    } while (0)
+    if (nsl > 0) BLK_FETCH(0);
     for (int sl = 0; sl < nsl; ++sl) {
         __syncthreads();  // the previous slice's MFMA reads are done
 #pragma unroll
@@ -101,7 +103,7 @@ __global__ __launch_bounds__(256) void k_blk_gemm(const int64_t* __restrict__ pa
             else Bs[(idx >> 4) * LK + (idx & 15)] = vb[q];
         }
         __syncthreads();
-        if (sl + 1 < nsl) tt = fetch(sl + 1);
+        if (sl + 1 < nsl) BLK_FETCH(sl + 1);
 #pragma unroll
         for (int kk = 0; kk < KS; kk += 4) {
             double av[4], bv[4];
@@ -115,6 +117,7 @@ __global__ __launch_bounds__(256) void k_blk_gemm(const int64_t* __restrict__ pa
                 for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
         }
     }
+#undef BLK_FETCH
     double* C = pk[3] >= 0 ? P + pk[3] * CB * CB : (tk[1] == 0 ? S : Y) + tk[0];
     const int64_t ldc = pk[3] < 0 && tk[1] == 0 ? ld : CB;
 #pragma unroll
@@ -125,7 +128,9 @@ __global__ __launch_bounds__(256) void k_blk_gemm(const int64_t* __restrict__ pa
             for (int r = 0; r < 4; ++r) C[(int64_t)(wr + 16 * a + lk + 4 * r) * ldc + wc + 16 * b + lr] = acc[a][b][r];
 }
 
-// k_blk_combine: one workgroup per split task, C = P[first] + P[first + 1] + ... (part order)
+// k_blk_combine: C = P[first] + P[first + 1] + ... (part order) for a split task; blockIdx.y = which
+// eighth of the 128 x 128 tile (16 rows), so a task split into many parts is summed by 8 workgroups
+constexpr int COMB_SEG = 8;
 __global__ __launch_bounds__(256) void k_blk_combine(const int64_t* __restrict__ combs, const int64_t* __restrict__ tasks,
                                                      double* __restrict__ S, int64_t ld, double* __restrict__ Y,
                                                      const double* __restrict__ P) {
@@ -133,8 +138,9 @@ __global__ __launch_bounds__(256) void k_blk_combine(const int64_t* __restrict__
     const int64_t* tk = tasks + 4 * cb[0];
     double* C = (tk[1] == 0 ? S : Y) + tk[0];
     const int64_t ldc = tk[1] == 0 ? ld : CB;
-    const double2* Pp = reinterpret_cast<const double2*>(P + cb[1] * CB * CB);
-    constexpr int NQ = CB * CB / 2 / 256;
+    constexpr int SEG = CB * CB / COMB_SEG, NQ = SEG / 2 / 256;  // 2048 doubles, 4 per thread
+    const int64_t e0 = (int64_t)blockIdx.y * SEG;
+    const double2* Pp = reinterpret_cast<const double2*>(P + cb[1] * CB * CB + e0);
     double2 acc[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) acc[q] = Pp[threadIdx.x + 256 * q];
@@ -148,8 +154,9 @@ __global__ __launch_bounds__(256) void k_blk_combine(const int64_t* __restrict__
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-        const int e = 2 * (threadIdx.x + 256 * q), r = e / CB, cc = e % CB;
-        *reinterpret_cast<double2*>(C + (int64_t)r * ldc + cc) = acc[q];
+        const int64_t e = e0 + 2 * (threadIdx.x + 256 * q);
+        const int64_t r = e / CB, cc = e % CB;
+        *reinterpret_cast<double2*>(C + r * ldc + cc) = acc[q];
     }
 }
 
@@ -258,8 +265,8 @@ __global__ __launch_bounds__(256) void k_cov_img(const double* __restrict__ S, i
 }
 
 // tie points: one wave per local point.  Row groups g = 0..m-1 (observation g: 6 rows of its image,
-// T = WT[o]), g = m (the camera: cw rows, Tc).  Lane pairs (g >= h) of groups add sum T_g' C_gh T_h
-// (diagonal of the 3x3 only, twice for g > h); lanes a < nz add the border term (Z_a' T)(Wz_a' T).  Fixed-order
+// T = WT[o]), g = m (the camera: cw rows, Tc).  The entries of the group pairs (g >= h) are dealt to
+// the lanes, which add sum T_g' C_gh T_h (diagonal of the 3x3 only, twice for g > h); lanes a < nz add the border term (Z_a' T)(Wz_a' T).  Fixed-order
 // wave reduction.
 __global__ __launch_bounds__(256) void k_cov_pts(const double* __restrict__ S, int64_t ld, const double* __restrict__ Z,
                                                  const double* __restrict__ Wz, int nz, int64_t n_pad,
@@ -280,26 +287,45 @@ __global__ __launch_bounds__(256) void k_cov_pts(const double* __restrict__ S, i
     };
     double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
     const int ng = m + 1;
-    // pairs g >= h only: diag(T_g' C_gh T_h) = diag(T_h' C_hg T_g), so an off-diagonal pair counts twice
-    for (int pr = lane; pr < ng * (ng + 1) / 2; pr += 64) {
-        int g = 0, h = pr;
-        while (h > g) { h -= g + 1; ++g; }
-        const double wgt = g == h ? 1.0 : 2.0;
+    // pairs g >= h only (diag(T_g' C_gh T_h) = diag(T_h' C_hg T_g): an off-diagonal pair counts twice),
+    // their entries flattened and dealt to the lanes so that every lane issues the same number of
+    // independent loads: first the image pairs (36 entries each, pair index = triangular (g, h)), then
+    // camera x image g (6 cw), then camera x camera (cw^2)
+    const int n_ii = m * (m + 1) / 2 * 36, n_ci = m * 6 * cw, n_all = n_ii + n_ci + cw * cw;
+#pragma unroll 4
+    for (int e = lane; e < n_all; e += 64) {
+        int g, h, a, b;
+        if (e < n_ii) {
+            const int pr = e / 36, en = e - 36 * pr;
+            g = 0;
+            h = pr;
+            while (h > g) { h -= g + 1; ++g; }
+            a = en / 6;
+            b = en - 6 * a;
+        } else if (e < n_ii + n_ci) {
+            const int e2 = e - n_ii;
+            g = m;
+            h = e2 / (6 * cw);
+            const int en = e2 - 6 * cw * h;
+            a = en / 6;
+            b = en - 6 * a;
+        } else {
+            const int e3 = e - n_ii - n_ci;
+            g = h = m;
+            a = e3 / cw;
+            b = e3 - cw * a;
+        }
         int64_t r0, c0;
         int nr, nc;
         const double *Tg, *Th;
         grp_rows(g, r0, nr, Tg);
         grp_rows(h, c0, nc, Th);
-        for (int a = 0; a < nr; ++a) {
-            double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-            for (int b = 0; b < nc; ++b) {
-                const int64_t r = r0 + a, c = c0 + b;
-                const int64_t rr = (r / CB >= c / CB) ? r : c, cc = (r / CB >= c / CB) ? c : r;
-                const double q = S[rr * ld + cc];
-                s0 += q * Th[3 * b]; s1 += q * Th[3 * b + 1]; s2 += q * Th[3 * b + 2];
-            }
-            acc0 += wgt * Tg[3 * a] * s0; acc1 += wgt * Tg[3 * a + 1] * s1; acc2 += wgt * Tg[3 * a + 2] * s2;
-        }
+        const int64_t r = r0 + a, c = c0 + b;
+        const int64_t rr = (r / CB >= c / CB) ? r : c, cc = (r / CB >= c / CB) ? c : r;
+        const double q = S[rr * ld + cc] * (g == h ? 1.0 : 2.0);
+        acc0 += Tg[3 * a] * q * Th[3 * b];
+        acc1 += Tg[3 * a + 1] * q * Th[3 * b + 1];
+        acc2 += Tg[3 * a + 2] * q * Th[3 * b + 2];
     }
     if (lane < nz) {
         double z0 = 0, z1 = 0, z2 = 0, w0 = 0, w1 = 0, w2 = 0;
@@ -486,7 +512,7 @@ int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, 
         k_blk_gemm<<<(unsigned)(ph[1] - ph[0]), 256, 0, c.stream>>>(d_parts + 4 * ph[0], d_tasks, d_terms, c.d_S, ld,
                                                                    c.d_linv, d_Y, d_P);
         if (ph[3] > ph[2])
-            k_blk_combine<<<(unsigned)(ph[3] - ph[2]), 256, 0, c.stream>>>(d_combs + 3 * ph[2], d_tasks, c.d_S, ld, d_Y, d_P);
+            k_blk_combine<<<dim3((unsigned)(ph[3] - ph[2]), COMB_SEG), 256, 0, c.stream>>>(d_combs + 3 * ph[2], d_tasks, c.d_S, ld, d_Y, d_P);
     }
     FBA_HIP(hipGetLastError());
 
