@@ -486,6 +486,11 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     // FBA_FLOW_DEFER = N (updates among the records of level min(source level + N, need - 1)): config 4
     // 1172-1180 iter/s at N = 0, 1135-1140 at 1, 1058-1063 at 2
     static const int defer = getenv("FBA_FLOW_DEFER") ? atoi(getenv("FBA_FLOW_DEFER")) : 0;
+    // FBA_FLOW_MERGE = G: writer groups over consecutive source levels when the target is read >= G levels later
+    // (config 4, k_chol_flow per launch: G = 0 / 1 / 2 / 3: 465 / 458 / 453 / 454 us; convergent config 4:
+    // 3.80 / 3.18 / 3.22 ms); FBA_FLOW_MSPLIT: the sources a merged group may hold (default SPLIT)
+    static const int merge_gap = getenv("FBA_FLOW_MERGE") ? atoi(getenv("FBA_FLOW_MERGE")) : 2;
+    static const int msplit = getenv("FBA_FLOW_MSPLIT") ? std::max(1, atoi(getenv("FBA_FLOW_MSPLIT"))) : SPLIT;
     static const int promote_mode = getenv("FBA_FLOW_PROMOTE") ? atoi(getenv("FBA_FLOW_PROMOTE")) : 0;
     static const int lookahead = getenv("FBA_FLOW_LOOKAHEAD") ? atoi(getenv("FBA_FLOW_LOOKAHEAD")) : 1000;
     int nslot = 0, ncnt = 0;
@@ -543,15 +548,35 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
         const int32_t a = t.first.first, b = t.first.second;
         std::map<int, std::vector<int32_t>> bylev;
         for (int32_t k : t.second) bylev[level[k]].push_back(k);
+        // the writer groups of the target: one per source level, except that consecutive levels are
+        // merged into one task (sources ascending, so the in-place sums are bitwise those of separate
+        // tasks) while they hold at most msplit sources together, none is the fused source's ("late")
+        // level, and the target is read at least merge_gap levels after the group's last source level
+        // (a dense network's chain of one-source writers per target otherwise becomes one record per
+        // source: 70k update records at convergent config 4)
+        const int need_t = a == b ? level[b] - 1 : level[b];
+        std::vector<std::pair<int, std::vector<int32_t>>> groups;  // (last source level, sources)
+        std::vector<char> glate;
+        for (auto& lv : bylev) {
+            const bool late_w = a == b && fsrc[b] >= 0 && lv.first == level[fsrc[b]];
+            if (merge_gap > 0 && !late_w && !groups.empty() && !glate.back() &&
+                groups.back().second.size() + lv.second.size() <= (size_t)msplit && need_t - lv.first >= merge_gap) {
+                groups.back().first = lv.first;
+                groups.back().second.insert(groups.back().second.end(), lv.second.begin(), lv.second.end());
+            } else {
+                groups.emplace_back(lv.first, lv.second);
+                glate.push_back(late_w);
+            }
+        }
         for (int q = 0; q < 4; ++q) {
             const int qr = q >> 1, qc = q & 1;
             if (a == b && qr == 0 && qc == 1) continue;
             if ((qr == 1 && halves(a) < 2) || (qc == 1 && halves(b) < 2)) continue;
             int32_t prev = -1;
-            for (auto& lv : bylev) {
-                const int w = lv.first;
-                const std::vector<int32_t>& S = lv.second;
-                const bool is_late = a == b && fsrc[b] >= 0 && w == level[fsrc[b]];
+            for (size_t gi = 0; gi < groups.size(); ++gi) {
+                const int w = groups[gi].first;
+                const std::vector<int32_t>& S = groups[gi].second;
+                const bool is_late = glate[gi] != 0;
                 const int ng = (int)((S.size() + SPLIT - 1) / SPLIT);
                 // urgency: the target is read at level level[b] (its column's potrf / panel solves)
                 const int rank = level[b] == w + 1 ? (a == b ? 2 : 3) : 4;

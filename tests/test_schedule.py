@@ -24,18 +24,22 @@ def checker(tmp_path_factory):
     return exe
 
 
-@pytest.mark.parametrize("n_img,seed,leaf", [(40, 1, None), (300, 2, None), (300, 1, 60), (420, 3, 100),
-                                             (200, 4, 0)])
-def test_level_schedule_matches_dense_cholesky(checker, n_img, seed, leaf):
+@pytest.mark.parametrize("n_img,seed,leaf,merge", [(40, 1, None, None), (300, 2, None, None), (300, 1, 60, None),
+                                                   (420, 3, 100, None), (200, 4, 0, None), (300, 2, None, 1),
+                                                   (300, 1, 60, 2)])
+def test_level_schedule_matches_dense_cholesky(checker, n_img, seed, leaf, merge):
     env = dict(os.environ)
     env.pop("FBA_ND_LEAF", None)
+    env.pop("FBA_FLOW_MERGE", None)
     if leaf is not None:
         env["FBA_ND_LEAF"] = str(leaf)
+    if merge is not None:  # writer groups over consecutive source levels (build_flow)
+        env["FBA_FLOW_MERGE"] = str(merge)
     r = subprocess.run([checker, str(n_img), str(seed)], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
     fields = dict(f.split("=") for f in r.stdout.split()[1:])
     assert int(fields["levels"]) <= int(fields["blocks"])
-    if (n_img, seed, leaf) == (300, 2, None):  # targets with > 2 source columns: split and combined
+    if (n_img, seed, leaf, merge) == (300, 2, None, None):  # targets with > 2 source columns: split and combined
         assert int(fields["split"]) > 0
     if leaf == 60:  # a dissected scene: independent subtrees share levels
         assert int(fields["levels"]) < int(fields["blocks"])
