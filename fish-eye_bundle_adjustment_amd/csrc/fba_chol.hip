@@ -33,6 +33,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <utility>
 
 namespace fba {
 
@@ -511,6 +512,12 @@ __device__ __forceinline__ void fset_tile(int set, int idx, int& ta, int& tb) { 
             }
 }
 
+// a fold over a compile-time index sequence (every index a constant expression in the body)
+template <int... Q, class F>
+__device__ __forceinline__ void bulk_for(std::integer_sequence<int, Q...>, F&& f) {
+    (f(std::integral_constant<int, Q>{}), ...);
+}
+
 // potrf_body (dataflow): factor the 128x128 diagonal block of column col (512 threads); flag != nullptr:
 // publish it column by column (k_panel hand-off).  No workgroup barriers after the load: the waves
 // coordinate through LDS counters (workgroup-scope release / acquire), so wave 0 runs the critical
@@ -639,22 +646,31 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
             if (s > 0) wait_ge(s_cc + s - 1, 1);  // row s+1 updated through column s-1
             POTRF_TS(4 + 4 * s);
             const double* Dl = Dall + s * IB * 17;
-            dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0}, d;
+            const dbl4 z = dbl4{0.0, 0.0, 0.0, 0.0};
+            dbl4 x1 = z, x2 = z, d, d2 = z;
 #pragma unroll
             for (int r = 0; r < 4; ++r) d[r] = AT((R + lk + 4 * r), R + lr);
+            // X' = D_s A' (the operands of X = A D_s' swapped): lane (lr, lk) gets xt[r] = X[lr][4r + lk],
+            // the diagonal update's operand as it stands (no LDS round trip before it); two accumulators
+            // halve each dependent MFMA chain
 #pragma unroll
-            for (int kk = 0; kk < IB; kk += 4) acc = mfma(AT((R + lr), c0 + kk + lk), Dl[lr * 17 + kk + lk], acc);
+            for (int kk = 0; kk < IB; kk += 8) {
+                x1 = mfma(Dl[lr * 17 + kk + lk], AT((R + lr), c0 + kk + lk), x1);
+                x2 = mfma(Dl[lr * 17 + kk + 4 + lk], AT((R + lr), c0 + kk + 4 + lk), x2);
+            }
+            dbl4 xt;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) AT((R + lk + 4 * r), c0 + lr) = acc[r];  // X = A D_s'
-            __builtin_amdgcn_wave_barrier();
-            double xa[4];
+            for (int r = 0; r < 4; ++r) xt[r] = x1[r] + x2[r];
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) xa[kk] = AT((R + lr), c0 + 4 * kk + lk);
+            for (int kk = 0; kk < 4; kk += 2) {  // C -= X X'
+                d = mfma(-xt[kk], xt[kk], d);
+                d2 = mfma(-xt[kk + 1], xt[kk + 1], d2);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) AT((R + lr), c0 + 4 * r + lk) = xt[r];  // X: panel tile (s+1, s)
             bump(s_pc + s);
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) d = mfma(-xa[kk], xa[kk], d);  // C -= X X'
-#pragma unroll
-            for (int r = 0; r < 4; ++r) AT((R + lk + 4 * r), R + lr) = d[r];
+            for (int r = 0; r < 4; ++r) AT((R + lk + 4 * r), R + lr) = d[r] + d2[r];
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
             for (int c = 0; c < IB; ++c) a[c] = AT((R + lr), R + c);
@@ -767,37 +783,45 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
             bump(s_bc + s);
         }
     } else {
-        // wave 4: block column s (tiles (s..7, s)) and D_s are final once column s is solved
+        // wave 4: block column s (tiles (s..7, s)) and D_s are final once column s is solved; per column
+        // every LDS read is issued before the stores (compile-time trip counts: the reads of a column
+        // are one batch, not a read-wait-store round per item, on the SIMD wave 0's chain runs on)
         const __amdgpu_buffer_rsrc_t rD = block_rsrc(dinv + dbase, (CB / IB) * IB * IB * 8);
-        for (int s = 0; s < CB / IB; ++s) {
-            if (s < CB / IB - 1) wait_ge(s_pc + s, CB / IB - 1 - s);
+        bulk_for(std::make_integer_sequence<int, CB / IB>{}, [&](auto sc) {
+            constexpr int s = decltype(sc)::value;
+            constexpr int NI = (CB / IB - s) * 2;  // 16-B items per lane: 128 per tile, 64 lanes
+            if constexpr (s < CB / IB - 1) wait_ge(s_pc + s, CB / IB - 1 - s);
             else wait_ge(s_leaf, CB / IB);
-            for (int i = lane; i < (CB / IB - s) * 128; i += 64) {
-                const int ti = s + (i >> 7), n = (i >> 3) & 15, m = (i & 7) * 2;
-                const int64_t off = ((int64_t)(ti * IB + n) * ld + s * IB + m) * 8;
+            double2 v[NI + 2];
+#pragma unroll
+            for (int u = 0; u < NI; ++u) {
+                const int i = lane + 64 * u, ti = s + (i >> 7), n = (i >> 3) & 15, m = (i & 7) * 2;
                 const double* t = smem + (ti * (ti + 1) / 2 + s) * IB * 17 + n * 17 + m;
-                if (ti > s || m + 1 <= n) {
-                    double2 v;
-                    v.x = t[0];
-                    v.y = t[1];
-                    st_sc1(rL, off, v);
-                } else if (m == n) {
-                    st_sc1(rL, off, t[0]);
-                }
+                v[u].x = t[0];
+                v[u].y = t[1];
             }
-            for (int i = 2 * lane; i < IB * IB; i += 128) {
-                double2 v;
-                v.x = Dall[s * IB * 17 + (i >> 4) * 17 + (i & 15)];
-                v.y = Dall[s * IB * 17 + (i >> 4) * 17 + (i & 15) + 1];
-                st_sc1(rD, (int64_t)(s * IB * IB + i) * 8, v);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int i = 2 * lane + 128 * u;
+                v[NI + u].x = Dall[s * IB * 17 + (i >> 4) * 17 + (i & 15)];
+                v[NI + u].y = Dall[s * IB * 17 + (i >> 4) * 17 + (i & 15) + 1];
             }
+#pragma unroll
+            for (int u = 0; u < NI; ++u) {
+                const int i = lane + 64 * u, ti = s + (i >> 7), n = (i >> 3) & 15, m = (i & 7) * 2;
+                const int64_t off = ((int64_t)(ti * IB + n) * ld + s * IB + m) * 8;
+                if (ti > s || m + 1 <= n) st_sc1(rL, off, v[u]);
+                else if (m == n) st_sc1(rL, off, v[u].x);
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) st_sc1(rD, (int64_t)(s * IB * IB + 2 * lane + 128 * u) * 8, v[NI + u]);
             if (flag) {
                 if (pubts && lane == 0) pubts[8 + s] = wall_clock64();  // FBA_PANEL_TRACE: column s solved
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0) __hip_atomic_store(flag, (unsigned)(s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (pubts && lane == 0) pubts[16 + s] = wall_clock64();  // ... and published
             }
-        }
+        });
     }
     if (!ok && lane == 0 && scal[1] == 0.0) scal[1] = (double)(k0 + 1);
     POTRF_TS(40);
@@ -1861,31 +1885,33 @@ __device__ __forceinline__ void fused_apply(const __amdgpu_buffer_rsrc_t rX, int
         if (p1) v = std::min(v, __hip_atomic_load(p1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         return v;
     };
-    // column block b (128 rows x 16) is loaded by ONE group of waves, block parity: waves 1-3 (even, six
-    // 16-B items per lane) or waves 4-7 (odd, four), item i -> row i >> 3, columns 2 (i & 7), +1; wave 0
+    // column block b (128 rows x 16) is loaded by ONE group of waves, b mod 3: waves 1-3 (six 16-B items
+    // per lane), waves 4-5 or waves 6-7 (eight each), item i -> row i >> 3, columns 2 (i & 7), +1; wave 0
     // loads nothing and thread 0 reads the progress flags.  So every wave has at most one block's loads
     // in flight and the compiler's wait before storing a block into LDS waits for that block alone,
-    // while the other group's block (t + 2) stays in flight across the barrier (with both slots in
-    // every wave, the wait for block t + 1 also waited for t + 2's loads)
-    const int grp = wave == 0 ? -1 : (wave < 4 ? 0 : 1);
-    const int gl = grp == 0 ? tid - 64 : tid - 256;
-    constexpr int GM = 6;  // items per lane, group 0 (group 1: 4)
+    // while the other groups' blocks (t + 1, t + 2) stay in flight across the barrier: three blocks in
+    // flight, so a diagonal workgroup that starts behind its panel halves catches up at about a third
+    // of an sc1 round trip per block (with two groups it took ~2 us per block, the loads' latency / 2)
+    constexpr int NGRP = 3;
+    const int grp = wave == 0 ? -1 : (wave < 4 ? 0 : (wave < 6 ? 1 : 2));
+    const int gl = grp == 0 ? tid - 64 : (grp == 1 ? tid - 256 : tid - 384);
+    constexpr int GM = 8;  // items per lane (group 0: 6)
     double2 xl[GM];
     auto issue = [&](int b) {
-        if (grp != (b & 1)) return;
+        if (grp != b % NGRP) return;
 #pragma unroll
         for (int m = 0; m < GM; ++m) {
-            const int i = gl + (grp == 0 ? 192 : 256) * m;
-            if ((grp == 0 || m < 4) && i < 1024)
+            const int i = gl + (grp == 0 ? 192 : 128) * m;
+            if ((grp != 0 || m < 6) && i < 1024)
                 xl[m] = ld_sc1(rX, ((int64_t)(i >> 3) * ld + IB * b + 2 * (i & 7)) * 8);
         }
     };
     auto store = [&](int b, double* X) {
-        if (grp != (b & 1)) return;
+        if (grp != b % NGRP) return;
 #pragma unroll
         for (int m = 0; m < GM; ++m) {
-            const int i = gl + (grp == 0 ? 192 : 256) * m;
-            if ((grp == 0 || m < 4) && i < 1024) {
+            const int i = gl + (grp == 0 ? 192 : 128) * m;
+            if ((grp != 0 || m < 6) && i < 1024) {
                 X[(i >> 3) * 17 + 2 * (i & 7)] = xl[m].x;
                 X[(i >> 3) * 17 + 2 * (i & 7) + 1] = xl[m].y;
             }
@@ -1929,7 +1955,8 @@ __device__ __forceinline__ void fused_apply(const __amdgpu_buffer_rsrc_t rX, int
             issued = t + 1;
         }
         store(t, X);
-        if (tr && tid == ((t & 1) ? 256 : 64)) tr[40 + t] = wall_clock64();  // FBA_PANEL_TRACE: group's share stored
+        if (tr && tid == (t % NGRP == 0 ? 64 : (t % NGRP == 1 ? 256 : 384)))
+            tr[40 + t] = wall_clock64();  // FBA_PANEL_TRACE: group's share stored
         // (block t + 1 not in flight yet: read the flags now rather than use the values read during the
         // last update, which would issue it one update later)
         if (tid == 0) sy[31] = (int)(issued == t + 1 && t + 1 < CB / IB ? published() : std::min(fv0, fv1));
@@ -1937,16 +1964,14 @@ __device__ __forceinline__ void fused_apply(const __amdgpu_buffer_rsrc_t rX, int
         if (tr && tid == 0) tr[8 + t] = wall_clock64();  // FBA_PANEL_TRACE: block t in LDS
         const int pub = sy[31];
         const bool pre = issued > t + 1 || (t + 1 < CB / IB && pub > t + 1);
-        // blocks t+1 (the other group, idle since it stored t-1) and t+2 (this block's group) in flight
-        // during this update
-        if (issued == t + 1 && t + 1 < CB / IB && pub > t + 1) {
-            issue(t + 1);
-            issued = t + 2;
-        }
-        if (issued == t + 2 && t + 2 < CB / IB && pub > t + 2) {
-            issue(t + 2);
-            issued = t + 3;
-        }
+        // blocks t+1, t+2 (the groups idle since they stored t-2, t-1) and t+3 (this block's group) in
+        // flight during this update, as far as published
+#pragma unroll
+        for (int d = 1; d <= NGRP; ++d)
+            if (issued == t + d && t + d < CB / IB && pub > t + d) {
+                issue(t + d);
+                issued = t + d + 1;
+            }
         if (tid == 0) {  // consumed before the next barrier, after this update
             fv0 = __hip_atomic_load(p0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             fv1 = p1 ? __hip_atomic_load(p1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
