@@ -2165,12 +2165,76 @@ __device__ __forceinline__ void syrk_flow_body(double* __restrict__ S, int64_t l
     }
     const __amdgpu_buffer_rsrc_t rA = block_rsrc(S + r0 * ld, ((int64_t)63 * ld + ld) * 8);
     const __amdgpu_buffer_rsrc_t rB = block_rsrc(S + c0 * ld, ((int64_t)63 * ld + ld) * 8);
-    for (int s = 0; s < ns; ++s) {
+    const int t0 = rec[13], t_end = rec[14];
+    // the sources complete at the start (both panel halves have published every column block; thread 0,
+    // one flag pair each): such a source's whole panel is prefetched into registers during the previous
+    // source's MFMAs, so a many-source task (a dense network's updates) is not load-then-compute per source
+    if (tid == 0) {
+        unsigned m = 0;
+        for (int s = 1; s < ns; ++s)
+            if (__hip_atomic_load(fl + sl[3 * s + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)t_end &&
+                __hip_atomic_load(fl + sl[3 * s + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)t_end)
+                m |= 1u << s;
+        sv[2] = (int)m;
+    }
+    __syncthreads();
+    const unsigned full = (unsigned)sv[2];
+    double2 xa[8], xb[8];  // columns [16 t, 16 v) of the 64 rows of A and of B: row item / wpr, column pair item % wpr
+    auto load_rng = [&](int s, int t, int v) {
         const int64_t kc = (int64_t)sl[3 * s] * CB;
+        const int wpr = 8 * (v - t), nit = 64 * wpr;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = tid + POTRF_THREADS * u;
+            if (i < nit) {
+                const int row = i / wpr, col = IB * t + 2 * (i % wpr);
+                xa[u] = ld_sc1(rA, ((int64_t)row * ld + kc + col) * 8);
+                xb[u] = ld_sc1(rB, ((int64_t)row * ld + kc + col) * 8);
+            }
+        }
+    };
+    auto store_rng = [&](int t, int v) {
+        const int wpr = 8 * (v - t), nit = 64 * wpr;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = tid + POTRF_THREADS * u;
+            if (i < nit) {
+                const int row = i / wpr, col = IB * t + 2 * (i % wpr);
+                As[row][col] = xa[u].x; As[row][col + 1] = xa[u].y;
+                Bs[row][col] = xb[u].x; Bs[row][col + 1] = xb[u].y;
+            }
+        }
+    };
+    auto compute = [&](int t, int v) {
+        for (int kb = IB * t; kb < IB * v; kb += IB) {
+            double av[4], b0[4], b1[4];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                av[kk] = -As[wr + lr][kb + 4 * kk + lk];
+                b0[kk] = Bs[wc + lr][kb + 4 * kk + lk];
+                b1[kk] = Bs[wc + 16 + lr][kb + 4 * kk + lk];
+            }
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                acc[0] = mfma(av[kk], b0[kk], acc[0]);
+                acc[1] = mfma(av[kk], b1[kk], acc[1]);
+            }
+        }
+    };
+    bool held = false;  // xa / xb hold source s's columns [t0, t_end)
+    for (int s = 0; s < ns; ++s) {
+        if (held) {
+            __syncthreads();  // every wave done with the previous source's panel in LDS
+            store_rng(t0, t_end);
+            __syncthreads();
+            held = s + 1 < ns && ((full >> (s + 1)) & 1u);
+            if (held) load_rng(s + 1, t0, t_end);
+            compute(t0, t_end);
+            continue;
+        }
         const unsigned* pa = fl + sl[3 * s + 1];
         const unsigned* pb = fl + sl[3 * s + 2];
-        int t = rec[13];
-        const int t_end = rec[14];
+        int t = t0;
         while (t < t_end) {
             if (tid == 0) {
                 unsigned spins = 0, va, vb;
@@ -2185,42 +2249,14 @@ __device__ __forceinline__ void syrk_flow_body(double* __restrict__ S, int64_t l
             }
             __syncthreads();
             const int v = sv[0];
-            // columns [16 t, 16 v) of the 64 rows of A and of B: row item / wpr, column pair item % wpr
-            const int wpr = 8 * (v - t), nit = 64 * wpr;
-            double2 xa[8], xb[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int i = tid + POTRF_THREADS * u;
-                if (i < nit) {
-                    const int row = i / wpr, col = IB * t + 2 * (i % wpr);
-                    xa[u] = ld_sc1(rA, ((int64_t)row * ld + kc + col) * 8);
-                    xb[u] = ld_sc1(rB, ((int64_t)row * ld + kc + col) * 8);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int i = tid + POTRF_THREADS * u;
-                if (i < nit) {
-                    const int row = i / wpr, col = IB * t + 2 * (i % wpr);
-                    As[row][col] = xa[u].x; As[row][col + 1] = xa[u].y;
-                    Bs[row][col] = xb[u].x; Bs[row][col + 1] = xb[u].y;
-                }
-            }
+            load_rng(s, t, v);
+            store_rng(t, v);
             __syncthreads();
-            for (int kb = IB * t; kb < IB * v; kb += IB) {
-                double av[4], b0[4], b1[4];
-#pragma unroll
-                for (int kk = 0; kk < 4; ++kk) {
-                    av[kk] = -As[wr + lr][kb + 4 * kk + lk];
-                    b0[kk] = Bs[wc + lr][kb + 4 * kk + lk];
-                    b1[kk] = Bs[wc + 16 + lr][kb + 4 * kk + lk];
-                }
-#pragma unroll
-                for (int kk = 0; kk < 4; ++kk) {
-                    acc[0] = mfma(av[kk], b0[kk], acc[0]);
-                    acc[1] = mfma(av[kk], b1[kk], acc[1]);
-                }
+            if (v == t_end && s + 1 < ns && ((full >> (s + 1)) & 1u)) {  // the next source's panel in flight
+                load_rng(s + 1, t0, t_end);
+                held = true;
             }
+            compute(t, v);
             t = v;
         }
     }
@@ -2283,7 +2319,7 @@ constexpr size_t FLOW_LDS_A = FLOWF_LDS > TRSMF_LDS ? FLOWF_LDS : TRSMF_LDS;
 constexpr size_t FLOW_LDS_B = SYRKW_LDS > TRTRI_LDS ? SYRKW_LDS : TRTRI_LDS;
 constexpr size_t FLOW_LDS = FLOW_LDS_A > FLOW_LDS_B ? FLOW_LDS_A : FLOW_LDS_B;
 static_assert(FLOW_LDS + 16 <= 160 * 1024, "k_chol_flow LDS (+ the static ticket word)");
-static_assert(SYRKW_LDS >= sizeof(double) * 128 * LDW + 2 * sizeof(int), "syrk_flow_body broadcast words");
+static_assert(SYRKW_LDS >= sizeof(double) * 128 * LDW + 3 * sizeof(int), "syrk_flow_body broadcast words");
 
 // Dynamic dispatch of k_chol_flow's records (FlowDyn, fba_order.cpp build_flow): one workgroup per record;
 // when it starts, a workgroup takes the next slot of a FIFO of READY records (one atomic add, then a poll of
