@@ -421,8 +421,12 @@ __constant__ int c_tri_b[21] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4, 0, 
 template <int NK>
 struct LR {
     static constexpr int CW = 5 + NK;
-    static constexpr int ES = 16 + 2 * CW;          // per-observation staging stride (doubles; even: 16-B aligned rows)
-    static constexpr int US = 20;                   // U row stride (16-B aligned rows: ds_read_b128)
+    // row strides of the per-observation LDS rows: even (16-B aligned rows, ds_read_b128) and = 2 mod 4
+    // doubles, so a row starts 4 x (odd) dwords apart from the next: 16 distinct bank quadruples over 16
+    // rows (the (D) loops read the rows of random observations; a stride = 0 mod 4 doubles gives 8)
+    static constexpr int ES = 14 + 2 * CW + ((14 + 2 * CW) % 4 == 0 ? 2 : 0);  // staging: Je | w | Jc (+ 2 for even nK)
+    static constexpr int US = 18;                   // U row (exactly)
+    static_assert(ES % 4 == 2 && US % 4 == 2, "LDS row strides of 2 mod 4 doubles");
     static constexpr int PPS = 15 + 3 * CW;         // per-point: Vinv 6 | R 6 | rb 3 | Uc 3CW
     static constexpr int NIMG = 27 + 6 * CW;        // image partial: 21 lower + 6 RHS + 6CW image-camera
     static constexpr int NCAM = CW * (CW + 1) / 2 + CW;
