@@ -5,6 +5,8 @@
 // pairs), allocates device memory once, and drives the kernels of fba_kernels.hip / fba_chol.hip.
 // The loop semantics are the reference's main.m:407-494; the unknown layout is Buildxhat.m:6-134.
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -725,6 +727,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     FBA_HIP(hipMemset(c->d_scal, 0, sizeof(double) * 16));
     FBA_HIP(hipHostMalloc((void**)&c->h_pinned, sizeof(double) * 64, hipHostMallocMapped | hipHostMallocCoherent));
     FBA_HIP(hipHostGetDevicePointer((void**)&c->d_hpinned, c->h_pinned, 0));
+    std::fill(c->h_pinned, c->h_pinned + 64, 0.0);
     for (auto& e : c->ev) FBA_HIP(hipEventCreate(&e));
     if (opt.verbose)
         fprintf(stderr, "[fba] rank %d/%d: n_obs %ld (tie %ld), points %ld, pairs %ld (%ld terms), u_c %ld, n_pad %ld; "
@@ -994,9 +997,28 @@ static void print_panel_trace(Ctx* c) {
     (void)hipMemset(c->d_ptrace, 0, t.size() * sizeof(uint64_t));
 }
 
+// Completion of a solve: k_sum_parts, the last kernel of every solve, writes its results to host-mapped
+// memory and then its sequence number; fba_step polls that number (a spin on coherent host memory returns
+// a few us after the GPU's write, where hipStreamSynchronize's wake-up is slower) -- later work on the
+// stream is ordered after the solve anyway.  The stream is synchronised when a caller re-copies scal (the
+// multi-GPU path), with tracing or timing on, with FBA_SYNC=1, and after ~5 s without the number (a
+// faulted launch: the synchronisation reports it).
+static bool wait_solve_seq(Ctx* c) {
+    static const bool force_sync = getenv("FBA_SYNC") && atoi(getenv("FBA_SYNC")) != 0;
+    if (force_sync || c->timing || c->d_ptrace || c->d_lrprof) return false;
+    const double want = c->solve_seq + 1.0;
+    volatile const double* seq = c->h_pinned + 4;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 0; *seq < want; ++it)
+        if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) return false;
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return true;
+}
+
 static int solve_finish(Ctx* c, double* dsum, bool recopy) {
     if (recopy) FBA_HIP(hipMemcpyAsync(c->h_pinned, c->d_scal, sizeof(double) * 4, hipMemcpyDeviceToHost, c->stream));
-    FBA_HIP(hipStreamSynchronize(c->stream));
+    if (recopy || !wait_solve_seq(c)) FBA_HIP(hipStreamSynchronize(c->stream));
+    c->solve_seq = c->h_pinned[4];
     if (c->d_ptrace) print_panel_trace(c);
     if (c->timing) {
         float ms;

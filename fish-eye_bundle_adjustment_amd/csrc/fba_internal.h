@@ -275,7 +275,9 @@ struct Ctx {
     uint8_t* d_active = nullptr; // [n_pad] 1 = estimated camera-side parameter
     uint8_t* d_counted = nullptr;// [u_full] 1 = counted in this rank's sumabs share
     int64_t* d_obs_pho = nullptr;// [n_obs] PHO row of each local observation
-    double* h_pinned = nullptr;  // pinned host scratch (coherent, mapped: k_sum_parts writes scal[0..3] here)
+    double* h_pinned = nullptr;  // pinned host scratch (coherent, mapped: k_sum_parts writes scal[0..3] here,
+                                 // then [4] = its running count of solves, scal[5])
+    double solve_seq = 0.0;      // solves the host has seen completed (h_pinned[4])
     double* d_hpinned = nullptr; // its device address
 
     // state

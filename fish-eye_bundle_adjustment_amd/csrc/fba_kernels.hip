@@ -1218,6 +1218,12 @@ __global__ void k_sum_parts(const double* __restrict__ part, int n, double* __re
             host[1] = scal[1];
             host[2] = red[0];
             host[3] = scal[3];
+            // the solve's sequence number last, behind the values (the host polls it instead of waiting
+            // for the stream: this kernel ends every solve)
+            __threadfence_system();
+            const double seq = scal[5] + 1.0;
+            scal[5] = seq;
+            host[4] = seq;
         }
     }
 }
