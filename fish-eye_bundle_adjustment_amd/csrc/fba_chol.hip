@@ -77,7 +77,41 @@ __device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, int64_t off_byt
 __device__ __forceinline__ double2 ld_sc1(__amdgpu_buffer_rsrc_t r, int64_t off_bytes) {
     return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off_bytes, 0, SC1));
 }
-constexpr unsigned FLAG_SPINS = 1u << 22;  // bounded poll (s_sleep 1 per spin): ~0.3 s, then give up
+// Bounded polls.  Every wait in this file gives up after g_flag_spins sleeps (default 1 << 22, ~0.3 s;
+// the FBA_FLAG_SPINS environment variable lowers it process-wide, to force the path in a test) and then
+// RAISES THE ABORT: scal[1] = -1.0 (agent-scope store).  Every other poll checks the abort word every 64
+// sleeps (not on its first miss: that load would sit on every hand-off's critical path) and stops too, so
+// after one expiry the whole launch drains within about a millisecond; a k_chol_flow record that has not started yet is skipped entirely, k_bwd_flow's
+// workgroups return at once, and k_update leaves xhat untouched (fba_kernels.hip): the step fails with
+// FBA_ERR_HIP and xhat is as before it.  The sync words are zeroed again ahead of the next factorisation
+// (k_border_rhs), so a later step runs normally.
+__device__ unsigned g_flag_spins = 1u << 22;
+
+__device__ __forceinline__ bool hand_off_aborted(const double* scal) {  // the timeout mark, sign bit of -1.0
+    return (long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(scal + 1), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT) < 0;
+}
+__device__ __forceinline__ void hand_off_abort(double* scal) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(scal + 1), __builtin_bit_cast(unsigned long long, -1.0),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// a non-positive pivot in the block at row k0: the first one is reported (scal[1] = k0 + 1) unless a
+// hand-off already aborted (a compare-and-swap from 0, so it never overwrites the abort mark)
+__device__ __forceinline__ void pivot_failed(double* scal, int64_t k0) {
+    unsigned long long zero = 0ull;
+    __hip_atomic_compare_exchange_strong(reinterpret_cast<unsigned long long*>(scal + 1), &zero,
+                                         __builtin_bit_cast(unsigned long long, (double)(k0 + 1)), __ATOMIC_RELAXED,
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// one missed poll: true when this wait must stop (its own bound reached, or another wait aborted)
+__device__ __forceinline__ bool spin_expired(unsigned& spins, double* scal) {
+    ++spins;
+    if (spins >= g_flag_spins || ((spins & 63u) == 0u && hand_off_aborted(scal))) {
+        hand_off_abort(scal);
+        return true;
+    }
+    return false;
+}
 
 // 1/sqrt(d) from v_rsq_f64 refined by two Newton steps (full double precision), no IEEE divide
 __device__ __forceinline__ double rsqrt_d(double d) {
@@ -274,7 +308,7 @@ __device__ __forceinline__ void wait_list(const int32_t* __restrict__ wl, int n,
             unsigned spins = 0;
             while (__hip_atomic_load(tflags + wl[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
                 __builtin_amdgcn_s_sleep(1);
-                if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }
+                if (spin_expired(spins, scal)) break;
             }
         }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -463,7 +497,7 @@ __device__ __forceinline__ void potrf_body_sync(double* __restrict__ S, int64_t 
             if (!flag) store_col(s, tid - 64, POTRF_THREADS - 64);  // block column s is final: written behind the update
         }
     }
-    if (!ok && lane == 0 && scal[1] == 0.0) scal[1] = (double)(k0 + 1);
+    if (!ok && lane == 0) pivot_failed(scal, k0);
     store_col(CB / IB - 1, tid, POTRF_THREADS);
     {   // the leaf inverses, row-major 16x16 each, two per thread-store (with a flag only D_7 is left)
         const __amdgpu_buffer_rsrc_t rD = block_rsrc(dinv + dbase, (CB / IB) * IB * IB * 8);
@@ -488,7 +522,7 @@ __device__ __forceinline__ void spin_ge(const unsigned* p, unsigned v, double* _
     unsigned spins = 0;
     while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
         __builtin_amdgcn_s_sleep(1);
-        if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }  // hand-off timeout (host reports it)
+        if (spin_expired(spins, scal)) break;  // hand-off timeout (host reports it)
     }
 }
 
@@ -563,7 +597,7 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
         unsigned spins = 0;
         while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }
+            if (spin_expired(spins, scal)) break;
         }
     };
     auto bump = [&](int* p) {  // after this wave's LDS writes
@@ -823,7 +857,7 @@ __device__ __forceinline__ void potrf_body(double* __restrict__ S, int64_t ld, i
             }
         });
     }
-    if (!ok && lane == 0 && scal[1] == 0.0) scal[1] = (double)(k0 + 1);
+    if (!ok && lane == 0) pivot_failed(scal, k0);
     POTRF_TS(40);
 #undef AT
 #undef POTRF_TS
@@ -947,7 +981,7 @@ __device__ __forceinline__ void trsm_body(double* __restrict__ S, int64_t ld, co
             unsigned spins = 0;
             while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
                 __builtin_amdgcn_s_sleep(1);
-                if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }  // hand-off timeout (host reports it)
+                if (spin_expired(spins, scal)) break;  // hand-off timeout (host reports it)
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the payload loads below the poll
@@ -968,10 +1002,7 @@ __device__ __forceinline__ void trsm_body(double* __restrict__ S, int64_t ld, co
                 unsigned spins = 0;
                 while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(t + 1)) {
                     __builtin_amdgcn_s_sleep(1);
-                    if (++spins == FLAG_SPINS) {
-                        if (lane == 0) scal[1] = -1.0;  // hand-off timeout (host reports it)
-                        break;
-                    }
+                    if (spin_expired(spins, scal)) break;  // (hand-off timeout or abort: reported by the host)
                 }
                 double2 v[16];
                 double* dst[16];
@@ -1005,7 +1036,7 @@ __device__ __forceinline__ void trsm_body(double* __restrict__ S, int64_t ld, co
                 unsigned sp = 0;
                 while (__hip_atomic_load(s_col + st, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
                     __builtin_amdgcn_s_sleep(1);
-                    if (++sp == FLAG_SPINS) break;  // (the loader reports the timeout)
+                    if (spin_expired(sp, scal)) break;
                 }
                 trsm_step(st, Xw, Tw, Lt, Dt, lr, lk);
                 if (tr && tid == 0 && st == CB / IB - 2) tr[5] = wall_clock64();
@@ -1740,10 +1771,7 @@ __device__ __forceinline__ void trsm_flow_body(double* __restrict__ S, int64_t l
             unsigned spins = 0;
             while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(t + 1)) {
                 __builtin_amdgcn_s_sleep(1);
-                if (++spins == FLAG_SPINS) {
-                    if (lane == 0) scal[1] = -1.0;  // hand-off timeout (host reports it)
-                    break;
-                }
+                if (spin_expired(spins, scal)) break;  // (hand-off timeout or abort: reported by the host)
             }
             double2 v[4];
             double* dst[4];
@@ -1788,7 +1816,7 @@ __device__ __forceinline__ void trsm_flow_body(double* __restrict__ S, int64_t l
         unsigned sp = 0;
         while (__hip_atomic_load(s_col + t, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4) {
             __builtin_amdgcn_s_sleep(1);
-            if (++sp == FLAG_SPINS) break;  // (the loader reports the timeout)
+            if (spin_expired(sp, scal)) break;
         }
         // X_t = A_t D_t': A_t to the operand layout through Tw
 #pragma unroll
@@ -1925,7 +1953,7 @@ __device__ __forceinline__ void fused_apply(const __amdgpu_buffer_rsrc_t rX, int
             unsigned spins = 0;
             while ((fv = published()) <= (unsigned)b) {
                 __builtin_amdgcn_s_sleep(1);
-                if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }
+                if (spin_expired(spins, scal)) break;
             }
             fv0 = fv;
             fv1 = ~0u;
@@ -2243,7 +2271,7 @@ __device__ __forceinline__ void syrk_flow_body(double* __restrict__ S, int64_t l
                     vb = __hip_atomic_load(pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (va > (unsigned)t && vb > (unsigned)t) break;
                     __builtin_amdgcn_s_sleep(1);
-                    if (++spins == FLAG_SPINS) { scal[1] = -1.0; va = vb = (unsigned)t_end; break; }
+                    if (spin_expired(spins, scal)) { va = vb = (unsigned)t_end; break; }
                 }
                 sv[0] = (int)std::min(std::min(va, vb), (unsigned)t_end);
             }
@@ -2370,7 +2398,7 @@ __device__ __forceinline__ int dyn_claim(const FlowDyn& d, double* __restrict__ 
     unsigned spins = 0, v;
     while ((v = __hip_atomic_load(d.ring + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
         __builtin_amdgcn_s_sleep(1);
-        if (++spins == FLAG_SPINS) { scal[1] = -1.0; return -1; }
+        if (spin_expired(spins, scal)) return -1;
     }
     return (int)v - 1;
 }
@@ -2445,8 +2473,15 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_chol_flow(double* __restrict_
         // order, nor on every record being co-resident
         s_ticket = (int)__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    // a record that starts after a hand-off timeout is skipped (its inputs may never be published); with
+    // the dynamic dispatch it still triggers its consumers, which then skip too
+    if (threadIdx.x == 0 && s_ticket >= 0 && hand_off_aborted(scal)) s_ticket = dyp ? -2 - s_ticket : -1;
     __syncthreads();
     const int rid = s_ticket;
+    if (rid < -1 && dyp) {
+        dyn_trigger(*dyp, -2 - rid, 0, dyp->info[8 * (-2 - rid) + 3] + dyp->info[8 * (-2 - rid) + 4], nullptr);
+        return;
+    }
     if (rid < 0) return;
     if (trace && threadIdx.x == 0) trace[FTRACE * (int64_t)rid + 48] = t_wg;
     flow_record(rid, S, ld, lists, recs, dinv, linv, scal, colflags, fl, cnt, P, trace, gblk, dyp, smem);
@@ -2557,9 +2592,13 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
     // the block columns top down -- every wait (a higher block's x, the combine's coefficients) points
     // to a workgroup that started earlier, so progress needs neither in-order dispatch nor co-residency
     __shared__ int s_ticket;
-    if (tid == 0) s_ticket = (int)__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) {
+        s_ticket = (int)__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (hand_off_aborted(scal)) s_ticket = -1;  // the factorisation timed out: nothing to solve
+    }
     __syncthreads();
     const int tk = s_ticket;
+    if (tk < 0) return;
     if (combine && tk == 0) {  // the border combine workgroup
         border_combine_body(gpart, gblk, nblk, reinterpret_cast<double (*)[15]>(Li), cs);
         if (tid < 14) {
@@ -2603,10 +2642,7 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
                 const bool ok = __builtin_bit_cast(uint64_t, v.x) != X_SENTINEL && __builtin_bit_cast(uint64_t, v.y) != X_SENTINEL;
                 if (__all(ok)) break;
                 __builtin_amdgcn_s_sleep(1);
-                if (++spins == FLAG_SPINS) {
-                    if (tid == 0) scal[1] = -1.0;
-                    break;
-                }
+                if (spin_expired(spins, scal)) break;
             }
             xs[2 * tid] = v.x;
             xs[2 * tid + 1] = v.y;
@@ -2627,7 +2663,7 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
             unsigned spins = 0;
             while (__hip_atomic_load(flags + nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1u) {
                 __builtin_amdgcn_s_sleep(1);
-                if (++spins == FLAG_SPINS) { scal[1] = -1.0; break; }
+                if (spin_expired(spins, scal)) break;
             }
         }
         __syncthreads();
@@ -2940,6 +2976,13 @@ int chol_setup(Ctx& c) {
     c.merge_max = getenv("FBA_MERGE_MAX") ? atoi(getenv("FBA_MERGE_MAX")) : (1 << 30);
     FBA_HIP(hipFuncSetAttribute((const void*)k_trtri128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRTRI_LDS));
 
+    // FBA_FLAG_SPINS (tests): the bound of every hand-off poll, process-wide (the device global is one per
+    // loaded code object), set by every context creation; unset: the default 1 << 22
+    {
+        const char* fs = getenv("FBA_FLAG_SPINS");
+        const unsigned v = fs ? (unsigned)std::max(1L, atol(fs)) : 1u << 22;
+        FBA_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_flag_spins), &v, sizeof v));
+    }
     c.probe_ev.assign(2 * std::max(c.sched.n_waves, 1), nullptr);
     for (auto& e : c.probe_ev) FBA_HIP(hipEventCreate(&e));
     return FBA_OK;

@@ -278,6 +278,7 @@ struct Ctx {
     double* h_pinned = nullptr;  // pinned host scratch (coherent, mapped: k_sum_parts writes scal[0..3] here,
                                  // then [4] = its running count of solves, scal[5])
     double solve_seq = 0.0;      // solves the host has seen completed (h_pinned[4])
+    int64_t solves_enqueued = 0; // solves enqueued on the stream (k_sum_parts' count once they are done)
     double* d_hpinned = nullptr; // its device address
 
     // state

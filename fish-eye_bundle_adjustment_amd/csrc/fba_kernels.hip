@@ -1167,12 +1167,15 @@ __global__ __launch_bounds__(256) void k_backsub(const double* __restrict__ WT, 
 // ------------------------------------------------------------------------------------------------
 // update: de-scale (main.m:460-482), xhat += delta, partial sumabs (fixed-order block sums)
 // ------------------------------------------------------------------------------------------------
+// (scal[1] < 0: a hand-off of the factorisation or backward solve timed out, fba_chol.hip -- delta is not
+// a solution, xhat stays as it was and the host reports FBA_ERR_HIP)
 __global__ __launch_bounds__(256) void k_update(double* __restrict__ xfull, double* __restrict__ delta,
                                                 const double* __restrict__ cam_tab, const uint8_t* __restrict__ counted,
                                                 double* __restrict__ part, int64_t u_full, int n_img, int n_cam, int nk,
-                                                int cw, int cam_stride) {
+                                                int cw, int cam_stride, const double* __restrict__ scal) {
     __shared__ double red[256];
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool apply = !(scal[1] < 0.0);
     double a = 0.0;
     if (i < u_full) {
         double d = delta[i];
@@ -1185,7 +1188,7 @@ __global__ __launch_bounds__(256) void k_update(double* __restrict__ xfull, doub
             else if (c >= 3 + nk) d = d / ct[6];                               // P / rmax^2
         }
         delta[i] = d;
-        xfull[i] += d;
+        if (apply) xfull[i] += d;
         if (counted[i]) a = fabs(d);
         if (!isfinite(d)) a = __builtin_nan("");
     }
@@ -1509,7 +1512,7 @@ int launch_backsub_update(Ctx& c) {
     const int nblk = (int)((L.u_full + 255) / 256);
     // (forming deltasum in k_update's last-arriving workgroup measured slower: 612 agent-scope atomics)
     k_update<<<nblk, 256, 0, c.stream>>>(c.d_xfull, c.d_delta, c.d_cam_tab, c.d_counted, c.d_part, L.u_full,
-                                         L.n_img, L.n_cam, L.nk, L.cw, c.cam_tab_stride);
+                                         L.n_img, L.n_cam, L.nk, L.cw, c.cam_tab_stride, c.d_scal);
     FBA_HIP(hipGetLastError());
     k_sum_parts<<<1, 256, 0, c.stream>>>(c.d_part, nblk, c.d_scal, c.d_hpinned);
     FBA_HIP(hipGetLastError());
