@@ -24,7 +24,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         snprintf(msg, sizeof msg, "BuildAwG: expects (data, xhat)");
         error = 1;
     }
-    if (!error && fm_settings(prhs[0], &m.s, 1, msg, sizeof msg)) error = 1;
+    if (!error && fm_settings(prhs[0], &m.s, 1, msg, sizeof msg, NULL)) error = 1;
     if (!error && fm_problem(prhs[0], &m, msg, sizeof msg)) error = 1;
     fba_ctx* ctx = error ? NULL : fm_context(&m);
     if (!error && !ctx) {

@@ -19,7 +19,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     memset(&m, 0, sizeof m);
     if (nrhs != 3 || !mxIsDouble(prhs[0]) || !mxIsStruct(prhs[1]) || !mxIsDouble(prhs[2]))
         mexErrMsgIdAndTxt("BuildRSD:args", "BuildRSD: expects (v, data, xhat)");
-    int r = fm_settings(prhs[1], &m.s, 1, msg, sizeof msg);
+    int r = fm_settings(prhs[1], &m.s, 0, msg, sizeof msg, NULL);
     if (r == 2) m.s.type = FBA_TYPE_FISHEYE;  /* BuildRSD does not read the model type */
     else if (r) mexErrMsgIdAndTxt("BuildRSD:data", "%s", msg);
     if (fm_problem(prhs[1], &m, msg, sizeof msg)) {

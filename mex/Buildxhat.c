@@ -17,20 +17,6 @@
 
 #include "fba_mex_common.h"
 
-/* cell (r, c) of an M x N cell array (1-based as in MATLAB) */
-static const mxArray* cell_at(const mxArray* C, mwIndex r, mwIndex c) {
-    const mwSize M = mxGetM(C);
-    return mxGetCell(C, (c - 1) * M + (r - 1));
-}
-static double cell_num(const mxArray* C, mwIndex r, mwIndex c) {
-    const mxArray* v = cell_at(C, r, c);
-    return (v && mxGetNumberOfElements(v) > 0) ? mxGetScalar(v) : 0.0;
-}
-static char* cell_str(const mxArray* C, mwIndex r, mwIndex c) {
-    const mxArray* v = cell_at(C, r, c);
-    return (v && mxIsChar(v)) ? mxArrayToString(v) : NULL;
-}
-
 static mxArray* make_name(const char* a, const char* b, const char* c) {
     char buf[512];
     snprintf(buf, sizeof buf, "%s%s%s", a, b ? b : "", c ? c : "");
@@ -48,50 +34,22 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         error = 1;
     }
     /* Buildxhat does not read data.settings.type (an invalid one is BuildAwG's error) */
+    int nk_ref = 1;  /* Num_Radial_Distortions as given: 0 means no K columns in INT (Buildxhat.m:71-72) */
     if (!error) {
-        const int r = fm_settings(prhs[0], &m.s, 0, msg, sizeof msg);
+        const int r = fm_settings(prhs[0], &m.s, 0, msg, sizeof msg, &nk_ref);
         if (r == 2) m.s.type = FBA_TYPE_FISHEYE;
         else if (r) error = 1;
     }
-    if (!error && m.s.num_radial < 1) {
-        snprintf(msg, sizeof msg, "Buildxhat: Num_Radial_Distortions must be >= 1");
+    if (!error && nk_ref < 0) {
+        snprintf(msg, sizeof msg, "Buildxhat: Num_Radial_Distortions must be >= 0");
         error = 1;
     }
     if (!error && fm_problem(prhs[0], &m, msg, sizeof msg)) error = 1;
-    const mxArray *EXT = prhs[1], *INT = prhs[2], *CNT = prhs[4];
-    const mxArray* TIE = nrhs > 3 ? prhs[3] : NULL;
-    if (!error && TIE && mxIsClass(TIE, "string")) {  /* ReadFiles' string array -> cellstr */
-        mxArray* in[1] = {(mxArray*)TIE};
-        if (mexCallMATLAB(1, &tie_cells, 1, in, "cellstr") == 0) TIE = tie_cells;
-    }
-    const int nimg = m.p.n_img, ncam = m.p.n_cam, nk = m.s.num_radial, cw = 5 + nk;
-    const int ntie = (TIE && mxIsCell(TIE)) ? (int)mxGetNumberOfElements(TIE) : 0;
-    if (!error && ntie != m.p.n_tie) {
-        snprintf(msg, sizeof msg, "Buildxhat: TIE has %d entries, data.numtie = %d", ntie, m.p.n_tie);
-        error = 1;
-    }
+    const mxArray *EXT = prhs[1], *INT = prhs[2], *TIE = NULL;
     /* start values from EXT / INT / CNT as Buildxhat.m:22-131 (not from data.points) */
-    for (int i = 1; !error && i <= nimg; ++i)
-        for (int a = 0; a < 6; ++a) m.eop0[6 * (i - 1) + a] = cell_num(EXT, i, 3 + a);
-    for (int k = 1; !error && k <= ncam; ++k)
-        for (int a = 0; a < cw; ++a) m.iop0[cw * (k - 1) + a] = cell_num(INT, 2 * k, 1 + a);
-    for (int t = 0; !error && t < ntie; ++t) {
-        char* id = mxIsChar(mxGetCell(TIE, t)) ? mxArrayToString(mxGetCell(TIE, t)) : NULL;
-        int found = 0;
-        for (mwIndex j = 1; id && j <= mxGetM(CNT) && !found; ++j) {
-            char* cid = cell_str(CNT, j, 1);
-            if (cid && strcmp(cid, id) == 0) {
-                for (int a = 0; a < 3; ++a) m.tie0[3 * t + a] = cell_num(CNT, j, 2 + a);
-                found = 1;
-            }
-            if (cid) mxFree(cid);
-        }
-        if (!found) {
-            snprintf(msg, sizeof msg, "Error Buildxhat(): can't find %s from .tie in .cnt", id ? id : "?");
-            error = 1;
-        }
-        if (id) mxFree(id);
-    }
+    if (!error && fm_start_values(&m, EXT, INT, prhs[3], prhs[4], nk_ref, &TIE, &tie_cells, msg, sizeof msg)) error = 1;
+    const int nimg = m.p.n_img, ncam = m.p.n_cam;
+    const int ntie = TIE ? (int)mxGetNumberOfElements(TIE) : 0;
     fba_ctx* ctx = error ? NULL : fm_context(&m);
     if (!error && !ctx) {
         snprintf(msg, sizeof msg, "Buildxhat: %s", fba_last_error());
@@ -114,7 +72,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         const int ee[6] = {s->est_Xc, s->est_Yc, s->est_Zc, s->est_omega, s->est_phi, s->est_kappa};
         static const char* en[6] = {"Xc_", "Yc_", "Zc_", "w_", "p_", "k_"};
         for (int i = 1; i <= nimg; ++i) {
-            char *img = cell_str(EXT, i, 1), *cam = cell_str(EXT, i, 2);
+            char *img = fm_cell_str(EXT, i, 1), *cam = fm_cell_str(EXT, i, 2);
             char suffix[256];
             snprintf(suffix, sizeof suffix, "%s_%s", img ? img : "", cam ? cam : "");
             for (int a = 0; a < 6; ++a)
@@ -123,12 +81,12 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
             if (cam) mxFree(cam);
         }
         for (int k = 1; k <= ncam; ++k) {
-            char* cam = cell_str(INT, 2 * k - 1, 1);
+            char* cam = fm_cell_str(INT, 2 * k - 1, 1);
             if (s->est_xp) mxSetCell(names, q++, make_name("xp_", cam, NULL));
             if (s->est_yp) mxSetCell(names, q++, make_name("yp_", cam, NULL));
             if (s->est_c) mxSetCell(names, q++, make_name("c_", cam, NULL));
             char head[32];
-            for (int j = 1; s->est_radial && j <= nk; ++j) {
+            for (int j = 1; s->est_radial && j <= nk_ref; ++j) {
                 snprintf(head, sizeof head, "k%d_", j);
                 mxSetCell(names, q++, make_name(head, cam, NULL));
             }

@@ -55,8 +55,13 @@ static int fm_type(const mxArray* settings) {
 }
 
 /* data.settings -> fba_settings (main.m:112-177); returns 0, 1 (settings missing) or 2 (invalid
- * type, BuildAwG.m:209-213) with a message */
-static int fm_settings(const mxArray* data, fba_settings* s, int clamp_nk, char* msg, size_t nmsg) {
+ * type, BuildAwG.m:209-213) with a message.
+ * Num_Radial_Distortions = 0 (nk_ref, when not NULL, receives the value as given):
+ *   clamp_nk = 1  BuildAwG.m:18-20 -- a local copy clamped to 1, Estimate_radial kept;
+ *   clamp_nk = 0  Buildxhat.m:13 / BuildRSD.m:3 -- no radial unknowns at all (the reference's K list is
+ *                 empty): the library's layout with one radial slot that is not estimated, which has the
+ *                 same unknowns in the same order. */
+static int fm_settings(const mxArray* data, fba_settings* s, int clamp_nk, char* msg, size_t nmsg, int* nk_ref) {
     const mxArray* st = mxIsStruct(data) ? mxGetField(data, 0, "settings") : NULL;
     if (!st || !mxIsStruct(st)) { snprintf(msg, nmsg, "data.settings is missing"); return 1; }
     memset(s, 0, sizeof *s);
@@ -72,7 +77,11 @@ static int fm_settings(const mxArray* data, fba_settings* s, int clamp_nk, char*
     s->est_radial = (int32_t)fm_num(st, 0, "Estimate_radial", 0, NULL);
     s->est_decent = (int32_t)fm_num(st, 0, "Estimate_decent", 0, NULL);
     s->num_radial = (int32_t)fm_num(st, 0, "Num_Radial_Distortions", 1, NULL);
-    if (clamp_nk && s->num_radial < 1) s->num_radial = 1; /* BuildAwG.m:18-20 (a local copy) */
+    if (nk_ref) *nk_ref = s->num_radial;
+    if (s->num_radial < 1) {
+        if (!clamp_nk) s->est_radial = 0; /* Buildxhat.m:88-93: an empty K, nothing estimated */
+        s->num_radial = 1;                /* BuildAwG.m:18-20 (a local copy) */
+    }
     s->type = fm_type(st);
     s->inner_constraints = (int32_t)fm_num(st, 0, "Inner_Constraints", 0, NULL);
     s->iteration_cap = (int32_t)fm_num(st, 0, "Iteration_Cap", 100, NULL);
@@ -163,23 +172,83 @@ static int fm_problem(const mxArray* data, mex_problem* m, char* msg, size_t nms
     return 0;
 }
 
+/* cell (r, c) of an M x N cell array (1-based as in MATLAB) */
+static inline const mxArray* fm_cell_at(const mxArray* C, mwIndex r, mwIndex c) {
+    const mwSize M = mxGetM(C);
+    if (r < 1 || c < 1 || r > M || c > mxGetN(C)) return NULL;
+    return mxGetCell(C, (c - 1) * M + (r - 1));
+}
+static inline double fm_cell_num(const mxArray* C, mwIndex r, mwIndex c) {
+    const mxArray* v = fm_cell_at(C, r, c);
+    return (v && mxGetNumberOfElements(v) > 0) ? mxGetScalar(v) : 0.0;
+}
+static inline char* fm_cell_str(const mxArray* C, mwIndex r, mwIndex c) {
+    const mxArray* v = fm_cell_at(C, r, c);
+    return (v && mxIsChar(v)) ? mxArrayToString(v) : NULL;
+}
+
+/* Buildxhat.m:22-131's start values from main.m's EXT / INT / TIE / CNT (EXT angles in radians,
+ * main.m:215-217) over the packed problem's eop0 / iop0 / tie0.  TIE may be a cellstr or ReadFiles'
+ * string array (*tie_cells receives the converted copy, to destroy); *tie_out the cellstr used.
+ * nk_ref: Num_Radial_Distortions as given (0: INT row 2 is xp yp c P1 P2, Buildxhat.m:71-72).
+ * Returns 0, or 1 with the reference's message (a TIE target not in CNT, Buildxhat.m:124-128). */
+static inline int fm_start_values(mex_problem* m, const mxArray* EXT, const mxArray* INT, const mxArray* TIE,
+                           const mxArray* CNT, int nk_ref, const mxArray** tie_out, mxArray** tie_cells,
+                           char* msg, size_t nmsg) {
+    *tie_cells = NULL;
+    if (TIE && mxIsClass(TIE, "string")) {  /* ReadFiles' string array -> cellstr */
+        mxArray* in[1] = {(mxArray*)TIE};
+        if (mexCallMATLAB(1, tie_cells, 1, in, "cellstr") == 0) TIE = *tie_cells;
+    }
+    *tie_out = TIE;
+    const int nimg = m->p.n_img, ncam = m->p.n_cam, nk = m->s.num_radial, cw = 5 + nk;
+    const int ntie = (TIE && mxIsCell(TIE)) ? (int)mxGetNumberOfElements(TIE) : 0;
+    if (ntie != m->p.n_tie || (TIE && !mxIsCell(TIE))) {
+        snprintf(msg, nmsg, "TIE has %d entries, data.numtie = %d", ntie, m->p.n_tie);
+        return 1;
+    }
+    for (int i = 1; i <= nimg; ++i)
+        for (int a = 0; a < 6; ++a) m->eop0[6 * (i - 1) + a] = fm_cell_num(EXT, i, 3 + a);
+    for (int k = 1; k <= ncam; ++k)  /* INT row 2: xp yp c K1..K_nk_ref P1 P2 */
+        for (int a = 0; a < cw; ++a) {
+            const int col = (a < 3 + nk_ref) ? a : (a < 3 + nk ? -1 : a - nk + nk_ref);
+            m->iop0[cw * (k - 1) + a] = col < 0 ? 0.0 : fm_cell_num(INT, 2 * k, 1 + col);
+        }
+    for (int t = 0; t < ntie; ++t) {
+        char* id = mxIsChar(mxGetCell(TIE, t)) ? mxArrayToString(mxGetCell(TIE, t)) : NULL;
+        int found = 0;
+        for (mwIndex j = 1; id && j <= mxGetM(CNT) && !found; ++j) {
+            char* cid = fm_cell_str(CNT, j, 1);
+            if (cid && strcmp(cid, id) == 0) {
+                for (int a = 0; a < 3; ++a) m->tie0[3 * t + a] = fm_cell_num(CNT, j, 2 + a);
+                found = 1;
+            }
+            if (cid) mxFree(cid);
+        }
+        if (!found) snprintf(msg, nmsg, "Error Buildxhat(): can't find %s from .tie in .cnt", id ? id : "?");
+        if (id) mxFree(id);
+        if (!found) return 1;
+    }
+    return 0;
+}
+
 /* ---- one cached context (the problem and settings hashed) ---- */
 static fba_ctx* g_fm_ctx = NULL;
 static uint64_t g_fm_key = 0;
 
-static void fm_release(void) {
+static inline void fm_release(void) {
     if (g_fm_ctx) fba_destroy(g_fm_ctx);
     g_fm_ctx = NULL;
     g_fm_key = 0;
 }
 
-static uint64_t fm_hash(uint64_t h, const void* d, size_t n) {
+static inline uint64_t fm_hash(uint64_t h, const void* d, size_t n) {
     const unsigned char* b = (const unsigned char*)d;
     for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
     return h;
 }
 
-static uint64_t fm_key(const mex_problem* m) {
+static inline uint64_t fm_key(const mex_problem* m) {
     const fba_problem* p = &m->p;
     const int cw = 5 + (m->s.num_radial < 1 ? 1 : m->s.num_radial);
     uint64_t h = 1469598103934665603ull;
@@ -199,7 +268,7 @@ static uint64_t fm_key(const mex_problem* m) {
 }
 
 /* the cached context for this problem (created on first use); NULL with fba_last_error() set */
-static fba_ctx* fm_context(const mex_problem* m) {
+static inline fba_ctx* fm_context(const mex_problem* m) {
     const uint64_t key = fm_key(m);
     if (g_fm_ctx && key == g_fm_key) return g_fm_ctx;
     fm_release();

@@ -5,12 +5,18 @@ matrix API, test infrastructure) and libfba.so, and its mexFunction is called wi
 of the ingest.
 
 * CPU: every drop-in (and the whole-loop gateway mex/fba_mex.c) compiles and links.
+* GPU: the whole-loop gateway, the reference's main.m:386-602 in one call,
+    [error, xhat, count, deltasum, v, RSD, stats, cx_diag, corr] = fba_mex(data, EXT, INT, TIE, CNT)
+  on cam0 Stage-3 against the dense oracle (count, deltasum history, xhat per element, v, RSD, sigma0^2,
+  diag(Cx), the EOP/IOP correlation blocks) and at config 3 (200 images x 5,000 tie points) against the
+  C oracle's direct bordered solve (count, xhat per element, sigma0^2);
 * GPU: on cam0 (shipped Stage-3 and a fish-eye variant, Stage-1) and a 2-camera rig --
     [error, xhat, xhatnames] = Buildxhat(data, EXT, INT, TIE, CNT)   bit-exact vs the oracle
     [error, A, misclosure, G, dist_scaling] = BuildAwG(data, xhat)   A per column <= 1e-12, w, G, ds
     RSD = BuildRSD(v, data, xhat)                                    <= 1e-12 (ids, x, y exact)
   and the reference's error behaviour: error = 1 for an invalid Type (BuildAwG.m:209-213), for a
-  TIE target missing from CNT (Buildxhat.m:124-128).
+  TIE target missing from CNT (Buildxhat.m:124-128); Num_Radial_Distortions = 0 accepted by Buildxhat
+  and BuildRSD as the reference does (an empty K list, Buildxhat.m:71-72, BuildRSD.m:3).
 """
 import ctypes as C
 import os
@@ -19,7 +25,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import ROOT, CAM0_VARIANTS  # noqa: F401
+from conftest import ROOT, CAM0_VARIANTS, dist_scaling_of, elem_rel_err, group_rel_err, variant_folder  # noqa: F401
 
 STUB = os.path.join(ROOT, "tests", "mexstub")
 LIBDIR = os.path.join(ROOT, "fish-eye_bundle_adjustment_amd")
@@ -161,7 +167,7 @@ def mexlibs(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("mex"))
     stub, libs = _build(out)
     mx = Mx(stub)
-    fns = {n: getattr(C.CDLL(libs[n]), "mexFunction") for n in DROPINS}
+    fns = {n: getattr(C.CDLL(libs[n]), "mexFunction") for n in DROPINS + ("fba_mex",)}
     yield mx, fns
     mx.L.mxstub_exit()  # mexAtExit: the cached libfba context
 
@@ -226,3 +232,96 @@ def test_mex_dropins_error_behaviour(fba, oracle, mexlibs, cam0_folders):
     data, EXT, INT, TIE, CNT = data_struct(mx, od)
     err, xhat, names = (mx.get(o) for o in mx.call(fns["Buildxhat"], 3, [data, EXT, INT, TIE, CNT]))
     assert err[0, 0] == 1 and xhat.size == 0
+
+
+def _mex_adjust(mx, fns, od, nlhs=9):
+    data, EXT, INT, TIE, CNT = data_struct(mx, od)
+    out = mx.call(fns["fba_mex"], nlhs, [data, EXT, INT, TIE, CNT])
+    assert mx.get(out[0])[0, 0] == 0
+    return out
+
+
+@pytest.mark.gpu
+def test_mex_whole_loop_matches_oracle_cam0(fba, oracle, mexlibs, cam0_folders):
+    """fba_mex(data, EXT, INT, TIE, CNT) -- main.m:386-602 from what main.m holds at line 386 -- on the
+    shipped cam0 Stage-3 (pinhole, inner constraints, tie points, 3 control points) against the dense
+    oracle: same count, the deltasum history, xhat per element <= 1e-9, v, the RSD cell, RMS, sigma0^2
+    <= 1e-9, diag(Cx) and the EOP/IOP correlation blocks (main.m:446-482, :602) <= 1e-7."""
+    mx, fns = mexlibs
+    od = oracle.load_folder(cam0_folders["stage3_pinhole"])
+    ro = oracle.adjust(od)
+    _, xhat, count, dsum, v, rsd, st, cxd, corr = _mex_adjust(mx, fns, od)
+    assert mx.get(count)[0, 0] == ro.iterations
+    np.testing.assert_allclose(mx.get(dsum)[0], ro.deltasum, rtol=0, atol=1e-9 * ro.deltasum[0])
+    x = mx.get(xhat)[:, 0]
+    for err in (group_rel_err(x, ro.xhat, ro.names, ro.dist_scaling), elem_rel_err(x, ro.xhat, ro.names, ro.dist_scaling)):
+        assert max(err.values()) <= 1e-9, err
+    st = mx.get(st)[:, 0]
+    assert abs(st[3] - ro.sigma02) <= 1e-9 * ro.sigma02
+    np.testing.assert_allclose(st[:3], ro.rms, rtol=1e-9)
+    assert np.abs(mx.get(v)[:, 0] - ro.v).max() <= 1e-8 * np.abs(ro.v).max()
+    cells = mx.get(rsd)
+    assert [r[0] for r in cells] == od.target and [r[1] for r in cells] == od.image
+    num = np.array([[c[0, 0] for c in r[4:]] for r in cells])
+    assert np.abs(num - ro.rsd).max() <= 1e-8 * np.abs(ro.rsd).max()
+    cdo, corro = oracle.covariance(od, ro)
+    np.testing.assert_allclose(mx.get(cxd)[:, 0], cdo, rtol=1e-7)
+    # corr: mu x mu x numImg (mxCreateNumericArray; the stub stores dims[0] x prod(dims[1:]))
+    u_img, u_cam = oracle.counts(od.settings)
+    mu = u_img + u_cam
+    cr = mx.get(corr).reshape(mu, mu, od.numImg, order="F")
+    for e in range(0, od.numImg, 7):
+        idx = list(range(e * u_img, (e + 1) * u_img))
+        k = int(od.cam_num[np.nonzero(od.ext_index == e)[0][0]])
+        idx += list(range(u_img * od.numImg + k * u_cam, u_img * od.numImg + (k + 1) * u_cam))
+        np.testing.assert_allclose(cr[:, :, e], corro[np.ix_(idx, idx)], rtol=0, atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_mex_whole_loop_matches_oracle_config3(fba, oracle, mexlibs, tmp_path):
+    """The same gateway at BASELINE.json config 3 (200 images x 5,000 tie points, 50k image points,
+    fish-eye, free network) against oracle/fba_cpu.c solving the reference's bordered system [S G; G' 0]
+    directly: count, xhat per element and per group <= 1e-9, sigma0^2 <= 1e-9."""
+    import fba_cpu
+    from fba_amd import synth
+    mx, fns = mexlibs
+    folder = synth.make_config(3, str(tmp_path / "c3"))
+    od = oracle.load_folder(folder)
+    ref = fba_cpu.CpuAdjustment(od, solver="kkt")
+    it = ref.adjust()
+    _, s02 = ref.residuals()
+    ref.close()
+    _, xhat, count, dsum, v, rsd, st = _mex_adjust(mx, fns, od, nlhs=7)
+    assert mx.get(count)[0, 0] == it
+    x = mx.get(xhat)[:, 0]
+    dsc = dist_scaling_of(od)
+    for err in (group_rel_err(x, ref.xhat, ref.names, dsc), elem_rel_err(x, ref.xhat, ref.names, dsc)):
+        assert max(err.values()) <= 1e-9, err
+    assert abs(mx.get(st)[3, 0] - s02) <= 1e-9 * s02
+
+
+@pytest.mark.gpu
+def test_mex_nk0_buildxhat_buildrsd(fba, oracle, mexlibs, tmp_path):
+    """Num_Radial_Distortions = 0: the reference's Buildxhat lays out no K (an empty list,
+    Buildxhat.m:71-72; INT row 2 is xp yp c P1 P2) and BuildRSD counts none (BuildRSD.m:3) -- both drop-ins
+    follow it (only BuildAwG clamps its local copy to 1, BuildAwG.m:18-20); the whole-loop gateway
+    rejects the combination with Estimate_Radial_Distortions = 1 (error = 1), where the reference's
+    xhat + delta would not conform."""
+    mx, fns = mexlibs
+    folder = variant_folder(str(tmp_path), "nk0", {"Num_Radial_Distortions": "0"})
+    od = oracle.load_folder(folder)
+    assert od.settings["Num_Radial_Distortions"] == 0
+    data, EXT, INT, TIE, CNT = data_struct(mx, od)
+    err, xhat, names = mx.call(fns["Buildxhat"], 3, [data, EXT, INT, TIE, CNT])
+    assert mx.get(err)[0, 0] == 0
+    xo, no = oracle.buildxhat(od)
+    np.testing.assert_array_equal(mx.get(xhat)[:, 0], xo)
+    assert [r[0] for r in mx.get(names)] == no and not any(n.startswith("k1_") for n in no)
+    rng = np.random.default_rng(5)
+    v = rng.standard_normal(2 * len(od.x))
+    rsd = mx.get(mx.call(fns["BuildRSD"], 1, [mx.mat(v.reshape(-1, 1)), data, mx.mat(xo.reshape(-1, 1))])[0])
+    num = np.array([[c[0, 0] for c in r[4:]] for r in rsd])
+    ref = oracle.build_rsd(od, v, xo)
+    assert np.abs(num - ref).max() <= 1e-12 * np.abs(ref).max()
+    out = mx.call(fns["fba_mex"], 2, [data, EXT, INT, TIE, CNT])
+    assert mx.get(out[0])[0, 0] == 1 and mx.get(out[1]).size == 0
