@@ -19,7 +19,7 @@ NK_MAX = 8
 
 # every symbol include/fba.h declares
 EXPORTS = (
-    "fba_last_error", "fba_abi_version", "fba_count_unknowns", "fba_partition", "fba_create",
+    "fba_last_error", "fba_abi_version", "fba_count_unknowns", "fba_partition", "fba_image_order", "fba_create",
     "fba_destroy", "fba_buildxhat", "fba_set_xhat", "fba_get_xhat", "fba_build_awg",
     "fba_accumulate", "fba_reduce_buffer", "fba_synchronize", "fba_solve_update", "fba_solve_update_async",
     "fba_deltasum_device", "fba_solve_finish", "fba_step", "fba_adjust",
@@ -64,6 +64,7 @@ def _load():
         "fba_abi_version": ([], C.c_int),
         "fba_count_unknowns": ([P, P, P], C.c_int),
         "fba_partition": ([P, I, P, P], C.c_int),
+        "fba_image_order": ([P, P, P], C.c_int),
         "fba_create": ([P, P, P, P], C.c_int),
         "fba_destroy": ([P], None),
         "fba_buildxhat": ([P, P, P], C.c_int),
@@ -304,6 +305,15 @@ def partition(packed: PackedProblem, world: int):
     q = np.zeros(max(packed.n_pts, 1), dtype=np.int32)
     check(lib.fba_partition(C.byref(packed.struct), int(world), ptr(t), ptr(q)))
     return t[: packed.n_tie], q[: packed.n_pts]
+
+
+def image_order(packed: PackedProblem):
+    """fba_image_order: slot -> EXT row (-1: padding slot) of the reduced system's image part."""
+    n = C.c_int32()
+    check(lib.fba_image_order(C.byref(packed.struct), None, C.byref(n)))
+    out = np.zeros(max(n.value, 1), dtype=np.int32)
+    check(lib.fba_image_order(C.byref(packed.struct), ptr(out), C.byref(n)))
+    return out[: n.value]
 
 
 def finish_stats(packed: PackedProblem, settings: Settings, sx2, sy2, vtpv):

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <map>
 #include <numeric>
 #include <tuple>
@@ -854,7 +855,9 @@ static int solve_body(Ctx* c) {
 
 static int solve_enqueue(Ctx* c) {
     if (!c->have_lin) { set_error("fba_solve_update before fba_accumulate"); return FBA_ERR_ARG; }
-    return run_graph(c, 1, [&] { return solve_body(c); });
+    const int rc = run_graph(c, 1, [&] { return solve_body(c); });
+    if (rc == FBA_OK) ++c->solves_enqueued;  // k_sum_parts' count once this solve is done
+    return rc;
 }
 
 // wait for the solve, read scal (again from the device when `recopy`: a caller may have all-reduced
@@ -998,26 +1001,36 @@ static void print_panel_trace(Ctx* c) {
 }
 
 // Completion of a solve: k_sum_parts, the last kernel of every solve, writes its results to host-mapped
-// memory and then its sequence number; fba_step polls that number (a spin on coherent host memory returns
-// a few us after the GPU's write, where hipStreamSynchronize's wake-up is slower) -- later work on the
-// stream is ordered after the solve anyway.  The stream is synchronised when a caller re-copies scal (the
-// multi-GPU path), with tracing or timing on, with FBA_SYNC=1, and after ~5 s without the number (a
-// faulted launch: the synchronisation reports it).
+// memory and then the device's count of finished solves; fba_step polls that count until it reaches the
+// number of solves enqueued on the context (a spin on coherent host memory returns a few us after the
+// GPU's write, where hipStreamSynchronize's wake-up is slower) -- later work on the stream is ordered after
+// the solve anyway.  The poll spins briefly, then yields the core between reads; once the count is there,
+// hipStreamQuery surfaces an asynchronous error of the stream at once.  The stream is synchronised instead
+// when a caller re-copies scal (the multi-GPU path), with tracing or timing on, with FBA_SYNC=1, and after
+// ~5 s without the count (a faulted launch: the synchronisation reports it).
 static bool wait_solve_seq(Ctx* c) {
     static const bool force_sync = getenv("FBA_SYNC") && atoi(getenv("FBA_SYNC")) != 0;
     if (force_sync || c->timing || c->d_ptrace || c->d_lrprof) return false;
-    const double want = c->solve_seq + 1.0;
+    const double want = (double)c->solves_enqueued;
     volatile const double* seq = c->h_pinned + 4;
     const auto t0 = std::chrono::steady_clock::now();
-    for (unsigned it = 0; *seq < want; ++it)
-        if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) return false;
+    for (unsigned it = 0; *seq < want; ++it) {
+        if (it < 4096) continue;  // ~the first 10-20 us: spin
+        std::this_thread::yield();
+        if ((it & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) return false;
+    }
     std::atomic_thread_fence(std::memory_order_acquire);
     return true;
 }
 
 static int solve_finish(Ctx* c, double* dsum, bool recopy) {
     if (recopy) FBA_HIP(hipMemcpyAsync(c->h_pinned, c->d_scal, sizeof(double) * 4, hipMemcpyDeviceToHost, c->stream));
-    if (recopy || !wait_solve_seq(c)) FBA_HIP(hipStreamSynchronize(c->stream));
+    if (recopy || !wait_solve_seq(c)) {
+        FBA_HIP(hipStreamSynchronize(c->stream));
+    } else {
+        const hipError_t q = hipStreamQuery(c->stream);  // (hipErrorNotReady: later work queued, no error)
+        if (q != hipSuccess && q != hipErrorNotReady) FBA_HIP(q);
+    }
     c->solve_seq = c->h_pinned[4];
     if (c->d_ptrace) print_panel_trace(c);
     if (c->timing) {
@@ -1029,16 +1042,19 @@ static int solve_finish(Ctx* c, double* dsum, bool recopy) {
         (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[7]);
         c->last_ms[7] = ms;
     }
-    c->have_delta = true;
-    c->have_factor = true;
     c->iterations++;
     const double info = c->h_pinned[1];
     *dsum = c->h_pinned[2];
     if (info < 0.0) {
-        set_error("device hand-off timeout in the block Cholesky / backward solve (a workgroup of k_panel or "
-                  "k_bwd_flow was not resident)");
+        // k_update left xhat as it was (fba_chol.hip, bounded polls): the context stays usable
+        set_error("device hand-off timeout in the block Cholesky / backward solve (a workgroup of k_chol_flow, "
+                  "k_panel or k_bwd_flow was not resident); xhat left unchanged");
+        c->have_delta = false;
+        c->have_factor = false;
         return FBA_ERR_HIP;
     }
+    c->have_delta = true;
+    c->have_factor = true;
     if (info != 0.0) {
         char buf[160];
         snprintf(buf, sizeof buf, "reduced normal matrix not positive definite (pivot %ld): singular / unconstrained network",
@@ -1079,6 +1095,20 @@ int fba_partition(const fba_problem* p, int32_t world, int32_t* tie_owner, int32
     partition(p, world, t, q);
     if (tie_owner) std::copy(t.begin(), t.end(), tie_owner);
     if (ctl_owner) std::copy(q.begin(), q.end(), ctl_owner);
+    return FBA_OK;
+}
+
+int fba_image_order(const fba_problem* p, int32_t* order, int32_t* n_slots) {
+    if (!p || !n_slots) { set_error("NULL argument"); return FBA_ERR_ARG; }
+    if (p->n_img < 0 || (p->n_pts > 0 && (!p->img || !p->tie))) { set_error("bad problem"); return FBA_ERR_ARG; }
+    for (int64_t i = 0; i < p->n_pts; ++i)
+        if (p->img[i] < 0 || p->img[i] >= p->n_img || p->tie[i] < -1 || p->tie[i] >= p->n_tie) {
+            set_error("image / tie index out of range");
+            return FBA_ERR_ARG;
+        }
+    const std::vector<int32_t> ord = camera_order(p);
+    *n_slots = (int32_t)ord.size();
+    if (order) std::copy(ord.begin(), ord.end(), order);
     return FBA_OK;
 }
 

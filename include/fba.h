@@ -117,6 +117,15 @@ int fba_count_unknowns(const fba_problem* p, const fba_settings* s, int64_t* u_o
 int fba_partition(const fba_problem* p, int32_t world, int32_t* tie_owner /*[n_tie]*/,
                   int32_t* ctl_owner /*[n_pts], -1 for tie observations*/);
 
+/* Camera-side elimination order of the reduced system the device factorisation uses (host only, no
+ * GPU): nested dissection of the images' co-visibility graph (fba_order.cpp).  Slot k of the reduced
+ * system's image part (unknowns 6k..6k+5) holds EXT row order[k], or -1 for a padding slot (padding
+ * keeps independent subtrees in separate 128-row blocks); the camera unknowns follow the last slot, and
+ * inner constraints are bordered on the first min(n_slots, 21) slots.  order may be NULL to query
+ * *n_slots.  No reference counterpart (main.m:432 inverts the dense bordered matrix): for callers that
+ * factor the reduced system themselves on the same block pattern (oracle/fba_cpu.c's cpu_baseline). */
+int fba_image_order(const fba_problem* p, int32_t* order /*[n_slots]*/, int32_t* n_slots);
+
 int fba_create(const fba_problem* p, const fba_settings* s, const fba_options* o, fba_ctx** out);
 void fba_destroy(fba_ctx* ctx);
 

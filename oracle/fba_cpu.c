@@ -74,7 +74,38 @@ typedef struct fbo_ctx {
     uint8_t* owned;                 /* [n_pts] observation shard mask (NULL = all)         */
     int count_cam;                  /* this shard's deltasum includes the camera unknowns  */
     int nthreads;
+    struct fbo_sparse* sparse;      /* block-sparse form of the reduced system (fbo_sparse_setup) or NULL */
+    int sparse_on;                  /* fbo_reduce writes into it instead of the dense S                */
 } fbo_ctx;
+static void sparse_free(struct fbo_sparse* sp);
+
+#define SB 128                /* block size (the GPU's NB)               */
+#define SBB (SB * SB)
+#define NRHS 15               /* -r | A (7) | B (7)                      */
+
+typedef struct fbo_sparse {
+    int64_t n_pad;            /* padded order (multiple of SB)           */
+    int nb, n_loc, n_slots;
+    int64_t* pos;             /* [u_c] compressed index -> position      */
+    int32_t* slot_of;         /* [n_img] EXT row -> slot                 */
+    int32_t* boff;            /* [nb * nb] block (i, j), i >= j -> index in pool, -1 outside the pattern */
+    int nblk;
+    double* pool;             /* nblk blocks, column-major SB x SB       */
+    int32_t *cptr, *crow;     /* rows(k) > k of L's pattern, ascending   */
+    int nlev;
+    int32_t *lptr, *lcol;     /* columns per level                       */
+    int32_t *pptr, *pblk;     /* per level: panel blocks (i, k) as pairs */
+    int32_t *tptr, *tgt;      /* per level: update targets (i, j) pairs  */
+    int32_t *sptr, *src;      /* per target: its source columns k, ascending */
+    double* rhs;              /* n_pad x NRHS column-major               */
+    double* Sc;               /* camera block partials (thread-private)  */
+} fbo_sparse;
+
+static inline double* sblk(const fbo_sparse* sp, int64_t pi, int64_t pj) {  /* entry (pi, pj), pi >= pj */
+    const int32_t b = sp->boff[(pi / SB) * sp->nb + pj / SB];
+    return b < 0 ? NULL : sp->pool + (int64_t)b * SBB + (pj % SB) * SB + pi % SB;
+}
+
 
 /* ---------------------------------------------------------------------------------------------
  * forward model, BuildAwG.m:160-212
@@ -297,6 +328,7 @@ void fbo_destroy(fbo_ctx* c) {
     free(c->img_ptr); free(c->img_obs); free(c->tie_ptr); free(c->tie_obs); free(c->rmax);
     free(c->J); free(c->w); free(c->Wc); free(c->Qc); free(c->Vinv); free(c->bp); free(c->delta);
     free(c->owned);
+    sparse_free(c->sparse);
     free(c);
 }
 
@@ -365,7 +397,25 @@ int fbo_reduce(fbo_ctx* c, const double* xhat, double* S, double* r, double* G) 
     }
     if (bad) return 1;
 
-    memset(S, 0, sizeof(double) * u_c * u_c);
+    /* sparse (fbo_sparse_solve's form): S's lower pattern blocks in the permuted order, no dense array;
+     * image-image entries written by the row that is lower in that order, image-camera entries
+     * (camera rows come last) into the camera rows by the image's thread */
+    fbo_sparse* sp = c->sparse_on ? c->sparse : NULL;
+#define SADD_L(i, j, v)                                                             \
+    do {                                                                            \
+        if (!sp) S[(i) * u_c + (j)] += (v);                                         \
+        else {                                                                      \
+            const int64_t pi_ = sp->pos[i], pj_ = sp->pos[j];                       \
+            if (pi_ >= pj_) *sblk(sp, pi_, pj_) += (v);                             \
+        }                                                                           \
+    } while (0)
+#define SADD_T(i, j, v)                                                             \
+    do {                                                                            \
+        if (!sp) S[(i) * u_c + (j)] += (v);                                         \
+        else *sblk(sp, sp->pos[j], sp->pos[i]) += (v);                              \
+    } while (0)
+    if (sp) memset(sp->pool, 0, sizeof(double) * SBB * (size_t)sp->nblk);
+    else memset(S, 0, sizeof(double) * u_c * u_c);
     memset(r, 0, sizeof(double) * u_c);
     /* image row blocks: direct terms + Schur terms of every point the image sees */
 #pragma omp parallel for schedule(dynamic, 1) num_threads(c->nthreads)
@@ -379,9 +429,8 @@ int fbo_reduce(fbo_ctx* c, const double* xhat, double* S, double* r, double* G) 
             split_row(c, c->J + 2 * NF * o + NF, je[1], jc[1], jp[1]);
             const double* wo = c->w + 2 * o;
             for (int a = 0; a < ui; ++a) {
-                double* Sa = S + (re + a) * u_c;
-                for (int bb = 0; bb < ui; ++bb) Sa[re + bb] += px * je[0][a] * je[0][bb] + py * je[1][a] * je[1][bb];
-                for (int bb = 0; bb < uc; ++bb) Sa[kc + bb] += px * je[0][a] * jc[0][bb] + py * je[1][a] * jc[1][bb];
+                for (int bb = 0; bb < ui; ++bb) SADD_L(re + a, re + bb, px * je[0][a] * je[0][bb] + py * je[1][a] * je[1][bb]);
+                for (int bb = 0; bb < uc; ++bb) SADD_T(re + a, kc + bb, px * je[0][a] * jc[0][bb] + py * je[1][a] * jc[1][bb]);
                 r[re + a] += px * je[0][a] * wo[0] + py * je[1][a] * wo[1];
             }
             if (t < 0) continue;
@@ -397,12 +446,33 @@ int fbo_reduce(fbo_ctx* c, const double* xhat, double* S, double* r, double* G) 
                 const int64_t o2 = c->tie_obs[q2], e2 = in->img[o2] * ui, k2 = cam0 + in->cam[o2] * uc;
                 const double* W2 = c->Wc + 18 * o2;
                 const double* Q2 = c->Qc + 3 * CWMAX * o2;
+                if (sp && ui > 0) {
+                    /* sparse fast path: the image pair's entries are all lower or all upper; when neither
+                     * image's positions straddle a block boundary they sit in one block, and so do the
+                     * camera columns of this row image */
+                    const int64_t pr = sp->pos[re], pc = sp->pos[e2], pk = sp->pos[k2];
+                    const int fit_r = pr % SB + ui <= SB, fit_c = pc % SB + ui <= SB, fit_k = uc == 0 || pk % SB + uc <= SB;
+                    if (fit_r && fit_c && fit_k && e2 != re) {
+                        if (pr > pc) {
+                            double* base = sblk(sp, pr, pc);
+                            for (int bb = 0; bb < ui; ++bb)
+                                for (int a = 0; a < ui; ++a)
+                                    base[bb * SB + a] -= Y[a][0] * W2[bb * 3] + Y[a][1] * W2[bb * 3 + 1] + Y[a][2] * W2[bb * 3 + 2];
+                        }
+                        if (uc > 0) {
+                            double* kb = sblk(sp, pk, pr);  /* (camera row, image column), column-major */
+                            for (int a = 0; a < ui; ++a)
+                                for (int bb = 0; bb < uc; ++bb)
+                                    kb[a * SB + bb] -= Y[a][0] * Q2[bb * 3] + Y[a][1] * Q2[bb * 3 + 1] + Y[a][2] * Q2[bb * 3 + 2];
+                        }
+                        continue;
+                    }
+                }
                 for (int a = 0; a < ui; ++a) {
-                    double* Sa = S + (re + a) * u_c;
                     for (int bb = 0; bb < ui; ++bb)
-                        Sa[e2 + bb] -= Y[a][0] * W2[bb * 3] + Y[a][1] * W2[bb * 3 + 1] + Y[a][2] * W2[bb * 3 + 2];
+                        SADD_L(re + a, e2 + bb, -(Y[a][0] * W2[bb * 3] + Y[a][1] * W2[bb * 3 + 1] + Y[a][2] * W2[bb * 3 + 2]));
                     for (int bb = 0; bb < uc; ++bb)
-                        Sa[k2 + bb] -= Y[a][0] * Q2[bb * 3] + Y[a][1] * Q2[bb * 3 + 1] + Y[a][2] * Q2[bb * 3 + 2];
+                        SADD_T(re + a, k2 + bb, -(Y[a][0] * Q2[bb * 3] + Y[a][1] * Q2[bb * 3 + 1] + Y[a][2] * Q2[bb * 3 + 2]));
                 }
             }
         }
@@ -475,16 +545,20 @@ int fbo_reduce(fbo_ctx* c, const double* xhat, double* S, double* r, double* G) 
         for (int t = 0; t < nt; ++t) {
             const double* Sc = part + (size_t)t * (nc * nc + nc);
             for (int64_t a = 0; a < nc; ++a) {
-                for (int64_t bb = 0; bb < nc; ++bb) S[(cam0 + a) * u_c + cam0 + bb] += Sc[a * nc + bb];
+                for (int64_t bb = 0; bb < nc; ++bb) SADD_L(cam0 + a, cam0 + bb, Sc[a * nc + bb]);
                 r[cam0 + a] += Sc[nc * nc + a];
             }
         }
         free(part);
-        /* camera-image blocks are the transpose of the image-camera blocks */
+        /* camera-image blocks are the transpose of the image-camera blocks (the sparse form has them) */
+        if (!sp) {
 #pragma omp parallel for schedule(static) num_threads(c->nthreads)
-        for (int64_t a = 0; a < nc; ++a)
-            for (int64_t bb = 0; bb < cam0; ++bb) S[(cam0 + a) * u_c + bb] = S[bb * u_c + cam0 + a];
+            for (int64_t a = 0; a < nc; ++a)
+                for (int64_t bb = 0; bb < cam0; ++bb) S[(cam0 + a) * u_c + bb] = S[bb * u_c + cam0 + a];
+        }
     }
+#undef SADD_L
+#undef SADD_T
 
     if (G) {
         memset(G, 0, sizeof(double) * u_c * 7);
@@ -585,3 +659,401 @@ double fbo_residuals(const fbo_ctx* c, double* v) {
     }
     return vtpv;
 }
+
+/* =============================================================================================
+ * Block-sparse Cholesky of the reduced camera system (bench.py's cpu_baseline; also a third solver
+ * the parity tests cross-check).  The reference inverts the dense bordered matrix (main.m:428-440);
+ * here -- as on the GPU, on the SAME block pattern -- the reduced system's unknowns are permuted into
+ * the device factorisation's camera-side order (fba_image_order: nested dissection of the image
+ * co-visibility graph, padding slots, camera unknowns last), S is accumulated straight into its
+ * 128 x 128 lower pattern blocks (no dense u_c x u_c array), the inner-constraint border is folded in
+ * locally (M = S + A A', A = G_l W_l^1/2 on the first n_loc slots, B = G D; the 14 x 14 combine below
+ * restores the exact bordered solution), and M is factored right-looking, one elimination-tree level
+ * at a time: the level's diagonal blocks (dpotrf), its panel blocks (dtrsm), then every target block
+ * of the level's updates (dsyrk / dgemm, a target's sources in order), each step an OpenMP loop over
+ * independent blocks with single-threaded BLAS calls (the caller's OpenBLAS through scipy's function
+ * pointers, fbo_set_blas).
+ * ============================================================================================= */
+typedef void (*dgemm_fn)(const char*, const char*, const int*, const int*, const int*, const double*, const double*,
+                         const int*, const double*, const int*, const double*, double*, const int*);
+typedef void (*dsyrk_fn)(const char*, const char*, const int*, const int*, const double*, const double*, const int*,
+                         const double*, double*, const int*);
+typedef void (*dtrsm_fn)(const char*, const char*, const char*, const char*, const int*, const int*, const double*,
+                         const double*, const int*, double*, const int*);
+typedef void (*dpotrf_fn)(const char*, const int*, double*, const int*, int*);
+static dgemm_fn g_dgemm;
+static dsyrk_fn g_dsyrk;
+static dtrsm_fn g_dtrsm;
+static dpotrf_fn g_dpotrf;
+
+void fbo_set_blas(void* dgemm, void* dsyrk, void* dtrsm, void* dpotrf) {
+    g_dgemm = (dgemm_fn)dgemm;
+    g_dsyrk = (dsyrk_fn)dsyrk;
+    g_dtrsm = (dtrsm_fn)dtrsm;
+    g_dpotrf = (dpotrf_fn)dpotrf;
+}
+
+/* symbolic factorisation on the permuted block pattern; slots[n_slots]: EXT row per slot (-1 padding) */
+int fbo_sparse_setup(fbo_ctx* c, const int32_t* slots, int n_slots) {
+    const fbo_input* in = &c->in;
+    fbo_sparse* sp = calloc(1, sizeof(fbo_sparse));
+    const int ui = c->u_img, uc = c->u_cam;
+    sp->n_slots = n_slots;
+    const int64_t cam0p = 6 * (int64_t)n_slots;
+    sp->n_pad = ((cam0p + (int64_t)uc * in->n_cam + SB - 1) / SB) * SB;
+    if (sp->n_pad == 0) sp->n_pad = SB;
+    const int nb = sp->nb = (int)(sp->n_pad / SB);
+    sp->n_loc = in->ic ? (n_slots < SB / 6 ? n_slots : SB / 6) : 0;
+    sp->slot_of = malloc(sizeof(int32_t) * (in->n_img + 1));
+    for (int e = 0; e < in->n_img; ++e) sp->slot_of[e] = -1;
+    for (int s = 0; s < n_slots; ++s)
+        if (slots[s] >= 0 && slots[s] < in->n_img) sp->slot_of[slots[s]] = s;
+    for (int e = 0; e < in->n_img; ++e)
+        if (sp->slot_of[e] < 0) { free(sp->slot_of); free(sp); return 1; }
+    sp->pos = malloc(sizeof(int64_t) * (c->u_c + 1));
+    for (int64_t e = 0; e < in->n_img; ++e)
+        for (int a = 0; a < ui; ++a) sp->pos[e * ui + a] = 6 * (int64_t)sp->slot_of[e] + a;
+    for (int64_t k = 0; k < in->n_cam; ++k)
+        for (int a = 0; a < uc; ++a) sp->pos[(int64_t)ui * in->n_img + k * uc + a] = cam0p + k * uc + a;
+    /* the initial block pattern (lower): diagonal, co-visible image pairs, camera rows, local border */
+    uint8_t* pat = calloc((size_t)nb * nb, 1);
+    for (int b = 0; b < nb; ++b) pat[b * nb + b] = 1;
+#define MARK(pi, pj) do { int64_t a_ = (pi) / SB, b_ = (pj) / SB; if (a_ < b_) { int64_t t_ = a_; a_ = b_; b_ = t_; } pat[a_ * nb + b_] = 1; } while (0)
+    for (int64_t p = 0; p < in->n_tie; ++p)
+        for (int64_t q1 = c->tie_ptr[p]; q1 < c->tie_ptr[p + 1]; ++q1)
+            for (int64_t q2 = c->tie_ptr[p]; q2 < c->tie_ptr[p + 1]; ++q2) {
+                const int64_t s1 = 6 * (int64_t)sp->slot_of[in->img[c->tie_obs[q1]]], s2 = 6 * (int64_t)sp->slot_of[in->img[c->tie_obs[q2]]];
+                MARK(s1, s2); MARK(s1 + 5, s2); MARK(s1, s2 + 5); MARK(s1 + 5, s2 + 5);
+            }
+    for (int64_t e = 0; e < in->n_img; ++e) MARK(6 * (int64_t)sp->slot_of[e] + 5, 6 * (int64_t)sp->slot_of[e]);  /* own 6 x 6 */
+    for (int64_t r = cam0p; r < cam0p + (int64_t)uc * in->n_cam; ++r)
+        for (int b = 0; b <= r / SB; ++b) pat[(r / SB) * nb + b] = 1;  /* camera rows couple to every image */
+    /* (the local border, positions < 6 n_loc <= 126, lies inside diagonal block 0) */
+#undef MARK
+    /* fill: for k ascending, every pair of rows below k's diagonal */
+    int32_t* rows = malloc(sizeof(int32_t) * nb);
+    for (int k = 0; k < nb; ++k) {
+        int n = 0;
+        for (int i = k + 1; i < nb; ++i)
+            if (pat[i * nb + k]) rows[n++] = i;
+        for (int x = 0; x < n; ++x)
+            for (int y = 0; y <= x; ++y) pat[rows[x] * nb + rows[y]] = 1;
+    }
+    sp->boff = malloc(sizeof(int32_t) * nb * nb);
+    sp->cptr = calloc(nb + 1, sizeof(int32_t));
+    int nblk = 0, nrow = 0;
+    for (int i = 0; i < nb; ++i)
+        for (int j = 0; j < nb; ++j) sp->boff[i * nb + j] = (j <= i && pat[i * nb + j]) ? nblk++ : -1;
+    for (int k = 0; k < nb; ++k)
+        for (int i = k + 1; i < nb; ++i) nrow += pat[i * nb + k];
+    sp->nblk = nblk;
+    sp->crow = malloc(sizeof(int32_t) * (nrow + 1));
+    for (int k = 0, q = 0; k < nb; ++k) {
+        for (int i = k + 1; i < nb; ++i)
+            if (pat[i * nb + k]) sp->crow[q++] = i;
+        sp->cptr[k + 1] = q;
+    }
+    /* elimination-tree levels: a column's level is one above its children's highest */
+    int32_t* lev = calloc(nb, sizeof(int32_t));
+    int nlev = 0;
+    for (int k = 0; k < nb; ++k) {
+        if (sp->cptr[k + 1] > sp->cptr[k]) {
+            const int par = sp->crow[sp->cptr[k]];
+            if (lev[par] < lev[k] + 1) lev[par] = lev[k] + 1;
+        }
+        if (lev[k] + 1 > nlev) nlev = lev[k] + 1;
+    }
+    sp->nlev = nlev;
+    sp->lptr = calloc(nlev + 1, sizeof(int32_t));
+    sp->lcol = malloc(sizeof(int32_t) * nb);
+    for (int k = 0; k < nb; ++k) sp->lptr[lev[k] + 1]++;
+    for (int l = 0; l < nlev; ++l) sp->lptr[l + 1] += sp->lptr[l];
+    {
+        int32_t* fill = malloc(sizeof(int32_t) * (nlev + 1));
+        memcpy(fill, sp->lptr, sizeof(int32_t) * (nlev + 1));
+        for (int k = 0; k < nb; ++k) sp->lcol[fill[lev[k]]++] = k;
+        free(fill);
+    }
+    /* per level: panel blocks (i, k) and update targets (i, j) with their sources */
+    sp->pptr = calloc(nlev + 1, sizeof(int32_t));
+    sp->pblk = malloc(sizeof(int32_t) * 2 * (nrow + 1));
+    int np = 0;
+    int64_t cap_t = 1024, nt = 0, cap_s = 4096, ns = 0;
+    sp->tptr = calloc(nlev + 1, sizeof(int32_t));
+    sp->tgt = malloc(sizeof(int32_t) * 2 * cap_t);
+    sp->sptr = malloc(sizeof(int32_t) * (cap_t + 1));
+    sp->src = malloc(sizeof(int32_t) * cap_s);
+    sp->sptr[0] = 0;
+    int32_t* tmark = malloc(sizeof(int32_t) * nb * nb);
+    int64_t* tkeys = malloc(sizeof(int64_t) * ((int64_t)nb * nb + 1));
+    for (int64_t q = 0; q < (int64_t)nb * nb; ++q) tmark[q] = -1;
+    for (int l = 0; l < nlev; ++l) {
+        int64_t nk = 0;
+        for (int x = sp->lptr[l]; x < sp->lptr[l + 1]; ++x) {
+            const int k = sp->lcol[x];
+            for (int q = sp->cptr[k]; q < sp->cptr[k + 1]; ++q) {
+                sp->pblk[2 * np] = sp->crow[q];
+                sp->pblk[2 * np + 1] = k;
+                ++np;
+                for (int q2 = sp->cptr[k]; q2 <= q; ++q2) {
+                    const int64_t key = (int64_t)sp->crow[q] * nb + sp->crow[q2];
+                    if (tmark[key] != l) { tmark[key] = l; tkeys[nk++] = key; }
+                }
+            }
+        }
+        sp->pptr[l + 1] = np;
+        /* targets in ascending (i, j) order (shell sort of the keys); each target's sources: the level's
+         * columns k with both i and j in rows(k), ascending */
+        if (nk > 1) {
+            int64_t* ks = tkeys;
+            for (int64_t gap = nk / 2; gap > 0; gap /= 2)
+                for (int64_t a = gap; a < nk; ++a) {
+                    int64_t v = ks[a], b = a;
+                    while (b >= gap && ks[b - gap] > v) { ks[b] = ks[b - gap]; b -= gap; }
+                    ks[b] = v;
+                }
+        }
+        for (int64_t t = 0; t < nk; ++t) {
+            const int i = (int)(tkeys[t] / nb), j = (int)(tkeys[t] % nb);
+            if (nt >= cap_t) {
+                cap_t *= 2;
+                sp->tgt = realloc(sp->tgt, sizeof(int32_t) * 2 * cap_t);
+                sp->sptr = realloc(sp->sptr, sizeof(int32_t) * (cap_t + 1));
+            }
+            sp->tgt[2 * nt] = i;
+            sp->tgt[2 * nt + 1] = j;
+            for (int x = sp->lptr[l]; x < sp->lptr[l + 1]; ++x) {
+                const int k = sp->lcol[x];
+                if (sp->boff[i * nb + k] >= 0 && sp->boff[j * nb + k] >= 0 && i > k && j > k) {
+                    if (ns >= cap_s) { cap_s *= 2; sp->src = realloc(sp->src, sizeof(int32_t) * cap_s); }
+                    sp->src[ns++] = k;
+                }
+            }
+            sp->sptr[++nt] = (int32_t)ns;
+        }
+        sp->tptr[l + 1] = (int32_t)nt;
+    }
+    free(tmark);
+    free(tkeys);
+    free(rows);
+    free(lev);
+    free(pat);
+    sp->pool = malloc(sizeof(double) * SBB * (size_t)(nblk > 0 ? nblk : 1));
+    sp->rhs = malloc(sizeof(double) * sp->n_pad * NRHS);
+    const int64_t ncam = (int64_t)uc * in->n_cam;
+    sp->Sc = malloc(sizeof(double) * ((size_t)c->nthreads * (ncam * ncam + ncam) + 1));
+    c->sparse = sp;
+    return 0;
+}
+
+void fbo_sparse_info(const fbo_ctx* c, int64_t* out /*[6]: n_pad, blocks, levels, panel blocks, targets, sources*/) {
+    const fbo_sparse* sp = c->sparse;
+    out[0] = sp->n_pad;
+    out[1] = sp->nblk;
+    out[2] = sp->nlev;
+    out[3] = sp->pptr[sp->nlev];
+    out[4] = sp->tptr[sp->nlev];
+    out[5] = sp->sptr[sp->tptr[sp->nlev]];
+}
+
+static void sparse_free(fbo_sparse* sp) {
+    if (!sp) return;
+    free(sp->pos); free(sp->slot_of); free(sp->boff); free(sp->pool); free(sp->cptr); free(sp->crow);
+    free(sp->lptr); free(sp->lcol); free(sp->pptr); free(sp->pblk); free(sp->tptr); free(sp->tgt); free(sp->sptr);
+    free(sp->src); free(sp->rhs); free(sp->Sc);
+    free(sp);
+}
+
+/* 14 x 14 (or smaller) dense solve with partial pivoting, in place: returns 0, or 1 if singular */
+static int small_solve(int n, double* H /* n x n row-major */, double* b) {
+    for (int col = 0; col < n; ++col) {
+        int piv = col;
+        for (int i = col + 1; i < n; ++i)
+            if (fabs(H[i * n + col]) > fabs(H[piv * n + col])) piv = i;
+        if (!(fabs(H[piv * n + col]) > 0.0)) return 1;
+        if (piv != col) {
+            for (int j = 0; j < n; ++j) { double t = H[col * n + j]; H[col * n + j] = H[piv * n + j]; H[piv * n + j] = t; }
+            double t = b[col]; b[col] = b[piv]; b[piv] = t;
+        }
+        for (int i = col + 1; i < n; ++i) {
+            const double f = H[i * n + col] / H[col * n + col];
+            for (int j = col; j < n; ++j) H[i * n + j] -= f * H[col * n + j];
+            b[i] -= f * b[col];
+        }
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        double v = b[i];
+        for (int j = i + 1; j < n; ++j) v -= H[i * n + j] * b[j];
+        b[i] = v / H[i * n + i];
+    }
+    return 0;
+}
+
+/*
+ * Solve the reduced system accumulated by fbo_reduce in sparse form (fbo_set_sparse(c, 1)):
+ * S dc = -r, bordered by G (u_c x 7 row-major, inner constraints) as [S G; G' 0][dc; l] = [-r; 0]
+ * (main.m:428-440).  dc: u_c, compressed order.  times (may be NULL): [border + RHS, factor, solves] s.
+ * Returns 0, 1 (a non-positive pivot), 2 (singular border combine), 3 (no BLAS / setup).
+ */
+int fbo_sparse_solve(fbo_ctx* c, const double* r, const double* G, double* dc, double* times) {
+    fbo_sparse* sp = c->sparse;
+    if (!sp || !g_dgemm || !g_dsyrk || !g_dtrsm || !g_dpotrf) return 3;
+    const fbo_input* in = &c->in;
+    const int64_t n = sp->n_pad, u_c = c->u_c;
+    const int nb = sp->nb, ui = c->u_img;
+    const int ic = in->ic && G;
+    const int nr = ic ? NRHS : 1;
+    const int sb = SB, ldy = (int)n;
+    const double one = 1.0, mone = -1.0;
+    double t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+#ifdef _OPENMP
+    t0 = omp_get_wtime();
+#endif
+    double* Y = sp->rhs;
+    double* AB = NULL;  /* the border's A | B columns (n x 14), kept for the combine */
+    memset(Y, 0, sizeof(double) * n * nr);
+    /* unit diagonal (zero RHS) for the positions that hold no unknown: padding slots, EOPs not estimated,
+     * the padding after the camera unknowns */
+    {
+        uint8_t* used = calloc(n, 1);
+        for (int64_t i = 0; i < u_c; ++i) used[sp->pos[i]] = 1;
+        for (int64_t q = 0; q < n; ++q)
+            if (!used[q]) *sblk(sp, q, q) = 1.0;
+        free(used);
+    }
+    for (int64_t i = 0; i < u_c; ++i) Y[sp->pos[i]] = -r[i];
+    if (ic) {
+        /* equilibrating weights from diag(S) (the GPU's k_border_weights): W_l over the first n_loc slots,
+         * D over all images; A = G_l W_l^1/2, B = G D as RHS columns 1..7, 8..14; M = S + A A' */
+        double sa[7] = {0}, sb7[7] = {0};
+        const int64_t nimg_u = (int64_t)ui * in->n_img;
+        for (int64_t i = 0; i < nimg_u; ++i) {
+            const int64_t p = sp->pos[i];
+            const double d = *sblk(sp, p, p);
+            const double inv = d > 0.0 ? 1.0 / d : 0.0;
+            for (int m = 0; m < 7; ++m) {
+                const double v = G[i * 7 + m] * G[i * 7 + m] * inv;
+                sb7[m] += v;
+                if (p < 6 * (int64_t)sp->n_loc) sa[m] += v;
+            }
+        }
+        double wa[7], wb[7];
+        for (int m = 0; m < 7; ++m) {
+            wa[m] = sqrt(sa[m] > 0.0 ? 1.0 / sa[m] : 1.0);
+            wb[m] = sqrt(sb7[m] > 0.0 ? 1.0 / sb7[m] : 1.0);
+        }
+        for (int64_t i = 0; i < nimg_u; ++i) {
+            const int64_t p = sp->pos[i];
+            for (int m = 0; m < 7; ++m) {
+                if (p < 6 * (int64_t)sp->n_loc) Y[(1 + m) * n + p] = wa[m] * G[i * 7 + m];
+                Y[(8 + m) * n + p] = wb[m] * G[i * 7 + m];
+            }
+        }
+        AB = malloc(sizeof(double) * (size_t)n * 14);
+        memcpy(AB, Y + n, sizeof(double) * (size_t)n * 14);
+        for (int64_t pi = 0; pi < 6 * (int64_t)sp->n_loc; ++pi)
+            for (int64_t pj = 0; pj <= pi; ++pj) {
+                double acc = 0.0;
+                for (int m = 0; m < 7; ++m) acc += Y[(1 + m) * n + pi] * Y[(1 + m) * n + pj];
+                if (acc != 0.0) *sblk(sp, pi, pj) += acc;
+            }
+    }
+#define BLK(i, j) (sp->pool + (int64_t)sp->boff[(i) * nb + (j)] * SBB)
+#ifdef _OPENMP
+    t1 = omp_get_wtime();
+#endif
+    int bad = 0;
+    for (int l = 0; l < sp->nlev; ++l) {
+#pragma omp parallel for schedule(dynamic, 1) num_threads(c->nthreads) reduction(| : bad)
+        for (int x = sp->lptr[l]; x < sp->lptr[l + 1]; ++x) {
+            const int k = sp->lcol[x];
+            int info = 0;
+            g_dpotrf("L", &sb, BLK(k, k), &sb, &info);
+            if (info != 0) bad |= 1;
+        }
+        if (bad) break;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(c->nthreads)
+        for (int q = sp->pptr[l]; q < sp->pptr[l + 1]; ++q) {
+            const int i = sp->pblk[2 * q], k = sp->pblk[2 * q + 1];
+            g_dtrsm("R", "L", "T", "N", &sb, &sb, &one, BLK(k, k), &sb, BLK(i, k), &sb);
+        }
+#pragma omp parallel for schedule(dynamic, 1) num_threads(c->nthreads)
+        for (int t = sp->tptr[l]; t < sp->tptr[l + 1]; ++t) {
+            const int i = sp->tgt[2 * t], j = sp->tgt[2 * t + 1];
+            for (int e = sp->sptr[t]; e < sp->sptr[t + 1]; ++e) {
+                const int k = sp->src[e];
+                if (i == j) g_dsyrk("L", "N", &sb, &sb, &mone, BLK(i, k), &sb, &one, BLK(i, i), &sb);
+                else g_dgemm("N", "T", &sb, &sb, &sb, &mone, BLK(i, k), &sb, BLK(j, k), &sb, &one, BLK(i, j), &sb);
+            }
+        }
+    }
+#ifdef _OPENMP
+    t2 = omp_get_wtime();
+#endif
+    if (bad) { free(AB); return 1; }
+    /* forward Y = L^-1 Y, level by level: the level's columns, then each row block's updates from them
+     * (the level's diagonal targets (i, i) list exactly those sources); backward Y = L^-T Y top down */
+    for (int l = 0; l < sp->nlev; ++l) {
+#pragma omp parallel for schedule(dynamic, 1) num_threads(c->nthreads)
+        for (int x = sp->lptr[l]; x < sp->lptr[l + 1]; ++x) {
+            const int k = sp->lcol[x];
+            g_dtrsm("L", "L", "N", "N", &sb, &nr, &one, BLK(k, k), &sb, Y + (int64_t)k * SB, &ldy);
+        }
+#pragma omp parallel for schedule(dynamic, 1) num_threads(c->nthreads)
+        for (int t = sp->tptr[l]; t < sp->tptr[l + 1]; ++t) {
+            const int i = sp->tgt[2 * t];
+            if (sp->tgt[2 * t + 1] != i) continue;
+            for (int e = sp->sptr[t]; e < sp->sptr[t + 1]; ++e) {
+                const int k = sp->src[e];
+                g_dgemm("N", "N", &sb, &nr, &sb, &mone, BLK(i, k), &sb, Y + (int64_t)k * SB, &ldy, &one,
+                        Y + (int64_t)i * SB, &ldy);
+            }
+        }
+    }
+    for (int l = sp->nlev - 1; l >= 0; --l) {
+#pragma omp parallel for schedule(dynamic, 1) num_threads(c->nthreads)
+        for (int x = sp->lptr[l]; x < sp->lptr[l + 1]; ++x) {
+            const int k = sp->lcol[x];
+            for (int q = sp->cptr[k]; q < sp->cptr[k + 1]; ++q) {
+                const int i = sp->crow[q];
+                g_dgemm("T", "N", &sb, &nr, &sb, &mone, BLK(i, k), &sb, Y + (int64_t)i * SB, &ldy, &one,
+                        Y + (int64_t)k * SB, &ldy);
+            }
+            g_dtrsm("L", "L", "T", "N", &sb, &nr, &one, BLK(k, k), &sb, Y + (int64_t)k * SB, &ldy);
+        }
+    }
+#undef BLK
+    if (ic) {
+        /* the exact bordered solution (the GPU's border combine): d = y0 + YA z + YB k with
+         * [A'YA - I, A'YB; B'YA, B'YB] [z; k] = -[A'y0; B'y0], A and B the RHS columns kept in AB */
+        double H[14 * 14], b[14];
+        for (int a = 0; a < 14; ++a) {
+            const double* va = AB + (int64_t)a * n;
+            double s0 = 0.0;
+            for (int64_t q = 0; q < n; ++q) s0 += va[q] * Y[q];
+            b[a] = -s0;
+            for (int m = 0; m < 14; ++m) {
+                const double* ym = Y + (int64_t)(1 + m) * n;
+                double s1 = 0.0;
+                for (int64_t q = 0; q < n; ++q) s1 += va[q] * ym[q];
+                H[a * 14 + m] = s1 - ((a < 7 && m == a) ? 1.0 : 0.0);
+            }
+        }
+        free(AB);
+        AB = NULL;
+        if (small_solve(14, H, b)) return 2;
+        for (int64_t q = 0; q < n; ++q) {
+            double v = Y[q];
+            for (int m = 0; m < 14; ++m) v += Y[(int64_t)(1 + m) * n + q] * b[m];
+            Y[q] = v;
+        }
+    }
+    for (int64_t i = 0; i < u_c; ++i) dc[i] = Y[sp->pos[i]];
+#ifdef _OPENMP
+    t3 = omp_get_wtime();
+#endif
+    if (times) { times[0] = t1 - t0; times[1] = t2 - t1; times[2] = t3 - t2; }
+    return 0;
+}
+
+void fbo_set_sparse(fbo_ctx* c, int on) { c->sparse_on = on && c->sparse; }

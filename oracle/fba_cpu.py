@@ -7,9 +7,12 @@ solved here with LAPACK through SciPy, ``fbo_update`` (C) back-substitutes, de-s
 Two solvers for the bordered system (main.m:432, inner constraints on):
 * ``"kkt"``  -- the reference's bordered matrix [S G; G' 0] solved directly (symmetric-indefinite
   LAPACK solve); independent of the GPU's method, used by the parity tests.
-* ``"chol"`` -- the regularised border M = S + G W G' (W = equilibrated, as the GPU path) with a
-  Cholesky factorisation and a 7x7 border correction; the fastest CPU method, used as bench.py's
-  ``cpu_baseline``.
+* ``"chol"`` -- the regularised border M = S + G W G' (W = equilibrated) with a dense Cholesky
+  factorisation and a 7x7 border correction (bench.py's dense ``cpu_baseline_dense``).
+* ``"sparse"`` -- the GPU's method on the GPU's block pattern: the reduced system accumulated straight
+  into 128 x 128 blocks in the device factorisation's camera-side order (libfba's fba_image_order,
+  nested dissection), the local border M = S + A A' with the 14 x 14 combine, and a level-by-level
+  block Cholesky in C/OpenMP calling OpenBLAS per block (fbo_sparse_solve); bench.py's ``cpu_baseline``.
 
 Only ``tests/``, ``__graft_entry__`` and ``bench.py``'s ``cpu_baseline`` leg may import this.
 """
@@ -56,7 +59,44 @@ def _lib():
     lib.fbo_set_shard.argtypes = [P, P, C.c_int]
     lib.fbo_residuals.argtypes = [P, P]
     lib.fbo_residuals.restype = C.c_double
+    lib.fbo_set_blas.argtypes = [P, P, P, P]
+    lib.fbo_sparse_setup.argtypes = [P, P, C.c_int]
+    lib.fbo_sparse_setup.restype = C.c_int
+    lib.fbo_sparse_info.argtypes = [P, P]
+    lib.fbo_set_sparse.argtypes = [P, C.c_int]
+    lib.fbo_sparse_solve.argtypes = [P, P, P, P, P]
+    lib.fbo_sparse_solve.restype = C.c_int
+    lib.fbo_set_blas(*_blas_pointers())
     return lib
+
+
+def _blas_pointers():
+    """dgemm / dsyrk / dtrsm / dpotrf of the OpenBLAS SciPy ships, from its Cython function-pointer
+    capsules (called per 128 x 128 block by fbo_sparse_solve's OpenMP threads, OpenBLAS itself on one
+    thread)."""
+    import scipy.linalg.cython_blas as cb
+    import scipy.linalg.cython_lapack as cl
+    name = C.pythonapi.PyCapsule_GetName
+    name.argtypes, name.restype = [C.py_object], C.c_char_p
+    get = C.pythonapi.PyCapsule_GetPointer
+    get.argtypes, get.restype = [C.py_object, C.c_char_p], C.c_void_p
+    caps = [cb.__pyx_capi__["dgemm"], cb.__pyx_capi__["dsyrk"], cb.__pyx_capi__["dtrsm"], cl.__pyx_capi__["dpotrf"]]
+    return [get(c, name(c)) for c in caps]
+
+
+def image_order(data):
+    """The device factorisation's camera-side order (libfba.so fba_image_order, host only): slot -> EXT
+    row, -1 for a padding slot."""
+    import fba_import
+    fba = fba_import.load()
+    n = len(data.x)
+    eop0 = np.array([r[2:8] for r in data.EXT[: data.numImg]], dtype=np.float64).reshape(-1)
+    packed = fba.capi.PackedProblem(np.column_stack([data.x, data.y]), data.ext_index, data.cam_num, data.tie_index,
+                                    data.xyz_fixed, eop0, np.zeros(max(data.numCam, 1) * 6),
+                                    np.tile([1.0, 0, 0, 0, 0], max(data.numCam, 1)), np.zeros(3 * max(data.numtie, 1)),
+                                    data.numImg, data.numCam, data.numtie)
+    assert packed.n_pts == n
+    return fba.capi.image_order(packed)
 
 
 _LIB = None
@@ -113,12 +153,26 @@ class CpuAdjustment:
         self.ic = bool(s["Inner_Constraints"])
         self.xhat, self.names = buildxhat(data)
         assert len(self.xhat) == self.u
+        self.G = np.zeros((self.u_c, 7)) if self.ic else None
+        self.deltasum = []
+        self.solve_times = np.zeros(3)  # sparse: border + RHS, factor, triangular solves (s, last solve)
+        if solver == "sparse":
+            slots = np.ascontiguousarray(image_order(data), dtype=np.int32)
+            if lib().fbo_sparse_setup(self.h, _p(slots), len(slots)) != 0:
+                raise ValueError("fbo_sparse_setup: the image order does not cover every image")
+            lib().fbo_set_sparse(self.h, 1)
+            info = np.zeros(6, np.int64)
+            lib().fbo_sparse_info(self.h, _p(info))
+            self.sparse_info = dict(zip(("n_pad", "blocks", "levels", "panel_blocks", "targets", "updates"),
+                                        (int(v) for v in info)))
+            self.flat = None
+            self.S = None
+            self.r = np.zeros(self.u_c)
+            return
         # S and r share one flat buffer: the unit a multi-rank caller all-reduces
         self.flat = np.zeros(self.u_c * self.u_c + self.u_c)
         self.S = self.flat[: self.u_c * self.u_c].reshape(self.u_c, self.u_c)
         self.r = self.flat[self.u_c * self.u_c:]
-        self.G = np.zeros((self.u_c, 7)) if self.ic else None
-        self.deltasum = []
 
     def close(self):
         if getattr(self, "h", None):
@@ -130,6 +184,12 @@ class CpuAdjustment:
 
     def _solve(self):
         S, r, G = self.S, self.r, self.G
+        if self.solver == "sparse":
+            dc = np.zeros(self.u_c)
+            rc = lib().fbo_sparse_solve(self.h, _p(r), _p(G) if self.ic else None, _p(dc), _p(self.solve_times))
+            if rc != 0:
+                raise FloatingPointError(f"fbo_sparse_solve: {('', 'not positive definite', 'singular border', 'no BLAS')[rc]}")
+            return dc
         if not self.ic:
             return sla.cho_solve(sla.cho_factor(S, lower=True, overwrite_a=True, check_finite=False), -r,
                                  check_finite=False)
@@ -158,7 +218,8 @@ class CpuAdjustment:
 
     def accumulate(self):
         """Linearise + point-reduce into ``self.flat`` (= [S | r])."""
-        rc = lib().fbo_reduce(self.h, _p(self.xhat), _p(self.S), _p(self.r), _p(self.G) if self.ic else None)
+        rc = lib().fbo_reduce(self.h, _p(self.xhat), None if self.S is None else _p(self.S), _p(self.r),
+                              _p(self.G) if self.ic else None)
         if rc != 0:
             raise FloatingPointError("singular tie-point block")
 
@@ -194,17 +255,21 @@ class CpuAdjustment:
         return v, vtpv / (len(v) - self.u)
 
 
-def time_iterations(folder, seconds=20.0, threads=None, data=None):
-    """cpu_baseline: Gauss-Newton passes per second of the block-sparse CPU restatement
-    ("chol" solver, OpenMP + threaded LAPACK) on ``folder``'s scene, bounded to ~``seconds``."""
+def time_iterations(folder, seconds=20.0, threads=None, data=None, solver="sparse"):
+    """cpu_baseline: Gauss-Newton passes per second of the CPU restatement on ``folder``'s scene,
+    bounded to ~``seconds``: OpenMP linearise + per-point Schur, then ``solver`` -- "sparse" (the
+    default: the block Cholesky of the reduced system on the device factorisation's block pattern,
+    OpenMP over blocks, one OpenBLAS thread per block) or "chol" (the dense Cholesky of the bordered
+    reduced system, threaded LAPACK) -- then back-substitution and update."""
     from threadpoolctl import threadpool_limits
     import fba_oracle
     if data is None:
         data = fba_oracle.load_folder(folder)
     threads = threads or default_threads()
     ph = {"linearize_reduce": 0.0, "solve": 0.0, "update": 0.0}
-    with threadpool_limits(limits=threads):
-        adj = CpuAdjustment(data, threads=threads, solver="chol")
+    sub = np.zeros(3)
+    with threadpool_limits(limits=1 if solver == "sparse" else threads):
+        adj = CpuAdjustment(data, threads=threads, solver=solver)
         t0 = time.perf_counter()
         n = 0
         while True:
@@ -219,14 +284,19 @@ def time_iterations(folder, seconds=20.0, threads=None, data=None):
             ph["linearize_reduce"] += tb - ta
             ph["solve"] += tc - tb
             ph["update"] += td - tc
+            sub += adj.solve_times
             n += 1
             el = time.perf_counter() - t0
             if el >= seconds or n >= 1000:
                 break
         adj.close()
-    return {"value": n / el, "iterations": n, "seconds": el, "cores": threads,
-            "n_pts": len(data.x), "u": adj.u, "u_c": adj.u_c, "cpu_model": cpu_model(),
-            "phase_ms": {k: 1e3 * v / n for k, v in ph.items()}}
+    out = {"value": n / el, "iterations": n, "seconds": el, "cores": threads, "solver": solver,
+           "n_pts": len(data.x), "u": adj.u, "u_c": adj.u_c, "cpu_model": cpu_model(),
+           "phase_ms": {k: 1e3 * v / n for k, v in ph.items()}}
+    if solver == "sparse":
+        out["solve_ms"] = {k: 1e3 * v / n for k, v in zip(("border_rhs", "factor", "triangular_solves"), sub)}
+        out["pattern"] = adj.sparse_info
+    return out
 
 
 def cpu_model():

@@ -5,7 +5,8 @@ oracle/fba_cpu.c is the checker for scenes too large for the dense oracle (the G
 tests) and bench.py's cpu_baseline, so it is pinned here against the dense oracle, which is itself
 pinned by the reference-expression goldens (tests/test_oracle.py).
 
-Tolerances: xhat 1e-9 relative per parameter group (north_star bar) and sigma0^2 1e-9 on every
+Tolerances: xhat 1e-9 relative per element and per parameter group (north_star bar; conftest.
+elem_rel_err) and sigma0^2 1e-9 on every
 scene whose reference restatement is not path-sensitive (conftest.solver_spread: the pinhole cam0
 variants and the synthetic scenes); the first deltasum 1e-8 (its own 1-ulp-of-w spread is ~2e-9
 on cam0).
@@ -13,7 +14,7 @@ on cam0).
 import numpy as np
 import pytest
 
-from conftest import CAM0_VARIANTS, dist_scaling_of, group_rel_err
+from conftest import CAM0_VARIANTS, ELEM_FLOOR, SMALL_SCENE_FLOOR, dist_scaling_of, elem_rel_err, group_rel_err
 
 PINHOLE = sorted(k for k in CAM0_VARIANTS if "pinhole" in k)
 
@@ -25,8 +26,10 @@ def fbo():
     return fba_cpu
 
 
-def _compare(ca, ro, dtol=1e-8):
+def _compare(ca, ro, dtol=1e-8, floor=ELEM_FLOOR):
     err = group_rel_err(ca.xhat, ro.xhat, ro.names, ro.dist_scaling)
+    assert max(err.values()) <= 1e-9, err
+    err = elem_rel_err(ca.xhat, ro.xhat, ro.names, ro.dist_scaling, floor=floor)
     assert max(err.values()) <= 1e-9, err
     v, s02 = ca.residuals()
     assert abs(s02 - ro.sigma02) <= 1e-9 * ro.sigma02
@@ -52,7 +55,7 @@ def test_synthetic_matches_dense_oracle(fba, fbo, oracle, tmp_path, typ):
     ro = oracle.adjust(od)
     ca = fbo.CpuAdjustment(od, threads=2)
     assert ca.adjust() == ro.iterations
-    _compare(ca, ro, dtol=1e-9)
+    _compare(ca, ro, dtol=1e-9, floor=SMALL_SCENE_FLOOR)
 
 
 def test_chol_border_matches_kkt(fba, fbo, oracle, tmp_path):
@@ -137,4 +140,49 @@ def test_general_points_match_dense_oracle(fba, fbo, oracle, tmp_path, kind):
     ro = oracle.adjust(od)
     ca = fbo.CpuAdjustment(od, threads=2)
     assert ca.adjust() == ro.iterations
-    _compare(ca, ro, dtol=1e-9)
+    _compare(ca, ro, dtol=1e-9, floor=SMALL_SCENE_FLOOR)
+
+
+def test_restatements_agree_per_element(fba, fbo, oracle, tmp_path):
+    """The measured solver spread behind conftest.elem_rel_err's floor: at config 3 (200 images x
+    5,000 tie points, synth.make_config) exact restatements of main.m:407-494 -- the reference's
+    bordered system [S G; G' 0] solved directly vs the regularised-border dense Cholesky, the direct
+    solve on 3 threads instead of 2, and the block-sparse Cholesky on the GPU's block pattern (bench.py's
+    cpu_baseline) -- agree per element to ~1e-12 (measured 1.2e-12 / 2.7e-12), with no entry below 1e-6
+    of its group's scale (smallest |x| / max: 3e-5)."""
+    from fba_amd import synth
+    folder = synth.make_config(3, str(tmp_path / "c3"))
+    od = oracle.load_folder(folder)
+    runs = []
+    for kw in (dict(solver="kkt", threads=2), dict(solver="chol", threads=2), dict(solver="kkt", threads=3),
+               dict(solver="sparse", threads=2)):
+        ca = fbo.CpuAdjustment(od, **kw)
+        runs.append((ca.adjust(), ca.xhat.copy(), ca.residuals()[1]))
+        ca.close()
+    names = oracle.buildxhat(od)[1]
+    dsc = dist_scaling_of(od)
+    for it, x, s02 in runs[1:]:
+        assert it == runs[0][0]
+        err = elem_rel_err(x, runs[0][1], names, dsc, floor=0.0)
+        assert max(err.values()) <= 1e-11, err
+        assert abs(s02 - runs[0][2]) <= 1e-12 * runs[0][2]
+
+
+@pytest.mark.parametrize("kind", ["control", "rig3", "stage1"])
+def test_sparse_solver_matches_kkt(fba, fbo, oracle, tmp_path, cam0_folders, kind):
+    """The block-sparse solver (fbo_sparse_solve: the reduced system in the device factorisation's
+    camera-side order, fba_image_order) without inner constraints (control points; cam0 Stage-1: EOPs
+    only, so the IOP positions of the block pattern hold unit rows) and with them on a 3-camera rig:
+    the same iterates as the direct bordered solve."""
+    from fba_amd import synth
+    if kind == "stage1":
+        folder = cam0_folders["stage1_pinhole"]
+    else:
+        kw = dict(n_control=12) if kind == "control" else dict(n_cam=3)
+        folder = synth.write_folder(synth.generate(30, 900, seed=5, **kw), str(tmp_path / kind))
+    od = oracle.load_folder(folder)
+    a, b = (fbo.CpuAdjustment(od, threads=2, solver=s) for s in ("kkt", "sparse"))
+    assert a.adjust() == b.adjust()
+    err = group_rel_err(b.xhat, a.xhat, a.names, dist_scaling_of(od))
+    assert max(err.values()) <= 1e-10, err
+    assert abs(a.residuals()[1] - b.residuals()[1]) <= 1e-10 * a.residuals()[1]
