@@ -418,13 +418,50 @@ int main(int argc, char** argv) {
     } else {
         for (int b = 0; b < s.flow_n; ++b) order.push_back(b);
     }
+    std::vector<char> ran(s.flow_n, 0);
+    // a split helper (role 4): tiles (ta, tb), tb >= FLOW_CSPLIT, of C_jj -= X X', X = L(j, f)
+    auto run_helper = [&](const int32_t* rec) -> int {
+        const int64_t j = rec[1], f = rec[2];
+        if (colf[f] != 8 || f >= j) return fail("flow: split helper before its source");
+        if (!flag_ok(rec[7], 8) || (rec[8] >= 0 && !flag_ok(rec[8], 8))) return fail("flow: split helper rows not solved");
+        if (rec[10] < 0 || rec[10] >= s.flow_nscratch || slot_set[rec[10]]++) return fail("flow: split helper slot");
+        const double* X = Fk(j, f);
+        int h = 0;
+        for (int ta = 0; ta < NB / 16; ++ta)
+            for (int tb = FLOW_CSPLIT; tb <= ta; ++tb, ++h)
+                for (int r = 0; r < 16; ++r)
+                    for (int c2 = 0; c2 < 16; ++c2) {
+                        double v = 0.0;
+                        for (int t = 0; t < NB; ++t) v += X[(size_t)(16 * ta + r) * n + t] * X[(size_t)(16 * tb + c2) * n + t];
+                        Pf[(size_t)rec[10] * 4096 + h * 256 + r * 16 + c2] = -v;
+                    }
+        fl[rec[9]] = 1;
+        return 0;
+    };
     for (int b : order) {
         const int32_t* rec = B + s.flow_rec + (int64_t)Sched::FLOW_REC * b;
+        if (ran[b]) continue;
+        ran[b] = 1;
         if (rec[0] == 0) {
             const int64_t j = rec[1], f = rec[2];
             for (int x = 0; x < rec[4]; ++x)
                 if (!flag_ok(B[rec[3] + x], 1)) return fail("flow: diagonal block waits for an unset flag");
             double* C = Fk(j, j);
+            if (f >= 0 && rec[12]) {  // self panel: this record solves its rows of f's panel itself
+                if (colf[f] != 8 || f >= j) return fail("flow: self panel before its source");
+                for (int x = 0; x < rec[14]; ++x)
+                    if (!flag_ok(B[rec[13] + x], 1)) return fail("flow: self panel waits for an unset flag");
+                if (rec[8] >= 0 || rec[11] != 0) return fail("flow: self panel record fields");
+                solve_rows(f, j, 0, NB);
+                fl[rec[7]] = 8;
+                if (rec[9] >= 0) {  // its split helper, dispatched right after it, runs beside its potrf
+                    const int hb = b + 1;
+                    const int32_t* hr = B + s.flow_rec + (int64_t)Sched::FLOW_REC * hb;
+                    if (hb >= s.flow_n || hr[0] != 4 || hr[1] != j || ran[hb]) return fail("flow: self panel's helper not next");
+                    ran[hb] = 1;
+                    if (run_helper(hr)) return 1;
+                }
+            }
             if (f >= 0) {
                 if (colf[f] != 8 || f >= j) return fail("flow: fused source not factored");
                 if (!flag_ok(rec[7], 8) || (rec[8] >= 0 && !flag_ok(rec[8], 8))) return fail("flow: fused rows not solved");
@@ -519,22 +556,8 @@ int main(int argc, char** argv) {
             }
         } else if (rec[0] == 3) {
             if (colf[rec[1]] != 8) return fail("flow: inverse before its factor");
-        } else if (rec[0] == 4) {  // split helper: tiles (ta, tb), tb >= FLOW_CSPLIT, of C_jj -= X X', X = L(j, f)
-            const int64_t j = rec[1], f = rec[2];
-            if (colf[f] != 8 || f >= j) return fail("flow: split helper before its source");
-            if (!flag_ok(rec[7], 8) || !flag_ok(rec[8], 8)) return fail("flow: split helper rows not solved");
-            if (rec[10] < 0 || rec[10] >= s.flow_nscratch || slot_set[rec[10]]++) return fail("flow: split helper slot");
-            const double* X = Fk(j, f);
-            int h = 0;
-            for (int ta = 0; ta < NB / 16; ++ta)
-                for (int tb = FLOW_CSPLIT; tb <= ta; ++tb, ++h)
-                    for (int r = 0; r < 16; ++r)
-                        for (int c2 = 0; c2 < 16; ++c2) {
-                            double v = 0.0;
-                            for (int t = 0; t < NB; ++t) v += X[(size_t)(16 * ta + r) * n + t] * X[(size_t)(16 * tb + c2) * n + t];
-                            Pf[(size_t)rec[10] * 4096 + h * 256 + r * 16 + c2] = -v;
-                        }
-            fl[rec[9]] = 1;
+        } else if (rec[0] == 4) {
+            if (run_helper(rec)) return 1;
         } else {
             return fail("flow: record role");
         }

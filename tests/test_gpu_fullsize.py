@@ -7,7 +7,8 @@
 * config 4 (1,000 x 50,000, the bench workload): the whole adjustment against the same oracle --
   iteration count, deltasum history, xhat, sigma0^2, RMS and v.
 * config 5 (4,000 x 200,000, 2M image points): every Gauss-Newton pass to convergence against the C
-  oracle's direct solve of the dense bordered system (iteration count, xhat, sigma0^2); then
+  oracle's direct solve of the dense bordered system (each to its own stop: there the threshold sits at
+  the rounding floor of deltasum; converged xhat, sigma0^2); then
   size-independent properties of the converged run -- bit-identical repeat runs, monotone convergence below Threshold_Value within
   Iteration_Cap, and sigma0^2 = 1 +- 5% (the generator's noise equals Meas_std, so the a posteriori
   variance factor of a correct adjustment is ~1).
@@ -160,22 +161,29 @@ def test_config4_adjust_matches_oracle(fba, fbo, oracle, scenes):
 
 
 DISTORTION = ("k1", "k2", "k3", "k4", "k5", "p1", "p2")
+# config 5: how far two exact CPU restatements land apart per element after each of the first passes
+# (the direct bordered KKT solve vs the block-sparse Cholesky of oracle/fba_cpu.c, both from the same
+# start; profiles/r04_c5_elem_spread.log): the first passes' large corrections make the small entries
+# sensitive (the group scale agrees to 1e-9 / 1e-11); from pass 3 on both agree to <= 2.1e-10 per element
+C5_ELEM_SPREAD = {1: 3.0e-8, 2: 4.7e-9}
 
 
 def test_config5_adjust_matches_oracle(fba, fbo, oracle, scenes):
     """config 5 (4,000 images x 200,000 tie points, 2M image points, u_c = 24,010), converged: every
     Gauss-Newton pass against the C oracle solving the dense bordered system [S G; G' 0] (4.6 GB)
-    directly, to the reference's stop rule (main.m:412, :490-493) -- same iteration count, xhat after the
-    last update (main.m:484-493) and sigma0^2 (main.m:601).
+    directly, each run to the reference's stop rule (main.m:412, :490-493); xhat after the last update
+    (main.m:484-493) and sigma0^2 (main.m:601).
 
-    deltasum <= 1e-9 relative after each pass; xhat <= 1e-9 per parameter group and per element after
-    each pass, except the distortion groups after the FIRST pass (the linearisation at the start
-    values): there the pass is sensitive to the association of the reduced system's sums at the 1e-7
-    level -- the C oracle itself moves k1 by 1.2e-7 / 2.1e-7 (k2..p2 ~1e-8) when only its OpenMP thread
-    count changes (scripts/order_spread.py, profiles/r03_order_spread_c5.log) -- so that pass is held to
-    5e-8 (measured: 1.06e-8 for k1, profiles/r03_c5_solver_spread.log).  The later passes damp the
-    first's rounding (Gauss-Newton contraction): 1e-9 for every group and element (measured after the
-    second pass: 7e-11).  sigma0^2 and RMSx / RMSy of the converged adjustment <= 1e-9."""
+    Pass by pass while deltasum is above the stop rule's rounding floor: deltasum <= 1e-9 relative; xhat
+    <= 1e-9 per parameter group, except the distortion groups after the FIRST pass (the linearisation at
+    the start values: the C oracle itself moves k1 by 1.2e-7 / 2.1e-7 when only its OpenMP thread count
+    changes, profiles/r03_order_spread_c5.log) -- 5e-8 there (measured: 1.06e-8 for k1); per element the
+    first two passes are held to 20x the spread of two exact restatements (C5_ELEM_SPREAD), later passes
+    to 1e-9.  At convergence deltasum is the sum of |delta| over 624,010 unknowns of rounding-level
+    corrections, ~1e-6 -- the very Threshold_Value 1e-6 -- so WHEN it drops below the threshold is decided
+    by rounding: two exact CPU restatements stop after 9 and 7 passes (profiles/r04_c5_elem_spread.log).
+    Each run therefore stops by its own rule; the passes both stay within 3 of each other, and the
+    converged xhat agree to 1e-9 per element and per group, sigma0^2 and RMSx / RMSy to 1e-9."""
     folder = _scene(5, scenes)
     ds = fba.load_folder(folder)
     od = oracle.load_folder(folder)
@@ -184,25 +192,35 @@ def test_config5_adjust_matches_oracle(fba, fbo, oracle, scenes):
     dsc = dist_scaling_of(od)
     thr, cap = ds.settings["threshold"], ds.settings["Iteration_Cap"]
     try:
-        d_ref, it = 100.0, 0
-        while d_ref > thr:  # main.m:412
-            it += 1
-            d_ref = ref.step()
-            d = ctx.step()
+        d_ref = d = 100.0  # main.m:407
+        it_ref = it = 0
+        while (d_ref > thr and it_ref < cap) or (d > thr and it < cap):  # main.m:412, :490-493, each run by its own deltasum
+            if d_ref > thr and it_ref < cap:
+                it_ref += 1
+                d_ref = ref.step()
+            if d > thr and it < cap:
+                it += 1
+                d = ctx.step()
+            if it != it_ref or ref.deltasum[-1] < 1e3 * thr:
+                continue  # below the comparison range: the tail is rounding noise
             assert abs(d - d_ref) <= 1e-9 * ref.deltasum[0], (it, d, d_ref)
             x = ctx.get_xhat()
-            for kind, err in (("group", group_rel_err(x, ref.xhat, ref.names, dsc)),
-                              ("element", elem_rel_err(x, ref.xhat, ref.names, dsc))):
-                print(f"pass {it} {kind}:", {g: f"{e:.2e}" for g, e in err.items()})
-                for g, e in err.items():
-                    assert e <= (5e-8 if it == 1 and g in DISTORTION else 1e-9), (it, kind, g, e)
-            assert (d <= thr) == (d_ref <= thr)  # the same stop decision every pass
-            if it >= cap:  # main.m:490-493
-                break
-        assert it < cap
+            err = group_rel_err(x, ref.xhat, ref.names, dsc)
+            print(f"pass {it} group:", {g: f"{e:.2e}" for g, e in err.items()})
+            for g, e in err.items():
+                assert e <= (5e-8 if it == 1 and g in DISTORTION else 1e-9), (it, g, e)
+            err = elem_rel_err(x, ref.xhat, ref.names, dsc)
+            print(f"pass {it} element:", {g: f"{e:.2e}" for g, e in err.items()})
+            assert max(err.values()) <= max(1e-9, 20 * C5_ELEM_SPREAD.get(it, 0.0)), (it, err)
+        print(f"stopped after {it} passes (oracle {it_ref}); last deltasum {d:.3e} (oracle {d_ref:.3e})")
+        assert d <= thr and d_ref <= thr and it < cap and it_ref < cap and abs(it - it_ref) <= 3
+        x = ctx.get_xhat()
+        for err in (group_rel_err(x, ref.xhat, ref.names, dsc), elem_rel_err(x, ref.xhat, ref.names, dsc)):
+            print("converged:", {g: f"{e:.2e}" for g, e in err.items()})
+            assert max(err.values()) <= 1e-9, err
         v_ref, s02 = ref.residuals()
         v, _, st = ctx.residuals()
-        print(f"converged after {it} passes: sigma0^2 {st[3]:.15g} (oracle {s02:.15g})")
+        print(f"sigma0^2 {st[3]:.15g} (oracle {s02:.15g})")
         assert abs(st[3] - s02) <= 1e-9 * s02
         rms_ref = (np.sqrt(np.mean(v_ref[0::2] ** 2)), np.sqrt(np.mean(v_ref[1::2] ** 2)))
         assert abs(st[0] - rms_ref[0]) <= 1e-9 * rms_ref[0] and abs(st[1] - rms_ref[1]) <= 1e-9 * rms_ref[1]
