@@ -1890,8 +1890,12 @@ __device__ __forceinline__ void wait_list_sc1(const int32_t* __restrict__ wl, in
 // LDS of the diagonal-block role: the potrf's lower tiles, leaf inverses and counters, then a second
 // 128 x 17 buffer for the fused source's published column blocks (the first is the leaf-inverse area,
 // free until the potrf starts)
-constexpr size_t FLOWF_LDS = sizeof(double) * (POTRF_NT * IB * 17 + (CB / IB) * IB * 17) + 32 * sizeof(int) +
-                             sizeof(double) * CB * 17;
+constexpr size_t FLOWF_LDS_FUSED = sizeof(double) * (POTRF_NT * IB * 17 + (CB / IB) * IB * 17) + 32 * sizeof(int) +
+                                   sizeof(double) * CB * 17;
+// self panel (selfpanel_apply): + two column-block buffers of L_ff (8 tiles each) and the waves' transposes
+constexpr size_t FLOWF_LDS_SELF = sizeof(double) * (POTRF_NT * IB * 17 + (CB / IB) * IB * 17) + 32 * sizeof(int) +
+                                  sizeof(double) * (2 * (CB / IB) + POTRF_NW) * IB * 17;
+constexpr size_t FLOWF_LDS = FLOWF_LDS_FUSED > FLOWF_LDS_SELF ? FLOWF_LDS_FUSED : FLOWF_LDS_SELF;
 static_assert(CB * 17 == (CB / IB) * IB * 17, "a column-block buffer is exactly the leaf-inverse area");
 
 // fused_apply<SET>: C -= X X' on the tiles of SET, X = L(j, f) consumed column block by column block as
@@ -2038,6 +2042,160 @@ __device__ __forceinline__ void fused_apply(const __amdgpu_buffer_rsrc_t rX, int
     }
 }
 
+// selfpanel_apply<SET> (role 0 with rec[12] = 1): the diagonal workgroup of block j solves its own rows of
+// the fused source's panel, X = L(j, f) = S(j, f) L_ff^-T, column block by column block as f's potrf
+// publishes L_ff (its column flag: block column t of L_ff and the leaf inverse D_t), and applies
+// C_jj -= X_t X_t' on the tiles of SET at each step -- one hand-off (potrf -> this workgroup) on the chain
+// between two levels instead of two (potrf -> panel halves -> diagonal workgroup).  Wave w owns rows
+// 16w .. 16w+15 of X in registers (right-looking: X_t = A_t D_t', A_s -= X_t L_st' for s > t, the panel
+// halves' arithmetic on eight waves); X_t's rows go to HBM write-through (the update tasks of later targets,
+// the split helper and the backward solve read them) and to Xb for the update.  Progress flag prog =
+// column blocks published, raised one step late (each wave drains its stores at the end of a step), the
+// last block before its update.  Lb: two
+// [8][16][17] column-block buffers (tiles (t+1 .. 7, t), D_t in slot 7); Tws: [8][16][17] per-wave
+// transposes; C: SET's tiles in registers, from and back to the potrf's LDS layout (smem).
+template <int SET>
+__device__ __forceinline__ void selfpanel_apply(double* __restrict__ S, int64_t ld, int64_t k0, int64_t f0,
+                                                const double* __restrict__ dinv_f, const unsigned* __restrict__ colflag,
+                                                unsigned* __restrict__ prog, double* __restrict__ smem,
+                                                double* __restrict__ Xb, double* __restrict__ Lb, double* __restrict__ Tws,
+                                                double* __restrict__ scal, uint64_t* __restrict__ tr) {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int lr = lane & 15, lk = lane >> 4;
+    constexpr int NCB = CB / IB, LT = IB * 17;  // column blocks; one LDS tile
+    const __amdgpu_buffer_rsrc_t rX = block_rsrc(S + (k0 + IB * wave) * ld + f0, ((int64_t)(IB - 1) * ld + CB) * 8);
+    const __amdgpu_buffer_rsrc_t rL = block_rsrc(S + f0 * ld + f0, ((int64_t)(CB - 1) * ld + CB) * 8);
+    const __amdgpu_buffer_rsrc_t rD = block_rsrc(dinv_f, NCB * IB * IB * 8);
+    double* Tw = Tws + wave * LT;
+    // this wave's 16 rows of A = S(j, f) (final: the workgroup waited for its writers), MFMA output layout:
+    // acc[t][r] = A[lk + 4 r][16 t + lr]; sc1 loads (written by other workgroups in this launch)
+    dbl4 acc[NCB];
+#pragma unroll
+    for (int t = 0; t < NCB; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            acc[t][r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                       rX, (int)(((int64_t)(lk + 4 * r) * ld + IB * t + lr) * 8), 0, SC1));
+    constexpr int NS = fset_count(SET), NT = (NS + POTRF_NW - 1) / POTRF_NW;
+    int ta[NT], tb[NT];
+    dbl4 c[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+        fset_tile(SET, wave + POTRF_NW * i, ta[i], tb[i]);
+        if (wave + POTRF_NW * i < NS)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) c[i][r] = smem[(ta[i] * (ta[i] + 1) / 2 + tb[i]) * LT + (lk + 4 * r) * 17 + lr];
+    }
+#pragma unroll
+    for (int t = 0; t < NCB; ++t) {
+        double* L = Lb + (t & 1) * NCB * LT;
+        if (tid == 0) {  // column block t of L_ff and D_t published
+            unsigned spins = 0;
+            while (__hip_atomic_load(colflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(t + 1)) {
+                __builtin_amdgcn_s_sleep(1);
+                if (spin_expired(spins, scal)) break;
+            }
+        }
+        // every wave drained its X_{t-1} stores before this barrier (end of the previous step): blocks
+        // [0, t) are published; the previous step's readers of Xb are done
+        __syncthreads();
+        if (t > 0 && tid == 0) __hip_atomic_store(prog, (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        {   // tiles (t+1+u, t), u < 7 - t, into slots u; D_t into slot 7: (8 - t) x 128 double2 items
+            double2 v[2];
+            int dst[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int i = tid + POTRF_THREADS * q, u = i >> 7, n = (i >> 3) & 15, m = (i & 7) * 2;
+                dst[q] = -1;
+                if (u < NCB - 1 - t) {
+                    v[q] = ld_sc1(rL, ((int64_t)((t + 1 + u) * IB + n) * ld + t * IB + m) * 8);
+                    dst[q] = u * LT + n * 17 + m;
+                } else if (u == NCB - 1 - t) {
+                    v[q] = ld_sc1(rD, (int64_t)(t * IB * IB + n * IB + m) * 8);
+                    dst[q] = (NCB - 1) * LT + n * 17 + m;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                if (dst[q] >= 0) {
+                    L[dst[q]] = v[q].x;
+                    L[dst[q] + 1] = v[q].y;
+                }
+        }
+        __syncthreads();  // column block t in LDS
+        if (tr && tid == 0) tr[8 + t] = wall_clock64();  // FBA_PANEL_TRACE: block t in LDS
+        // X_t = A_t D_t'
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Tw[(lk + 4 * r) * 17 + lr] = acc[t][r];
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+        double av[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) av[kk] = Tw[lr * 17 + 4 * kk + lk];
+        dbl4 x = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) x = mfma(av[kk], L[(NCB - 1) * LT + lr * 17 + 4 * kk + lk], x);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Tw[(lk + 4 * r) * 17 + lr] = x[r];
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+        double xa[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) xa[kk] = -Tw[lr * 17 + 4 * kk + lk];
+        {   // X_t's rows: write-through to S(j, f), and into Xb for the update
+            const int n = lane >> 2, m = 4 * (lane & 3);
+            double2 v0, v1;
+            v0.x = Tw[n * 17 + m];
+            v0.y = Tw[n * 17 + m + 1];
+            v1.x = Tw[n * 17 + m + 2];
+            v1.y = Tw[n * 17 + m + 3];
+            st_sc1(rX, ((int64_t)n * ld + IB * t + m) * 8, v0);
+            st_sc1(rX, ((int64_t)n * ld + IB * t + m + 2) * 8, v1);
+            double* xr = Xb + (IB * wave + n) * 17 + m;
+            xr[0] = v0.x;
+            xr[1] = v0.y;
+            xr[2] = v1.x;
+            xr[3] = v1.y;
+        }
+        // right-looking: A_s -= X_t L_st' for s > t
+#pragma unroll
+        for (int s2 = t + 1; s2 < NCB; ++s2)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+                acc[s2] = mfma(xa[kk], L[(s2 - t - 1) * LT + lr * 17 + 4 * kk + lk], acc[s2]);
+        if (t == NCB - 1) {  // the last block: published before the update (the split helper waits for it)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(prog, (unsigned)NCB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __syncthreads();  // X_t complete in Xb
+        }
+        // C(a, b) -= X_t(a) X_t(b)' on this wave's tiles of SET
+        double xu[NT][4], yu[NT][4];
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+            if (wave + POTRF_NW * i < NS) {
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    xu[i][kk] = -Xb[(IB * ta[i] + lr) * 17 + 4 * kk + lk];
+                    yu[i][kk] = Xb[(IB * tb[i] + lr) * 17 + 4 * kk + lk];
+                }
+            }
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+                if (wave + POTRF_NW * i < NS) c[i] = mfma(xu[i][kk], yu[i][kk], c[i]);
+        if (tr && tid == 0) tr[16 + t] = wall_clock64();  // FBA_PANEL_TRACE: block t applied
+        if (t < NCB - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // X_t drained: published at the next barrier
+    }
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+        if (wave + POTRF_NW * i < NS)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) smem[(ta[i] * (ta[i] + 1) / 2 + tb[i]) * LT + (lk + 4 * r) * 17 + lr] = c[i][r];
+}
+
 // diag_body (role 0): diagonal block j.  C_jj (its final in-place writers done) is loaded into LDS; with
 // a fused source f (rec[2] >= 0) C_jj -= X X', X = L(j, f), as the panel halves of (f, j) publish X
 // (fused_apply: all tiles, or with a split helper, rec[9] >= 0, those of tile columns < FLOW_CSPLIT);
@@ -2083,7 +2241,17 @@ __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, co
             smem[p * IB * 17 + n * 17 + m + 1] = v[q].y;
         }
     }
-    if (f >= 0) {
+    if (f >= 0 && rec[12]) {  // self panel: this workgroup solves its rows of f's panel itself
+        const int64_t f0 = (int64_t)f * CB;
+        wait_list_sc1(lists + rec[13], rec[14], fl, scal);  // the final writers of S(j, f)'s quarters
+        double* Lb = reinterpret_cast<double*>(sy + 32);
+        double* Tws = Lb + 2 * (CB / IB) * IB * 17;
+        const double* dinv_f = dinv + (int64_t)f * (CB / IB) * IB * IB;
+        if (rec[9] >= 0)
+            selfpanel_apply<1>(S, ld, k0, f0, dinv_f, colflags + f, fl + rec[7], smem, Dall, Lb, Tws, scal, tr);
+        else
+            selfpanel_apply<0>(S, ld, k0, f0, dinv_f, colflags + f, fl + rec[7], smem, Dall, Lb, Tws, scal, tr);
+    } else if (f >= 0) {
         const int64_t f0 = (int64_t)f * CB;
         const __amdgpu_buffer_rsrc_t rX = block_rsrc(S + k0 * ld + f0, ((int64_t)(CB - 1) * ld + CB) * 8);
         const unsigned* p0 = fl + rec[7];
@@ -2146,7 +2314,7 @@ __device__ __forceinline__ void split_helper_body(double* __restrict__ S, int64_
     const __amdgpu_buffer_rsrc_t rX = block_rsrc(S + k0 * ld + f0, ((int64_t)(CB - 1) * ld + CB) * 8);
     double* Dall = smem + POTRF_NT * IB * 17;
     int* sy = reinterpret_cast<int*>(Dall + (CB / IB) * IB * 17);
-    fused_apply<2>(rX, ld, fl + rec[7], fl + rec[8], 0, Dall, reinterpret_cast<double*>(sy + 32), sy, smem,
+    fused_apply<2>(rX, ld, fl + rec[7], rec[8] >= 0 ? fl + rec[8] : nullptr, 0, Dall, reinterpret_cast<double*>(sy + 32), sy, smem,
                    P + (int64_t)rec[10] * 4096, scal, tr);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

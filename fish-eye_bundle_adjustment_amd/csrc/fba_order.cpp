@@ -439,12 +439,27 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
         for (int32_t k : srcs[j])
             if (fsrc[j] < 0 || level[k] > level[fsrc[j]] || (level[k] == level[fsrc[j]] && k > fsrc[j])) fsrc[j] = k;
     auto halves = [&](int64_t r) { return real_rows(r) > NB / 2 ? 2 : 1; };
-    // progress flags of every panel half (k, r, h), r in R[k] (the RHS block row included)
+    // the fused source's panel rows of block j are solved by two panel-half records and handed to j's
+    // diagonal workgroup.  FBA_FLOW_SELF=1: that workgroup solves them itself (selfpanel_apply: one
+    // hand-off between two levels' potrfs instead of two) -- measured and not kept (config 4, two runs
+    // each: 1133 / 1139 iter/s, k_chol_flow 521.5 us, vs 1228 / 1222 and 454.4 us): one CU's f64 MFMA rate
+    // paces the panel solve plus the fused update at ~3 us per column block, behind the potrf's ~2.4 us,
+    // so the diagonal block lands 14 us after the source's last column instead of 12
+    static const bool selfp = getenv("FBA_FLOW_SELF") && atoi(getenv("FBA_FLOW_SELF")) == 1;
+    auto self_panel = [&](int64_t k, int64_t r) { return selfp && r < nb && fsrc[r] == (int32_t)k; };
+    // progress flags of every panel half (k, r, h), r in R[k] (the RHS block row included); a self panel
+    // has one flag for both halves (raised by the diagonal workgroup of r)
     std::map<std::tuple<int32_t, int32_t, int32_t>, int32_t> prog;
     int np = 0;
     for (int64_t k = 0; k < nb; ++k)
-        for (int32_t r : R[k])
+        for (int32_t r : R[k]) {
+            if (self_panel(k, r)) {
+                for (int h = 0; h < halves(r); ++h) prog[std::make_tuple((int32_t)k, r, h)] = np;
+                ++np;
+                continue;
+            }
             for (int h = 0; h < halves(r); ++h) prog[std::make_tuple((int32_t)k, r, h)] = np++;
+        }
     struct Task {
         std::array<int32_t, REC> rec;
         std::array<int, 3> key;  // level of need, role rank, tie-break
@@ -452,6 +467,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     };
     std::vector<Task> T;
     std::vector<int> col_task(nb, -1), prog_task(np, -1);
+    std::map<int, int> follow;  // record -> the record dispatched right after it (a self panel's split helper)
     std::vector<std::vector<int>> uflag_tasks;  // update flag -> the records that may raise it
     std::vector<std::vector<int32_t>> flag_deps;  // per record: flags it waits for (resolved to records)
     auto new_uflag = [&]() { uflag_tasks.emplace_back(); return (int32_t)(np + uflag_tasks.size() - 1); };
@@ -498,27 +514,41 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     for (int64_t j = 0; j < nb; ++j) {
         const int32_t f = fsrc[j];
         int need = level[j] - 1;
+        const bool sp = f >= 0 && self_panel(f, j);
         const int32_t p0 = f >= 0 ? prog[std::make_tuple(f, (int32_t)j, 0)] : -1;
-        const int32_t p1 = (f >= 0 && halves(j) > 1) ? prog[std::make_tuple(f, (int32_t)j, 1)] : -1;
-        const bool split = csplit && f >= 0 && p1 >= 0 && ksplit == 0;
+        const int32_t p1 = (f >= 0 && halves(j) > 1 && !sp) ? prog[std::make_tuple(f, (int32_t)j, 1)] : -1;
+        const bool split = csplit && f >= 0 && halves(j) > 1 && ksplit == 0;
         const int32_t hflag = split ? new_uflag() : -1, hslot = split ? nslot++ : -1;
-        col_task[j] = add({0, (int32_t)j, f, 0, 0, 0, 0, p0, p1, hflag, hslot, f >= 0 ? ksplit : 0}, {need, 0, (int)j});
-        if (f >= 0) {
+        // (rec[12] = 1: self panel, rec[7] its progress flag; rec[13..14]: the panel block's writer list)
+        col_task[j] = add({0, (int32_t)j, f, 0, 0, 0, 0, p0, p1, hflag, hslot, f >= 0 ? (sp ? 0 : ksplit) : 0, sp ? 1 : 0},
+                          {need, 0, (int)j});
+        if (sp) {
+            prog_task[p0] = col_task[j];
+            T[col_task[j]].deps.push_back(col_task[f]);  // consumes f's potrf progressively
+            s.flow_flops += 2.0 * 64.0 * NB * NB;       // the panel rows (two halves' worth)
+        } else if (f >= 0) {
             flag_deps[col_task[j]].push_back(p0);
             if (p1 >= 0) flag_deps[col_task[j]].push_back(p1);
         }
         if (split) {
             const int hid = add({4, (int32_t)j, f, 0, 0, 0, 0, p0, p1, hflag, hslot}, {need, 0, (int)j});
-            flag_deps[hid] = {p0, p1};
+            flag_deps[hid] = {p0};
+            if (p1 >= 0) flag_deps[hid].push_back(p1);
             uflag_tasks[hflag - np].push_back(hid);
-            flag_deps[col_task[j]].push_back(hflag);
+            // a self panel's helper consumes the diagonal workgroup's own published rows, and that
+            // workgroup adds the helper's partial only inside its potrf, after its panel is published: the
+            // helper is dispatched right after it (follow[]), and that wait is the one exception to "every
+            // wait points to an earlier record" -- every record dispatched before the helper is running or
+            // done and none of them waits for this block, so the helper gets a CU
+            if (sp) follow[col_task[j]] = hid;
+            else flag_deps[col_task[j]].push_back(hflag);
         }
         s.flow_flops += (double)NB * NB * NB / 3.0 + (f >= 0 ? (double)NB * NB * NB * (8 - ksplit) / 8.0 : 0.0);
     }
     // panel-half solves
     for (int64_t k = 0; k < nb; ++k)
         for (int32_t r : R[k])
-            for (int h = 0; h < halves(r); ++h) {
+            for (int h = 0; h < halves(r) && !self_panel(k, r); ++h) {
                 const int32_t p = prog[std::make_tuple((int32_t)k, r, h)];
                 // rec[7]: the RHS block row's half 0 accumulates its rows' Gram into partial k
                 // FBA_FLOW_PROMOTE: 1 = the panel halves feeding a fused diagonal update (the critical
@@ -632,7 +662,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     // the helpers of the fused updates: column blocks [0, ksplit) of f_j's panel rows j, per quarter
     for (int64_t j = 0; j < nb && ksplit > 0; ++j) {
         const int32_t f = fsrc[j];
-        if (f < 0) continue;
+        if (f < 0 || self_panel(f, j)) continue;
         for (int q : {0, 2, 3}) {
             const int qr = q >> 1, qc = q & 1;
             if (q > 0 && halves(j) < 2) continue;
@@ -673,6 +703,17 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
             X.rec[3] = woff;
             X.rec[4] = (int32_t)buf.size() - woff;
             for (int32_t x = woff; x < (int32_t)buf.size(); ++x) flag_deps[id].push_back(buf[x]);
+            if (X.rec[12]) {  // self panel: the final writers of S(j, f)'s quarters, as a panel half waits
+                const int32_t f = X.rec[2], poff = (int32_t)buf.size();
+                for (int h = 0; h < halves(j); ++h)
+                    for (int qc = 0; qc < halves(f); ++qc) {
+                        auto it = writer.find(std::make_tuple(j, f, 2 * h + qc));
+                        if (it != writer.end() && it->second >= 0) buf.push_back(it->second);
+                    }
+                X.rec[13] = poff;
+                X.rec[14] = (int32_t)buf.size() - poff;
+                for (int32_t x = poff; x < (int32_t)buf.size(); ++x) flag_deps[id].push_back(buf[x]);
+            }
             const int32_t loff = (int32_t)buf.size();
             for (auto& l : late[j]) {
                 buf.insert(buf.end(), l.begin(), l.end());
@@ -716,12 +757,20 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
         std::priority_queue<int, std::vector<int>, decltype(cmp)> ready(cmp);
         for (int i = 0; i < n; ++i)
             if (indeg[i] == 0) ready.push(i);
+        std::vector<char> placed(n, 0);
         while (!ready.empty()) {
             const int i = ready.top();
             ready.pop();
-            ord.push_back(i);
-            for (int x : succ[i])
-                if (--indeg[x] == 0) ready.push(x);
+            if (placed[i]) continue;
+            std::vector<int> emit{i};
+            auto fw = follow.find(i);
+            if (fw != follow.end()) emit.push_back(fw->second);  // (its only producer is i)
+            for (int e : emit) {
+                placed[e] = 1;
+                ord.push_back(e);
+                for (int x : succ[e])
+                    if (--indeg[x] == 0 && !placed[x]) ready.push(x);
+            }
         }
     }
     if ((int)ord.size() != n) ok = false;  // a dependency cycle
@@ -772,7 +821,9 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
         };
         auto start_edge = [&](int d, int i) {
             if (!eager(i)) return false;
-            if (T[d].rec[0] == 0) return T[i].rec[0] == 1;  // a panel half of the block: at its potrf's start
+            // a panel half of the block, or a self-panel diagonal workgroup consuming it: at its potrf's start
+            if (T[d].rec[0] == 0)
+                return T[i].rec[0] == 1 || T[i].rec[0] == 4 || (T[i].rec[0] == 0 && T[i].rec[12] != 0);
             return true;  // consumed progressively, or waited for by a running record
         };
         auto dur = [&](int i) {

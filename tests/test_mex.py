@@ -25,7 +25,8 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import ROOT, CAM0_VARIANTS, dist_scaling_of, elem_rel_err, group_rel_err, variant_folder  # noqa: F401
+from conftest import (ROOT, CAM0_VARIANTS, dist_scaling_of, elem_rel_err, group_rel_err, solver_spread,  # noqa: F401
+                      variant_folder)
 
 STUB = os.path.join(ROOT, "tests", "mexstub")
 LIBDIR = os.path.join(ROOT, "fish-eye_bundle_adjustment_amd")
@@ -253,12 +254,15 @@ def test_mex_whole_loop_matches_oracle_cam0(fba, oracle, mexlibs, cam0_folders):
     _, xhat, count, dsum, v, rsd, st, cxd, corr = _mex_adjust(mx, fns, od)
     assert mx.get(count)[0, 0] == ro.iterations
     # the deltasum history: the gateway runs the library's loop (fba_adjust), so the Python mirror's to
-    # rounding; against the oracle the first pass at 1e-9 (the later ones are differences of nearly equal
-    # iterates, at the restatements' own rounding spread, conftest.solver_spread)
+    # rounding; against the oracle the first pass at 1e-9 or 20x the restatements' own spread, the bound
+    # test_gpu_parity.test_adjust_cam0 holds the library to (this scene's first Sigma|delta| moves by ~7e-9
+    # between exact restatements: inner constraints + control points; the later passes are differences of
+    # nearly equal iterates)
     d = mx.get(dsum)[0]
     lib = fba.adjust(fba.load_folder(cam0_folders["stage3_pinhole"]), covariance=False).deltasum
     np.testing.assert_allclose(d, lib, rtol=0, atol=1e-12 * ro.deltasum[0])
-    assert abs(d[0] - ro.deltasum[0]) <= 1e-9 * ro.deltasum[0]
+    spread = solver_spread(oracle, od, ro)
+    assert abs(d[0] - ro.deltasum[0]) <= max(1e-9, 20 * spread["deltasum0"]) * ro.deltasum[0], spread["deltasum0"]
     x = mx.get(xhat)[:, 0]
     for err in (group_rel_err(x, ro.xhat, ro.names, ro.dist_scaling), elem_rel_err(x, ro.xhat, ro.names, ro.dist_scaling)):
         assert max(err.values()) <= 1e-9, err

@@ -24,13 +24,16 @@ def checker(tmp_path_factory):
     return exe
 
 
-@pytest.mark.parametrize("n_img,seed,leaf,merge", [(40, 1, None, None), (300, 2, None, None), (300, 1, 60, None),
-                                                   (420, 3, 100, None), (200, 4, 0, None), (300, 2, None, 1),
-                                                   (300, 1, 60, 2)])
-def test_level_schedule_matches_dense_cholesky(checker, n_img, seed, leaf, merge):
+@pytest.mark.parametrize("n_img,seed,leaf,merge,self_panel", [
+    (40, 1, None, None, 0), (300, 2, None, None, 0), (300, 1, 60, None, 0), (420, 3, 100, None, 0),
+    (200, 4, 0, None, 0), (300, 2, None, 1, 0), (300, 1, 60, 2, 0),
+    # FBA_FLOW_SELF=1 (diagonal workgroups solving their fused source's panel rows; measured, off by default)
+    (300, 2, None, None, 1), (420, 3, 100, None, 1)])
+def test_level_schedule_matches_dense_cholesky(checker, n_img, seed, leaf, merge, self_panel):
     env = dict(os.environ)
     env.pop("FBA_ND_LEAF", None)
     env.pop("FBA_FLOW_MERGE", None)
+    env["FBA_FLOW_SELF"] = str(self_panel)
     if leaf is not None:
         env["FBA_ND_LEAF"] = str(leaf)
     if merge is not None:  # writer groups over consecutive source levels (build_flow)
