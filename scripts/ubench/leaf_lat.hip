@@ -48,6 +48,31 @@ __device__ __forceinline__ bool leaf_factor_noinv_ub(double (&a)[IB]) {
     return ok;
 }
 
+// the factor without the inverse, with a per-column hook put(j, inv) (inv = 1 / L[j][j])
+template <class PUT>
+__device__ __forceinline__ bool leaf_factor_noinv(double (&a)[IB], PUT&& put) {
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < IB; ++j) {
+        const double d = bcl(a[j], j);
+        ok &= d > 0.0;
+        const double r = __builtin_amdgcn_rsq(d);
+        const double ar = a[j] * r;
+        const double t = d * r;
+        const double e = __builtin_fma(t, r, -1.0);
+        const double p = __builtin_fma(e, 0.375, -0.5);
+        const double inv = __builtin_fma(r * e, p, r);
+        a[j] = __builtin_fma(ar * e, p, ar);
+#pragma unroll
+        for (int l = j + 1; l < IB; ++l) {
+            if (l == j + 1) fmac_bcn_first(a[l], a[j], a[j], l);
+            else fmac_bcn(a[l], a[j], a[j], l);
+        }
+        put(j, inv);
+    }
+    return ok;
+}
+
 template <int MODE>
 __global__ void k_leaf(const double* __restrict__ A, double* __restrict__ out, long long* clk, int reps) {
     const int lane = threadIdx.x & 63, lr = lane & 15;
@@ -90,6 +115,71 @@ __global__ void k_leaf(const double* __restrict__ A, double* __restrict__ out, l
     if (threadIdx.x == 0) *clk = t1 - t0;
 }
 
+// MODE 9: wave 0 factors without the inverse and stores each column of L once (lanes 0-15); wave 1
+// (another SIMD) polls the columns (NaN sentinel, every lane of a column in the one ds_write_b64) and
+// runs the substitutions beside it: row 0 of its lanes the inverse D_s (lane c = column c), row 1 a
+// panel tile's rows X = A L^-T (lane i = row i).  Clocks: wave 0's leaf, wave 1 done (same start)
+__global__ __launch_bounds__(128) void k_leaf_split(const double* __restrict__ A, double* __restrict__ out,
+                                                      long long* clk, int reps) {
+    const int lane = threadIdx.x & 63, lr = lane & 15, wave = threadIdx.x >> 6;
+    __shared__ double Lw[16 * 17], junk[64];
+    double a0[IB], y0[IB];
+#pragma unroll
+    for (int c = 0; c < IB; ++c) {
+        a0[c] = A[lr * IB + c];
+        y0[c] = (lane < 16) ? (c == lr ? 1.0 : 0.0) : A[((lr + 3) & 15) * IB + c] * 0.5;
+    }
+    long long s0 = 0, s1 = 0, s2 = 0;
+    double acc = 0.0;
+    const double SENT = __builtin_nan("");
+    for (int it = 0; it < reps; ++it) {
+        if (wave == 1 && lane < 16)
+            for (int c = 0; c < IB; ++c) Lw[lane * 17 + c] = SENT;
+        __syncthreads();
+        const long long t0 = clock64();
+        if (wave == 0) {
+            double a[IB];
+#pragma unroll
+            for (int c = 0; c < IB; ++c) a[c] = a0[c] + acc * 1e-300;
+            bool ok = leaf_factor_noinv(a, [&](int j, double) { *(lane < 16 ? &Lw[lr * 17 + j] : &junk[lane]) = a[j]; });
+            const long long t1 = clock64();
+            s1 += t1 - t0;
+            acc += a[IB - 1] + (ok ? 0.0 : 1.0);
+        } else {
+            double y[IB];
+#pragma unroll
+            for (int c = 0; c < IB; ++c) y[c] = y0[c];
+#pragma unroll
+            for (int j = 0; j < IB; ++j) {
+                double lc;
+                for (;;) {  // column j of L: lane l holds L[l][j] (lanes >= j meaningful)
+                    lc = *(volatile double*)&Lw[lr * 17 + j];
+                    const bool miss = (lr >= j) && (lc != lc);
+                    if (!__builtin_amdgcn_ballot_w64(miss)) break;
+                }
+                const double dj = bcl(lc, j);
+                double inv = __builtin_amdgcn_rcp(dj);
+                const double e = __builtin_fma(-dj, inv, 1.0);
+                inv = __builtin_fma(inv, e, inv);
+                inv = __builtin_fma(inv, __builtin_fma(-dj, inv, 1.0), inv);
+                y[j] *= inv;
+#pragma unroll
+                for (int l = j + 1; l < IB; ++l) {
+                    if (l == j + 1) fmac_bcn_first(y[l], lc, y[j], l);
+                    else fmac_bcn(y[l], lc, y[j], l);
+                }
+            }
+            const long long t2 = clock64();
+            s2 += t2 - t0;
+            acc += y[IB - 1];
+        }
+        __syncthreads();
+    }
+    out[threadIdx.x] = acc;
+    if (threadIdx.x == 0) clk[0] = s1;
+    if (threadIdx.x == 64) clk[1] = s2;
+}
+
 int main() {
     double hA[256];
     for (int i = 0; i < 16; ++i)
@@ -97,7 +187,7 @@ int main() {
     double *dA, *out; long long* clk;
     (void)hipMalloc(&dA, sizeof(hA));
     (void)hipMalloc(&out, 64 * sizeof(double));
-    (void)hipMalloc(&clk, sizeof(long long));
+    (void)hipMalloc(&clk, 2 * sizeof(long long));
     (void)hipMemcpy(dA, hA, sizeof(hA), hipMemcpyHostToDevice);
     const int reps = 200;
     auto run = [&](auto kern, const char* name) {
@@ -126,5 +216,12 @@ int main() {
     run8(k_leaf<3>, "  same, 7 waves reading LDS");
     run8(k_leaf<4>, "  same (inverse), 7 waves reading LDS");
     run8(k_leaf<1>, "  factor only, 7 waves reading LDS");
+    for (int r = 0; r < 2; ++r) {
+        k_leaf_split<<<1, 128>>>(dA, out, clk, reps);
+        long long c[2] = {0, 0};
+        (void)hipMemcpy(c, clk, sizeof(c), hipMemcpyDeviceToHost);
+        printf("split: wave 0 factor-only leaf %6.0f clocks, wave 1 inverse + panel rows done %6.0f clocks\n",
+               (double)c[0] / reps, (double)c[1] / reps);
+    }
     return 0;
 }
