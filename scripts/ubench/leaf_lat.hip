@@ -180,6 +180,86 @@ __global__ __launch_bounds__(128) void k_leaf_split(const double* __restrict__ A
     if (threadIdx.x == 64) clk[1] = s2;
 }
 
+// MODE 10: as MODE 9, with wave 1 prefetching column j+1 while it works on column j; WINV: wave 0's
+// column store also carries 1 / L[j][j] (lane 16 -> invs[j], the same ds_write), else wave 1 forms it
+template <bool WINV>
+__global__ __launch_bounds__(128) void k_leaf_split2(const double* __restrict__ A, double* __restrict__ out,
+                                                       long long* clk, int reps) {
+    const int lane = threadIdx.x & 63, lr = lane & 15, wave = threadIdx.x >> 6;
+    __shared__ double Lw[16 * 17], invs[16], junk[64];
+    double a0[IB], y0[IB];
+#pragma unroll
+    for (int c = 0; c < IB; ++c) {
+        a0[c] = A[lr * IB + c];
+        y0[c] = (lane < 16) ? (c == lr ? 1.0 : 0.0) : A[((lr + 3) & 15) * IB + c] * 0.5;
+    }
+    long long s1 = 0, s2 = 0;
+    double acc = 0.0;
+    const double SENT = __builtin_nan("");
+    for (int it = 0; it < reps; ++it) {
+        if (wave == 1 && lane < 16) {
+            for (int c = 0; c < IB; ++c) Lw[lane * 17 + c] = SENT;
+            invs[lane] = SENT;
+        }
+        __syncthreads();
+        const long long t0 = clock64();
+        if (wave == 0) {
+            double a[IB];
+#pragma unroll
+            for (int c = 0; c < IB; ++c) a[c] = a0[c] + acc * 1e-300;
+            bool ok;
+            if (WINV)
+                ok = leaf_factor_noinv(a, [&](int j, double inv) {
+                    *(lane < 16 ? &Lw[lr * 17 + j] : lane == 16 ? &invs[j] : &junk[lane]) = lane == 16 ? inv : a[j];
+                });
+            else
+                ok = leaf_factor_noinv(a, [&](int j, double) { *(lane < 16 ? &Lw[lr * 17 + j] : &junk[lane]) = a[j]; });
+            const long long t1 = clock64();
+            s1 += t1 - t0;
+            acc += a[IB - 1] + (ok ? 0.0 : 1.0);
+        } else {
+            double y[IB];
+#pragma unroll
+            for (int c = 0; c < IB; ++c) y[c] = y0[c];
+            double lcn = *(volatile double*)&Lw[lr * 17], ivn = WINV ? *(volatile double*)&invs[0] : 0.0;
+#pragma unroll
+            for (int j = 0; j < IB; ++j) {
+                double lc = lcn, iv = ivn;
+                for (;;) {
+                    const bool miss = ((lr >= j) && (lc != lc)) || (WINV && iv != iv);
+                    if (!__builtin_amdgcn_ballot_w64(miss)) break;
+                    lc = *(volatile double*)&Lw[lr * 17 + j];
+                    if (WINV) iv = *(volatile double*)&invs[j];
+                }
+                if (j + 1 < IB) {
+                    lcn = *(volatile double*)&Lw[lr * 17 + j + 1];
+                    if (WINV) ivn = *(volatile double*)&invs[j + 1];
+                }
+                double inv = iv;
+                if (!WINV) {
+                    const double dj = bcl(lc, j);
+                    inv = __builtin_amdgcn_rcp(dj);
+                    inv = __builtin_fma(inv, __builtin_fma(-dj, inv, 1.0), inv);
+                    inv = __builtin_fma(inv, __builtin_fma(-dj, inv, 1.0), inv);
+                }
+                y[j] *= inv;
+#pragma unroll
+                for (int l = j + 1; l < IB; ++l) {
+                    if (l == j + 1) fmac_bcn_first(y[l], lc, y[j], l);
+                    else fmac_bcn(y[l], lc, y[j], l);
+                }
+            }
+            const long long t2 = clock64();
+            s2 += t2 - t0;
+            acc += y[IB - 1];
+        }
+        __syncthreads();
+    }
+    out[threadIdx.x] = acc;
+    if (threadIdx.x == 0) clk[0] = s1;
+    if (threadIdx.x == 64) clk[1] = s2;
+}
+
 int main() {
     double hA[256];
     for (int i = 0; i < 16; ++i)
@@ -222,6 +302,15 @@ int main() {
         (void)hipMemcpy(c, clk, sizeof(c), hipMemcpyDeviceToHost);
         printf("split: wave 0 factor-only leaf %6.0f clocks, wave 1 inverse + panel rows done %6.0f clocks\n",
                (double)c[0] / reps, (double)c[1] / reps);
+    }
+    for (int r = 0; r < 2; ++r) {
+        k_leaf_split2<false><<<1, 128>>>(dA, out, clk, reps);
+        long long c[2] = {0, 0};
+        (void)hipMemcpy(c, clk, sizeof(c), hipMemcpyDeviceToHost);
+        printf("split, prefetch: wave 0 %6.0f, wave 1 done %6.0f clocks\n", (double)c[0] / reps, (double)c[1] / reps);
+        k_leaf_split2<true><<<1, 128>>>(dA, out, clk, reps);
+        (void)hipMemcpy(c, clk, sizeof(c), hipMemcpyDeviceToHost);
+        printf("split, prefetch, inv from wave 0: wave 0 %6.0f, wave 1 done %6.0f clocks\n", (double)c[0] / reps, (double)c[1] / reps);
     }
     return 0;
 }
