@@ -239,6 +239,12 @@ __device__ __forceinline__ void fmac_bcn(double& d, double s, double m, int l) {
     }
 }
 
+// a fold over a compile-time index sequence (every index a constant expression in the body)
+template <int... Q, class F>
+__device__ __forceinline__ void bulk_for(std::integer_sequence<int, Q...>, F&& f) {
+    (f(std::integral_constant<int, Q>{}), ...);
+}
+
 // lane i (< 16) of a wave holds row i of a 16x16 SPD block in a[]; on return a[] holds row i of L
 // (lower part) and x[] COLUMN i of L^-1 (x[r] = (L^-1)[r][i]).  Every broadcast L[l][j] feeds both
 // the rank-1 update of the factor and the forward substitution of the inverse's columns, each as
@@ -247,7 +253,10 @@ __device__ __forceinline__ void fmac_bcn(double& d, double s, double m, int l) {
 // update: rsq is good to 2^-24 (measured), so e = d r^2 - 1 and r (1 - e/2 + 3e^2/8) is accurate to
 // rounding (max rel. error 2.7e-16 measured, vs 3.0e-16 for two Newton steps).  The pivot test is
 // off the chain: a non-positive pivot propagates NaN and is reported (returns false).
-// put(j): called once column j of L (a[j] on lanes >= j) and row j of L^-1 (x[j]) are final
+// put(j): called once column j of L (a[j] on lanes >= j) and row j of L^-1 (x[j]) are final.
+// Issue-bound: ~400 f64 VALU instructions at ~5.6 shader clocks each on one wave (a dependent f64 fma
+// is 8.6 clocks, an independent one 5.7: scripts/ubench/leaf_lat.hip); a software-pipelined order that
+// spreads each column's updates over the next pivot chain's steps measured slower.
 template <class PUT>
 __device__ __forceinline__ bool leaf_factor(double (&a)[IB], double (&x)[IB], int lane16, PUT&& put) {
     bool ok = true;
@@ -276,6 +285,7 @@ __device__ __forceinline__ bool leaf_factor(double (&a)[IB], double (&x)[IB], in
     }
     return ok;
 }
+
 __device__ __forceinline__ bool leaf_factor(double (&a)[IB], double (&x)[IB], int lane16) {
     return leaf_factor(a, x, lane16, [](int) {});
 }
@@ -546,11 +556,6 @@ __device__ __forceinline__ void fset_tile(int set, int idx, int& ta, int& tb) { 
             }
 }
 
-// a fold over a compile-time index sequence (every index a constant expression in the body)
-template <int... Q, class F>
-__device__ __forceinline__ void bulk_for(std::integer_sequence<int, Q...>, F&& f) {
-    (f(std::integral_constant<int, Q>{}), ...);
-}
 
 // potrf_body (dataflow): factor the 128x128 diagonal block of column col (512 threads); flag != nullptr:
 // publish it column by column (k_panel hand-off).  No workgroup barriers after the load: the waves

@@ -3,9 +3,124 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 leaf_lat.hip -o leaf_lat
 #include "../../fish-eye_bundle_adjustment_amd/csrc/fba_chol.hip"
 #include <cstdio>
+#include <cstring>
 
 namespace fba { void set_error(const std::string&) {} }
 using namespace fba;
+template <class PUT>
+__device__ __forceinline__ bool leaf_factor_ref(double (&a)[IB], double (&x)[IB], int lane16, PUT&& put) {
+    return leaf_factor(a, x, lane16, put);
+}
+
+// The scheduled leaf.  Every instruction of the pivot chain is its own asm statement too, so program
+// order is issue order (a wave issues in order; asm volatile statements keep their source order), and
+// column C's bulk work -- x[C] *= 1/L[C][C], the a-updates of rows C+2..15 and the inverse's updates,
+// 30 - 2C instructions that only need L's column C -- is spread over the dependent steps of column
+// C+1's pivot chain (DPP broadcast -> rsq -> correction -> L[.][C+1] -> the first update of column C+2),
+// filling their latencies instead of queueing in front of them.  Same instructions, same operands and
+// the same order of updates per register as leaf_factor_ref: bit-identical results.
+// Hazards the compiler cannot see inside asm: 2 wait states between a VALU write and a DPP read of the
+// same VGPR (s_nop 1 in as_bcl and fmac_bcn_first), 1 after a transcendental (s_nop 0 after rsq).
+__device__ __forceinline__ double as_mul(double a, double b) {
+    double r;
+    asm volatile("v_mul_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double as_fma(double a, double b, double c) {
+    double r;
+    asm volatile("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ double as_rsq(double a) {
+    double r;
+    asm volatile("v_rsq_f64 %0, %1\n\ts_nop 0" : "=v"(r) : "v"(a));
+    return r;
+}
+template <int J>
+__device__ __forceinline__ double as_bcl(double v) {
+    double r;
+    asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+                 : "=v"(r) : "v"(v), "i"(J));
+    return r;
+}
+// column C's bulk: op 0 x[C] *= inv_C, ops 1..NA a[l] -= L[l][C] L[i][C] (l = C+2..15), then
+// x[l] -= L[l][C] x[C] (l = C+1..15)
+template <int C>
+constexpr int leaf_nbulk() { return C < 0 ? 0 : 1 + (C < IB - 2 ? IB - 2 - C : 0) + (IB - 1 - C); }
+template <int C, int K>
+__device__ __forceinline__ void leaf_bulk_op(double (&a)[IB], double (&x)[IB], double inv) {
+    constexpr int NA = C < IB - 2 ? IB - 2 - C : 0;
+    if constexpr (K == 0) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(x[C]) : "v"(inv));
+    else if constexpr (K <= NA) fmac_bcn(a[C + 1 + K], a[C], a[C], C + 1 + K);
+    else fmac_bcn(x[C + K - NA], a[C], x[C], C + K - NA);
+}
+template <int C, int K0, int K1>
+__device__ __forceinline__ void leaf_bulk(double (&a)[IB], double (&x)[IB], double inv) {
+    if constexpr (K0 < K1) {
+        leaf_bulk_op<C, K0>(a, x, inv);
+        leaf_bulk<C, K0 + 1, K1>(a, x, inv);
+    }
+}
+// cumulative shares (of 18) of the bulk placed in the gaps after each chain step: bcl, rsq, ar/t, e,
+// p/re/are, inv/a[J], F
+template <int SCHED>
+struct LeafGaps;
+template <> struct LeafGaps<0> { static constexpr int w[6] = {2, 7, 9, 11, 14, 16}; };
+template <> struct LeafGaps<1> { static constexpr int w[6] = {0, 18, 18, 18, 18, 18}; };  // all behind the rsq
+template <> struct LeafGaps<2> { static constexpr int w[6] = {0, 9, 9, 18, 18, 18}; };    // rsq / e
+template <> struct LeafGaps<3> { static constexpr int w[6] = {0, 9, 9, 9, 9, 18}; };      // rsq / a[J]
+template <> struct LeafGaps<4> { static constexpr int w[6] = {0, 6, 6, 12, 12, 18}; };    // rsq / e / a[J]
+// window J: column J's pivot chain with column J-1's bulk between its steps (J = IB: the last bulk)
+template <int J, int SCHED, class PUT>
+__device__ __forceinline__ void leaf_window(double (&a)[IB], double (&x)[IB], double& inv, bool& ok,
+                                            const double m1, const double c38, const double mh, PUT& put) {
+    constexpr int C = J - 1, NB = leaf_nbulk<C>();
+    const double invc = inv;  // 1 / L[C][C]
+    if constexpr (J == IB) {
+        leaf_bulk<C, 0, NB>(a, x, invc);
+        put(C);
+    } else {
+        using G = LeafGaps<SCHED>;
+        constexpr int b0 = NB * G::w[0] / 18, b1 = NB * G::w[1] / 18, b2 = NB * G::w[2] / 18,
+                      b3 = NB * G::w[3] / 18, b4 = NB * G::w[4] / 18, b5 = NB * G::w[5] / 18;
+        const double d = as_bcl<J>(a[J]);
+        if constexpr (C >= 0) leaf_bulk<C, 0, b0>(a, x, invc);
+        const double r = as_rsq(d);
+        if constexpr (C >= 0) leaf_bulk<C, b0, b1>(a, x, invc);
+        const double ar = as_mul(a[J], r);
+        const double t = as_mul(d, r);
+        if constexpr (C >= 0) leaf_bulk<C, b1, b2>(a, x, invc);
+        const double e = as_fma(t, r, m1);
+        if constexpr (C >= 0) leaf_bulk<C, b2, b3>(a, x, invc);
+        const double p = as_fma(e, c38, mh);
+        const double re = as_mul(r, e);
+        const double are = as_mul(ar, e);
+        if constexpr (C >= 0) leaf_bulk<C, b3, b4>(a, x, invc);
+        inv = as_fma(re, p, r);
+        a[J] = as_fma(are, p, ar);  // lane J: sqrt(d); lanes > J: L[i][J]
+        if constexpr (C >= 0) leaf_bulk<C, b4, b5>(a, x, invc);
+        if constexpr (J + 1 < IB) fmac_bcn_first(a[J + 1], a[J], a[J], J + 1);
+        if constexpr (C >= 0) {
+            leaf_bulk<C, b5, NB>(a, x, invc);
+            put(C);
+        }
+        ok &= d > 0.0;
+    }
+}
+template <int SCHED, class PUT>
+__device__ __forceinline__ bool leaf_factor_s(double (&a)[IB], double (&x)[IB], int lane16, PUT&& put) {
+    bool ok = true;
+    double inv = 0.0;
+#pragma unroll
+    for (int r = 0; r < IB; ++r) x[r] = (r == lane16) ? 1.0 : 0.0;
+    const double m1 = -1.0, c38 = 0.375, mh = -0.5;
+    bulk_for(std::make_integer_sequence<int, IB + 1>{}, [&](auto jc) {
+        leaf_window<decltype(jc)::value, SCHED>(a, x, inv, ok, m1, c38, mh, put);
+    });
+    return ok;
+}
+
+
 
 // the pivot chain alone: per column broadcast -> rsq -> correction -> next column's first update
 __device__ __forceinline__ bool leaf_chain_only(double (&a)[IB]) {
@@ -260,6 +375,82 @@ __global__ __launch_bounds__(128) void k_leaf_split2(const double* __restrict__ 
     if (threadIdx.x == 64) clk[1] = s2;
 }
 
+// the potrf's use: rows from LDS, factor + inverse, column stores (put); REF: leaf_factor_ref.  Writes
+// L and D of the last rep to out2 (bit-identity check on the host)
+template <int REF>
+__global__ __launch_bounds__(64) void k_leaf_lds(const double* __restrict__ A, double* __restrict__ out2,
+                                                 long long* clk, int reps) {
+    const int lane = threadIdx.x & 63, lr = lane & 15;
+    __shared__ double Ash[16 * 17], Lw[16 * 17], Dw[16 * 17];
+    if (lane < 16)
+        for (int c = 0; c < IB; ++c) Ash[lane * 17 + c] = A[lane * IB + c];
+    __syncthreads();
+    long long t = 0;
+    for (int it = 0; it < reps; ++it) {
+        double a[IB], x[IB];
+#pragma unroll
+        for (int c = 0; c < IB; ++c) a[c] = Ash[lr * 17 + c];
+        const long long t0 = clock64();
+        auto put = [&](int j) { Lw[lr * 17 + j] = a[j]; Dw[j * 17 + lr] = x[j]; };
+        bool ok;
+        if constexpr (REF < 0) ok = leaf_factor_ref(a, x, lr, put);
+        else ok = leaf_factor_s<REF>(a, x, lr, put);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        const long long t1 = clock64();
+        t += t1 - t0;
+        if (!ok) Ash[0] = 0.0;
+        // feed back (a dependence on this rep, numerically nothing)
+        if (lane == 0) Ash[17 * 15 + 15] += Lw[0] * 0.0;
+        __syncthreads();
+    }
+    if (lane < 16)
+        for (int c = 0; c < IB; ++c) {
+            out2[lane * IB + c] = Lw[lane * 17 + c];
+            out2[256 + lane * IB + c] = Dw[lane * 17 + c];
+        }
+    if (lane == 0) *clk = t;
+}
+
+// raw issue / latency of f64 VALU ops on one wave (clocks per op, 64 ops a rep)
+template <int MODE>
+__global__ __launch_bounds__(64) void k_lat(const double* __restrict__ A, double* __restrict__ out, long long* clk, int reps) {
+    const int lane = threadIdx.x;
+    double c = A[lane & 15], d = c * 0.5, e = c * 0.25, v[8];
+    for (int i = 0; i < 8; ++i) v[i] = A[(lane + i) & 15];
+    const long long t0 = clock64();
+    for (int it = 0; it < reps; ++it) {
+#pragma unroll
+        for (int k = 0; k < 64; ++k) {
+            if constexpr (MODE == 0) asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(c) : "v"(d), "v"(e));
+            else if constexpr (MODE == 1) fmac_bcn(v[k & 7], d, e, 1 + (k & 7));
+            else if constexpr (MODE == 2) fmac_bcn(c, d, e, 1 + (k & 7));
+            else if constexpr (MODE == 3) {
+                asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(c) : "v"(d), "v"(e));
+                fmac_bcn(v[(2 * k) & 7], d, e, 1 + (k & 7));
+                fmac_bcn(v[(2 * k + 1) & 7], d, e, 2 + (k & 7));
+            } else if constexpr (MODE == 4) {
+                asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(c) : "v"(d), "v"(e));
+                asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(v[(2 * k) & 7]) : "v"(d), "v"(e));
+                asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(v[(2 * k + 1) & 7]) : "v"(d), "v"(e));
+            } else if constexpr (MODE == 5) {  // dependent chain with 4 DPP fmacs between
+                asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(c) : "v"(d), "v"(e));
+#pragma unroll
+                for (int q = 0; q < 4; ++q) fmac_bcn(v[(4 * k + q) & 7], d, e, 1 + q);
+            } else if constexpr (MODE == 6) {  // 1 non-DPP fma independent, 1 DPP: mix
+                asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(v[k & 7]) : "v"(d), "v"(e));
+                fmac_bcn(v[(k + 4) & 7], d, e, 1 + (k & 7));
+            } else if constexpr (MODE == 7) {  // rsq chain
+                asm volatile("v_rsq_f64 %0, %0\n\ts_nop 0" : "+v"(c));
+            }
+        }
+    }
+    const long long t1 = clock64();
+    double acc = c;
+    for (int i = 0; i < 8; ++i) acc += v[i];
+    out[lane] = acc;
+    if (lane == 0) *clk = t1 - t0;
+}
+
 int main() {
     double hA[256];
     for (int i = 0; i < 16; ++i)
@@ -277,6 +468,23 @@ int main() {
         (void)hipMemcpy(&c, clk, sizeof(c), hipMemcpyDeviceToHost);
         printf("%-40s %8.0f clocks per leaf (%.0f per column)\n", name, (double)c / reps, (double)c / reps / 16);
     };
+    {
+        auto lat = [&](auto kern, const char* name, int ops) {
+            long long c = 0;
+            kern<<<1, 64>>>(dA, out, clk, 50);
+            kern<<<1, 64>>>(dA, out, clk, 50);
+            (void)hipMemcpy(&c, clk, sizeof(c), hipMemcpyDeviceToHost);
+            printf("%-58s %6.2f clocks per step (%d instr)\n", name, (double)c / (50 * 64), ops);
+        };
+        lat(k_lat<0>, "dependent v_fma_f64 chain", 1);
+        lat(k_lat<1>, "independent v_fmac_f64_dpp (8 accumulators)", 1);
+        lat(k_lat<2>, "dependent v_fmac_f64_dpp chain", 1);
+        lat(k_lat<3>, "dependent fma + 2 independent dpp fmacs", 3);
+        lat(k_lat<4>, "dependent fma + 2 independent fmas", 3);
+        lat(k_lat<5>, "dependent fma + 4 independent dpp fmacs", 5);
+        lat(k_lat<6>, "independent fma + independent dpp fmac", 2);
+        lat(k_lat<7>, "dependent v_rsq_f64 chain", 1);
+    }
     run(k_leaf<0>, "factor + inverse (leaf_factor)");
     run(k_leaf<1>, "factor only");
     run(k_leaf<2>, "pivot chain only");
@@ -296,6 +504,33 @@ int main() {
     run8(k_leaf<3>, "  same, 7 waves reading LDS");
     run8(k_leaf<4>, "  same (inverse), 7 waves reading LDS");
     run8(k_leaf<1>, "  factor only, 7 waves reading LDS");
+    {
+        double *o1, *o2;
+        (void)hipMalloc(&o1, 512 * sizeof(double));
+        (void)hipMalloc(&o2, 512 * sizeof(double));
+        auto one = [&](auto kern, double* o) {
+            long long c = 0;
+            kern<<<1, 64>>>(dA, o, clk, reps);
+            (void)hipMemcpy(&c, clk, sizeof(c), hipMemcpyDeviceToHost);
+            return (double)c / reps;
+        };
+        for (int r = 0; r < 3; ++r) {
+            const double t_ref = one(k_leaf_lds<-1>, o1), t1 = one(k_leaf_lds<1>, o2), t2 = one(k_leaf_lds<2>, o2),
+                         t3 = one(k_leaf_lds<3>, o2), t4 = one(k_leaf_lds<4>, o2), t0 = one(k_leaf_lds<0>, o2);
+            printf("potrf-style leaf (LDS rows, column stores): reference order %6.0f, scheduled 0..4: %6.0f %6.0f %6.0f %6.0f %6.0f clocks\n",
+                   t_ref, t0, t1, t2, t3, t4);
+        }
+        double h1[512], h2[512];
+        (void)hipMemcpy(h1, o1, sizeof(h1), hipMemcpyDeviceToHost);
+        (void)hipMemcpy(h2, o2, sizeof(h2), hipMemcpyDeviceToHost);
+        int diff = 0;
+        for (int i = 0; i < 512; ++i) {
+            const int r = (i & 255) / 16, c = i & 15;
+            const bool used = c <= r;  // lower triangles of L and of L^-1 (Dw[j][lane] = (L^-1)[j][lane])
+            if (used && memcmp(&h1[i], &h2[i], 8) != 0) ++diff;
+        }
+        printf("scheduled vs reference leaf: %d differing entries of L and L^-1 (bitwise)\n", diff);
+    }
     for (int r = 0; r < 2; ++r) {
         k_leaf_split<<<1, 128>>>(dA, out, clk, reps);
         long long c[2] = {0, 0};
