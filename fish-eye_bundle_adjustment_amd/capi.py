@@ -50,7 +50,7 @@ class Problem(C.Structure):
 
 class Options(C.Structure):
     _fields_ = [("device", C.c_int32), ("rank", C.c_int32), ("world", C.c_int32), ("verbose", C.c_int32),
-                ("stream", C.c_void_p)]
+                ("stream", C.c_void_p), ("split", C.c_int32)]
 
 
 def _load():
@@ -153,11 +153,12 @@ class Context:
     """One device-resident adjustment (one GPU / one rank)."""
 
     def __init__(self, packed: PackedProblem, settings: Settings, device=0, rank=0, world=1, stream=None,
-                 verbose=False):
+                 verbose=False, split=False):
         self.packed = packed
         self.settings = settings
         self.world = world
-        opts = Options(device, rank, world, int(verbose), stream)
+        self.split = bool(split) and world > 1
+        opts = Options(device, rank, world, int(verbose), stream, int(bool(split)))
         h = C.c_void_p()
         check(lib.fba_create(C.byref(packed.struct), C.byref(settings), C.byref(opts), C.byref(h)))
         self.h = h

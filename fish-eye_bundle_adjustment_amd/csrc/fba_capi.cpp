@@ -167,7 +167,7 @@ static void destroy(Ctx* c) {
                     c->d_acc, c->d_ppart, c->d_ipart, c->d_cpart, c->d_cseg, c->d_bscr, c->d_gblk, c->d_lrprof, c->d_ptrace, c->d_gpairs, c->d_red, c->d_xfull, c->d_xlin, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
                     c->d_pt_tab, c->d_P, c->d_flags, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
                     c->d_active, c->d_counted, c->d_obs_pho, c->d_sched, c->d_gpt, c->d_gcu, c->d_gug, c->d_xpart,
-                    c->d_kpart, c->d_dynargs};
+                    c->d_kpart, c->d_dynargs, c->d_bown, c->d_rown, c->d_topdiag};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     for (auto& w : c->ws)
@@ -227,9 +227,72 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     for (int64_t i = 0; i < (int64_t)L.cw * L.n_cam; ++i) c->xfull0[6 * (int64_t)L.n_img + i] = p->iop0[i];
     for (int64_t i = 0; i < 3 * (int64_t)L.n_tie; ++i) c->xfull0[L.u_c + i] = p->tie0[i];
 
+    // the co-visible image pairs of ALL tie points (identical on every rank): the compact reduce
+    // buffer of ranks > 1 and the block envelope of the reduced system
+    std::vector<std::pair<int32_t, int32_t>> gp;
+    {
+        std::vector<std::pair<int32_t, int32_t>> pi;  // (tie, internal image)
+        for (int64_t i = 0; i < p->n_pts; ++i)
+            if (p->tie[i] >= 0) pi.emplace_back(p->tie[i], c->img_new[p->img[i]]);
+        std::sort(pi.begin(), pi.end());
+        for (size_t a = 0; a < pi.size();) {
+            size_t b = a;
+            while (b < pi.size() && pi[b].first == pi[a].first) ++b;
+            for (size_t x = a; x < b; ++x)
+                for (size_t y = a; y < b; ++y)
+                    if (pi[x].second > pi[y].second) gp.emplace_back(pi[x].second, pi[y].second);
+            a = b;
+        }
+        std::sort(gp.begin(), gp.end());
+        gp.erase(std::unique(gp.begin(), gp.end()), gp.end());
+        // inner constraints: the border is applied on the first n_loc image slots only (local
+        // border, DESIGN.md section 2), so M keeps the sparsity of S
+        c->n_loc = s->inner_constraints ? std::min<int>(L.n_img, (int)(NB / 6)) : 0;
+        build_schedule(*c, gp);
+    }
+    const bool split = c->sched.split;
+
     // shard
     std::vector<int32_t> ctl_owner;
-    partition(p, opt.world, c->tie_owner, ctl_owner);
+    if (!split) {
+        partition(p, opt.world, c->tie_owner, ctl_owner);
+    } else {
+        // subtree split: a point's images lie on one root path of the elimination tree (every two of them
+        // share a block of S), so at most one rank's subtree: the point goes to that rank; points of top
+        // images only (and control observations of top images) go to the least loaded rank
+        const std::vector<int32_t>& br = c->sched.blk_rank;
+        auto img_rank = [&](int64_t e) {  // EXT image -> rank of its rows' subtree, or -1
+            const int64_t slot = c->img_new[e];
+            int r = -1;
+            for (int64_t blk = 6 * slot / NB; blk <= (6 * slot + 5) / NB; ++blk) r = std::max(r, (int)br[blk]);
+            return r;
+        };
+        std::vector<int64_t> load(opt.world, 0);
+        std::vector<int32_t> tr(L.n_tie, -1);
+        std::vector<int64_t> tcnt(L.n_tie, 0);
+        for (int64_t i = 0; i < p->n_pts; ++i)
+            if (p->tie[i] >= 0) {
+                tr[p->tie[i]] = std::max(tr[p->tie[i]], img_rank(p->img[i]));
+                tcnt[p->tie[i]]++;
+            }
+        c->tie_owner.assign(L.n_tie, 0);
+        for (int t = 0; t < L.n_tie; ++t)
+            if (tr[t] >= 0) { c->tie_owner[t] = tr[t]; load[tr[t]] += tcnt[t]; }
+        for (int t = 0; t < L.n_tie; ++t)
+            if (tr[t] < 0) {
+                const int r = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+                c->tie_owner[t] = r;
+                load[r] += tcnt[t];
+            }
+        ctl_owner.assign(p->n_pts, -1);
+        for (int64_t i = 0; i < p->n_pts; ++i)
+            if (p->tie[i] < 0) {
+                int r = img_rank(p->img[i]);
+                if (r < 0) r = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+                ctl_owner[i] = r;
+                load[r]++;
+            }
+    }
 
     // local tie points sorted by camera; their observations in PHO order
     std::vector<std::vector<int64_t>> tie_obs(L.n_tie);
@@ -613,43 +676,49 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     G.kt_start = put(kt_start);
     G.kt_list = put(kt_list);
     G.kt_key = put(kt_key);
-    // the co-visible image pairs of ALL tie points (identical on every rank): the compact reduce
-    // buffer of ranks > 1 and the block envelope of the reduced system
     std::vector<int32_t> gpairs;
-    {
-        std::vector<std::pair<int32_t, int32_t>> pi;  // (tie, internal image)
-        for (int64_t i = 0; i < p->n_pts; ++i)
-            if (p->tie[i] >= 0) pi.emplace_back(p->tie[i], c->img_new[p->img[i]]);
-        std::sort(pi.begin(), pi.end());
-        std::vector<std::pair<int32_t, int32_t>> gp;
-        for (size_t a = 0; a < pi.size();) {
-            size_t b = a;
-            while (b < pi.size() && pi[b].first == pi[a].first) ++b;
-            for (size_t x = a; x < b; ++x)
-                for (size_t y = a; y < b; ++y)
-                    if (pi[x].second > pi[y].second) gp.emplace_back(pi[x].second, pi[y].second);
-            a = b;
-        }
-        std::sort(gp.begin(), gp.end());
-        gp.erase(std::unique(gp.begin(), gp.end()), gp.end());
-        // inner constraints: the border is applied on the first n_loc image slots only (local
-        // border, DESIGN.md section 2), so M keeps the sparsity of S
-        c->n_loc = s->inner_constraints ? std::min<int>(L.n_img, (int)(NB / 6)) : 0;
-        build_schedule(*c, gp);
-        if (opt.world > 1) {
-            for (auto& q : gp) { gpairs.push_back(q.first); gpairs.push_back(q.second); }
-            c->n_gpairs = (int64_t)gp.size();
-            c->n_red = 36 * (c->n_gpairs + L.n_img) + (int64_t)L.cw * L.n_cam * L.n_pad + L.n_pad;
-        }
+    if (opt.world > 1 && !split) {
+        for (auto& q : gp) { gpairs.push_back(q.first); gpairs.push_back(q.second); }
+        c->n_gpairs = (int64_t)gp.size();
+        c->n_red = 36 * (c->n_gpairs + L.n_img) + (int64_t)L.cw * L.n_cam * L.n_pad + L.n_pad;
     }
-
+    // subtree split: the reduce buffer's layout (k_pack_split) and the per-block roles
+    std::vector<int8_t> bown, rown;
+    std::vector<int32_t> topdiag;
+    if (split) {
+        const Sched& sc = c->sched;
+        const int64_t nb = L.n_pad / NB;
+        bown.assign(nb, 0);
+        for (int64_t k = 0; k < nb; ++k) bown[k] = sc.blk_rank[k] < 0 ? 2 : (sc.blk_rank[k] == opt.rank ? 1 : 0);
+        rown.assign(L.n_pad, 0);
+        for (int64_t i = 0; i < L.n_pad; ++i) {
+            rown[i] = bown[i / NB];
+            if (i < 6 * (int64_t)L.n_img && c->img_ord[i / 6] >= 0) {
+                int r = -1;  // the rank of the image's subtree (any of its rows in one), -1 wholly top
+                for (int64_t blk = 6 * (i / 6) / NB; blk <= (6 * (i / 6) + 5) / NB; ++blk) r = std::max(r, (int)sc.blk_rank[blk]);
+                rown[i] = r < 0 ? 2 : (r == opt.rank ? 1 : 0);
+            }
+        }
+        int64_t n = 0, ng = 0;
+        for (int q = 0; q < sc.n_top_blocks; ++q) n += (int64_t)(sc.buf[sc.top_blocks + 2 * q] == nb ? L.nrhs : NB) * NB;
+        for (int64_t i = 0; i < 6 * (int64_t)L.n_img; ++i)
+            if (rown[i] == 2) topdiag.push_back((int32_t)i);
+        for (int64_t k = 0; k < nb; ++k) ng += bown[k] != 2;
+        c->n_topdiag = (int64_t)topdiag.size();
+        c->red_diag = n;
+        c->red_gblk = c->red_diag + c->n_topdiag;
+        c->red_w = c->red_gblk + 256 * ng;
+        c->n_red = c->red_w + 8;
+    }
     // which full-space entries are estimated / owned / counted
     std::vector<uint8_t> active(L.n_pad, 0), counted(L.u_full, 0);
     c->full_owned.assign(L.u_full, 0);
     for (int64_t i = 0; i < L.u_c; ++i) {
         active[i] = c->full_to_ref[i] >= 0 ? 1 : 0;
-        counted[i] = (opt.rank == 0 && active[i]) ? 1 : 0;
-        c->full_owned[i] = opt.rank == 0 ? 1 : 0;
+        // (split: this rank's subtree rows, and the top rows on rank 0)
+        const bool mine = split ? (bown[i / NB] == 1 || (bown[i / NB] == 2 && opt.rank == 0)) : opt.rank == 0;
+        counted[i] = (mine && active[i]) ? 1 : 0;
+        c->full_owned[i] = mine ? 1 : 0;
     }
     for (int t = 0; t < L.n_tie; ++t)
         for (int m = 0; m < 3; ++m) {
@@ -680,7 +749,9 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         (rc = upload(&c->d_counted, counted)) || (rc = upload(&c->d_obs_pho, pho)) ||
         (rc = upload(&c->d_chunk_obs, chunk_obs)) || (rc = upload(&c->d_chunk_pt, chunk_pt)) ||
         (rc = upload(&c->d_sched, c->sched.buf)) ||
-        (opt.world > 1 && ((rc = upload(&c->d_gpairs, gpairs)) || (rc = dalloc(&c->d_red, (size_t)c->n_red))))) {
+        (opt.world > 1 && !split && ((rc = upload(&c->d_gpairs, gpairs)) || (rc = dalloc(&c->d_red, (size_t)c->n_red)))) ||
+        (split && ((rc = upload(&c->d_bown, bown)) || (rc = upload(&c->d_rown, rown)) || (rc = upload(&c->d_topdiag, topdiag)) ||
+                   (rc = dalloc(&c->d_red, (size_t)c->n_red))))) {
         destroy(c);
         return rc;
     }
@@ -702,7 +773,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         (rc = dalloc(&c->d_gug, (size_t)G.n_gi * 36)) || (rc = dalloc(&c->d_xpart, (size_t)G.n_gx * 6 * L.cw)) ||
         (rc = dalloc(&c->d_kpart, (size_t)G.n_gkk * L.cw * L.cw)) ||
         (rc = dalloc(&c->d_cseg, (size_t)std::max(L.n_cam, 1) * 64 * npk)) ||
-        (rc = dalloc(&c->d_bscr, (size_t)(32 * 14 + 16 * 120 + 16))) ||  // k_border_weights / k_border_gram segments, combine coefficients
+        (rc = dalloc(&c->d_bscr, (size_t)(BSC_OFF + 16))) ||  // k_border_weights / k_border_gram segments, combine coefficients, split scales
         (rc = dalloc(&c->d_gblk, (size_t)(L.n_pad / NB) * 256)) ||
         (rc = dalloc(&c->d_S, (size_t)(L.n_pad + NB) * L.ld)) ||
         (rc = dalloc(&c->d_P, (size_t)std::max(c->sched.n_scratch, 1) * 4096)) || (rc = dalloc(&c->d_X, (size_t)L.n_pad)) ||
@@ -821,7 +892,16 @@ static int accumulate_body(Ctx* c) {
         fprintf(stderr, "[fba] k_lin_reduce per chunk (us): model %.2f points %.2f couplings %.2f stage+camera %.2f "
                 "image keys %.2f pair keys %.2f; span %.1f\n", ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], (double)(hi - lo) * 0.01);
     }
-    if (c->opt.world > 1 && (rc = launch_pack(*c, 0))) return rc;
+    if (c->sched.split) {
+        // subtree split: the top rows' accumulated diagonal (before k_border_rhs writes unit rows), the
+        // border rows, this rank's subtree columns (flow A: their factor, forward solve and Schur updates of
+        // the top blocks), then the buffer
+        if ((rc = launch_pack_split(*c, 2)) || (rc = launch_border(*c)) || (rc = launch_cholesky(*c, 0)) ||
+            (rc = launch_pack_split(*c, 0)))
+            return rc;
+    } else if (c->opt.world > 1 && (rc = launch_pack(*c, 0))) {
+        return rc;
+    }
     mark(c, 3);
     return FBA_OK;
 }
@@ -836,10 +916,16 @@ static int accumulate(Ctx* c) {
 static int solve_body(Ctx* c) {
     int rc;
     const Layout& L = c->L;
-    if (c->opt.world > 1 && (rc = launch_pack(*c, 1))) return rc;
-    if ((rc = launch_border(*c))) return rc;
-    mark(c, 4);
-    if ((rc = launch_cholesky(*c))) return rc;
+    if (c->sched.split) {  // the summed top blocks (+ the B rows' weights), then the top columns (flow B)
+        if ((rc = launch_pack_split(*c, 1))) return rc;
+        mark(c, 4);
+        if ((rc = launch_cholesky(*c, 1))) return rc;
+    } else {
+        if (c->opt.world > 1 && (rc = launch_pack(*c, 1))) return rc;
+        if ((rc = launch_border(*c))) return rc;
+        mark(c, 4);
+        if ((rc = launch_cholesky(*c))) return rc;
+    }
     mark(c, 5);
     // tie-point corrections of other ranks' points stay zero (a single rank writes every one of them in
     // k_backsub; a zero-byte memset is not a valid graph node)
@@ -1032,7 +1118,13 @@ static int solve_finish(Ctx* c, double* dsum, bool recopy) {
         if (q != hipSuccess && q != hipErrorNotReady) FBA_HIP(q);
     }
     c->solve_seq = c->h_pinned[4];
-    if (c->d_ptrace) print_panel_trace(c);
+    if (c->d_ptrace && !c->sched.split) print_panel_trace(c);
+    if (getenv("FBA_DEBUG_WEIGHTS")) {  // (diagnostic) the inner-constraint weights W_l, W_d of this solve
+        double w[24];
+        if (hipMemcpy(w, c->d_scal, sizeof w, hipMemcpyDeviceToHost) == hipSuccess)
+            fprintf(stderr, "[fba] rank %d weights W_l %.17g %.17g %.17g W_d %.17g %.17g %.17g %.17g\n", c->opt.rank, w[8], w[9],
+                    w[14], w[16], w[17], w[18], w[22]);
+    }
     if (c->timing) {
         float ms;
         for (int i = 0; i < 7; ++i) {
@@ -1364,6 +1456,10 @@ int fba_covariance(fba_ctx* ctx, double sigma02, double* cx_diag, double* corr) 
     if (!c->have_factor || !c->have_delta) {
         set_error("fba_covariance needs the factor of the last solve (call it once, right after the iterations)");
         return FBA_ERR_ARG;
+    }
+    if (c->sched.split) {
+        set_error("fba_covariance: a subtree-split context holds only its own subtrees' factor");
+        return FBA_ERR_UNSUPPORTED;
     }
     const Layout& L = c->L;
     const int m = 6 + L.cw;

@@ -1442,8 +1442,12 @@ __global__ __launch_bounds__(256) void k_border_gram(const double* __restrict__ 
 // gblk != nullptr: the Gram comes as nblk per-column-block 16x16 partials (k_chol_flow's RHS panel
 // halves, row-major, rows/columns 15 zero), added in block order instead of the GRAM_SEG segments
 // the 14 coefficients into coef[] (LDS, 256 threads; g: 15 x 15 LDS scratch); ends with a barrier
+// bsc (subtree split): the B rows were forward-solved unscaled; their Gram entries take the factors
+// sqrt(W_d) here (rows / columns 8..14) and so do the B coefficients handed on, so u = y + A z + B (bsc k)
+// is the one-GPU combine's y + A z + (B bsc) k
 __device__ __forceinline__ void border_combine_body(const double* __restrict__ gpart, const double* __restrict__ gblk,
-                                                    int nblk, double (*g)[15], double* coef) {
+                                                    int nblk, double (*g)[15], double* coef,
+                                                    const double* __restrict__ bsc = nullptr) {
     const int tid = threadIdx.x;
     if (tid < 120) {
         int a = 0, rem = tid;
@@ -1466,6 +1470,7 @@ __device__ __forceinline__ void border_combine_body(const double* __restrict__ g
 #pragma unroll
             for (int q = 0; q < GRAM_SEG; ++q) v += x[q];
         }
+        if (bsc) v *= (a >= 8 ? bsc[a - 8] : 1.0) * (b >= 8 ? bsc[b - 8] : 1.0);
         g[a][b] = g[b][a] = v;
     }
     __syncthreads();
@@ -1525,7 +1530,7 @@ __device__ __forceinline__ void border_combine_body(const double* __restrict__ g
             double mine = c[0];
 #pragma unroll
             for (int q = 1; q < 14; ++q) mine = (tid == q) ? c[q] : mine;
-            coef[tid] = mine;
+            coef[tid] = (bsc && tid >= 7) ? mine * bsc[tid - 7] : mine;
         }
     }
     __syncthreads();
@@ -2751,7 +2756,8 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
                                                   unsigned* __restrict__ flags, double* __restrict__ scal,
                                                   double* __restrict__ coef, int combine,
                                                   const double* __restrict__ gpart, const double* __restrict__ gblk, int nblk,
-                                                  unsigned* __restrict__ ticket) {
+                                                  unsigned* __restrict__ ticket, const int8_t* __restrict__ bown,
+                                                  const double* __restrict__ bsc) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* Li = smem;              // [128][128] Linv_j, or L_jj for a root column
     double* Dt = Li + CB * CB;      // [8][16][16] the leaf inverses of a root column
@@ -2773,7 +2779,7 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
     const int tk = s_ticket;
     if (tk < 0) return;
     if (combine && tk == 0) {  // the border combine workgroup
-        border_combine_body(gpart, gblk, nblk, reinterpret_cast<double (*)[15]>(Li), cs);
+        border_combine_body(gpart, gblk, nblk, reinterpret_cast<double (*)[15]>(Li), cs, bsc);
         if (tid < 14) {
             const __amdgpu_buffer_rsrc_t rc = block_rsrc(coef, 16 * 8);
             st_sc1(rc, (int64_t)tid * 8, cs[tid]);
@@ -2784,6 +2790,8 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
         return;
     }
     const int j = nb - 1 - (tk - combine);
+    // (subtree split: another rank's subtree column -- nothing of this rank depends on it)
+    if (bown && bown[j] == 0) return;
     const int c2 = tid & 63, h = tid >> 6;  // gemv_t128's thread map: columns 2 c2 + {0,1}, rows 32 h ..
     // a root of the elimination tree (no source blocks: the top level) is solved by substitution with
     // its factor and leaf inverses, so its Linv (k_trtri128, 30 us) is off the critical path
@@ -2921,9 +2929,24 @@ __global__ void k_neg_copy(const double* __restrict__ X, double* __restrict__ de
 // the panel solves of their columns (RHS block row included: the forward solve), the trailing
 // updates they cause.  Three launches per level on one stream.
 // ------------------------------------------------------------------------------------------------
-int launch_cholesky(Ctx& c) {
+// part (subtree split): 0 = this rank's subtree columns (flow A), 1 = the top columns (flow B, its
+// flag / counter / scratch ids after flow A's, its own start ticket)
+int launch_cholesky(Ctx& c, int part) {
     const int64_t ld = c.L.ld;
     const Sched& s = c.sched;
+    if (s.split) {
+        const Sched::FlowPart& T = s.top;
+        const bool b = part == 1;
+        const int n = b ? T.n : s.flow_n;
+        if (n == 0) return FBA_OK;
+        const int64_t fo = b ? s.flow_nprog + s.flow_nuflag : 0, co = b ? s.flow_ncounter : 0, so = b ? s.flow_nscratch : 0;
+        k_chol_flow<<<(unsigned)n, POTRF_THREADS, FLOW_LDS, c.stream>>>(
+            c.d_S, ld, c.d_sched, c.d_sched + (b ? T.rec : s.flow_rec), c.d_dinv, c.d_linv, c.d_scal, c.d_flags,
+            c.d_tflags + fo, c.d_counters + co, c.d_P + so * 4096, nullptr, c.set.inner_constraints ? c.d_gblk : nullptr,
+            c.d_tickets + (b ? 2 : 0), nullptr);
+        FBA_HIP(hipGetLastError());
+        return FBA_OK;
+    }
     if (c.chol_flow && s.flow_ok && s.flow_n > 0) {
         // the whole factorisation + forward solve in one persistent launch (flags zeroed by k_border_rhs)
         const bool pp = c.probe == 2 && c.probe_n < (int)c.probe_ev.size() / 2;
@@ -3058,7 +3081,7 @@ int launch_backward(Ctx& c) {
     const int64_t nb = c.L.n_pad / CB;
     const bool flow = c.bwd_flow;  // (ticket-ordered roles: no co-residency requirement)
     double* coef = c.d_bscr + 32 * 14 + 16 * 120;
-    const bool gblk = c.chol_flow && s.flow_ok && s.flow_n > 0;
+    const bool gblk = c.chol_flow && s.flow_ok && (s.flow_n > 0 || s.split);
     // the combine inside k_bwd_flow (one more workgroup) when the Gram comes from k_chol_flow
     const int combine = (c.set.inner_constraints && flow && gblk) ? 1 : 0;
     if (c.set.inner_constraints && !combine) {
@@ -3078,7 +3101,8 @@ int launch_backward(Ctx& c) {
         k_bwd_flow<<<(unsigned)(nb + combine), 256, BWD_LDS, c.stream>>>(
             c.d_S, ld, c.L.n_pad, c.d_linv, c.d_dinv, c.d_X, c.d_delta, c.L.u_c, c.d_sched + s.bf_start,
             c.d_sched + s.bf_src, c.d_bflags, c.d_scal, c.set.inner_constraints ? coef : nullptr, combine,
-            c.d_bscr + 32 * 14, c.d_gblk, (int)nb, c.d_tickets + 1);
+            c.d_bscr + 32 * 14, c.d_gblk, (int)nb, c.d_tickets + 1, s.split ? c.d_bown : nullptr,
+            s.split ? c.d_bscr + BSC_OFF : nullptr);
         FBA_HIP(hipGetLastError());
         return FBA_OK;
     }
@@ -3116,14 +3140,18 @@ int chol_setup(Ctx& c) {
     // 519 / 515 / 559 us vs 466 us static -- the static order's level priorities beat FIFO-of-ready dispatch
     c.flow_dyn = getenv("FBA_FLOW_DYN") && atoi(getenv("FBA_FLOW_DYN")) != 0 && c.sched.flow_dyn_n > 0;
     const int64_t ndyn = c.flow_dyn ? 2 * (int64_t)c.sched.flow_dyn_n + 2 : 0;
-    c.n_sync = (int64_t)(2 * nf + std::max(c.sched.n_counters, 1) + std::max(c.sched.n_tflags, 1) + 2) + ndyn;
+    c.n_sync = (int64_t)(2 * nf + std::max(c.sched.n_counters, 1) + std::max(c.sched.n_tflags, 1) + 3) + ndyn;
     FBA_HIP(hipMalloc((void**)&c.d_flags, sizeof(unsigned) * c.n_sync));
     FBA_HIP(hipMemset(c.d_flags, 0, sizeof(unsigned) * c.n_sync));
     c.d_bflags = c.d_flags + nf;
     c.d_counters = c.d_bflags + nf;
     c.d_tflags = c.d_counters + std::max(c.sched.n_counters, 1);
     c.d_tickets = c.d_tflags + std::max(c.sched.n_tflags, 1);
-    c.d_dyn = c.flow_dyn ? c.d_tickets + 2 : nullptr;
+    c.d_dyn = c.flow_dyn ? c.d_tickets + 3 : nullptr;
+    if (c.sched.split && (!c.chol_flow || c.flow_dyn || !c.sched.flow_ok || !c.sched.top.ok)) {
+        set_error("subtree split needs the static-order k_chol_flow schedule (FBA_CHOL_FLOW / FBA_FLOW_DYN unset)");
+        return FBA_ERR_UNSUPPORTED;
+    }
     if (c.flow_dyn) {  // the dispatch state's addresses, uploaded once
         FlowDyn dy{};
         dy.info = c.d_sched + c.sched.flow_dyn_info;

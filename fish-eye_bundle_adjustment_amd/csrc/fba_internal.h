@@ -36,6 +36,9 @@ constexpr int chunk_terms(int nk) { return nk <= 5 ? 2048 : 1024; }
 constexpr int IMG_TAB = 48;
 // per-camera device table: xp yp c ydir P1 P2 rmax2 pad, K[nK], scale[nK] (rmax^(2j))
 constexpr int CAM_TAB_HDR = 8;
+// d_bscr: [32][14] k_border_weights segments | [16][120] Gram segments | [16] combine coefficients |
+// [16] the subtree split's B-row scales sqrt(W_d)
+constexpr int BSC_OFF = 32 * 14 + 16 * 120 + 16;
 
 struct Layout {
     int n_img = 0, n_cam = 0, n_tie = 0, nk = 1, cw = 6;  // n_img: internal image slots (padding included)
@@ -104,6 +107,25 @@ struct Sched {
     // start consumers, done consumers, 0, 0, 0], the consumer lists, the records ready at launch
     int flow_dyn_n = 0, flow_dyn_ninit = 0;
     int64_t flow_dyn_info = 0, flow_dyn_cons = 0, flow_dyn_init = 0;
+
+    // subtree split (fba_options.split, world > 1): the elimination tree is cut into a TOP part (the
+    // columns above the cut: separators, camera rows) and subtrees dealt to the ranks.  A rank's points
+    // touch only its own subtrees' blocks and the top, so its subtree columns are factored from its own
+    // accumulation alone -- flow A, the flow_* fields above -- Schur-updating its partial copy of the top
+    // blocks; the ranks sum the top blocks (the reduce buffer), then every rank factors the top columns:
+    // flow B (`top`), whose flag, counter and scratch ids follow flow A's (offsets below).
+    struct FlowPart {
+        int64_t rec = 0;
+        int n = 0, nprog = 0, nuflag = 0, ncounter = 0, nscratch = 0;
+        int cnt[5] = {0, 0, 0, 0, 0};
+        bool ok = false;
+        double flops = 0.0;
+    };
+    bool split = false;
+    FlowPart top;
+    std::vector<int32_t> blk_rank;   // per block column: owner rank of its subtree, -1 top
+    int64_t top_blocks = 0;          // offset of the (block row, block column) list of the top blocks
+    int n_top_blocks = 0;            // (lower blocks (a, b) with a, b top, the RHS block row's included)
 };
 
 // Accumulation plan (fba_capi.cpp create, run by k_lin_reduce and the k_red_* kernels): offsets
@@ -217,6 +239,17 @@ struct Ctx {
     // multi-rank compact reduce buffer: the entries of S that any rank can write (global co-visible
     // image pairs, diagonal blocks, camera rows, RHS row), packed after fba_accumulate
     int64_t n_gpairs = 0, n_red = 0;
+    // subtree split (Sched::split): the reduce buffer holds [top blocks | the raw diagonal of the top rows
+    // | Gram partials of the subtree columns | this rank's 7 inner-constraint weight sums]; offsets
+    int64_t red_diag = 0, red_gblk = 0, red_w = 0;
+    int8_t* d_bown = nullptr;        // [nb] 1: this rank's subtree block, 2: top, 0: another rank's
+    // [n_pad] per camera-side row, by its IMAGE: 1 an image of this rank's subtrees (its rows in a top block
+    // included -- an image straddling a subtree block and a top block has its other EOPs, which its G rows
+    // read, current on its subtree's rank only), 2 an image wholly in the top (and top camera / padding
+    // rows), 0 another rank's; the once-only border entries, the weight sums and the top diagonal follow it
+    int8_t* d_rown = nullptr;
+    int32_t* d_topdiag = nullptr;    // [n_topdiag] rows of the top blocks carrying image unknowns
+    int64_t n_topdiag = 0;
     // camera-side image order (nested dissection, fba_order.cpp) and the factorisation schedule
     std::vector<int32_t> img_ord, img_new;  // internal slot -> EXT row (-1: padding), EXT row -> slot
     int n_loc = 0;                          // image slots carrying the (local) inner-constraint border
@@ -349,7 +382,9 @@ int launch_border(Ctx& c);       // alpha, G G^T border, RHS rows
 int chol_setup(Ctx& c);
 int acc_setup(Ctx& c);            // kernel attributes of the accumulation kernels          // one-time kernel attributes, streams, events
 int launch_pack(Ctx& c, int dir);  // multi-rank compact reduce buffer: 0 = S -> buffer, 1 = buffer -> S
-int launch_cholesky(Ctx& c);     // factor + forward solve of RHS rows
+int launch_cholesky(Ctx& c, int part = 0);  // factor + forward solve of RHS rows (split: 0 subtrees, 1 top)
+int launch_pack_split(Ctx& c, int dir);      // subtree split's reduce buffer: 0 pack, 1 unpack + weights,
+                                             // 2 the top rows' accumulated diagonal
 int launch_backward(Ctx& c);     // border combine + backward solve -> delta_c
 int launch_backsub_update(Ctx& c);
 int launch_residuals(Ctx& c);    // v per obs, partial sums

@@ -1009,9 +1009,11 @@ __global__ __launch_bounds__(128) void k_red_cam(const double* __restrict__ cseg
 // EOP rows -> part[seg][14]; the consumer (k_border_rhs) adds the segments in order
 constexpr int BW_SEG = 32;
 
+// rown (subtree split, per row): the weight sums over all images (7..13) take only this rank's images'
+// rows -- a wholly-top image's diagonal is complete only after the ranks' sum (k_split_weights adds them)
 __global__ __launch_bounds__(256) void k_border_weights(const double* __restrict__ S, const double* __restrict__ G,
                                                         double* __restrict__ scal, double* __restrict__ part, int64_t ld,
-                                                        int n_img, int n_loc, int ic) {
+                                                        int n_img, int n_loc, int ic, const int8_t* __restrict__ rown) {
     __shared__ double red[4][14];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int64_t n = 6 * (int64_t)n_img;
@@ -1023,12 +1025,12 @@ __global__ __launch_bounds__(256) void k_border_weights(const double* __restrict
         for (int64_t i = i0 + tid; i < i1; i += 256) {
             const double sii = S[i * ld + i];
             const double* g = G + (i / 6) * 42 + (i % 6) * 7;
-            const bool ok = sii > 0.0, loc = i < 6 * (int64_t)n_loc;
+            const bool ok = sii > 0.0, loc = i < 6 * (int64_t)n_loc, all = !rown || rown[i] == 1;
             const double inv = ok ? 1.0 / sii : 0.0;
 #pragma unroll
             for (int m = 0; m < 7; ++m) {
                 const double v = g[m] * g[m] * inv;
-                a[7 + m] += v;
+                if (all) a[7 + m] += v;
                 if (loc) a[m] += v;
             }
         }
@@ -1067,11 +1069,15 @@ __device__ __forceinline__ void border_weights_lds(const double* __restrict__ pa
 //   workgroups [nbr, ..): one thread per row i of S: unit row for fixed parameters and padding, the
 //                        border's RHS rows A = G_l W_l^1/2 and B = G D; the hand-off flags and counters
 //                        of the factorisation / backward solve zeroed
+// rown (subtree split): the B rows unscaled (k_split_weights' scales enter the border combine), and the
+// unit diagonal and B entries of a wholly-top image's row written by rank 0 only, of an image of a rank's
+// subtree by that rank (the ranks' top blocks are summed)
 __global__ __launch_bounds__(256) void k_border_rhs(double* __restrict__ S, const double* __restrict__ G,
                                                     double* __restrict__ scal, const double* __restrict__ part,
                                                     const uint8_t* __restrict__ active, int64_t ld, int64_t n_pad,
                                                     int64_t u_c, int n_img, int n_loc, int ic, int nbr,
-                                                    unsigned* __restrict__ sync, int64_t n_sync, double* __restrict__ X) {
+                                                    unsigned* __restrict__ sync, int64_t n_sync, double* __restrict__ X,
+                                                    const int8_t* __restrict__ rown, int rank) {
     __shared__ double w[14];
     if (ic) border_weights_lds(part, w);
     if ((int)blockIdx.x < nbr) {
@@ -1097,16 +1103,18 @@ __global__ __launch_bounds__(256) void k_border_rhs(double* __restrict__ S, cons
     if (ic && blockIdx.x == nbr && threadIdx.x < 14) scal[8 + (threadIdx.x / 7) * 8 + threadIdx.x % 7] = w[threadIdx.x];
     if (i >= n_pad) return;
     X[i] = __builtin_bit_cast(double, X_SENTINEL);  // k_bwd_flow's solution blocks: not yet published
+    // (split: a wholly-top row's once-only entries on rank 0; another rank's rows are never read here)
+    const bool once = !rown || rown[i] == 1 || (rown[i] == 2 && rank == 0);
     if (i >= u_c || !active[i]) {
         // fixed parameter or padding: decoupled unit row, zero RHS
-        S[i * ld + i] = 1.0;
+        S[i * ld + i] = once ? 1.0 : 0.0;
         S[n_pad * ld + i] = 0.0;
     }
     if (ic) {
         const double* g = G + (i / 6) * 42 + (i % 6) * 7;
         for (int m = 0; m < 7; ++m) {
-            S[(n_pad + 1 + m) * ld + i] = (i < 6 * (int64_t)n_loc) ? sqrt(w[m]) * g[m] : 0.0;      // A
-            S[(n_pad + 8 + m) * ld + i] = (i < 6 * (int64_t)n_img) ? sqrt(w[7 + m]) * g[m] : 0.0;  // B
+            S[(n_pad + 1 + m) * ld + i] = (i < 6 * (int64_t)n_loc) ? sqrt(w[m]) * g[m] : 0.0;  // A
+            S[(n_pad + 8 + m) * ld + i] = (i < 6 * (int64_t)n_img && once) ? (rown ? g[m] : sqrt(w[7 + m]) * g[m]) : 0.0;  // B
         }
     }
 }
@@ -1486,12 +1494,13 @@ int acc_setup(Ctx& c) {
 int launch_border(Ctx& c) {
     const Layout& L = c.L;
     const int ic = c.set.inner_constraints;
-    k_border_weights<<<BW_SEG, 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, c.d_bscr, L.ld, L.n_img, c.n_loc, ic);
+    const int8_t* rown = c.sched.split ? c.d_rown : nullptr;
+    k_border_weights<<<BW_SEG, 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, c.d_bscr, L.ld, L.n_img, c.n_loc, ic, rown);
     FBA_HIP(hipGetLastError());
     const int nbr = (ic && c.n_loc > 0) ? 6 * c.n_loc : 0;
     k_border_rhs<<<(unsigned)(nbr + (L.n_pad + 255) / 256), 256, 0, c.stream>>>(
         c.d_S, c.d_G, c.d_scal, c.d_bscr, c.d_active, L.ld, L.n_pad, L.u_c, L.n_img, c.n_loc, ic, nbr, c.d_flags,
-        c.n_sync, c.d_X);
+        c.n_sync, c.d_X, rown, c.opt.rank);
     FBA_HIP(hipGetLastError());
     return FBA_OK;
 }
@@ -1572,6 +1581,107 @@ __global__ void k_pack(double* __restrict__ S, int64_t ld, double* __restrict__ 
         if (dir == 0) red[q] = S[pos];
         else S[pos] = red[q];
     }
+}
+
+// Subtree split: the reduce buffer (fba_reduce_buffer) is
+//   [top blocks: 128 x 128 each, row-major, an RHS block row's its nrhs rows only]
+//   [the accumulated diagonal of the top rows carrying image unknowns, packed before the subtree flow]
+//   [Gram partials (16 x 16) of every non-top block column: this rank's own, zeros for the others']
+//   [this rank's 7 inner-constraint weight sums over its subtree rows (k_border_weights' segments)]
+// dir 0: S (+ gblk, weight segments) -> buffer; dir 1: buffer -> S top blocks, gblk.  (The diagonal part
+// is written by k_pack_topdiag ahead of the subtree flow.)
+__global__ __launch_bounds__(256) void k_pack_split(double* __restrict__ S, int64_t ld, double* __restrict__ red,
+                                                    const int32_t* __restrict__ tb, int ntb, int64_t n_pad, int nrhs,
+                                                    double* __restrict__ gblk, const int8_t* __restrict__ bown, int nb,
+                                                    int64_t red_gblk, int64_t red_w, const double* __restrict__ wseg, int dir) {
+    const int q = blockIdx.x;
+    if (q < ntb) {  // one top block per workgroup
+        const int64_t a = tb[2 * q], b = tb[2 * q + 1];
+        const int rows = a * 128 == n_pad ? nrhs : 128;
+        int64_t off = 0;  // blocks before q: 128 rows each except RHS blocks
+        for (int x = 0; x < q; ++x) off += (int64_t)(tb[2 * x] * 128 == n_pad ? nrhs : 128) * 128;
+        double2* R = reinterpret_cast<double2*>(red + off);
+        for (int e = threadIdx.x; e < rows * 64; e += 256) {
+            const int r = e >> 6, c2 = (e & 63) * 2;
+            double2* Sp = reinterpret_cast<double2*>(S + (a * 128 + r) * ld + b * 128 + c2);
+            if (dir == 0) R[e] = *Sp;
+            else *Sp = R[e];
+        }
+        return;
+    }
+    if (q == ntb) {  // the Gram partials of the non-top columns, and the weight sums
+        int g = 0;
+        for (int k = 0; k < nb; ++k) {
+            if (bown[k] == 2) continue;
+            for (int e = threadIdx.x; e < 256; e += 256) {
+                if (dir == 0) red[red_gblk + 256 * (int64_t)g + e] = bown[k] == 1 ? gblk[256 * (int64_t)k + e] : 0.0;
+                else gblk[256 * (int64_t)k + e] = red[red_gblk + 256 * (int64_t)g + e];
+            }
+            ++g;
+        }
+        if (dir == 0 && threadIdx.x < 7) {
+            double v = 0.0;
+            for (int sg = 0; sg < 32; ++sg) v += wseg[sg * 14 + 7 + threadIdx.x];  // (BW_SEG segments)
+            red[red_w + threadIdx.x] = v;
+        }
+    }
+}
+
+// the accumulated diagonal of the top image rows (before the subtree flow updates them) -> buffer
+__global__ void k_pack_topdiag(const double* __restrict__ S, int64_t ld, const int32_t* __restrict__ rows, int64_t n,
+                               double* __restrict__ out) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n) out[q] = S[(int64_t)rows[q] * ld + rows[q]];
+}
+
+// after the ranks' sum: the 7 weights of the B rows, W_d = 1 / (sum over every image row of g^2 / s_ii)
+// = 1 / (the ranks' subtree sums + the top rows' part from the summed diagonal), as k_border_weights
+// forms them on one GPU; the border combine scales the B rows' Gram by sqrt(W_d) (bsc) and the
+// coefficients it hands the backward solve by the same factors
+__global__ __launch_bounds__(256) void k_split_weights(const double* __restrict__ red, int64_t red_diag, int64_t red_w,
+                                                       const int32_t* __restrict__ rows, int64_t n, const double* __restrict__ G,
+                                                       double* __restrict__ bsc, double* __restrict__ scal) {
+    __shared__ double part[256][7];
+    double a[7] = {0, 0, 0, 0, 0, 0, 0};
+    for (int64_t q = threadIdx.x; q < n; q += 256) {
+        const int64_t i = rows[q];
+        const double sii = red[red_diag + q];
+        const double inv = sii > 0.0 ? 1.0 / sii : 0.0;
+        const double* g = G + (i / 6) * 42 + (i % 6) * 7;
+#pragma unroll
+        for (int m = 0; m < 7; ++m) a[m] += g[m] * g[m] * inv;
+    }
+#pragma unroll
+    for (int m = 0; m < 7; ++m) part[threadIdx.x][m] = a[m];
+    __syncthreads();
+    if (threadIdx.x < 7) {
+        double v = red[red_w + threadIdx.x];
+        for (int t = 0; t < 256; ++t) v += part[t][threadIdx.x];
+        const double w = v > 0.0 ? 1.0 / v : 1.0;
+        bsc[threadIdx.x] = sqrt(w);
+        scal[16 + threadIdx.x] = w;
+    }
+}
+
+int launch_pack_split(Ctx& c, int dir) {
+    const Sched& s = c.sched;
+    if (dir == 2) {  // the top rows' accumulated diagonal
+        if (c.n_topdiag > 0)
+            k_pack_topdiag<<<(unsigned)((c.n_topdiag + 255) / 256), 256, 0, c.stream>>>(c.d_S, c.L.ld, c.d_topdiag, c.n_topdiag,
+                                                                                     c.d_red + c.red_diag);
+        FBA_HIP(hipGetLastError());
+        return FBA_OK;
+    }
+    k_pack_split<<<(unsigned)(s.n_top_blocks + 1), 256, 0, c.stream>>>(
+        c.d_S, c.L.ld, c.d_red, c.d_sched + s.top_blocks, s.n_top_blocks, c.L.n_pad, c.L.nrhs, c.d_gblk, c.d_bown,
+        (int)(c.L.n_pad / 128), c.red_gblk, c.red_w, c.d_bscr, dir);
+    FBA_HIP(hipGetLastError());
+    if (dir == 1 && c.set.inner_constraints) {
+        k_split_weights<<<1, 256, 0, c.stream>>>(c.d_red, c.red_diag, c.red_w, c.d_topdiag, c.n_topdiag, c.d_G,
+                                                 c.d_bscr + BSC_OFF, c.d_scal);
+        FBA_HIP(hipGetLastError());
+    }
+    return FBA_OK;
 }
 
 int launch_pack(Ctx& c, int dir) {

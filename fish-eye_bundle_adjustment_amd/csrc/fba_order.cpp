@@ -418,9 +418,12 @@ std::vector<int32_t> camera_order(const fba_problem* p) {
 // the smallest (level of need, role rank): diagonal blocks first (each placed right after the last
 // record it waits for), then panel halves, the updates feeding the next level, the others, inverses.
 // Every wait points to an earlier record, so in-order dispatch always progresses (checked here).
+// inc (subtree split): the block columns whose records this flow holds -- their diagonal blocks,
+// panel halves and inverses, and the updates they source, whatever the target; nullptr: every column
 static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<std::vector<int32_t>>& R,
                        const std::vector<int32_t>& level, int64_t nb, const std::function<int64_t(int64_t)>& real_rows,
-                       bool verbose) {
+                       bool verbose, const std::vector<char>* inc = nullptr) {
+    auto in = [&](int64_t k) { return !inc || (*inc)[k] != 0; };
     constexpr int REC = Sched::FLOW_REC, CB_BLOCKS = NB / 16, IB_BLOCK = 16;
     // sources per update task (FBA_FLOW_SPLIT; a target quarter's sources of one level are split into
     // groups of at most SPLIT, summed through scratch partials when there are several groups); config 4
@@ -431,12 +434,13 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     std::vector<std::vector<int32_t>> srcs(nb);
     for (int64_t k = 0; k < nb; ++k)
         for (int32_t i : R[k])
-            if (i < nb) srcs[i].push_back((int32_t)k);
+            if (i < nb && in(k)) srcs[i].push_back((int32_t)k);
     std::vector<int32_t> fsrc(nb, -1);
     // FBA_FLOW_FUSE=0: no fused sources (every diagonal update by update tasks; the potrf loads its block)
     static const bool fuse = !(getenv("FBA_FLOW_FUSE") && atoi(getenv("FBA_FLOW_FUSE")) == 0);
     for (int64_t j = 0; j < nb && fuse; ++j)
         for (int32_t k : srcs[j])
+            if (in(j))
             if (fsrc[j] < 0 || level[k] > level[fsrc[j]] || (level[k] == level[fsrc[j]] && k > fsrc[j])) fsrc[j] = k;
     auto halves = [&](int64_t r) { return real_rows(r) > NB / 2 ? 2 : 1; };
     // the fused source's panel rows of block j are solved by two panel-half records and handed to j's
@@ -453,6 +457,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     int np = 0;
     for (int64_t k = 0; k < nb; ++k)
         for (int32_t r : R[k]) {
+            if (!in(k)) break;
             if (self_panel(k, r)) {
                 for (int h = 0; h < halves(r); ++h) prog[std::make_tuple((int32_t)k, r, h)] = np;
                 ++np;
@@ -512,6 +517,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     int nslot = 0, ncnt = 0;
     // diagonal blocks
     for (int64_t j = 0; j < nb; ++j) {
+        if (!in(j)) continue;
         const int32_t f = fsrc[j];
         int need = level[j] - 1;
         const bool sp = f >= 0 && self_panel(f, j);
@@ -548,6 +554,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     // panel-half solves
     for (int64_t k = 0; k < nb; ++k)
         for (int32_t r : R[k])
+            if (in(k))
             for (int h = 0; h < halves(r) && !self_panel(k, r); ++h) {
                 const int32_t p = prog[std::make_tuple((int32_t)k, r, h)];
                 // rec[7]: the RHS block row's half 0 accumulates its rows' Gram into partial k
@@ -563,7 +570,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     // update tasks, target quarter by target quarter, a chain of writers over the source levels
     std::map<std::pair<int32_t, int32_t>, std::vector<int32_t>> tg;  // (a, b) -> sources, ascending
     for (int64_t k = 0; k < nb; ++k)
-        for (size_t bi = 0; bi < R[k].size(); ++bi) {
+        for (size_t bi = 0; bi < R[k].size() && in(k); ++bi) {
             const int32_t b = R[k][bi];
             if (b == nb) continue;
             for (size_t ai = bi; ai < R[k].size(); ++ai) {
@@ -662,6 +669,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     // the helpers of the fused updates: column blocks [0, ksplit) of f_j's panel rows j, per quarter
     for (int64_t j = 0; j < nb && ksplit > 0; ++j) {
         const int32_t f = fsrc[j];
+        if (!in(j)) continue;
         if (f < 0 || self_panel(f, j)) continue;
         for (int q : {0, 2, 3}) {
             const int qr = q >> 1, qc = q & 1;
@@ -727,7 +735,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     // records, so they hold no CU while the middle levels run; config 4: 1160-1167 vs 1162-1170 iter/s)
     static const bool inv_last = getenv("FBA_FLOW_INV_LAST") && atoi(getenv("FBA_FLOW_INV_LAST")) != 0;
     for (int64_t j = 0; j < nb; ++j)
-        if (level[j] < nw - 1) {
+        if (level[j] < nw - 1 && in(j)) {
             const int id = add({3, (int32_t)j}, {inv_last ? nw : level[j] + 1, 5, (int)j});
             T[id].deps.push_back(col_task[j]);
             s.flow_flops += (double)NB * NB * NB / 3.0;
@@ -1092,10 +1100,117 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
     }
     s.nzero = (int)((at() - s.zero) / 2);
     s.n_tiles = ntile_total;
-    build_flow(s, buf, R, level, nb, real_rows, c.opt.verbose);
-    s.n_tflags = std::max(s.n_tflags, s.flow_nprog + s.flow_nuflag);
-    s.n_counters = std::max(s.n_counters, s.flow_ncounter);
-    s.n_scratch = std::max(s.n_scratch, s.flow_nscratch);
+    // subtree split (Sched::split): cut the elimination tree.  parent(k) = the first block row below
+    // column k; a subtree's columns touch only their own rows and their ancestors', so two subtrees never
+    // share a block.  Starting from the roots, the subtree of the largest work (1 + r + r^2 block
+    // products for a column of r panel blocks) moves its root column to the top until there are at
+    // least `world` subtrees and none holds more than 1.25x the average; the subtrees are then dealt to
+    // the ranks largest first, each to the least loaded (LPT).  The local inner-constraint border's block
+    // rows must stay in a subtree (their weights come from one rank's diagonal); otherwise no split.
+    s.split = false;
+    std::vector<char> inc_own, inc_top;
+    if (c.opt.split && c.opt.world > 1 && nb > 1) {
+        const int W = c.opt.world;
+        std::vector<int32_t> parent(nb, -1);
+        std::vector<std::vector<int32_t>> kids(nb);
+        for (int64_t k = 0; k < nb; ++k)
+            for (int32_t r : R[k])
+                if (r < nb) { parent[k] = r; kids[r].push_back((int32_t)k); break; }
+        std::vector<double> sw(nb, 0.0);  // children have smaller indices than their parents
+        for (int64_t k = 0; k < nb; ++k) {
+            const double r = (double)R[k].size();
+            sw[k] += 1.0 + r + r * r;
+            if (parent[k] >= 0) sw[parent[k]] += sw[k];
+        }
+        std::vector<int32_t> frontier;
+        for (int64_t k = 0; k < nb; ++k)
+            if (parent[k] < 0) frontier.push_back((int32_t)k);
+        std::vector<char> top(nb, 0);
+        for (;;) {
+            double tot = 0.0, mx = -1.0;
+            int imx = -1;
+            for (size_t q = 0; q < frontier.size(); ++q) {
+                tot += sw[frontier[q]];
+                if (sw[frontier[q]] > mx) { mx = sw[frontier[q]]; imx = (int)q; }
+            }
+            if (imx < 0 || ((int)frontier.size() >= W && mx <= 1.25 * tot / W)) break;
+            const int32_t k = frontier[imx];
+            if (kids[k].empty()) break;  // one column: no further cut
+            top[k] = 1;
+            frontier.erase(frontier.begin() + imx);
+            frontier.insert(frontier.end(), kids[k].begin(), kids[k].end());
+        }
+        std::stable_sort(frontier.begin(), frontier.end(), [&](int32_t a, int32_t b) { return sw[a] > sw[b]; });
+        std::vector<double> load(W, 0.0);
+        std::vector<int32_t> root_rank(nb, -1);
+        for (int32_t k : frontier) {
+            const int r = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+            root_rank[k] = r;
+            load[r] += sw[k];
+        }
+        std::vector<int32_t> br(nb, -1);
+        for (int64_t k = nb - 1; k >= 0; --k)  // parents first
+            br[k] = top[k] ? -1 : (root_rank[k] >= 0 ? root_rank[k] : (parent[k] >= 0 ? br[parent[k]] : -1));
+        bool ok = !frontier.empty();
+        if (c.n_loc > 0)
+            for (int64_t i = 0; i <= (6 * (int64_t)c.n_loc - 1) / NB; ++i) ok = ok && br[i] >= 0;
+        if (ok) {
+            s.split = true;
+            s.blk_rank = br;
+            inc_own.assign(nb, 0);
+            inc_top.assign(nb, 0);
+            for (int64_t k = 0; k < nb; ++k) {
+                inc_own[k] = br[k] == c.opt.rank;
+                inc_top[k] = br[k] < 0;
+            }
+            // the top blocks the ranks sum: (b, b) and (a, b), a in R[b] (top rows and the RHS block row)
+            s.top_blocks = at();
+            for (int64_t b = 0; b < nb; ++b)
+                if (br[b] < 0) {
+                    buf.push_back((int32_t)b);
+                    buf.push_back((int32_t)b);
+                    for (int32_t a : R[b]) { buf.push_back(a); buf.push_back((int32_t)b); }
+                }
+            s.n_top_blocks = (int)((at() - s.top_blocks) / 2);
+            if (c.opt.verbose) {
+                int ntop = 0;
+                for (int64_t k = 0; k < nb; ++k) ntop += br[k] < 0;
+                fprintf(stderr, "[fba] subtree split: %d top columns (%d top blocks), %zu subtrees; work per rank:", ntop,
+                        s.n_top_blocks, frontier.size());
+                for (double v : load) fprintf(stderr, " %.0f", v);
+                fprintf(stderr, "; top columns:");
+                for (int64_t k = 0; k < nb; ++k)
+                    if (br[k] < 0) fprintf(stderr, " %ld", (long)k);
+                fprintf(stderr, "\n");
+            }
+        } else if (c.opt.verbose) {
+            fprintf(stderr, "[fba] subtree split not possible for this block pattern: replicated solve\n");
+        }
+    }
+    if (s.split) {  // flow B (the top columns) first, saved; flow A (this rank's subtrees) in the main fields
+        build_flow(s, buf, R, level, nb, real_rows, c.opt.verbose, &inc_top);
+        Sched::FlowPart& T = s.top;
+        T.rec = s.flow_rec;
+        T.n = s.flow_n;
+        T.nprog = s.flow_nprog;
+        T.nuflag = s.flow_nuflag;
+        T.ncounter = s.flow_ncounter;
+        T.nscratch = s.flow_nscratch;
+        for (int r = 0; r < 5; ++r) T.cnt[r] = s.flow_cnt[r];
+        T.ok = s.flow_ok;
+        T.flops = s.flow_flops;
+        s.flow_flops = 0.0;
+        build_flow(s, buf, R, level, nb, real_rows, c.opt.verbose, &inc_own);
+        s.flow_dyn_n = 0;  // (static ticket order only)
+        s.n_tflags = std::max(s.n_tflags, s.flow_nprog + s.flow_nuflag + T.nprog + T.nuflag);
+        s.n_counters = std::max(s.n_counters, s.flow_ncounter + T.ncounter);
+        s.n_scratch = std::max(s.n_scratch, s.flow_nscratch + T.nscratch);
+    } else {
+        build_flow(s, buf, R, level, nb, real_rows, c.opt.verbose);
+        s.n_tflags = std::max(s.n_tflags, s.flow_nprog + s.flow_nuflag);
+        s.n_counters = std::max(s.n_counters, s.flow_ncounter);
+        s.n_scratch = std::max(s.n_scratch, s.flow_nscratch);
+    }
     s.buf = std::move(buf);
     if (c.opt.verbose)
         fprintf(stderr, "[fba] camera system: %ld blocks, %d levels, %ld update tiles, %d images + %d padding slots\n",

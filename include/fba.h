@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define FBA_ABI_VERSION 1
+#define FBA_ABI_VERSION 2
 
 /* projection models, BuildAwG.m:184-213 (the reference's `typeint`) */
 enum {
@@ -101,6 +101,12 @@ typedef struct fba_options {
     int32_t world;       /* number of ranks, 1 for single GPU                               */
     int32_t verbose;
     void* stream;        /* hipStream_t to run on, or NULL for a context-owned stream       */
+    int32_t split;       /* world > 1: 0 = replicated solve (every rank factors the summed reduced
+                          * system), 1 = subtree split: the elimination tree is cut into top
+                          * columns and subtrees dealt to the ranks; tie points follow their
+                          * images' subtree, each rank factors its subtrees in fba_accumulate and
+                          * the reduce buffer carries only the top blocks (no reference
+                          * counterpart: main.m:432 inverts the dense matrix on one CPU)          */
 } fba_options;
 
 typedef struct fba_ctx fba_ctx;

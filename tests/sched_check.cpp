@@ -20,6 +20,7 @@
 #include <random>
 #include <map>
 #include <set>
+#include <functional>
 
 #include "../fish-eye_bundle_adjustment_amd/csrc/fba_internal.h"
 
@@ -148,6 +149,16 @@ int main(int argc, char** argv) {
         double prods = 0.0;
         for (int64_t r : nr) prods += (double)(2 * r + r * r + 1);
         printf("selected inversion: %.0f block products, %.1f GFLOP\n", prods, prods * 2.0 * NB * NB * NB * 1e-9);
+        for (int w : {2, 4, 8}) {  // the subtree split's cut (fba_options.split)
+            Ctx cr;
+            cr.img_ord = c.img_ord;
+            cr.L = c.L;
+            cr.n_loc = c.n_loc;
+            cr.opt.verbose = 1;
+            cr.opt.world = w;
+            cr.opt.split = 1;
+            build_schedule(cr, pairs);
+        }
         return 0;
     }
     const int64_t n = L.n_pad, nb = n / NB, nr = n + NB;  // rows: matrix + RHS block row
@@ -337,13 +348,9 @@ int main(int argc, char** argv) {
     }
     // -- the persistent dataflow schedule (k_chol_flow): records run to completion in an order the
     // dispatch can produce; every flag a record waits for must already be raised --
-    if (!s.flow_ok) return fail("flow schedule order check");
     std::vector<double> F = M0;
     auto Fk = [&](int64_t i, int64_t j) { return &F[(size_t)(i * NB) * n + j * NB]; };
-    std::vector<unsigned> fl((size_t)s.flow_nprog + s.flow_nuflag, 0), colf(nb, 0), cntr(std::max(s.flow_ncounter, 1), 0);
-    std::vector<double> Pf((size_t)std::max(s.flow_nscratch, 1) * 4096, 0.0);
-    std::vector<int> slot_set(std::max(s.flow_nscratch, 1), 0);
-    auto flag_ok = [&](int32_t x, unsigned v) { return x >= 0 && x < (int32_t)fl.size() && fl[x] >= v; };
+    std::vector<unsigned> colf(nb, 0);
     auto solve_rows = [&](int64_t k, int64_t r, int i0, int i1) {  // rows i0..i1 of block (r, k): X = A L_kk^-T
         const double* Lk = Fk(k, k);
         double* X = Fk(r, k);
@@ -354,26 +361,36 @@ int main(int argc, char** argv) {
                 X[(size_t)i * n + j] = v / Lk[(size_t)j * n + j];
             }
     };
-    if (s.flow_rec + (int64_t)Sched::FLOW_REC * s.flow_n > nbuf) return fail("flow record bounds");
+    // one flow: its records (at rec_off, n_rec), flag / counter / scratch spaces of its own; cols_ok(k):
+    // the columns the flow may factor, tgt_ok(a, b): the blocks it may write (subtree split checks)
+    struct FlowView { const int32_t* B; int64_t rec; int n, nfl, ncnt, nscr, dyn_n; int64_t dyn_info, dyn_cons, dyn_init; int dyn_ninit; int64_t nbuf; };
+    auto emulate = [&](const FlowView& v, const std::function<bool(int64_t)>& cols_ok,
+                       const std::function<bool(int64_t, int64_t)>& tgt_ok) -> int {
+    const int32_t* B = v.B;
+    std::vector<unsigned> fl((size_t)std::max(v.nfl, 1), 0), cntr(std::max(v.ncnt, 1), 0);
+    std::vector<double> Pf((size_t)std::max(v.nscr, 1) * 4096, 0.0);
+    std::vector<int> slot_set(std::max(v.nscr, 1), 0);
+    auto flag_ok = [&](int32_t x, unsigned q) { return x >= 0 && x < (int32_t)fl.size() && fl[x] >= q; };
+    if (v.rec + (int64_t)Sched::FLOW_REC * v.n > v.nbuf) return fail("flow record bounds");
     // -- the dynamic dispatch (k_chol_flow FlowDyn): W workers take FIFO slots of ready records (the
     // records ready at launch first); a claimed record completes once every producer has completed (a
     // diagonal block's start triggers fire then: its potrf start); no state may be stuck.  The completion
     // order is a valid execution of the records and is emulated below like the static order --
     std::vector<int> order;
-    if (s.flow_dyn_n > 0) {
-        const int nd = s.flow_dyn_n, W = 3 + seed % 29;
-        const int32_t* info = B + s.flow_dyn_info;
-        const int32_t* cons = B + s.flow_dyn_cons;
-        const int32_t* init = B + s.flow_dyn_init;
-        if (nd != s.flow_n) return fail("dyn: record count");
+    if (v.dyn_n > 0) {
+        const int nd = v.dyn_n, W = 3 + seed % 29;
+        const int32_t* info = B + v.dyn_info;
+        const int32_t* cons = B + v.dyn_cons;
+        const int32_t* init = B + v.dyn_init;
+        if (nd != v.n) return fail("dyn: record count");
         std::vector<int> cnt(nd, 0), pdone(nd, 0), started(nd, 0), fifo;
-        for (int q = 0; q < s.flow_dyn_ninit; ++q) {
+        for (int q = 0; q < v.dyn_ninit; ++q) {
             if (init[q] < 0 || init[q] >= nd || info[8 * init[q]] != 0) return fail("dyn: initial ready list");
             fifo.push_back(init[q]);
         }
         int nzero = 0;
         for (int r = 0; r < nd; ++r) nzero += info[8 * r] == 0;
-        if (nzero != s.flow_dyn_ninit) return fail("dyn: initial ready count");
+        if (nzero != v.dyn_ninit) return fail("dyn: initial ready count");
         auto trig = [&](int r, int first, int count, bool completion) {
             for (int i = 0; i < count; ++i) {
                 const int c = cons[info[8 * r + 2] + first + i];
@@ -392,12 +409,12 @@ int main(int argc, char** argv) {
             while (head < fifo.size() && (int)running.size() < W) {
                 const int r = fifo[head++];
                 running.push_back(r);
-                if (B[s.flow_rec + (int64_t)Sched::FLOW_REC * r] != 0 && !trig(r, 0, info[8 * r + 3], false))
+                if (B[v.rec + (int64_t)Sched::FLOW_REC * r] != 0 && !trig(r, 0, info[8 * r + 3], false))
                     return fail("dyn: trigger count");
                 prog = true;
             }
             for (int r : running)  // diagonal blocks whose producers are all complete start their potrf
-                if (!started[r] && B[s.flow_rec + (int64_t)Sched::FLOW_REC * r] == 0 && pdone[r] == info[8 * r]) {
+                if (!started[r] && B[v.rec + (int64_t)Sched::FLOW_REC * r] == 0 && pdone[r] == info[8 * r]) {
                     started[r] = 1;
                     if (!trig(r, 0, info[8 * r + 3], false)) return fail("dyn: trigger count");
                     prog = true;
@@ -416,15 +433,15 @@ int main(int argc, char** argv) {
         }
         if (fifo.size() != (size_t)nd) return fail("dyn: a record appended twice or never");
     } else {
-        for (int b = 0; b < s.flow_n; ++b) order.push_back(b);
+        for (int b = 0; b < v.n; ++b) order.push_back(b);
     }
-    std::vector<char> ran(s.flow_n, 0);
+    std::vector<char> ran(v.n, 0);
     // a split helper (role 4): tiles (ta, tb), tb >= FLOW_CSPLIT, of C_jj -= X X', X = L(j, f)
     auto run_helper = [&](const int32_t* rec) -> int {
         const int64_t j = rec[1], f = rec[2];
         if (colf[f] != 8 || f >= j) return fail("flow: split helper before its source");
         if (!flag_ok(rec[7], 8) || (rec[8] >= 0 && !flag_ok(rec[8], 8))) return fail("flow: split helper rows not solved");
-        if (rec[10] < 0 || rec[10] >= s.flow_nscratch || slot_set[rec[10]]++) return fail("flow: split helper slot");
+        if (rec[10] < 0 || rec[10] >= v.nscr || slot_set[rec[10]]++) return fail("flow: split helper slot");
         const double* X = Fk(j, f);
         int h = 0;
         for (int ta = 0; ta < NB / 16; ++ta)
@@ -439,11 +456,12 @@ int main(int argc, char** argv) {
         return 0;
     };
     for (int b : order) {
-        const int32_t* rec = B + s.flow_rec + (int64_t)Sched::FLOW_REC * b;
+        const int32_t* rec = B + v.rec + (int64_t)Sched::FLOW_REC * b;
         if (ran[b]) continue;
         ran[b] = 1;
         if (rec[0] == 0) {
             const int64_t j = rec[1], f = rec[2];
+            if (!cols_ok(j)) return fail("flow: diagonal block of a column outside the flow");
             for (int x = 0; x < rec[4]; ++x)
                 if (!flag_ok(B[rec[3] + x], 1)) return fail("flow: diagonal block waits for an unset flag");
             double* C = Fk(j, j);
@@ -456,8 +474,8 @@ int main(int argc, char** argv) {
                 fl[rec[7]] = 8;
                 if (rec[9] >= 0) {  // its split helper, dispatched right after it, runs beside its potrf
                     const int hb = b + 1;
-                    const int32_t* hr = B + s.flow_rec + (int64_t)Sched::FLOW_REC * hb;
-                    if (hb >= s.flow_n || hr[0] != 4 || hr[1] != j || ran[hb]) return fail("flow: self panel's helper not next");
+                    const int32_t* hr = B + v.rec + (int64_t)Sched::FLOW_REC * hb;
+                    if (hb >= v.n || hr[0] != 4 || hr[1] != j || ran[hb]) return fail("flow: self panel's helper not next");
                     ran[hb] = 1;
                     if (run_helper(hr)) return 1;
                 }
@@ -485,7 +503,7 @@ int main(int argc, char** argv) {
                         if (64 * qr + a >= 64 * qc + c2) C[(size_t)(64 * qr + a) * n + 64 * qc + c2] += Pf[(size_t)l3[1] * 4096 + a * 64 + c2];
             }
             if (rec[9] >= 0) {  // the split helper's partial (the potrf's bulk waves add it)
-                if (!flag_ok(rec[9], 1) || rec[10] < 0 || rec[10] >= s.flow_nscratch || !slot_set[rec[10]])
+                if (!flag_ok(rec[9], 1) || rec[10] < 0 || rec[10] >= v.nscr || !slot_set[rec[10]])
                     return fail("flow: split helper partial not ready");
                 int h = 0;
                 for (int ta = 0; ta < NB / 16; ++ta)
@@ -511,6 +529,7 @@ int main(int argc, char** argv) {
         } else if (rec[0] == 1) {
             const int64_t k = rec[1], r = rec[2] >> 1, h = rec[2] & 1;
             if (colf[k] != 8 || r <= k || r > nb) return fail("flow: panel half before its column");
+            if (!cols_ok(k)) return fail("flow: panel half of a column outside the flow");
             for (int x = 0; x < rec[4]; ++x)
                 if (!flag_ok(B[rec[3] + x], 1)) return fail("flow: panel half waits for an unset flag");
             solve_rows(k, r, 64 * (int)h, 64 * (int)h + 64);
@@ -519,6 +538,7 @@ int main(int argc, char** argv) {
             const int64_t a = rec[1], bb = rec[2];
             const int qr = rec[3] >> 1, qc = rec[3] & 1, mode = rec[7];
             if (bb >= nb || a < bb || a > nb) return fail("flow: update target");
+            if (!tgt_ok(a, bb)) return fail("flow: update target outside the flow's blocks");
             std::vector<double> acc(4096, 0.0);
             for (int u = 0; u < rec[5]; ++u) {
                 const int32_t* tri = B + rec[4] + 3 * u;
@@ -544,7 +564,7 @@ int main(int argc, char** argv) {
                 add_c(acc.data());
                 fl[rec[8]] = 1;
             } else {
-                if (rec[6] < 0 || rec[6] >= s.flow_nscratch || slot_set[rec[6]]++) return fail("flow: scratch slot");
+                if (rec[6] < 0 || rec[6] >= v.nscr || slot_set[rec[6]]++) return fail("flow: scratch slot");
                 std::copy(acc.begin(), acc.end(), Pf.begin() + (size_t)rec[6] * 4096);
                 if (mode == 2) {
                     fl[rec[8]] = 1;
@@ -561,6 +581,60 @@ int main(int argc, char** argv) {
         } else {
             return fail("flow: record role");
         }
+    }
+    return 0;
+    };
+    if (!s.flow_ok) return fail("flow schedule order check");
+    const char* sw = getenv("SCHED_SPLIT_WORLD");
+    const int split_world = sw ? atoi(sw) : 0;
+    if (split_world > 1) {
+        // subtree split: every rank's flow A on the same matrix (their updates of the top blocks add up
+        // in place, as the all-reduce sums them), then the top flow B; each rank's flow may only factor
+        // its own columns and write its own or top blocks
+        std::vector<int> seen(nb, 0);
+        std::vector<Sched> per(split_world);
+        for (int r = 0; r < split_world; ++r) {
+            Ctx cr;
+            cr.img_ord = c.img_ord;
+            cr.L = c.L;
+            cr.n_loc = c.n_loc;
+            cr.opt.verbose = 0;
+            cr.opt.rank = r;
+            cr.opt.world = split_world;
+            cr.opt.split = 1;
+            build_schedule(cr, pairs);
+            per[r] = cr.sched;
+            if (!per[r].split) return fail("split: no subtree split");
+            if (per[r].blk_rank != per[0].blk_rank) return fail("split: ranks disagree on the cut");
+            if (!per[r].flow_ok || !per[r].top.ok) return fail("split: flow order check");
+        }
+        const std::vector<int32_t>& br = per[0].blk_rank;
+        for (int64_t k = 0; k < nb; ++k) seen[k] = br[k];
+        for (int r = 0; r < split_world; ++r) {
+            const Sched& q = per[r];
+            FlowView v{q.buf.data(), q.flow_rec, q.flow_n, q.flow_nprog + q.flow_nuflag, q.flow_ncounter, q.flow_nscratch,
+                       0, 0, 0, 0, 0, (int64_t)q.buf.size()};
+            auto own = [&](int64_t k) { return k < nb && br[k] == r; };
+            auto topb = [&](int64_t k) { return k == nb || br[k] < 0; };
+            if (emulate(v, own, [&](int64_t a, int64_t bb) { return (own(a) || topb(a)) && (own(bb) || topb(bb)); })) return 1;
+            for (int64_t k = 0; k < nb; ++k)
+                if (own(k) && colf[k] != 8) return fail("split: a subtree column left unfactored");
+        }
+        const Sched& q = per[0];
+        FlowView vt{q.buf.data(), q.top.rec, q.top.n, q.top.nprog + q.top.nuflag, q.top.ncounter, q.top.nscratch, 0, 0, 0, 0, 0,
+                    (int64_t)q.buf.size()};
+        auto topc = [&](int64_t k) { return k < nb && br[k] < 0; };
+        if (emulate(vt, topc, [&](int64_t a, int64_t bb) { return (a == nb || br[a] < 0) && br[bb] < 0; })) return 1;
+        int ntop = 0;
+        for (int64_t k = 0; k < nb; ++k) {
+            if (colf[k] != 8) return fail("split: a column left unfactored");
+            ntop += br[k] < 0;
+        }
+        printf("split world=%d top_columns=%d top_blocks=%d ", split_world, ntop, per[0].n_top_blocks);
+    } else {
+        FlowView v{s.buf.data(), s.flow_rec, s.flow_n, s.flow_nprog + s.flow_nuflag, s.flow_ncounter, s.flow_nscratch,
+                   s.flow_dyn_n, s.flow_dyn_info, s.flow_dyn_cons, s.flow_dyn_init, s.flow_dyn_ninit, nbuf};
+        if (emulate(v, [](int64_t) { return true; }, [](int64_t, int64_t) { return true; })) return 1;
     }
     double ferr = 0.0;
     for (int64_t i = 0; i < nr; ++i)

@@ -293,6 +293,57 @@ def test_config4_two_rank_shards_match_single_context(fba, scenes):
             c.close()
 
 
+@pytest.mark.parametrize("config", [3, 4, 5])
+def test_subtree_split_two_ranks_match_single_context(fba, scenes, config):
+    """The subtree-split factorisation (fba_options.split): two rank contexts on one
+    GPU, each factoring its own subtrees of the elimination tree inside fba_accumulate, their reduce
+    buffers (the top blocks of the Schur complement, the top rows' accumulated diagonal, the subtree
+    columns' Gram partials and inner-constraint weight sums) summed on the host as the RCCL all-reduce
+    would; each then factors the top columns, back-substitutes and updates.  Over two Gauss-Newton passes
+    at configs 3, 4 and 5 the ranks' owned entries reassemble the single context's xhat to 1e-10 per
+    parameter group and 1e-9 per element, and the deltasum shares add up to the single context's
+    deltasum.  (One GPU stands in for two: the collective itself is unmeasured here.)"""
+    import ctypes
+    folder = _scene(config, scenes)
+    ds = fba.load_folder(folder)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    mk = lambda **kw: fba.capi.Context(ds.pack(), fba.capi.make_settings(ds.settings), **kw)  # noqa: E731
+    single = mk()
+    ranks = [mk(rank=r, world=2, split=True) for r in range(2)]
+    try:
+        d_first = None
+        for _ in range(2):
+            d1 = single.step()
+            d_first = d_first or d1
+            for c in ranks:
+                c.accumulate()
+                c.synchronize()
+            bufs = [c.reduce_buffer() for c in ranks]
+            assert bufs[0][1] == bufs[1][1]
+            total = np.zeros(bufs[0][1])
+            for p, n in bufs:
+                a = np.empty(n)
+                assert hip.hipMemcpy(a.ctypes.data, p, n * 8, 2) == 0
+                total += a
+            for p, n in bufs:
+                assert hip.hipMemcpy(p, total.ctypes.data, n * 8, 1) == 0
+            parts = [c.solve_update() for c in ranks]
+            assert abs(sum(parts) - d1) <= 1e-9 * d_first, (parts, d1)
+        xs = single.get_xhat()
+        xr = sum(c.get_xhat(owned_only=True) for c in ranks)
+        names = fba.xhat_names(ds)
+        dsc = dist_scaling_of(__import__("fba_oracle").load_folder(folder))
+        err = group_rel_err(xr, xs, names, dsc)
+        assert max(err.values()) <= 1e-10, err
+        err = elem_rel_err(xr, xs, names, dsc)
+        assert max(err.values()) <= 1e-9, err
+    finally:
+        single.close()
+        for c in ranks:
+            c.close()
+
+
 def test_handoff_timeout_fails_safe(fba, scenes, monkeypatch):
     """A device hand-off timeout in the factorisation (every poll bounded, fba_chol.hip) must not leave a
     wrong iterate behind: with the poll bound forced down to one sleep (FBA_FLAG_SPINS, read when a context

@@ -17,7 +17,7 @@ def test_library_exports_every_declared_symbol(fba):
     lib = ctypes.CDLL(fba.capi.LIB_PATH)
     for name in declared:
         assert hasattr(lib, name), name
-    assert fba.capi.lib.fba_abi_version() == 1
+    assert fba.capi.lib.fba_abi_version() == 2
 
 
 def test_ingest_matches_oracle(fba, oracle, cam0_folders):

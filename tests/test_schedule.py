@@ -46,3 +46,24 @@ def test_level_schedule_matches_dense_cholesky(checker, n_img, seed, leaf, merge
         assert int(fields["split"]) > 0
     if leaf == 60:  # a dissected scene: independent subtrees share levels
         assert int(fields["levels"]) < int(fields["blocks"])
+
+
+@pytest.mark.parametrize("n_img,seed,leaf,world", [(300, 2, None, 2), (420, 3, 60, 2), (420, 3, 60, 4), (300, 1, 40, 8)])
+def test_subtree_split_schedule(checker, n_img, seed, leaf, world):
+    """fba_options.split: the elimination tree cut into top columns and per-rank subtrees.  Every rank's
+    flow A (its subtree columns: factor, forward solve, Schur updates of the top blocks) runs on the same
+    matrix -- their top-block updates add up in place as the ranks' buffers are summed -- then the top
+    flow B; the result matches the dense Cholesky (< 1e-12), every column is factored by exactly one
+    flow, and a rank's flow writes only its own subtree's blocks and the top blocks."""
+    env = dict(os.environ)
+    env.pop("FBA_ND_LEAF", None)
+    env.pop("FBA_FLOW_MERGE", None)
+    env["FBA_FLOW_SELF"] = "0"
+    if leaf is not None:
+        env["FBA_ND_LEAF"] = str(leaf)
+    env["SCHED_SPLIT_WORLD"] = str(world)
+    r = subprocess.run([checker, str(n_img), str(seed)], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("split"), r.stdout + r.stderr
+    fields = dict(f.split("=") for f in r.stdout.split() if "=" in f)
+    assert int(fields["top_columns"]) < int(fields["blocks"])
+
