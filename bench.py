@@ -114,6 +114,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    # N > 1: "replicated" = observations sharded, the summed reduced system factored on every rank (the
+    # north star's all-reduce of A'PA / A'Pw); "subtree" = the elimination tree's subtrees factored by the
+    # ranks that own their tie points, only the top blocks all-reduced (fba_options.split)
+    ap.add_argument("--solve", default=os.environ.get("FBA_BENCH_SOLVE", "replicated"), choices=("replicated", "subtree"))
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -142,7 +146,7 @@ def main():
         torch.cuda.set_stream(torch.cuda.Stream(dev))
     stream = torch.cuda.current_stream(dev).cuda_stream if world > 1 else None
     ctx = fba.capi.Context(ds.pack(), fba.capi.make_settings(ds.settings), device=local, rank=rank, world=world,
-                           stream=stream, verbose=args.verbose)
+                           stream=stream, verbose=args.verbose, split=args.solve == "subtree")
     if world > 1:
         from fba_amd.parallel import ShardedStep
         step = ShardedStep(ctx, device=dev)
@@ -229,7 +233,7 @@ def main():
                                f"{'' if args.network == 'grid' else ' (' + args.network + ' network)'}: {ds.numImg} "
                                f"images x {ds.numtie} tie points, {ds.n_pts} image points, inner constraints, nK=5",
                    "n_pts": ds.n_pts, "n_img": ds.numImg, "n_tie": ds.numtie, "u": int(ctx.u),
-                   "parallelism": f"obs-shard{world}"},
+                   "parallelism": f"{'subtree-split' if ctx.split else 'obs-shard'}{world}"},
         "obs_per_s": ds.n_pts * value,
         "phase_ms": {k: t[k] for k in names},
         "deltasum_last": dsum[-1] if dsum else None,

@@ -2940,10 +2940,17 @@ int launch_cholesky(Ctx& c, int part) {
         const int n = b ? T.n : s.flow_n;
         if (n == 0) return FBA_OK;
         const int64_t fo = b ? s.flow_nprog + s.flow_nuflag : 0, co = b ? s.flow_ncounter : 0, so = b ? s.flow_nscratch : 0;
+        const bool pp = c.probe == 2 && c.probe_n < (int)c.probe_ev.size() / 2;
+        if (pp) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
         k_chol_flow<<<(unsigned)n, POTRF_THREADS, FLOW_LDS, c.stream>>>(
             c.d_S, ld, c.d_sched, c.d_sched + (b ? T.rec : s.flow_rec), c.d_dinv, c.d_linv, c.d_scal, c.d_flags,
             c.d_tflags + fo, c.d_counters + co, c.d_P + so * 4096, nullptr, c.set.inner_constraints ? c.d_gblk : nullptr,
             c.d_tickets + (b ? 2 : 0), nullptr);
+        if (pp) {
+            FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], c.stream));
+            c.probe_flops += b ? T.flops : s.flow_flops;
+            ++c.probe_n;
+        }
         FBA_HIP(hipGetLastError());
         return FBA_OK;
     }
