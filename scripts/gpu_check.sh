@@ -6,8 +6,12 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 run() {
   local name=$1 t=$2; shift 2
+  # a heartbeat file while the step runs (a long test -- the config-5 oracle passes -- prints nothing for minutes)
+  ( while sleep 50; do date >> gpurun_out/heartbeat.log; done ) &
+  local hb=$!
   timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
+  kill "$hb" 2>/dev/null; wait "$hb" 2>/dev/null
   echo "== $name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
   if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit "$rc"; fi
 }
