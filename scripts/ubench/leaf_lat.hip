@@ -411,6 +411,90 @@ __global__ __launch_bounds__(64) void k_leaf_lds(const double* __restrict__ A, d
     if (lane == 0) *clk = t;
 }
 
+// The row-shared leaf: the four 16-lane rows of the wave run ONE instruction stream on different data --
+// row 0 the leaf's rows (the factor), row 1 the columns of its inverse (identity at the start), row 2 the
+// leaf again, row 3 the rows of the panel tile below (X = A L^-T); one update instruction per (j, l) serves
+// all four, its broadcast source being L's column j on every row (rows 1 / 3 get it from rows 0 / 2 with
+// v_permlane16_swap).  The pivot d comes from lane j by v_readlane (uniform), so the pivot chain's values
+// (r, e, p, 1/L_jj) are the same on every row and column j is scaled by one multiply on all four.
+// put(j): after column j (row 0: L col j, row 1: row j of L^-1, row 3: column j of X)
+template <class PUT>
+__device__ __forceinline__ bool leaf_rows(double (&v)[IB], PUT&& put) {
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < IB; ++j) {
+        const uint64_t bits = __builtin_bit_cast(uint64_t, v[j]);
+        const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)bits, j);
+        const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(bits >> 32), j);
+        const double d = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+        ok &= d > 0.0;
+        const double r = __builtin_amdgcn_rsq(d);
+        const double t = d * r;
+        const double e = __builtin_fma(t, r, -1.0);
+        const double p = __builtin_fma(e, 0.375, -0.5);
+        const double inv = __builtin_fma(r * e, p, r);
+        v[j] *= inv;  // row 0: L[.][j] (lane j: sqrt(d)); row 1: (L^-1)[j][c]; row 3: X[.][j]
+        // src = L's column j on every row: rows 1, 3 take rows 0, 2's v[j]
+        const uint64_t vb = __builtin_bit_cast(uint64_t, v[j]);
+        const auto slo = __builtin_amdgcn_permlane16_swap((uint32_t)vb, (uint32_t)vb, false, false);
+        const auto shi = __builtin_amdgcn_permlane16_swap((uint32_t)(vb >> 32), (uint32_t)(vb >> 32), false, false);
+        // (the swap exchanges odd rows of its first operand with even rows of its second: element 0 is the
+        // first operand after the swap -- odd rows now hold the even rows' values, even rows their own)
+        const double src = __builtin_bit_cast(double, ((uint64_t)shi[0] << 32) | slo[0]);
+#pragma unroll
+        for (int l = j + 1; l < IB; ++l) {
+            if (l == j + 1) fmac_bcn_first(v[l], src, v[j], l);
+            else fmac_bcn(v[l], src, v[j], l);
+        }
+        put(j);
+    }
+    return ok;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(64) void k_leaf_rows(const double* __restrict__ A, const double* __restrict__ Pn,
+                                                  double* __restrict__ out2, long long* clk, int reps) {
+    const int lane = threadIdx.x & 63, lr = lane & 15, row = lane >> 4;
+    __shared__ double Ash[16 * 17], Psh[16 * 17], Lw[16 * 17], Dw[16 * 17], Xw[16 * 17], junk[64];
+    if (lane < 16)
+        for (int c = 0; c < IB; ++c) {
+            Ash[lane * 17 + c] = A[lane * IB + c];
+            Psh[lane * 17 + c] = Pn[lane * IB + c];
+        }
+    __syncthreads();
+    long long t = 0;
+    for (int it = 0; it < reps; ++it) {
+        double v[IB];
+#pragma unroll
+        for (int c = 0; c < IB; ++c)
+            v[c] = row == 1 ? (c == lr ? 1.0 : 0.0) : (row == 3 ? Psh[lr * 17 + c] : Ash[lr * 17 + c]);
+        const long long t0 = clock64();
+        bool ok;
+        if (MODE == 0) {
+            ok = leaf_rows(v, [&](int j) {  // one store: row 0 L col j, row 1 D row j, row 3 X col j
+                double* dst = row == 0 ? &Lw[lr * 17 + j] : row == 1 ? &Dw[j * 17 + lr] : row == 3 ? &Xw[lr * 17 + j] : &junk[lane];
+                *dst = v[j];
+            });
+        } else {
+            double x[IB];
+            ok = leaf_factor(v, x, lr, [&](int j) { Lw[lr * 17 + j] = v[j]; Dw[j * 17 + lr] = x[j]; });
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        const long long t1 = clock64();
+        t += t1 - t0;
+        if (!ok) Ash[0] = 0.0;
+        if (lane == 0) Ash[17 * 15 + 15] += Lw[0] * 0.0;
+        __syncthreads();
+    }
+    if (lane < 16)
+        for (int c = 0; c < IB; ++c) {
+            out2[lane * IB + c] = Lw[lane * 17 + c];
+            out2[256 + lane * IB + c] = Dw[lane * 17 + c];
+            out2[512 + lane * IB + c] = Xw[lane * 17 + c];
+        }
+    if (lane == 0) *clk = t;
+}
+
 // raw issue / latency of f64 VALU ops on one wave (clocks per op, 64 ops a rep)
 template <int MODE>
 __global__ __launch_bounds__(64) void k_lat(const double* __restrict__ A, double* __restrict__ out, long long* clk, int reps) {
@@ -530,6 +614,55 @@ int main() {
             if (used && memcmp(&h1[i], &h2[i], 8) != 0) ++diff;
         }
         printf("scheduled vs reference leaf: %d differing entries of L and L^-1 (bitwise)\n", diff);
+        // the row-shared leaf against the reference leaf (L, L^-1) and X = P L^-T from that L
+        double hP[256];
+        for (int i = 0; i < 16; ++i)
+            for (int j = 0; j < 16; ++j) hP[i * 16 + j] = 0.3 * std::sin(1.0 + i * 0.7 + j * 1.3);
+        double* dP;
+        (void)hipMalloc(&dP, sizeof(hP));
+        (void)hipMemcpy(dP, hP, sizeof(hP), hipMemcpyHostToDevice);
+        double *r1, *r2;
+        (void)hipMalloc(&r1, 768 * sizeof(double));
+        (void)hipMalloc(&r2, 768 * sizeof(double));
+        for (int r = 0; r < 3; ++r) {
+            long long c1 = 0, c2 = 0;
+            k_leaf_rows<1><<<1, 64>>>(dA, dP, r1, clk, reps);
+            (void)hipMemcpy(&c1, clk, sizeof(c1), hipMemcpyDeviceToHost);
+            k_leaf_rows<0><<<1, 64>>>(dA, dP, r2, clk, reps);
+            (void)hipMemcpy(&c2, clk, sizeof(c2), hipMemcpyDeviceToHost);
+            printf("leaf, LDS rows + stores: reference %6.0f clocks; row-shared (factor + inverse + a panel tile) %6.0f clocks\n",
+                   (double)c1 / reps, (double)c2 / reps);
+        }
+        double g1[768], g2[768];
+        (void)hipMemcpy(g1, r1, sizeof(g1), hipMemcpyDeviceToHost);
+        (void)hipMemcpy(g2, r2, sizeof(g2), hipMemcpyDeviceToHost);
+        double eL = 0, eD = 0, eX = 0, mL = 0, mD = 0, mX = 0;
+        for (int i = 0; i < 16; ++i)
+            for (int c = 0; c <= i; ++c) {
+                eL = std::max(eL, std::fabs(g1[i * 16 + c] - g2[i * 16 + c]));
+                mL = std::max(mL, std::fabs(g1[i * 16 + c]));
+                eD = std::max(eD, std::fabs(g1[256 + i * 16 + c] - g2[256 + i * 16 + c]));
+                mD = std::max(mD, std::fabs(g1[256 + i * 16 + c]));
+            }
+        for (int i = 0; i < 16; ++i)  // X = P L^-T by substitution with the reference L
+            for (int j = 0; j < 16; ++j) {
+                double x = hP[((i + 3) & 15) * 0 + i * 16 + j];
+                (void)x;
+            }
+        {
+            double X[256];
+            for (int i = 0; i < 16; ++i)
+                for (int j = 0; j < 16; ++j) {
+                    double s2 = hP[i * 16 + j];
+                    for (int k = 0; k < j; ++k) s2 -= X[i * 16 + k] * g1[j * 16 + k];
+                    X[i * 16 + j] = s2 / g1[j * 16 + j];
+                }
+            for (int q = 0; q < 256; ++q) {
+                eX = std::max(eX, std::fabs(X[q] - g2[512 + q]));
+                mX = std::max(mX, std::fabs(X[q]));
+            }
+        }
+        printf("row-shared vs reference: L %.2e, L^-1 %.2e, X %.2e (max abs diff / max abs)\n", eL / mL, eD / mD, eX / mX);
     }
     for (int r = 0; r < 2; ++r) {
         k_leaf_split<<<1, 128>>>(dA, out, clk, reps);
