@@ -2521,8 +2521,211 @@ __device__ __forceinline__ void syrk_flow_body(double* __restrict__ S, int64_t l
     raise(rec[8]);
 }
 
+// syrk_block_body (role 2, rec[3] == 4): one update task over a WHOLE off-diagonal target block,
+// C(a, b) += -sum_k X_ak X_bk' (128 x 128): per source its 128 rows of A and of B are loaded once for all
+// four quarters (half the operand bytes of four quarter tasks), in windows of <= 4 published column blocks
+// (LDS: 128 x 64 of each operand).  Eight waves, each 32 rows x 64 columns (2 x 4 tiles of 16 x 16).
+// Source entries are 5 ints: k, then the progress flags of A's two panel halves and of B's.  Modes as
+// syrk_flow_body: 0 in place after rec[9]; 1 a split target's partial to scratch slots [slot, slot + 4)
+// (one 128 x 128 block, row-major), the last group to arrive adds the groups' blocks (slots rec[11] + 4 g)
+constexpr int BLK_KW = 64, BLK_LDK = BLK_KW + 2;
+constexpr size_t SYRKB_LDS = sizeof(double) * 2 * 128 * BLK_LDK + 16;
+__device__ __forceinline__ void syrk_block_body(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ rec,
+                                                const int32_t* __restrict__ lists, double* __restrict__ P,
+                                                unsigned* __restrict__ fl, unsigned* __restrict__ cnt,
+                                                double* __restrict__ scal, double* __restrict__ smem,
+                                                uint64_t* __restrict__ tr) {
+    double (*As)[BLK_LDK] = reinterpret_cast<double (*)[BLK_LDK]>(smem);
+    double (*Bs)[BLK_LDK] = reinterpret_cast<double (*)[BLK_LDK]>(smem + 128 * BLK_LDK);
+    int* sv = reinterpret_cast<int*>(smem + 256 * BLK_LDK);
+    const int a = rec[1], b = rec[2], ns = rec[5], slot = rec[6], mode = rec[7];
+    const int32_t* sl = lists + rec[4];
+    const int64_t r0 = (int64_t)a * CB, c0 = (int64_t)b * CB;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int lr = lane & 15, lk = lane >> 4;
+    const int wr = (wave >> 1) * 32, wc = (wave & 1) * 64;
+    const __amdgpu_buffer_rsrc_t rC = block_rsrc(S + r0 * ld + c0, ((int64_t)127 * ld + 128) * 8);
+    dbl4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
+    if (mode == 0) {  // in place: the target (after its previous writer) is the accumulators' start
+        if (rec[9] >= 0 && tid == 0) spin_ge(fl + rec[9], 1u, scal);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    acc[i][j][r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                        rC, (int)(((int64_t)(wr + 16 * i + lk + 4 * r) * ld + wc + 16 * j + lr) * 8), 0, SC1));
+    }
+    const __amdgpu_buffer_rsrc_t rA = block_rsrc(S + r0 * ld, ((int64_t)127 * ld + ld) * 8);
+    const __amdgpu_buffer_rsrc_t rB = block_rsrc(S + c0 * ld, ((int64_t)127 * ld + ld) * 8);
+    const int t0 = rec[13], t_end = rec[14];
+    // the sources complete at the start (all four panel halves published every column block): their
+    // windows need no poll, and the next such window is loaded into registers during this one's MFMAs
+    if (tid == 0) {
+        unsigned m = 0;
+        for (int s = 0; s < ns && s < 32; ++s) {
+            bool done = true;
+            for (int x = 1; x <= 4; ++x)
+                done = done && __hip_atomic_load(fl + sl[5 * s + x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)t_end;
+            if (done) m |= 1u << s;
+        }
+        sv[2] = (int)m;
+    }
+    __syncthreads();
+    const unsigned full = (unsigned)sv[2];
+    auto complete = [&](int s) { return s < 32 && ((full >> s) & 1u); };
+    double2 xa[8], xb[8];
+    auto load_win = [&](int s, int t, int v) {  // rows 0..127 of A and B, columns [16 t, 16 v)
+        const int64_t kc = (int64_t)sl[5 * s] * CB;
+        const int wpr = 8 * (v - t), nit = 128 * wpr;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = tid + POTRF_THREADS * u;
+            if (i < nit) {
+                const int row = i / wpr, col = IB * t + 2 * (i % wpr);
+                xa[u] = ld_sc1(rA, ((int64_t)row * ld + kc + col) * 8);
+                xb[u] = ld_sc1(rB, ((int64_t)row * ld + kc + col) * 8);
+            }
+        }
+    };
+    auto store_win = [&](int t, int v) {
+        const int wpr = 8 * (v - t), nit = 128 * wpr;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = tid + POTRF_THREADS * u;
+            if (i < nit) {
+                const int row = i / wpr, col = 2 * (i % wpr);
+                As[row][col] = xa[u].x; As[row][col + 1] = xa[u].y;
+                Bs[row][col] = xb[u].x; Bs[row][col + 1] = xb[u].y;
+            }
+        }
+    };
+    bool held = false;  // xa / xb hold the window (s, t, .) about to be stored
+    for (int s = 0; s < ns; ++s) {
+        const int32_t* e = sl + 5 * s;
+        int t = t0;
+        while (t < t_end) {
+            int v;
+            if (complete(s)) {
+                v = std::min(t + BLK_KW / IB, t_end);
+            } else {
+                if (tid == 0) {  // the column blocks both operands' four panel halves have published
+                    unsigned spins = 0, m;
+                    for (;;) {
+                        m = (unsigned)t_end;
+#pragma unroll
+                        for (int x = 1; x <= 4; ++x)
+                            m = std::min(m, __hip_atomic_load(fl + e[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                        if (m > (unsigned)t) break;
+                        __builtin_amdgcn_s_sleep(1);
+                        if (spin_expired(spins, scal)) { m = (unsigned)t_end; break; }
+                    }
+                    sv[0] = (int)m;
+                }
+                __syncthreads();
+                v = std::min(sv[0], t + BLK_KW / IB);  // a window of <= 4 column blocks
+            }
+            if (!held) load_win(s, t, v);
+            store_win(t, v);
+            __syncthreads();
+            // the next window, when its source is complete: in flight during this window's MFMAs
+            held = false;
+            if (v < t_end ? complete(s) : (s + 1 < ns && complete(s + 1))) {
+                if (v < t_end) load_win(s, v, std::min(v + BLK_KW / IB, t_end));
+                else load_win(s + 1, t0, std::min(t0 + BLK_KW / IB, t_end));
+                held = true;
+            }
+            for (int kb = 0; kb < IB * (v - t); kb += IB) {
+                double av[2][4], bv[4][4];
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) av[i][kk] = -As[wr + 16 * i + lr][kb + 4 * kk + lk];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) bv[j][kk] = Bs[wc + 16 * j + lr][kb + 4 * kk + lk];
+                }
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) acc[i][j] = mfma(av[i][kk], bv[j][kk], acc[i][j]);
+            }
+            __syncthreads();  // the window is rewritten next
+            t = v;
+        }
+    }
+    if (tr && tid == 0) tr[4] = wall_clock64();
+    auto raise = [&](int32_t flag) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(fl + flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    if (mode == 0) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    st_sc1(rC, ((int64_t)(wr + 16 * i + lk + 4 * r) * ld + wc + 16 * j + lr) * 8, acc[i][j][r]);
+        raise(rec[8]);
+        return;
+    }
+    {   // the partial to its four scratch slots (one row-major 128 x 128 block), write-through
+        const __amdgpu_buffer_rsrc_t rP = block_rsrc(P + (int64_t)slot * 4096, 4 * 4096 * 8);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    st_sc1(rP, (int64_t)((wr + 16 * i + lk + 4 * r) * 128 + wc + 16 * j + lr) * 8, acc[i][j][r]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+        sv[1] = __hip_atomic_fetch_add(cnt + rec[10], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(rec[12] - 1);
+    __syncthreads();
+    if (!sv[1]) return;
+    if (rec[9] >= 0 && tid == 0) spin_ge(fl + rec[9], 1u, scal);
+    __syncthreads();  // (also orders the partial loads below after the arrival)
+    for (int h = 0; h < 2; ++h) {  // the block in two 64-row halves: 4 double2 per thread each
+        double2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e2 = 2 * (tid + POTRF_THREADS * u), r = 64 * h + (e2 >> 7), cl = e2 & 127;
+            v[u] = ld_sc1(rC, ((int64_t)r * ld + cl) * 8);
+        }
+        for (int g = 0; g < rec[12]; ++g) {
+            const __amdgpu_buffer_rsrc_t rg = block_rsrc(P + (int64_t)(rec[11] + 4 * g) * 4096, 4 * 4096 * 8);
+            double2 pv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e2 = 2 * (tid + POTRF_THREADS * u), r = 64 * h + (e2 >> 7), cl = e2 & 127;
+                pv[u] = ld_sc1(rg, (int64_t)(r * 128 + cl) * 8);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) { v[u].x += pv[u].x; v[u].y += pv[u].y; }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e2 = 2 * (tid + POTRF_THREADS * u), r = 64 * h + (e2 >> 7), cl = e2 & 127;
+            st_sc1(rC, ((int64_t)r * ld + cl) * 8, v[u]);
+        }
+    }
+    raise(rec[8]);
+}
+
 constexpr size_t FLOW_LDS_A = FLOWF_LDS > TRSMF_LDS ? FLOWF_LDS : TRSMF_LDS;
-constexpr size_t FLOW_LDS_B = SYRKW_LDS > TRTRI_LDS ? SYRKW_LDS : TRTRI_LDS;
+constexpr size_t FLOW_LDS_B0 = SYRKW_LDS > TRTRI_LDS ? SYRKW_LDS : TRTRI_LDS;
+constexpr size_t FLOW_LDS_B = FLOW_LDS_B0 > SYRKB_LDS ? FLOW_LDS_B0 : SYRKB_LDS;
 constexpr size_t FLOW_LDS = FLOW_LDS_A > FLOW_LDS_B ? FLOW_LDS_A : FLOW_LDS_B;
 static_assert(FLOW_LDS + 16 <= 160 * 1024, "k_chol_flow LDS (+ the static ticket word)");
 static_assert(SYRKW_LDS >= sizeof(double) * 128 * LDW + 3 * sizeof(int), "syrk_flow_body broadcast words");
@@ -2606,7 +2809,8 @@ __device__ __forceinline__ void flow_record(int rid, double* __restrict__ S, int
         trsm_flow_body(S, ld, rec + 1, dinv, colflags + rec[1], scal, smem, tr, fl + rec[5],
                        (gblk && rec[7] >= 0) ? gblk + (int64_t)rec[7] * 256 : nullptr);
     } else if (role == 2) {
-        syrk_flow_body(S, ld, rec, lists, P, fl, cnt, scal, smem, tr);
+        if (rec[3] == 4) syrk_block_body(S, ld, rec, lists, P, fl, cnt, scal, smem, tr);
+        else syrk_flow_body(S, ld, rec, lists, P, fl, cnt, scal, smem, tr);
     } else if (role == 4) {
         split_helper_body(S, ld, rec, fl, P, scal, smem, tr);
     } else {

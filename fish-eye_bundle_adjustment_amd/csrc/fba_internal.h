@@ -103,6 +103,7 @@ struct Sched {
     int flow_cnt[5] = {0, 0, 0, 0, 0};  // records per role
     bool flow_ok = false;
     double flow_flops = 0.0;
+    double flow_bytes = 0.0;      // operand bytes the records load and store (build_flow)
     // dynamic dispatch of the records (k_chol_flow FlowDyn): per record [need, 0, consumer offset,
     // start consumers, done consumers, 0, 0, 0], the consumer lists, the records ready at launch
     int flow_dyn_n = 0, flow_dyn_ninit = 0;

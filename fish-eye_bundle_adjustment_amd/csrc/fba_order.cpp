@@ -605,12 +605,67 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
                 glate.push_back(late_w);
             }
         }
+        // FBA_FLOW_BLOCK=0: off-diagonal targets by quarter tasks too.  Default: a whole-block task (q = 4)
+        // for an off-diagonal target with both row halves real -- its sources' rows loaded once for the four
+        // quarters (syrk_block_body); source entries k, A's two panel halves' flags, B's two
+        // FBA_FLOW_BLOCK=1: every group of such a target whole; 2 (default): the groups whose target is
+        // read later than the next level whole, the urgent last group by quarter tasks after them
+        static const int blockm = getenv("FBA_FLOW_BLOCK") ? atoi(getenv("FBA_FLOW_BLOCK")) : 2;
+        const bool whole = blockm > 0 && a != b && halves(a) == 2 && halves(b) == 2;
+        size_t gq = 0;        // the first group by quarter tasks
+        int32_t wprev = -1;   // the whole-block chain's last writer flag
+        if (whole) {
+            gq = groups.size();
+            if (blockm == 2 && level[b] == groups.back().first + 1) gq = groups.size() - 1;
+            int32_t prev = -1;
+            for (size_t gi = 0; gi < gq; ++gi) {
+                const int w = groups[gi].first;
+                const std::vector<int32_t>& S = groups[gi].second;
+                const int ng = (int)((S.size() + SPLIT - 1) / SPLIT);
+                const int rank = level[b] == w + 1 ? 3 : 4;
+                const int32_t wflag = new_uflag();
+                const int32_t cidx = ng > 1 ? ncnt++ : -1;
+                const int first = nslot;
+                for (int g = 0; g < ng; ++g) {
+                    const int32_t soff = (int32_t)buf.size();
+                    std::vector<int32_t> fd;
+                    const int g0 = g * SPLIT, g1 = std::min((int)S.size(), g0 + SPLIT);
+                    for (int x = g0; x < g1; ++x) {
+                        const int32_t k = S[x];
+                        const int32_t f4[4] = {prog.at(std::make_tuple(k, a, 0)), prog.at(std::make_tuple(k, a, 1)),
+                                               prog.at(std::make_tuple(k, b, 0)), prog.at(std::make_tuple(k, b, 1))};
+                        buf.insert(buf.end(), {k, f4[0], f4[1], f4[2], f4[3]});
+                        fd.insert(fd.end(), f4, f4 + 4);
+                        s.flow_flops += 4 * 2.0 * 64 * 64 * NB;
+                    }
+                    int32_t mode = 0, slot = -1;
+                    if (ng > 1) {
+                        mode = 1;
+                        slot = nslot;
+                        nslot += 4;
+                    }
+                    const int need = level[b];
+                    const int lev = defer > 0 ? std::max(w, std::min(w + defer, need - 1)) : std::max(w, need - lookahead);
+                    const int id = add({2, a, b, 4, soff, g1 - g0, slot, mode, wflag, prev, cidx, first, ng, 0, CB_BLOCKS},
+                                       {lev, rank, (int)(b * (nb + 1) + a) * 4});
+                    flag_deps[id] = fd;
+                    if (prev >= 0) flag_deps[id].push_back(prev);
+                    uflag_tasks[wflag - np].push_back(id);
+                }
+                prev = wflag;
+            }
+            wprev = prev;
+            if (gq == groups.size()) {
+                for (int q = 0; q < 4; ++q) writer[std::make_tuple(a, b, q)] = prev;
+                continue;
+            }
+        }
         for (int q = 0; q < 4; ++q) {
             const int qr = q >> 1, qc = q & 1;
             if (a == b && qr == 0 && qc == 1) continue;
             if ((qr == 1 && halves(a) < 2) || (qc == 1 && halves(b) < 2)) continue;
-            int32_t prev = -1;
-            for (size_t gi = 0; gi < groups.size(); ++gi) {
+            int32_t prev = wprev;
+            for (size_t gi = gq; gi < groups.size(); ++gi) {
                 const int w = groups[gi].first;
                 const std::vector<int32_t>& S = groups[gi].second;
                 const bool is_late = glate[gi] != 0;
@@ -877,6 +932,34 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
             if (T[i].deps.empty()) { buf.push_back(pos[i]); s.flow_dyn_ninit++; }
         s.flow_dyn_n = n;
     }
+    // operand bytes the records move (each record's global loads and stores as the kernels issue them:
+    // a diagonal block its 128x128 block, the fused source's 128 panel rows, late / helper partials, the
+    // published factor and leaf inverses; a panel half its 64 rows in and out, the column's factor and
+    // leaf inverses; an update 2 x 64 x 128 per source plus its target quarter or scratch partial in and
+    // out; an inverse the factor in, the inverse out) -- the HBM-side traffic of the decomposition, to set
+    // against the PMC bytes of a launch
+    s.flow_bytes = 0.0;
+    double rb[5] = {0, 0, 0, 0, 0};
+    if (ok)
+        for (int i : ord) {
+            const auto& r = T[i].rec;
+            const double blk = 8.0 * NB * NB, q = 8.0 * 64 * 64, dv = 8.0 * 8 * 16 * 16;
+            double b = 0.0;
+            switch (r[0]) {
+                case 0: b = blk + (r[2] >= 0 ? blk : 0.0) + r[6] * q + (r[9] >= 0 ? 21 * 8.0 * 256 : 0.0) + blk + dv; break;
+                case 1: b = 2 * 8.0 * 64 * NB + blk + dv; break;
+                case 2: b = r[3] == 4 ? r[5] * 2 * blk + 8 * q : r[5] * 2 * 8.0 * 64 * NB + 2 * q; break;
+                case 3: b = 2 * blk; break;
+                case 4: b = blk + 21 * 8.0 * 256; break;
+                default: break;
+            }
+            rb[r[0]] += b;
+            s.flow_bytes += b;
+        }
+    if (verbose)
+        fprintf(stderr, "[fba] flow schedule: operand bytes %.1f MB (diagonal %.1f, panel halves %.1f, updates %.1f, inverses %.1f, "
+                "split helpers %.1f), %.2f GFLOP\n", s.flow_bytes * 1e-6, rb[0] * 1e-6, rb[1] * 1e-6, rb[2] * 1e-6,
+                rb[3] * 1e-6, rb[4] * 1e-6, s.flow_flops * 1e-9);
     if (verbose)
         fprintf(stderr, "[fba] flow schedule: %d records (%d diagonal, %d panel halves, %d updates, %d inverses, "
                 "%d split helpers), %d progress + %d update flags, %d scratch quarters%s\n", n, s.flow_cnt[0],

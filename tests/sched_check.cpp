@@ -97,7 +97,7 @@ int main(int argc, char** argv) {
     L.ld = L.n_pad;
     L.nrhs = 15;
     c.n_loc = std::min(L.n_img, NB / 6);
-    c.opt.verbose = 0;
+    c.opt.verbose = stats_only ? 1 : 0;
     std::vector<int32_t> slot(n_img);
     for (int e = 0; e < L.n_img; ++e)
         if (ord[e] >= 0) slot[ord[e]] = e;
@@ -534,6 +534,45 @@ int main(int argc, char** argv) {
                 if (!flag_ok(B[rec[3] + x], 1)) return fail("flow: panel half waits for an unset flag");
             solve_rows(k, r, 64 * (int)h, 64 * (int)h + 64);
             fl[rec[5]] = 8;
+        } else if (rec[0] == 2 && rec[3] == 4) {  // a whole off-diagonal block (syrk_block_body)
+            const int64_t a = rec[1], bb = rec[2];
+            const int mode = rec[7];
+            if (bb >= nb || a <= bb || a > nb) return fail("flow: block update target");
+            if (!tgt_ok(a, bb)) return fail("flow: update target outside the flow's blocks");
+            std::vector<double> acc(NB * NB, 0.0);
+            for (int u = 0; u < rec[5]; ++u) {
+                const int32_t* e = B + rec[4] + 5 * u;
+                for (int x = 1; x <= 4; ++x)
+                    if (!flag_ok(e[x], 8)) return fail("flow: block update source not published");
+                const double* Xa = Fk(a, e[0]);
+                const double* Xb = Fk(bb, e[0]);
+                for (int x = 0; x < NB; ++x)
+                    for (int y = 0; y < NB; ++y) {
+                        double v = 0.0;
+                        for (int t = 16 * rec[13]; t < 16 * rec[14]; ++t) v += Xa[(size_t)x * n + t] * Xb[(size_t)y * n + t];
+                        acc[x * NB + y] -= v;
+                    }
+            }
+            double* C = Fk(a, bb);
+            auto add_c = [&](const double* src) {
+                for (int x = 0; x < NB; ++x)
+                    for (int y = 0; y < NB; ++y) C[(size_t)x * n + y] += src[x * NB + y];
+            };
+            if (mode == 0) {
+                if (rec[9] >= 0 && !flag_ok(rec[9], 1)) return fail("flow: previous writer not done");
+                add_c(acc.data());
+                fl[rec[8]] = 1;
+            } else {
+                if (rec[6] < 0 || rec[6] + 4 > v.nscr) return fail("flow: block scratch slot");
+                for (int g = 0; g < 4; ++g)
+                    if (slot_set[rec[6] + g]++) return fail("flow: block scratch slot reused");
+                std::copy(acc.begin(), acc.end(), Pf.begin() + (size_t)rec[6] * 4096);
+                if (++cntr[rec[10]] == (unsigned)rec[12]) {
+                    if (rec[9] >= 0 && !flag_ok(rec[9], 1)) return fail("flow: previous writer not done (combine)");
+                    for (int g = 0; g < rec[12]; ++g) add_c(&Pf[(size_t)(rec[11] + 4 * g) * 4096]);
+                    fl[rec[8]] = 1;
+                }
+            }
         } else if (rec[0] == 2) {
             const int64_t a = rec[1], bb = rec[2];
             const int qr = rec[3] >> 1, qc = rec[3] & 1, mode = rec[7];
