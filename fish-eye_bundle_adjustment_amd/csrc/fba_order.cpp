@@ -514,7 +514,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     static const int msplit = getenv("FBA_FLOW_MSPLIT") ? std::max(1, atoi(getenv("FBA_FLOW_MSPLIT"))) : SPLIT;
     static const int promote_mode = getenv("FBA_FLOW_PROMOTE") ? atoi(getenv("FBA_FLOW_PROMOTE")) : 0;
     static const int lookahead = getenv("FBA_FLOW_LOOKAHEAD") ? atoi(getenv("FBA_FLOW_LOOKAHEAD")) : 1000;
-    int nslot = 0, ncnt = 0;
+    int nslot = 0, ncnt = 0, n_whole_t = 0;
     // diagonal blocks
     for (int64_t j = 0; j < nb; ++j) {
         if (!in(j)) continue;
@@ -581,6 +581,28 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
         }
     std::map<std::tuple<int32_t, int32_t, int32_t>, int32_t> writer;  // final in-place writer flag per quarter
     std::vector<std::vector<std::array<int32_t, 3>>> late(nb);          // (quarter, slot, flag) per diagonal block
+    // whole-block update tasks (syrk_block_body, FBA_FLOW_BLOCK): an off-diagonal target with both row
+    // halves real in one record instead of four quarter records -- the sources' rows are loaded once for
+    // the four quarters (config 4 operand bytes 1047 -> 814 MB) but the record runs ~4x a quarter's
+    // latency on one CU (MFMA-bound, ~14 us per 128-deep source).  Measured (iter/s | k_chol_flow us):
+    //   config 4:    quarters 1224-1239 | 446-449, all whole 881-889 | 763-776, whole but the urgent last
+    //                group 909-913 | 739-744, whole while the sources fit the levels left (mode 3, R = 1)
+    //                971 | 670 -- a latency-bound factorisation: the writer chains' latency delays the
+    //                panel halves (mean wait 4.7 -> 33 us) and every diagonal block after them
+    //   config 5:    quarters 276.1 | 2390-2398, all whole 276.7-277.3 | 2367-2374
+    //                mode 3 272.0-272.3 | 2445-2446 (vs 276.0 | 2394-2399 and 276.4-276.7 | 2362-2383, same box)
+    //   convergent:  quarters 234-236 | 3076-3134, all whole 252-254 | 2781-2828, mode 3 258-258.5 | 2717-2739
+    // so the default (FBA_FLOW_BLOCK unset) makes every group whole (mode 1, the one setting that gains on
+    // both) for a throughput-bound factorisation -- update work per elimination-tree level >= 1 GFLOP
+    // (config 4: 0.39, config 5: 1.9, convergent: 1.6) -- and keeps quarters otherwise.  0: quarters,
+    // 1: every group whole, 2: all but the urgent last group, 3: the leading groups whose sources fit the
+    // levels left
+    double upd_flops = 0.0;
+    for (auto& t : tg) upd_flops += (double)t.second.size() * (t.first.first == t.first.second ? 3 : 4) * 2.0 * 64 * 64 * NB;
+    const int blockm = getenv("FBA_FLOW_BLOCK") ? atoi(getenv("FBA_FLOW_BLOCK")) : (nw > 0 && upd_flops / nw >= 1e9 ? 1 : 0);
+    if (verbose)
+        fprintf(stderr, "[fba] flow schedule: update work %.2f GFLOP over %d levels, update records mode %d\n", upd_flops * 1e-9,
+                nw, blockm);
     for (auto& t : tg) {
         const int32_t a = t.first.first, b = t.first.second;
         std::map<int, std::vector<int32_t>> bylev;
@@ -605,19 +627,21 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
                 glate.push_back(late_w);
             }
         }
-        // FBA_FLOW_BLOCK=0: off-diagonal targets by quarter tasks too.  Default: a whole-block task (q = 4)
-        // for an off-diagonal target with both row halves real -- its sources' rows loaded once for the four
-        // quarters (syrk_block_body); source entries k, A's two panel halves' flags, B's two
-        // FBA_FLOW_BLOCK=1: every group of such a target whole; 2 (default): the groups whose target is
-        // read later than the next level whole, the urgent last group by quarter tasks after them
-        static const int blockm = getenv("FBA_FLOW_BLOCK") ? atoi(getenv("FBA_FLOW_BLOCK")) : 2;
         const bool whole = blockm > 0 && a != b && halves(a) == 2 && halves(b) == 2;
         size_t gq = 0;        // the first group by quarter tasks
         int32_t wprev = -1;   // the whole-block chain's last writer flag
         if (whole) {
             gq = groups.size();
             if (blockm == 2 && level[b] == groups.back().first + 1) gq = groups.size() - 1;
+            // 3: a group is whole while its sources fit the levels left before the target is read
+            // (FBA_FLOW_BLOCK_R levels per source, default 1)
+            static const double blk_r = getenv("FBA_FLOW_BLOCK_R") ? atof(getenv("FBA_FLOW_BLOCK_R")) : 1.0;
+            if (blockm == 3)
+                for (gq = 0; gq < groups.size(); ++gq)
+                    if (std::min<double>((double)groups[gq].second.size(), SPLIT) * blk_r > level[b] - groups[gq].first - 1)
+                        break;
             int32_t prev = -1;
+            if (gq > 0) ++n_whole_t;
             for (size_t gi = 0; gi < gq; ++gi) {
                 const int w = groups[gi].first;
                 const std::vector<int32_t>& S = groups[gi].second;
@@ -962,9 +986,9 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
                 rb[3] * 1e-6, rb[4] * 1e-6, s.flow_flops * 1e-9);
     if (verbose)
         fprintf(stderr, "[fba] flow schedule: %d records (%d diagonal, %d panel halves, %d updates, %d inverses, "
-                "%d split helpers), %d progress + %d update flags, %d scratch quarters%s\n", n, s.flow_cnt[0],
-                s.flow_cnt[1], s.flow_cnt[2], s.flow_cnt[3], s.flow_cnt[4], np, s.flow_nuflag, nslot,
-                ok ? "" : " -- ORDER CHECK FAILED, not used");
+                "%d split helpers), %d progress + %d update flags, %d scratch quarters, %d of %d targets by whole-block "
+                "tasks, %d levels%s\n", n, s.flow_cnt[0], s.flow_cnt[1], s.flow_cnt[2], s.flow_cnt[3], s.flow_cnt[4], np,
+                s.flow_nuflag, nslot, n_whole_t, (int)tg.size(), nw, ok ? "" : " -- ORDER CHECK FAILED, not used");
 }
 
 void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pairs) {

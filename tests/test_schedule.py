@@ -24,16 +24,23 @@ def checker(tmp_path_factory):
     return exe
 
 
-@pytest.mark.parametrize("n_img,seed,leaf,merge,self_panel", [
-    (40, 1, None, None, 0), (300, 2, None, None, 0), (300, 1, 60, None, 0), (420, 3, 100, None, 0),
-    (200, 4, 0, None, 0), (300, 2, None, 1, 0), (300, 1, 60, 2, 0),
+@pytest.mark.parametrize("n_img,seed,leaf,merge,self_panel,block", [
+    (40, 1, None, None, 0, None), (300, 2, None, None, 0, None), (300, 1, 60, None, 0, None),
+    (420, 3, 100, None, 0, None), (200, 4, 0, None, 0, None), (300, 2, None, 1, 0, None), (300, 1, 60, 2, 0, None),
     # FBA_FLOW_SELF=1 (diagonal workgroups solving their fused source's panel rows; measured, off by default)
-    (300, 2, None, None, 1), (420, 3, 100, None, 1)])
-def test_level_schedule_matches_dense_cholesky(checker, n_img, seed, leaf, merge, self_panel):
+    (300, 2, None, None, 1, None), (420, 3, 100, None, 1, None),
+    # FBA_FLOW_BLOCK: whole-block update tasks -- every group (1, the default of a throughput-bound
+    # factorisation), all but the urgent last group (2), the groups with slack (3): whole-block and
+    # quarter writers of one target chained
+    (300, 2, None, None, 0, 1), (420, 3, 100, None, 0, 2), (300, 1, 60, 2, 0, 3), (40, 1, None, None, 0, 1)])
+def test_level_schedule_matches_dense_cholesky(checker, n_img, seed, leaf, merge, self_panel, block):
     env = dict(os.environ)
     env.pop("FBA_ND_LEAF", None)
     env.pop("FBA_FLOW_MERGE", None)
+    env.pop("FBA_FLOW_BLOCK", None)
     env["FBA_FLOW_SELF"] = str(self_panel)
+    if block is not None:
+        env["FBA_FLOW_BLOCK"] = str(block)
     if leaf is not None:
         env["FBA_ND_LEAF"] = str(leaf)
     if merge is not None:  # writer groups over consecutive source levels (build_flow)
@@ -42,7 +49,7 @@ def test_level_schedule_matches_dense_cholesky(checker, n_img, seed, leaf, merge
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
     fields = dict(f.split("=") for f in r.stdout.split()[1:])
     assert int(fields["levels"]) <= int(fields["blocks"])
-    if (n_img, seed, leaf, merge) == (300, 2, None, None):  # targets with > 2 source columns: split and combined
+    if (n_img, seed, leaf, merge, block) == (300, 2, None, None, None):  # targets with > 2 source columns: split and combined
         assert int(fields["split"]) > 0
     if leaf == 60:  # a dissected scene: independent subtrees share levels
         assert int(fields["levels"]) < int(fields["blocks"])
