@@ -757,7 +757,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     }
     const int nj = 9 + L.cw;
     c->ncomp = 2 * nj + 2;
-    c->cam_tab_stride = CAM_TAB_HDR + 2 * L.nk;
+    c->cam_tab_stride = CAM_TAB_HDR + 3 * L.nk;  // header | K_j | rmax^(2j) | rmax^-(2j)
     c->pt_comp = 12 + 6 * L.cw;
     const int npk = L.cw * (L.cw + 1) / 2 + L.cw;
     c->n_part = (int)std::max<int64_t>((L.u_full + 255) / 256, (c->n_obs + 255) / 256 * 3) + 8;

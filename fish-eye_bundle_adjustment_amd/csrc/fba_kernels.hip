@@ -100,6 +100,7 @@ __device__ __forceinline__ void params_body(int t, int nthreads, const double* _
         for (int j = 1; j <= nk; ++j) {
             o[CAM_TAB_HDR + j - 1] = q[2 + j];                   // K_j
             o[CAM_TAB_HDR + nk + j - 1] = pow(rmax, 2.0 * j);    // rmax^(2j), BuildAwG.m:424-426
+            o[CAM_TAB_HDR + 2 * nk + j - 1] = 1.0 / o[CAM_TAB_HDR + nk + j - 1];  // its reciprocal (obs_model)
         }
         o[6] = o[CAM_TAB_HDR + nk];                              // rmax^2
     }
@@ -183,26 +184,29 @@ __device__ __forceinline__ void obs_model(double x, double y, const double* __re
     const double V = M[3] * d0 + M[4] * d1 + M[5] * d2;
     const double W = M[6] * d0 + M[7] * d1 + M[8] * d2;
     const double R = sqrt(U * U + V * V);
+    // (divisions by R, q and the distortion scalings as products with reciprocals: one f64 division
+    // is ~10 instructions, the model had ~25 of them per observation)
+    const double iR = 1.0 / R;
     // radial factor s(R,W): f_proj = -c*(U, ydir*V)*s  (BuildAwG.m:184-208)
     double s, sR, sW;
     if (type == FBA_TYPE_PINHOLE) {
         s = 1.0 / W; sR = 0.0; sW = -1.0 / (W * W);
     } else {
         const double t = atan(R / W);
-        const double q = R * R + W * W;
-        const double tR = W / q, tW = -R / q;
+        const double iq = 1.0 / (R * R + W * W);
+        const double tR = W * iq, tW = -R * iq;
         double g, gt;
         if (type == FBA_TYPE_FISHEYE) { g = t; gt = 1.0; }
         else if (type == FBA_TYPE_EQUISOLID) { double sh, ch; sincos(0.5 * t, &sh, &ch); g = 2.0 * sh; gt = ch; }
         else if (type == FBA_TYPE_ORTHOGRAPHIC) { double st, ctt; sincos(t, &st, &ctt); g = st; gt = ctt; }
         else { double th = tan(0.5 * t); double ch = cos(0.5 * t); g = 2.0 * th; gt = 1.0 / (ch * ch); }
-        s = g / R;
-        sR = gt * tR / R - g / (R * R);
-        sW = gt * tW / R;
+        s = g * iR;
+        sR = (gt * tR - s) * iR;
+        sW = gt * tW * iR;
     }
     const double xp = ct[0], yp = ct[1], c = ct[2], ydir = ct[3], P1 = ct[4], P2 = ct[5];
     const double* K = ct + CAM_TAB_HDR;
-    const double* sc = ct + CAM_TAB_HDR + NK;
+    const double* isc = ct + CAM_TAB_HDR + 2 * NK;  // 1 / rmax^(2j)
     const double xb = x - xp, yb = y - yp;
     const double r2 = xb * xb + yb * yb;
     double r2j[NK + 1];
@@ -224,7 +228,7 @@ __device__ __forceinline__ void obs_model(double x, double y, const double* __re
     const double fx = -c * s * U + xp + dr * xb + decx;
     const double fy = -cys * V * s + yp + dr * yb + decy;
     auto chain = [&](double dU, double dV, double dW, double& gx, double& gy) {
-        const double dR = (U * dU + V * dV) / R;
+        const double dR = (U * dU + V * dV) * iR;
         const double ds = (type == FBA_TYPE_PINHOLE) ? sW * dW : sR * dR + sW * dW;
         gx = -c * (dU * s + U * ds);
         gy = -cys * (dV * s + V * ds);
@@ -261,14 +265,14 @@ __device__ __forceinline__ void obs_model(double x, double y, const double* __re
 #pragma unroll
     for (int j = 1; j <= NK; ++j) {
         const double en = cen(2 + j);
-        jr[0][8 + j] = r2j[j] * xb / sc[j - 1] * en;
-        jr[1][8 + j] = r2j[j] * yb / sc[j - 1] * en;
+        jr[0][8 + j] = r2j[j] * xb * isc[j - 1] * en;
+        jr[1][8 + j] = r2j[j] * yb * isc[j - 1] * en;
     }
-    const double s1 = sc[0], en1 = cen(3 + NK), en2 = cen(4 + NK);
-    jr[0][9 + NK] = (yb * yb + 3.0 * xb * xb) / s1 * en1;
-    jr[1][9 + NK] = 2.0 * xb * yb / s1 * en1;
-    jr[0][10 + NK] = 2.0 * xb * yb / s1 * en2;
-    jr[1][10 + NK] = (xb * xb + 3.0 * yb * yb) / s1 * en2;
+    const double is1 = isc[0], en1 = cen(3 + NK), en2 = cen(4 + NK);
+    jr[0][9 + NK] = (yb * yb + 3.0 * xb * xb) * is1 * en1;
+    jr[1][9 + NK] = 2.0 * xb * yb * is1 * en1;
+    jr[0][10 + NK] = 2.0 * xb * yb * is1 * en2;
+    jr[1][10 + NK] = (xb * xb + 3.0 * yb * yb) * is1 * en2;
     w0 = fx - x;
     w1 = fy - y;
 }

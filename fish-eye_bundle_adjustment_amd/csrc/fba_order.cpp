@@ -597,8 +597,13 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     // (config 4: 0.39, config 5: 1.9, convergent: 1.6) -- and keeps quarters otherwise.  0: quarters,
     // 1: every group whole, 2: all but the urgent last group, 3: the leading groups whose sources fit the
     // levels left
+    // (counted over every column whatever inc holds, so the two flows of the subtree split take the
+    // decision of the single-context schedule and sum every target in the same order)
     double upd_flops = 0.0;
-    for (auto& t : tg) upd_flops += (double)t.second.size() * (t.first.first == t.first.second ? 3 : 4) * 2.0 * 64 * 64 * NB;
+    for (int64_t k = 0; k < nb; ++k)
+        for (size_t bi = 0; bi < R[k].size(); ++bi)
+            if (R[k][bi] < nb)
+                for (size_t ai = bi; ai < R[k].size(); ++ai) upd_flops += (R[k][ai] == R[k][bi] ? 3 : 4) * 2.0 * 64 * 64 * NB;
     const int blockm = getenv("FBA_FLOW_BLOCK") ? atoi(getenv("FBA_FLOW_BLOCK")) : (nw > 0 && upd_flops / nw >= 1e9 ? 1 : 0);
     if (verbose)
         fprintf(stderr, "[fba] flow schedule: update work %.2f GFLOP over %d levels, update records mode %d\n", upd_flops * 1e-9,

@@ -305,7 +305,7 @@ def test_subtree_split_two_ranks_match_single_context(fba, scenes, config):
     columns' Gram partials and inner-constraint weight sums) summed on the host as the RCCL all-reduce
     would; each then factors the top columns, back-substitutes and updates.  Over two Gauss-Newton passes
     at configs 3, 4 and 5 the ranks' owned entries reassemble the single context's xhat to 1e-10 per
-    parameter group and 1e-9 per element, and the deltasum shares add up to the single context's
+    parameter group (1e-9 at config 5, below) and 1e-9 per element, and the deltasum shares add up to the single context's
     deltasum.  (One GPU stands in for two: the collective itself is unmeasured here.)"""
     import ctypes
     folder = _scene(config, scenes)
@@ -339,8 +339,13 @@ def test_subtree_split_two_ranks_match_single_context(fba, scenes, config):
         names = fba.xhat_names(ds)
         dsc = dist_scaling_of(__import__("fba_oracle").load_folder(folder))
         err = group_rel_err(xr, xs, names, dsc)
-        assert max(err.values()) <= 1e-10, err
+        print("split vs single, relative error per group:", {g: f"{e:.2e}" for g, e in err.items()})
+        # config 5's radial-distortion direction is the ill-conditioned one (the oracle's KKT solve reports
+        # rcond ~1e-16): reduction-order rounding moves k1 by up to ~2e-10 of its group there (2.9e-11 at
+        # config 3, 1.3e-12 at config 4), so config 5 is held to the oracle test's own 1e-9
+        assert max(err.values()) <= (1e-9 if config == 5 else 1e-10), err
         err = elem_rel_err(xr, xs, names, dsc)
+        print("split vs single, relative error per element:", {g: f"{e:.2e}" for g, e in err.items()})
         assert max(err.values()) <= 1e-9, err
     finally:
         single.close()
