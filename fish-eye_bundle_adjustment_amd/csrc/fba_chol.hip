@@ -2696,11 +2696,12 @@ __device__ __forceinline__ void syrk_block_body(double* __restrict__ S, int64_t 
     if (!sv[1]) return;
     if (rec[9] >= 0 && tid == 0) spin_ge(fl + rec[9], 1u, scal);
     __syncthreads();  // (also orders the partial loads below after the arrival)
-    for (int h = 0; h < 2; ++h) {  // the block in two 64-row halves: 4 double2 per thread each
+    static_assert(POTRF_THREADS * 4 * 2 == 32 * 128, "the combine's 32-row quarters: 4 double2 per thread each");
+    for (int h = 0; h < 4; ++h) {  // the block in four 32-row quarters: 4 double2 per thread each
         double2 v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int e2 = 2 * (tid + POTRF_THREADS * u), r = 64 * h + (e2 >> 7), cl = e2 & 127;
+            const int e2 = 2 * (tid + POTRF_THREADS * u), r = 32 * h + (e2 >> 7), cl = e2 & 127;
             v[u] = ld_sc1(rC, ((int64_t)r * ld + cl) * 8);
         }
         for (int g = 0; g < rec[12]; ++g) {
@@ -2708,7 +2709,7 @@ __device__ __forceinline__ void syrk_block_body(double* __restrict__ S, int64_t 
             double2 pv[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int e2 = 2 * (tid + POTRF_THREADS * u), r = 64 * h + (e2 >> 7), cl = e2 & 127;
+                const int e2 = 2 * (tid + POTRF_THREADS * u), r = 32 * h + (e2 >> 7), cl = e2 & 127;
                 pv[u] = ld_sc1(rg, (int64_t)(r * 128 + cl) * 8);
             }
 #pragma unroll
@@ -2716,7 +2717,7 @@ __device__ __forceinline__ void syrk_block_body(double* __restrict__ S, int64_t 
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int e2 = 2 * (tid + POTRF_THREADS * u), r = 64 * h + (e2 >> 7), cl = e2 & 127;
+            const int e2 = 2 * (tid + POTRF_THREADS * u), r = 32 * h + (e2 >> 7), cl = e2 & 127;
             st_sc1(rC, ((int64_t)r * ld + cl) * 8, v[u]);
         }
     }

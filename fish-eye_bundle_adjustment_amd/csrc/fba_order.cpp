@@ -429,7 +429,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     // groups of at most SPLIT, summed through scratch partials when there are several groups); config 4
     // (iter/s, two runs each): 1: 1050, 2: 1120 / 1137, 3: 1153 / 1143, 4: 1152 / 1147, all in one: 1087
     // -- fewer update records hold fewer CUs while waiting for their sources' columns
-    static const int SPLIT = getenv("FBA_FLOW_SPLIT") ? std::max(1, atoi(getenv("FBA_FLOW_SPLIT"))) : 4;
+    const int SPLIT = getenv("FBA_FLOW_SPLIT") ? std::max(1, atoi(getenv("FBA_FLOW_SPLIT"))) : 4;
     const int nw = nb > 0 ? 1 + *std::max_element(level.begin(), level.end()) : 0;
     std::vector<std::vector<int32_t>> srcs(nb);
     for (int64_t k = 0; k < nb; ++k)
@@ -510,8 +510,8 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     // FBA_FLOW_MERGE = G: writer groups over consecutive source levels when the target is read >= G levels later
     // (config 4, k_chol_flow per launch: G = 0 / 1 / 2 / 3: 465 / 458 / 453 / 454 us; convergent config 4:
     // 3.80 / 3.18 / 3.22 ms); FBA_FLOW_MSPLIT: the sources a merged group may hold (default SPLIT)
-    static const int merge_gap = getenv("FBA_FLOW_MERGE") ? atoi(getenv("FBA_FLOW_MERGE")) : 2;
-    static const int msplit = getenv("FBA_FLOW_MSPLIT") ? std::max(1, atoi(getenv("FBA_FLOW_MSPLIT"))) : SPLIT;
+    const int merge_gap = getenv("FBA_FLOW_MERGE") ? atoi(getenv("FBA_FLOW_MERGE")) : 2;
+    const int msplit = getenv("FBA_FLOW_MSPLIT") ? std::max(1, atoi(getenv("FBA_FLOW_MSPLIT"))) : SPLIT;
     static const int promote_mode = getenv("FBA_FLOW_PROMOTE") ? atoi(getenv("FBA_FLOW_PROMOTE")) : 0;
     static const int lookahead = getenv("FBA_FLOW_LOOKAHEAD") ? atoi(getenv("FBA_FLOW_LOOKAHEAD")) : 1000;
     int nslot = 0, ncnt = 0, n_whole_t = 0;
@@ -640,7 +640,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
             if (blockm == 2 && level[b] == groups.back().first + 1) gq = groups.size() - 1;
             // 3: a group is whole while its sources fit the levels left before the target is read
             // (FBA_FLOW_BLOCK_R levels per source, default 1)
-            static const double blk_r = getenv("FBA_FLOW_BLOCK_R") ? atof(getenv("FBA_FLOW_BLOCK_R")) : 1.0;
+            const double blk_r = getenv("FBA_FLOW_BLOCK_R") ? atof(getenv("FBA_FLOW_BLOCK_R")) : 1.0;
             if (blockm == 3)
                 for (gq = 0; gq < groups.size(); ++gq)
                     if (std::min<double>((double)groups[gq].second.size(), SPLIT) * blk_r > level[b] - groups[gq].first - 1)

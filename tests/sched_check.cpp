@@ -116,7 +116,8 @@ int main(int argc, char** argv) {
     std::vector<std::pair<int32_t, int32_t>> pairs(ps.begin(), ps.end());
     build_schedule(c, pairs);
     const Sched& s = c.sched;
-    if (stats_only) {
+    // (SCHED_EMULATE=1 with an observation file: the emulation below on that network instead of the stats)
+    if (stats_only && !getenv("SCHED_EMULATE")) {
         std::vector<int> per(s.n_waves);
         for (int w = 0; w < s.n_waves; ++w) per[w] = s.w[w].ncol;
         printf("ok levels=%d blocks=%ld slots=%d tiles=%ld cols/level:", s.n_waves, (long)(L.n_pad / NB), L.n_img,

@@ -72,16 +72,20 @@ def test_config3_adjust_matches_oracle(fba, fbo, oracle, scenes):
 
 @pytest.mark.parametrize("env", [{"FBA_CHOL_FLOW": "0"}, {"FBA_BWD_LEVELS": "1"},
                                  {"FBA_CHOL_FLOW": "0", "FBA_BWD_LEVELS": "1"},
-                                 {"FBA_FLOW_BLOCK": "1"}, {"FBA_FLOW_BLOCK": "3"}],
+                                 {"FBA_FLOW_BLOCK": "1"}, {"FBA_FLOW_BLOCK": "3"},
+                                 {"FBA_FLOW_BLOCK": "1", "FBA_FLOW_SPLIT": "1"},
+                                 {"FBA_FLOW_BLOCK": "1", "FBA_FLOW_MSPLIT": "8"}],
                          ids=["per-level-factor", "per-level-backward", "both", "whole-block-updates",
-                              "whole-block-then-quarters"])
+                              "whole-block-then-quarters", "whole-block-partials", "whole-block-merged-partials"])
 def test_config3_fallback_paths_match_oracle(fba, fbo, oracle, scenes, env, monkeypatch):
     """The non-default solve paths (read per context in chol_setup): the per-level k_panel launches
     instead of the persistent k_chol_flow (with k_border_gram -> k_border_combine), and the per-level
     k_bwd_wave backward solve instead of k_bwd_flow -- the paths build_flow's order check falls back
     to, and the one the 2-rank rehearsal used.  FBA_FLOW_BLOCK: k_chol_flow's whole-block update records
     (syrk_block_body; config 3 is latency-bound, so its default is quarter records) for every writer
-    group, or for the leading groups with the quarter records chained after them."""
+    group, or for the leading groups with the quarter records chained after them; with one source per
+    record (FBA_FLOW_SPLIT=1) or merged writer groups of up to 8 sources (FBA_FLOW_MSPLIT=8), so targets
+    are summed through the 128 x 128 scratch partials the last arriving record combines."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     _check_adjust(fba, fbo, oracle, _scene(3, scenes))

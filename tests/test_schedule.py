@@ -32,15 +32,22 @@ def checker(tmp_path_factory):
     # FBA_FLOW_BLOCK: whole-block update tasks -- every group (1, the default of a throughput-bound
     # factorisation), all but the urgent last group (2), the groups with slack (3): whole-block and
     # quarter writers of one target chained
-    (300, 2, None, None, 0, 1), (420, 3, 100, None, 0, 2), (300, 1, 60, 2, 0, 3), (40, 1, None, None, 0, 1)])
+    (300, 2, None, None, 0, 1), (420, 3, 100, None, 0, 2), (300, 1, 60, 2, 0, 3), (40, 1, None, None, 0, 1),
+    (300, 2, None, None, 0, "1s1"), (420, 3, 100, None, 0, "1m8")])
 def test_level_schedule_matches_dense_cholesky(checker, n_img, seed, leaf, merge, self_panel, block):
     env = dict(os.environ)
     env.pop("FBA_ND_LEAF", None)
     env.pop("FBA_FLOW_MERGE", None)
     env.pop("FBA_FLOW_BLOCK", None)
     env["FBA_FLOW_SELF"] = str(self_panel)
-    if block is not None:
-        env["FBA_FLOW_BLOCK"] = str(block)
+    env.pop("FBA_FLOW_SPLIT", None)
+    env.pop("FBA_FLOW_MSPLIT", None)
+    if block is not None:  # "1s1": one source per record, "1m8": merged groups of up to 8 sources
+        env["FBA_FLOW_BLOCK"] = str(block)[0]
+        if str(block)[1:2] == "s":
+            env["FBA_FLOW_SPLIT"] = str(block)[2:]
+        if str(block)[1:2] == "m":
+            env["FBA_FLOW_MSPLIT"] = str(block)[2:]
     if leaf is not None:
         env["FBA_ND_LEAF"] = str(leaf)
     if merge is not None:  # writer groups over consecutive source levels (build_flow)
