@@ -739,16 +739,23 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     // xor-butterfly over the 8 lanes; part-major unit order keeps the rows of a wave on one path
     constexpr int HALF = (CW + 1) / 2;
     constexpr int IV = 27 > 6 * HALF ? 27 : 6 * HALF;  // values per unit
-    constexpr int NV = (IV + 7) / 8 * 8, M = NV / 8;     // padded to the 8-lane reduce-scatter
+#ifndef FBA_IK_LANES
+#define FBA_IK_LANES 8
+#endif
+    // lanes per unit (8 or 4; -DFBA_IK_LANES=4 measured: image keys 6.54 -> 8.82 us per chunk, 1,229 ->
+    // 1,190 iter/s -- fewer lanes per key serialise more observations per lane)
+    constexpr int GL = FBA_IK_LANES;
+    static_assert(GL == 8 || GL == 4, "image-key lanes per unit");
+    constexpr int NV = (IV + GL - 1) / GL * GL, M = NV / GL;  // padded to the GL-lane reduce-scatter
     {
-        const int nk = ki1 - ki0, nu = 3 * nk, g8 = t & 7;
-        for (int ub = t >> 3; ub < nu && !(dbg & 1); ub += LR_THREADS / 8) {
+        const int nk = ki1 - ki0, nu = 3 * nk, g8 = t & (GL - 1);
+        for (int ub = t / GL; ub < nu && !(dbg & 1); ub += LR_THREADS / GL) {
             const int part = ub / nk, K = ki0 + ub % nk;
             const int x0 = s_iko[K - ki0], x1 = s_iko[K - ki0 + 1];
             double v[NV];
 #pragma unroll
             for (int q = 0; q < NV; ++q) v[q] = 0.0;
-            for (int x = x0 + g8; x < x1; x += 8) {
+            for (int x = x0 + g8; x < x1; x += GL) {
                 const int l = s_ikobs[x];
                 const double* E = QE + l * ES;
                 const double* u = Us + l * US;
@@ -792,16 +799,21 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
                     }
                 }
             }
-            // reduce-scatter over the group's 8 lanes in three DPP exchange steps (partners 7 - i, i ^ 2,
-            // i ^ 1): each step a lane keeps half of its values, adds the partner's copy of that half and
-            // hands over the other half, so lane g8 ends with the M fully summed values
-            // q = 4M b2 + 2M b1 + M b0 + j (b = bits of g8), in a fixed order
+            // reduce-scatter over the group's GL lanes in log2(GL) DPP exchange steps (partners 7 - i
+            // (GL = 8 only), i ^ 2, i ^ 1): each step a lane keeps half of its values, adds the partner's
+            // copy of that half and hands over the other half, so lane g8 ends with the M fully summed
+            // values q = 4M b2 + 2M b1 + M b0 + j (b = bits of g8), in a fixed order
             double h4[4 * M], h2[2 * M], h1[M];
             const bool bA = (g8 & 4) != 0, bB = (g8 & 2) != 0, bC = (g8 & 1) != 0;
+            if constexpr (GL == 8) {
 #pragma unroll
-            for (int j = 0; j < 4 * M; ++j) {
-                const double keep = bA ? v[4 * M + j] : v[j], give = bA ? v[j] : v[4 * M + j];
-                h4[j] = keep + dpp_d<0x141>(give);  // row_half_mirror
+                for (int j = 0; j < 4 * M; ++j) {
+                    const double keep = bA ? v[4 * M + j] : v[j], give = bA ? v[j] : v[4 * M + j];
+                    h4[j] = keep + dpp_d<0x141>(give);  // row_half_mirror
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4 * M; ++j) h4[j] = v[j];
             }
 #pragma unroll
             for (int j = 0; j < 2 * M; ++j) {
@@ -813,7 +825,7 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
                 const double keep = bC ? h2[M + j] : h2[j], give = bC ? h2[j] : h2[M + j];
                 h1[j] = keep + dpp_d<0xB1>(give);  // quad_perm [1,0,3,2]
             }
-            const int q0 = (bA ? 4 * M : 0) + (bB ? 2 * M : 0) + (bC ? M : 0);
+            const int q0 = (GL == 8 && bA ? 4 * M : 0) + (bB ? 2 * M : 0) + (bC ? M : 0);
             // part 0: the 27 values at out[0 ..]; parts 1, 2: the 6 nq values of cameras columns
             // (part - 1) HALF .. at out[27 + 6 (part - 1) HALF ..]
             const int nval = part == 0 ? 27 : 6 * min(HALF, CW - (part - 1) * HALF);
