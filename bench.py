@@ -209,7 +209,8 @@ def main():
     flow = os.environ.get("FBA_CHOL_FLOW", "1") != "0"
     roof = probe(2, "k_chol_flow", "the whole block Cholesky + forward solve in one persistent dataflow launch: "
                                    "128x128 f64 diagonal-block potrfs, 64-row panel-half solves, 64x64 trailing-"
-                                   "update quarters, diagonal-block inverses; flops = their algorithmic sum; a "
+                                   "update quarters (128x128 whole-block updates when the schedule is throughput-"
+                                   "bound), diagonal-block inverses; flops = their algorithmic sum; a "
                                    "latency-bound chain over the elimination-tree levels") if flow else \
         probe(2, "k_panel", "one elimination-tree level: the 128x128 f64 diagonal-block potrf, the panel "
                             "solves and the previous level's trailing updates as in-launch dataflow; a latency-"
