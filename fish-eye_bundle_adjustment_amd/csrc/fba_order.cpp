@@ -435,6 +435,23 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     for (int64_t k = 0; k < nb; ++k)
         for (int32_t i : R[k])
             if (i < nb && in(k)) srcs[i].push_back((int32_t)k);
+    // dispatch keys by "as late as possible" levels (FBA_FLOW_ALAP=1): a column's key level is its
+    // elimination-tree parent's minus one (the root keeps its own), so the records of a shallow subtree,
+    // which has slack before its parent needs it, sort behind the same-level records of the longest chain
+    // (levels count up from the leaves, so a shallow subtree's records otherwise come first).  Measured
+    // and not kept (iter/s | k_chol_flow us, same box): config 4 1197-1202 | 474-482 vs 1238-1244 |
+    // 456-458, config 5 265 | 2568 vs 279 | 2388, convergent unchanged (one chain) -- a shallow subtree's
+    // records dispatched late then hold the CUs when the chain's own records arrive
+    const bool alapm = getenv("FBA_FLOW_ALAP") && atoi(getenv("FBA_FLOW_ALAP")) != 0;
+    std::vector<int> klev(level.begin(), level.end());
+    if (alapm)
+        for (int64_t j = nb - 1; j >= 0; --j) {
+            int32_t par = -1;
+            for (int32_t r : R[j])
+                if (r > j && r < nb && (par < 0 || r < par)) par = r;
+            if (par >= 0) klev[j] = std::max(level[j], klev[par] - 1);
+        }
+    auto kl = [&](int64_t x) { return klev[x]; };
     std::vector<int32_t> fsrc(nb, -1);
     // FBA_FLOW_FUSE=0: no fused sources (every diagonal update by update tasks; the potrf loads its block)
     static const bool fuse = !(getenv("FBA_FLOW_FUSE") && atoi(getenv("FBA_FLOW_FUSE")) == 0);
@@ -519,7 +536,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     for (int64_t j = 0; j < nb; ++j) {
         if (!in(j)) continue;
         const int32_t f = fsrc[j];
-        int need = level[j] - 1;
+        int need = kl(j) - 1;
         const bool sp = f >= 0 && self_panel(f, j);
         const int32_t p0 = f >= 0 ? prog[std::make_tuple(f, (int32_t)j, 0)] : -1;
         const int32_t p1 = (f >= 0 && halves(j) > 1 && !sp) ? prog[std::make_tuple(f, (int32_t)j, 1)] : -1;
@@ -562,7 +579,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
                 // chain) are dispatched among the previous level's records, 2 = every panel half
                 const bool promote = promote_mode == 2 || (promote_mode == 1 && r < nb && fsrc[r] == (int32_t)k);
                 const int id = add({1, (int32_t)k, 2 * r + h, 0, 0, p, 0, (r == nb && h == 0) ? (int32_t)k : -1},
-                                   {level[k] - (promote ? 1 : 0), 1, (int)(k * (nb + 1) + r) * 2 + h});
+                                   {kl(k) - (promote ? 1 : 0), 1, (int)(k * (nb + 1) + r) * 2 + h});
                 T[id].deps.push_back(col_task[k]);
                 prog_task[p] = id;
                 s.flow_flops += 64.0 * NB * NB;
@@ -673,8 +690,10 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
                         slot = nslot;
                         nslot += 4;
                     }
-                    const int need = level[b];
-                    const int lev = defer > 0 ? std::max(w, std::min(w + defer, need - 1)) : std::max(w, need - lookahead);
+                    int wk = w;
+                    for (int32_t k : S) wk = std::max(wk, kl(k));
+                    const int need = kl(b);
+                    const int lev = defer > 0 ? std::max(wk, std::min(wk + defer, need - 1)) : std::max(wk, need - lookahead);
                     const int id = add({2, a, b, 4, soff, g1 - g0, slot, mode, wflag, prev, cidx, first, ng, 0, CB_BLOCKS},
                                        {lev, rank, (int)(b * (nb + 1) + a) * 4});
                     flag_deps[id] = fd;
@@ -734,10 +753,12 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
                     // target is read (its diagonal workgroup at level[b] - 1, its panel halves at
                     // level[b]), so updates of far-away targets do not hold CUs ahead of the next
                     // levels' panel halves
-                    const int need = a == b ? level[b] - 1 : level[b];
+                    int wk = w;
+                    for (int32_t k : S) wk = std::max(wk, kl(k));
+                    const int need = a == b ? kl(b) - 1 : kl(b);
                     // FBA_FLOW_DEFER = N: among the records of level min(source level + N, need - 1)
-                    const int lev = defer > 0 && !is_late ? std::max(w, std::min(w + defer, need - 1))
-                                                          : std::max(w, need - lookahead);
+                    const int lev = defer > 0 && !is_late ? std::max(wk, std::min(wk + defer, need - 1))
+                                                          : std::max(wk, need - lookahead);
                     const int id = add({2, a, b, q, soff, g1 - g0, slot, mode, flag, is_late ? -1 : prev, cidx, first, ng, 0,
                                         CB_BLOCKS},
                                        {lev, is_late ? 2 : rank, (int)(b * (nb + 1) + a) * 4 + q});
@@ -820,7 +841,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     static const bool inv_last = getenv("FBA_FLOW_INV_LAST") && atoi(getenv("FBA_FLOW_INV_LAST")) != 0;
     for (int64_t j = 0; j < nb; ++j)
         if (level[j] < nw - 1 && in(j)) {
-            const int id = add({3, (int32_t)j}, {inv_last ? nw : level[j] + 1, 5, (int)j});
+            const int id = add({3, (int32_t)j}, {inv_last ? nw : kl(j) + 1, 5, (int)j});
             T[id].deps.push_back(col_task[j]);
             s.flow_flops += (double)NB * NB * NB / 3.0;
         }
