@@ -493,11 +493,16 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     std::vector<std::vector<int>> uflag_tasks;  // update flag -> the records that may raise it
     std::vector<std::vector<int32_t>> flag_deps;  // per record: flags it waits for (resolved to records)
     auto new_uflag = [&]() { uflag_tasks.emplace_back(); return (int32_t)(np + uflag_tasks.size() - 1); };
+    // FBA_FLOW_TIE=1: within a (level, role) the records of higher block columns first (the nested
+    // dissection numbers the separators, the longest chain, last); measured and not kept: config 4
+    // 1228-1230 | 458-466 us vs 1240-1245 | 449-454 us, config 5 unchanged
+    const bool tie_desc = getenv("FBA_FLOW_TIE") && atoi(getenv("FBA_FLOW_TIE")) == 1;
     auto add = [&](std::initializer_list<int32_t> r, std::array<int, 3> key) {
         Task t;
         t.rec.fill(0);
         int q = 0;
         for (int32_t v : r) t.rec[q++] = v;
+        if (tie_desc) key[2] = -key[2];
         t.key = key;
         T.push_back(std::move(t));
         flag_deps.emplace_back();
