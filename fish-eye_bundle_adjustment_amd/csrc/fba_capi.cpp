@@ -653,6 +653,15 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     A.rp_list = put(rp_list);
     A.ri_start = put(ri_start);
     A.ri_list = put(ri_list);
+    {
+        std::vector<int32_t> pk_slot(rp_list.size()), ik_slot(ri_list.size());
+        for (size_t x = 0; x < rp_list.size(); ++x) pk_slot[rp_list[x]] = (int32_t)x;
+        for (size_t x = 0; x < ri_list.size(); ++x) ik_slot[ri_list[x]] = (int32_t)x;
+        A.pk_slot = put(pk_slot);
+        A.ik_slot = put(ik_slot);
+        G.pk_slot = A.pk_slot;
+        G.ik_slot = A.ik_slot;
+    }
     A.img_cam = put(img_cam);
     A.rc_start = put(rc_start);
     A.rc_list = put(rc_list);

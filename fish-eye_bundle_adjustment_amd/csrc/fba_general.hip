@@ -184,7 +184,7 @@ __global__ __launch_bounds__(256) void k_gen_keys(const double* __restrict__ J, 
         const int v = (int)(t % 36), a = v / 6, b = v % 6;
         const double* u1 = gug + (int64_t)A[g.gpk + 2 * k] * GUG;
         const double* u2 = gug + (int64_t)A[g.gpk + 2 * k + 1] * GUG;
-        ppart[(g.pk0 + k) * 36 + v] = -dot3(u1 + 3 * a, u2 + 3 * b);
+        ppart[(int64_t)A[g.pk_slot + g.pk0 + k] * 36 + v] = -dot3(u1 + 3 * a, u2 + 3 * b);
         return;
     }
     t -= g.n_gpk * 36;
@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256) void k_gen_keys(const double* __restrict__ J, 
             }
             r = dot3(ug + 3 * a, gcu + (int64_t)A[g.gi_gc + gi] * GC + 3 * b);
         }
-        ipart[(g.ik0 + gi) * NIMG + v] = s - r;
+        ipart[(int64_t)A[g.ik_slot + g.ik0 + gi] * NIMG + v] = s - r;
         return;
     }
     t -= g.n_gi * NIMG;

@@ -144,6 +144,11 @@ struct AccPlan {
     int64_t rp_list = 0;
     int64_t ri_start = 0;  // [n_img+1] image keys of each image
     int64_t ri_list = 0;
+    // partial slots: the partials are stored pair-major / image-major (ppart row pk_slot[K] for pair key
+    // K, ipart row ik_slot[K] for image key K), so k_red_blocks reads each pair's / image's partials as
+    // one contiguous range [rp_start, rp_start+1) / [ri_start, ..) in the same (chunk) order as rp_list
+    int64_t pk_slot = 0;   // [n_pk] = the inverse of rp_list
+    int64_t ik_slot = 0;   // [n_ik] = the inverse of ri_list
     int64_t img_cam = 0;   // [n_img] camera of each image (-1: no local observation)
     int64_t rc_start = 0;  // [n_cam+1] chunks of each camera
     int64_t rc_list = 0;
@@ -177,6 +182,7 @@ struct GenPlan {
     int64_t xt_start = 0, xt_list = 0, xt_key = 0;  // image x foreign camera blocks: [n_xt+1], slots, [2 n_xt] (e, k)
     int64_t kt_start = 0, kt_list = 0, kt_key = 0;  // camera x camera blocks: [n_kt+1], slots, [2 n_kt] (k1 > k2)
     int64_t pk0 = 0, ik0 = 0, ck0 = 0;  // first partial slot of the general keys in ppart / ipart / cpart
+    int64_t pk_slot = 0, ik_slot = 0;   // AccPlan::pk_slot / ik_slot (the keys' rows in ppart / ipart)
 };
 
 struct Ctx {

@@ -437,7 +437,7 @@ struct LR {
     // + ints: point of each observation, the chunk's plan (pair-key term offsets, terms, image-key
     // observation offsets, observations)
     static constexpr int CP = chunk_pts(NK), CT = chunk_terms(NK);
-    static constexpr int NI = CHUNK_OBS + (CT + 1) + CT + (CHUNK_OBS + 1) + CHUNK_OBS;
+    static constexpr int NI = CHUNK_OBS + (CT + 1) + CT + (CHUNK_OBS + 1) + CHUNK_OBS + CT + CHUNK_OBS;
     // camera entries: CAM_SPLIT - 1 observation sub-ranges and the points' Schur terms in parallel
     static constexpr int CAM_SPLIT = 512 / NCAM;
     static_assert(CAM_SPLIT >= 2, "camera entries: at least one observation part and the points' part");
@@ -495,6 +495,8 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     int* s_term = s_pkt + R_::CT + 1;                        // [<= CT]
     int* s_iko = s_term + R_::CT;                            // [<= CHUNK_OBS + 1] observation offsets of image keys
     int* s_ikobs = s_iko + CHUNK_OBS + 1;                    // [<= CHUNK_OBS]
+    int* s_pks = s_ikobs + CHUNK_OBS;                        // [<= CT] the pair keys' partial rows (pk_slot)
+    int* s_iks = s_pks + R_::CT;                             // [<= CHUNK_OBS] the image keys' rows (ik_slot)
     const int t = threadIdx.x;
     const int c = blockIdx.x;
     const int o0 = chunk_obs[c], o1 = chunk_obs[c + 1];
@@ -530,7 +532,9 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
         if (stage_terms) {
             stage(kp1 - kp0 + 1, A + plan.pk_t + kp0, tb0, s_pkt);
             stage(ntm, A + plan.pk_term + tb0, 0, s_term);
+            stage(kp1 - kp0, A + plan.pk_slot + kp0, 0, s_pks);
         }
+        stage(ki1 - ki0, A + plan.ik_slot + ki0, 0, s_iks);
         stage(ki1 - ki0 + 1, A + plan.ik_o + ki0, ob0, s_iko);
         stage(nio, A + plan.ik_obs + ob0, 0, s_ikobs);
     }
@@ -829,7 +833,7 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
             // part 0: the 27 values at out[0 ..]; parts 1, 2: the 6 nq values of cameras columns
             // (part - 1) HALF .. at out[27 + 6 (part - 1) HALF ..]
             const int nval = part == 0 ? 27 : 6 * min(HALF, CW - (part - 1) * HALF);
-            double* out = ipart + (int64_t)K * NIMG + (part == 0 ? 0 : 27 + 6 * (part - 1) * HALF);
+            double* out = ipart + (int64_t)s_iks[K - ki0] * NIMG + (part == 0 ? 0 : 27 + 6 * (part - 1) * HALF);
 #pragma unroll
             for (int j = 0; j < M; ++j)
                 if (q0 + j < nval) out[q0 + j] = h1[j];
@@ -863,9 +867,11 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
                     for (int b = 0; b < 6; ++b)
                         acc[6 * h + b] += vi[3 * h] * vj[3 * b] + vi[3 * h + 1] * vj[3 * b + 1] + vi[3 * h + 2] * vj[3 * b + 2];
             }
-            double* out = ppart + (int64_t)K * 36 + 6 * a0;
+            // (the key's row: pair-major slot, staged with the plan lists; 16-B aligned, as 6 double2 stores)
+            double2* out = reinterpret_cast<double2*>(
+                ppart + (int64_t)(stage_terms ? s_pks[K - kp0] : A[plan.pk_slot + K]) * 36 + 6 * a0);
 #pragma unroll
-            for (int q = 0; q < 12; ++q) out[q] = -acc[q];
+            for (int q = 0; q < 6; ++q) out[q] = double2{-acc[2 * q], -acc[2 * q + 1]};
         }
     };
     if (!(dbg & 2)) {  // FBA_LR_SKIP (profiling only): bit 2 leaves out the pair items
@@ -882,28 +888,25 @@ __device__ __forceinline__ void red_pairs_body(int blk, const double* __restrict
     const int64_t pr = (int64_t)blk * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (pr >= n_pairs || lane >= 36) return;
-    // the partials in chunk order, 8 (then 4) loads in flight (fixed association: ((s + p0) + p1) + ...)
+    // the partials in chunk order, one contiguous range (pair-major slots), 8 (then 4) loads in flight
+    // (fixed association: ((s + p0) + p1) + ...)
     const int q0 = A[plan.rp_start + pr], q1 = A[plan.rp_start + pr + 1];
+    const double* pp = ppart + lane;
     double s = 0.0;
     int q = q0;
     for (; q + 8 <= q1; q += 8) {
-        int id[8];
         double p[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) id[j] = A[plan.rp_list + q + j];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) p[j] = ppart[(int64_t)id[j] * 36 + lane];
+        for (int j = 0; j < 8; ++j) p[j] = pp[(int64_t)(q + j) * 36];
 #pragma unroll
         for (int j = 0; j < 8; ++j) s += p[j];
     }
     for (; q + 4 <= q1; q += 4) {
-        const int i0 = A[plan.rp_list + q], i1 = A[plan.rp_list + q + 1], i2 = A[plan.rp_list + q + 2],
-                  i3 = A[plan.rp_list + q + 3];
-        const double p0 = ppart[(int64_t)i0 * 36 + lane], p1 = ppart[(int64_t)i1 * 36 + lane],
-                     p2 = ppart[(int64_t)i2 * 36 + lane], p3 = ppart[(int64_t)i3 * 36 + lane];
+        const double p0 = pp[(int64_t)q * 36], p1 = pp[(int64_t)(q + 1) * 36], p2 = pp[(int64_t)(q + 2) * 36],
+                     p3 = pp[(int64_t)(q + 3) * 36];
         s = (((s + p0) + p1) + p2) + p3;
     }
-    for (; q < q1; ++q) s += ppart[(int64_t)A[plan.rp_list + q] * 36 + lane];
+    for (; q < q1; ++q) s += pp[(int64_t)q * 36];
     const int64_t e1 = A[plan.rp_e + 2 * pr], e2 = A[plan.rp_e + 2 * pr + 1];
     S[(6 * e1 + lane / 6) * ld + 6 * e2 + lane % 6] = s;
 }
@@ -917,21 +920,20 @@ __device__ __forceinline__ void red_images_body(int e, int q, const double* __re
     if (e >= n_img) return;
     const int r0 = A[plan.ri_start + e], r1 = A[plan.ri_start + e + 1];
     if (r0 == r1 || q >= NIMG) return;
-    // the partials in chunk order with 8 loads in flight; same association as the plain running sum
-    // (((s + p0) + p1) + ...), so the result does not depend on the batching
+    // the partials in chunk order (image-major slots: one contiguous range) with 8 loads in flight; same
+    // association as the plain running sum (((s + p0) + p1) + ...), so the result does not depend on the
+    // batching
+    const double* ip = ipart + q;
     double s = 0.0;
     int x = r0;
     for (; x + 8 <= r1; x += 8) {
-        int id[8];
         double p[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) id[j] = A[plan.ri_list + x + j];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) p[j] = ipart[(int64_t)id[j] * NIMG + q];
+        for (int j = 0; j < 8; ++j) p[j] = ip[(int64_t)(x + j) * NIMG];
 #pragma unroll
         for (int j = 0; j < 8; ++j) s += p[j];
     }
-    for (; x < r1; ++x) s += ipart[(int64_t)A[plan.ri_list + x] * NIMG + q];
+    for (; x < r1; ++x) s += ip[(int64_t)x * NIMG];
     if (q < 21) {
         S[(6 * (int64_t)e + c_tri_a[q]) * ld + 6 * e + c_tri_b[q]] = s;
     } else if (q < 27) {
