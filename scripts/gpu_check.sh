@@ -19,6 +19,7 @@ for step in "$@"; do
   case "$step" in
     tests) run tests 1100 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread -p no:cacheprovider ;;
     quick) run tests_quick 800 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -m gpu -v --timeout 400 --timeout-method thread -p no:cacheprovider ;;
+    reftext) run reftext 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -k reference_text -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 5 --warmup 1 --verbose ;;
     benchq) run bench 600 python bench.py --steps 5 --warmup 1 --no-cpu --verbose ;;

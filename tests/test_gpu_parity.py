@@ -88,6 +88,45 @@ def test_adjust_cam0(fba, oracle, cam0_folders, variant):
     assert np.abs(res.rsd[:, 1:] - ro.rsd[:, 1:]).max() <= 10 * vtol * np.abs(ro.rsd[:, 1:]).max()
 
 
+@pytest.mark.parametrize("variant", sorted(CAM0_VARIANTS))
+def test_adjust_cam0_matches_reference_text(fba, oracle, cam0_folders, variant):
+    """The HIP path against the reference's OWN .m text run on the same files (tests/golden/
+    ref_cam0_<variant>.npz: main.m:61-628, Buildxhat.m, BuildAwG.m, BuildRSD.m, sumabs.m executed by
+    tests/golden/mlang.py; bars as tests/test_reference_text.py holds the oracle): Buildxhat exact,
+    BuildAwG <= 1e-12, the same iteration count, xhat after every iteration <= 1e-9 per element on the
+    pinhole variants (the converged xhat against 20x the restatement spread on the fish-eye family),
+    deltasum history, sigma0^2, RMS, v, RSD, and on the pinhole variants diag(Cx) and the EOP/IOP
+    correlation blocks."""
+    from test_reference_text import PINHOLE, assert_within, check_awg, load_ref, loop_errors
+    g = load_ref(variant)
+    ds = fba.load_folder(cam0_folders[variant])
+    ctx = _ctx(fba, ds)
+    try:
+        x0 = ctx.buildxhat()
+        np.testing.assert_array_equal(x0, g["xhat_hist"][0])
+        A, w, G, dsc = ctx.build_awg(x0)
+        check_awg(A, w, G, dsc, g, np.abs(ds.xy).max())
+        hist, dsum = [x0], []
+        for _ in range(int(g["iterations"])):
+            dsum.append(ctx.step())
+            hist.append(ctx.get_xhat())
+        v, rsd, st = ctx.residuals()
+    finally:
+        ctx.close()
+    res = fba.adjust(ds)
+    assert res.iterations == int(g["iterations"])
+    np.testing.assert_array_equal(res.xhat, hist[-1])
+    err = loop_errors(g, hist, dsum, st[3], st[:3], v, rsd, g["dist_scaling"], every_iteration=variant in PINHOLE)
+    spread = {}
+    if variant not in PINHOLE:
+        od = oracle.load_folder(cam0_folders[variant])
+        spread = solver_spread(oracle, od, oracle.adjust(od))
+    assert_within(err, variant, spread)
+    if variant in PINHOLE:
+        np.testing.assert_allclose(res.cx_diag, g["cx_diag"], rtol=1e-9, atol=0)
+        np.testing.assert_allclose(res.corr, g["corr_blocks"], rtol=0, atol=1e-9)
+
+
 @pytest.mark.parametrize("typ", ["fisheye", "pinhole", "equisolid", "orthographic", "stereographic"])
 def test_adjust_synthetic_types(fba, oracle, tmp_path, typ):
     from fba_amd import synth

@@ -5,8 +5,8 @@
   :223-348, :401-414, :457-495, and the hand-written distortion / IOP / scaling / G statements
   :167-181, :373-398, :419-445, :516-523) at 40 digits (tests/golden/make_jac_golden.py), all 5
   types, at zero and at nonzero distortion.
-* The cam0 runs against the committed fixtures (tests/golden/cam0_*.npz, written by
-  tests/golden/make_cam0_golden.py) -- a regression pin of the restatement itself.
+* The whole cam0 runs (Buildxhat, the loop, v / RSD / sigma0^2, Cx) against the reference's own .m
+  text executed by tests/golden/mlang.py: tests/test_reference_text.py.
 * The block-sparse (Schur) restatement against the explicit bordered inverse of main.m:432.
 """
 import json
@@ -15,7 +15,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import CAM0, CAM0_VARIANTS, GOLDEN, group_rel_err
+from conftest import CAM0, GOLDEN, group_rel_err
 
 EOP_NAMES = {"A14": (0, 0), "A15": (0, 1), "A16": (0, 2), "A11": (0, 3), "A12": (0, 4), "A13": (0, 5),
              "A24": (1, 0), "A25": (1, 1), "A26": (1, 2), "A21": (1, 3), "A22": (1, 4), "A23": (1, 5)}
@@ -139,20 +139,6 @@ def test_cam0_ingest(oracle):
     x, names = oracle.buildxhat(d)
     assert len(x) == 580 and names[0].startswith("Xc_101") and names[252] == "xp_0"
     assert d.settings["type"] == "pinhole" and d.settings["Meas_std_y"] == 0.3
-
-
-@pytest.mark.parametrize("variant", sorted(CAM0_VARIANTS))
-def test_cam0_oracle_regression(oracle, cam0_folders, variant):
-    path = os.path.join(GOLDEN, f"cam0_{variant}.npz")
-    g = np.load(path, allow_pickle=False)
-    d = oracle.load_folder(cam0_folders[variant])
-    r = oracle.adjust(d)
-    assert r.iterations == int(g["iterations"])
-    names = [str(s) for s in g["names"]]
-    err = group_rel_err(r.xhat, g["xhat"], names, g["dist_scaling"])
-    assert max(err.values()) < 1e-10, err
-    assert r.sigma02 == pytest.approx(float(g["sigma02"]), rel=1e-10)
-    np.testing.assert_allclose(r.deltasum, g["deltasum"], rtol=1e-6)
 
 
 def test_schur_restatement_equals_bordered_inverse(oracle, fba, tmp_path):
