@@ -203,7 +203,10 @@ def main():
         r = {"bound": "mfma", "kernel": f"{name} ({note})",
              "achieved": flops_launch / avg_s / 1e12 if avg_s > 0 else None, "peak": FP64_PEAK_TFLOPS,
              "unit": "TFLOP/s", "launches": pr["launches"], "avg_launch_us": avg_s * 1e6,
-             "flops_per_launch": flops_launch, "traffic": pmc_traffic(args.config, name, args.network)}
+             "flops_per_launch": flops_launch,
+             # the committed PMC summaries are single-context launches: a subtree-split launch (flow A / B,
+             # a fraction of the records) has none
+             "traffic": None if ctx.split else pmc_traffic(args.config, name, args.network)}
         r["frac"] = r["achieved"] / r["peak"] if r["achieved"] else None
         return r
     flow = os.environ.get("FBA_CHOL_FLOW", "1") != "0"

@@ -20,11 +20,11 @@ NK_MAX = 8
 # every symbol include/fba.h declares
 EXPORTS = (
     "fba_last_error", "fba_abi_version", "fba_count_unknowns", "fba_partition", "fba_image_order", "fba_create",
-    "fba_destroy", "fba_buildxhat", "fba_set_xhat", "fba_get_xhat", "fba_build_awg",
+    "fba_destroy", "fba_solve_mode", "fba_buildxhat", "fba_set_xhat", "fba_get_xhat", "fba_build_awg",
     "fba_accumulate", "fba_reduce_buffer", "fba_synchronize", "fba_solve_update", "fba_solve_update_async",
     "fba_deltasum_device", "fba_solve_finish", "fba_step", "fba_adjust",
     "fba_residuals", "fba_build_rsd", "fba_finish_stats", "fba_covariance", "fba_last_timings", "fba_set_timing", "fba_set_probe",
-    "fba_probe_stats", "fba_test_border_solve",
+    "fba_probe_stats", "fba_set_spin_bound", "fba_test_border_solve",
 )
 
 
@@ -67,6 +67,7 @@ def _load():
         "fba_image_order": ([P, P, P], C.c_int),
         "fba_create": ([P, P, P, P], C.c_int),
         "fba_destroy": ([P], None),
+        "fba_solve_mode": ([P, P], C.c_int),
         "fba_buildxhat": ([P, P, P], C.c_int),
         "fba_set_xhat": ([P, P], C.c_int),
         "fba_get_xhat": ([P, P, I], C.c_int),
@@ -88,6 +89,7 @@ def _load():
         "fba_set_timing": ([P, I], C.c_int),
         "fba_set_probe": ([P, I], C.c_int),
         "fba_probe_stats": ([P, P], C.c_int),
+        "fba_set_spin_bound": ([P, C.c_int64], C.c_int),
         "fba_test_border_solve": ([I, P, P], C.c_int),
     }
     for name, (args, res) in sig.items():
@@ -157,11 +159,15 @@ class Context:
         self.packed = packed
         self.settings = settings
         self.world = world
-        self.split = bool(split) and world > 1
         opts = Options(device, rank, world, int(verbose), stream, int(bool(split)))
         h = C.c_void_p()
         check(lib.fba_create(C.byref(packed.struct), C.byref(settings), C.byref(opts), C.byref(h)))
         self.h = h
+        # the solve libfba runs: a split request falls back to the replicated solve when the block
+        # pattern cannot be cut (fba_solve_mode)
+        mode = C.c_int32()
+        check(lib.fba_solve_mode(self.h, C.byref(mode)))
+        self.split = bool(mode.value)
         u = C.c_int64()
         check(lib.fba_buildxhat(self.h, None, C.byref(u)))
         self.u = u.value
@@ -277,6 +283,10 @@ class Context:
         cr = np.zeros((max(self.packed.n_img, 1), mu, mu)) if corr else None
         check(lib.fba_covariance(self.h, float(sigma02), ptr(d), ptr(cr)))
         return d[: int(self.u)], (cr[: self.packed.n_img] if corr else None)
+
+    def set_spin_bound(self, spins=0):
+        """(tests) this context's hand-off poll bound in sleeps; 0 restores the default"""
+        check(lib.fba_set_spin_bound(self.h, int(spins)))
 
     def set_timing(self, on=True):
         check(lib.fba_set_timing(self.h, int(on)))

@@ -167,7 +167,7 @@ static void destroy(Ctx* c) {
                     c->d_acc, c->d_ppart, c->d_ipart, c->d_cpart, c->d_cseg, c->d_bscr, c->d_gblk, c->d_lrprof, c->d_ptrace, c->d_gpairs, c->d_red, c->d_xfull, c->d_xlin, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
                     c->d_pt_tab, c->d_P, c->d_flags, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
                     c->d_active, c->d_counted, c->d_obs_pho, c->d_sched, c->d_gpt, c->d_gcu, c->d_gug, c->d_xpart,
-                    c->d_kpart, c->d_dynargs, c->d_bown, c->d_rown, c->d_topdiag};
+                    c->d_kpart, c->d_bown, c->d_rown, c->d_topdiag};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     for (auto& w : c->ws)
@@ -198,6 +198,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     c->prob = *p;
     c->set = *s;
     c->opt = opt;
+    c->force_sync = getenv("FBA_SYNC") && atoi(getenv("FBA_SYNC")) != 0;  // (read per context)
     c->n_pts = p->n_pts;
     Layout& L = c->L;
     // camera-side order of the images: nested dissection with padding slots (fba_order.cpp)
@@ -793,6 +794,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         destroy(c);
         return rc;
     }
+    FBA_HIP(hipMemset(c->d_scal, 0, sizeof(double) * 16));  // (chol_setup then sets scal[SCAL_SPINS])
     if ((rc = chol_setup(*c)) || (rc = acc_setup(*c))) { destroy(c); return rc; }
     if (getenv("FBA_LR_PROFILE") && c->n_chunks_lr > 0) FBA_HIP(hipMalloc((void**)&c->d_lrprof, sizeof(uint64_t) * 8 * c->n_chunks_lr));
     if (getenv("FBA_PANEL_TRACE") && c->sched.n_waves > 0)
@@ -805,7 +807,6 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     // outside the factor's block pattern S stays zero; the pattern itself is zeroed per accumulation
     FBA_HIP(hipMemsetAsync(c->d_S, 0, sizeof(double) * (size_t)(L.n_pad + NB) * L.ld, c->stream));
     FBA_HIP(hipStreamSynchronize(c->stream));
-    FBA_HIP(hipMemset(c->d_scal, 0, sizeof(double) * 16));
     FBA_HIP(hipHostMalloc((void**)&c->h_pinned, sizeof(double) * 64, hipHostMallocMapped | hipHostMallocCoherent));
     FBA_HIP(hipHostGetDevicePointer((void**)&c->d_hpinned, c->h_pinned, 0));
     std::fill(c->h_pinned, c->h_pinned + 64, 0.0);
@@ -875,14 +876,12 @@ static int accumulate_body(Ctx* c) {
     int rc;
     mark(c, 0);
     // tables + the linearisation point; S's pattern is zeroed by k_lin_reduce's tail workgroups
-    // (FBA_ZERO_HEAD=1: by k_params_zero ahead of it, the previous arrangement)
-    static const bool zero_head = getenv("FBA_ZERO_HEAD") && atoi(getenv("FBA_ZERO_HEAD"));
-    if ((rc = zero_head ? launch_params_zero(*c, c->d_xlin) : launch_params(*c, nullptr, c->d_xlin))) return rc;
+    if ((rc = launch_params(*c, nullptr, c->d_xlin))) return rc;
     mark(c, 1);
     // general tie points: their Jacobian rows, point tables and partials (ahead of the reductions)
     if ((rc = launch_gen_tables(*c, nullptr)) || (rc = launch_gen_keys(*c))) return rc;
     mark(c, 2);
-    if ((rc = launch_accumulate(*c, zero_head)) || (rc = launch_gen_reduce(*c))) return rc;
+    if ((rc = launch_accumulate(*c)) || (rc = launch_gen_reduce(*c))) return rc;
     if (c->d_lrprof) {  // FBA_LR_PROFILE: per-phase averages of k_lin_reduce (us)
         std::vector<uint64_t> tp(8 * c->n_chunks_lr);
         FBA_HIP(hipMemcpyAsync(tp.data(), c->d_lrprof, sizeof(uint64_t) * tp.size(), hipMemcpyDeviceToHost, c->stream));
@@ -918,7 +917,10 @@ static int accumulate_body(Ctx* c) {
 static int accumulate(Ctx* c) {
     c->have_factor = false;
     const int rc = run_graph(c, 0, [&] { return accumulate_body(c); });
-    if (rc == FBA_OK) c->have_lin = true;
+    if (rc == FBA_OK) {
+        c->have_lin = true;
+        c->solved = false;
+    }
     return rc;
 }
 
@@ -950,8 +952,18 @@ static int solve_body(Ctx* c) {
 
 static int solve_enqueue(Ctx* c) {
     if (!c->have_lin) { set_error("fba_solve_update before fba_accumulate"); return FBA_ERR_ARG; }
+    // the solve factors S in place (and with the subtree split, flow A's sync words are not re-zeroed by
+    // the solve: flow B's tickets would be past its grid), so a second solve of one accumulation would
+    // factor a factor -- refused; accumulate again
+    if (c->solved) {
+        set_error("one fba_solve_update per fba_accumulate (the solve factors the accumulated system in place)");
+        return FBA_ERR_ARG;
+    }
     const int rc = run_graph(c, 1, [&] { return solve_body(c); });
-    if (rc == FBA_OK) ++c->solves_enqueued;  // k_sum_parts' count once this solve is done
+    if (rc == FBA_OK) {
+        ++c->solves_enqueued;  // k_sum_parts' count once this solve is done
+        c->solved = true;
+    }
     return rc;
 }
 
@@ -1023,19 +1035,6 @@ static void print_flow_trace(Ctx* c) {
             fprintf(stderr, "  end %.1f\n", us(q[2]));
         }
     }
-    if (c->flow_dyn) {  // the dynamic dispatch's final state: every trigger received, every slot taken
-        const int n = s.flow_dyn_n;
-        std::vector<unsigned> st(2 * (size_t)n + 2);
-        if (hipMemcpy(st.data(), c->d_dyn, st.size() * sizeof(unsigned), hipMemcpyDeviceToHost) == hipSuccess) {
-            const int32_t* info = s.buf.data() + s.flow_dyn_info;
-            int bad = 0;
-            for (int r = 0; r < n; ++r)
-                if (st[r] != (unsigned)info[8 * r] && bad++ < 10)
-                    fprintf(stderr, "[fba] dyn: record %d triggers %u of %d\n", r, st[r], info[8 * r]);
-            fprintf(stderr, "[fba] dyn: slots taken %u, records appended %u + %d at launch, of %d; %d incomplete\n",
-                    st[2 * n], st[2 * n + 1], s.flow_dyn_ninit, n, bad);
-        }
-    }
     fprintf(stderr, "[fba] flow: diag %d (last end %.1f), panel halves %d (%.1f), updates %d (%.1f), inverses %d (%.1f), "
             "split helpers %d (%.1f)\n", rn[0], us(rend[0]), rn[1], us(rend[1]), rn[2], us(rend[2]), rn[3], us(rend[3]),
             rn[4], us(rend[4]));
@@ -1104,8 +1103,7 @@ static void print_panel_trace(Ctx* c) {
 // when a caller re-copies scal (the multi-GPU path), with tracing or timing on, with FBA_SYNC=1, and after
 // ~5 s without the count (a faulted launch: the synchronisation reports it).
 static bool wait_solve_seq(Ctx* c) {
-    static const bool force_sync = getenv("FBA_SYNC") && atoi(getenv("FBA_SYNC")) != 0;
-    if (force_sync || c->timing || c->d_ptrace || c->d_lrprof) return false;
+    if (c->force_sync || c->timing || c->d_ptrace || c->d_lrprof) return false;
     const double want = (double)c->solves_enqueued;
     volatile const double* seq = c->h_pinned + 4;
     const auto t0 = std::chrono::steady_clock::now();
@@ -1181,6 +1179,21 @@ extern "C" {
 
 const char* fba_last_error(void) { return g_err.c_str(); }
 int fba_abi_version(void) { return FBA_ABI_VERSION; }
+
+int fba_set_spin_bound(fba_ctx* ctx, int64_t spins) {
+    if (!ctx || spins < 0) { set_error("fba_set_spin_bound: bad argument"); return FBA_ERR_ARG; }
+    Ctx* c = reinterpret_cast<Ctx*>(ctx);
+    const double v = spins > 0 ? (double)spins : (double)(1u << 22);
+    FBA_HIP(hipStreamSynchronize(c->stream));
+    FBA_HIP(hipMemcpy(c->d_scal + SCAL_SPINS, &v, sizeof v, hipMemcpyHostToDevice));
+    return FBA_OK;
+}
+
+int fba_solve_mode(fba_ctx* ctx, int32_t* split) {
+    if (!ctx || !split) { set_error("fba_solve_mode: null argument"); return FBA_ERR_ARG; }
+    *split = reinterpret_cast<Ctx*>(ctx)->sched.split ? 1 : 0;
+    return FBA_OK;
+}
 
 int fba_count_unknowns(const fba_problem* p, const fba_settings* s, int64_t* u_out) {
     if (!p || !s || !u_out) { set_error("NULL argument"); return FBA_ERR_ARG; }

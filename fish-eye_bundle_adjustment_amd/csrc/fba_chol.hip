@@ -77,16 +77,14 @@ __device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, int64_t off_byt
 __device__ __forceinline__ double2 ld_sc1(__amdgpu_buffer_rsrc_t r, int64_t off_bytes) {
     return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off_bytes, 0, SC1));
 }
-// Bounded polls.  Every wait in this file gives up after g_flag_spins sleeps (default 1 << 22, ~0.3 s;
-// the FBA_FLAG_SPINS environment variable lowers it process-wide, to force the path in a test) and then
+// Bounded polls.  Every wait in this file gives up after scal[SCAL_SPINS] sleeps (the context's bound:
+// default 1 << 22, ~0.3 s; FBA_FLAG_SPINS at context creation lowers it, to force the path in a test) and then
 // RAISES THE ABORT: scal[1] = -1.0 (agent-scope store).  Every other poll checks the abort word every 64
 // sleeps (not on its first miss: that load would sit on every hand-off's critical path) and stops too, so
 // after one expiry the whole launch drains within about a millisecond; a k_chol_flow record that has not started yet is skipped entirely, k_bwd_flow's
 // workgroups return at once, and k_update leaves xhat untouched (fba_kernels.hip): the step fails with
 // FBA_ERR_HIP and xhat is as before it.  The sync words are zeroed again ahead of the next factorisation
 // (k_border_rhs), so a later step runs normally.
-__device__ unsigned g_flag_spins = 1u << 22;
-
 __device__ __forceinline__ bool hand_off_aborted(const double* scal) {  // the timeout mark, sign bit of -1.0
     return (long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(scal + 1), __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT) < 0;
@@ -106,7 +104,7 @@ __device__ __forceinline__ void pivot_failed(double* scal, int64_t k0) {
 // one missed poll: true when this wait must stop (its own bound reached, or another wait aborted)
 __device__ __forceinline__ bool spin_expired(unsigned& spins, double* scal) {
     ++spins;
-    if (spins >= g_flag_spins || ((spins & 63u) == 0u && hand_off_aborted(scal))) {
+    if (spins >= (unsigned)scal[SCAL_SPINS] || ((spins & 63u) == 0u && hand_off_aborted(scal))) {
         hand_off_abort(scal);
         return true;
     }
@@ -1902,21 +1900,18 @@ __device__ __forceinline__ void wait_list_sc1(const int32_t* __restrict__ wl, in
 // free until the potrf starts)
 constexpr size_t FLOWF_LDS_FUSED = sizeof(double) * (POTRF_NT * IB * 17 + (CB / IB) * IB * 17) + 32 * sizeof(int) +
                                    sizeof(double) * CB * 17;
-// self panel (selfpanel_apply): + two column-block buffers of L_ff (8 tiles each) and the waves' transposes
-constexpr size_t FLOWF_LDS_SELF = sizeof(double) * (POTRF_NT * IB * 17 + (CB / IB) * IB * 17) + 32 * sizeof(int) +
-                                  sizeof(double) * (2 * (CB / IB) + POTRF_NW) * IB * 17;
-constexpr size_t FLOWF_LDS = FLOWF_LDS_FUSED > FLOWF_LDS_SELF ? FLOWF_LDS_FUSED : FLOWF_LDS_SELF;
+constexpr size_t FLOWF_LDS = FLOWF_LDS_FUSED;
 static_assert(CB * 17 == (CB / IB) * IB * 17, "a column-block buffer is exactly the leaf-inverse area");
 
 // fused_apply<SET>: C -= X X' on the tiles of SET, X = L(j, f) consumed column block by column block as
 // the two panel-half records of (f, j) publish it (progress flags p0, p1): block t + 1's loads are issued
 // before block t's update whenever it is already published, so the update (in registers, tiles spread
 // over all eight waves) keeps pace with the panel solves.  SET 0/1: C from and back to the LDS block
-// (smem, the potrf's tile layout); SET 2: from zero, to out (the helper's scratch partial).  X's column
-// blocks [t0, 8) (blocks [0, t0): helper update tasks).  X0, X1: two [128][17] LDS buffers; sy[31] a word.
+// (smem, the potrf's tile layout); SET 2: from zero, to out (the helper's scratch partial).  X0, X1: two
+// [128][17] LDS buffers; sy[31] a word.
 template <int SET>
 __device__ __forceinline__ void fused_apply(const __amdgpu_buffer_rsrc_t rX, int64_t ld, const unsigned* __restrict__ p0,
-                                            const unsigned* __restrict__ p1, int t0, double* __restrict__ X0,
+                                            const unsigned* __restrict__ p1, double* __restrict__ X0,
                                             double* __restrict__ X1, int* __restrict__ sy, double* __restrict__ smem,
                                             double* __restrict__ out, double* __restrict__ scal, uint64_t* __restrict__ tr) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1974,8 +1969,8 @@ __device__ __forceinline__ void fused_apply(const __amdgpu_buffer_rsrc_t rX, int
         }
         __syncthreads();
     };
-    int issued = t0;         // blocks [t0, issued) issued (uniform)
-    if (t0 < CB / IB) wait_pub(t0);  // (its barrier also completes the C_jj load)
+    int issued = 0;          // blocks [0, issued) issued (uniform)
+    wait_pub(0);             // (its barrier also completes the C_jj load)
     constexpr int NS = fset_count(SET), NT = (NS + POTRF_NW - 1) / POTRF_NW;  // tiles of the set, per wave at most
     int ta[NT], tb[NT];
     dbl4 c[NT];  // this wave's tiles wave + 8 i of the set, in registers until the last block
@@ -1989,7 +1984,6 @@ __device__ __forceinline__ void fused_apply(const __amdgpu_buffer_rsrc_t rX, int
     }
 #pragma unroll
     for (int t = 0; t < CB / IB; ++t) {
-        if (t < t0) continue;
         double* X = Xb[t & 1];
         if (issued <= t) {  // not in flight yet: wait for it
             wait_pub(t);
@@ -2052,178 +2046,20 @@ __device__ __forceinline__ void fused_apply(const __amdgpu_buffer_rsrc_t rX, int
     }
 }
 
-// selfpanel_apply<SET> (role 0 with rec[12] = 1): the diagonal workgroup of block j solves its own rows of
-// the fused source's panel, X = L(j, f) = S(j, f) L_ff^-T, column block by column block as f's potrf
-// publishes L_ff (its column flag: block column t of L_ff and the leaf inverse D_t), and applies
-// C_jj -= X_t X_t' on the tiles of SET at each step -- one hand-off (potrf -> this workgroup) on the chain
-// between two levels instead of two (potrf -> panel halves -> diagonal workgroup).  Wave w owns rows
-// 16w .. 16w+15 of X in registers (right-looking: X_t = A_t D_t', A_s -= X_t L_st' for s > t, the panel
-// halves' arithmetic on eight waves); X_t's rows go to HBM write-through (the update tasks of later targets,
-// the split helper and the backward solve read them) and to Xb for the update.  Progress flag prog =
-// column blocks published, raised one step late (each wave drains its stores at the end of a step), the
-// last block before its update.  Lb: two
-// [8][16][17] column-block buffers (tiles (t+1 .. 7, t), D_t in slot 7); Tws: [8][16][17] per-wave
-// transposes; C: SET's tiles in registers, from and back to the potrf's LDS layout (smem).
-template <int SET>
-__device__ __forceinline__ void selfpanel_apply(double* __restrict__ S, int64_t ld, int64_t k0, int64_t f0,
-                                                const double* __restrict__ dinv_f, const unsigned* __restrict__ colflag,
-                                                unsigned* __restrict__ prog, double* __restrict__ smem,
-                                                double* __restrict__ Xb, double* __restrict__ Lb, double* __restrict__ Tws,
-                                                double* __restrict__ scal, uint64_t* __restrict__ tr) {
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int lr = lane & 15, lk = lane >> 4;
-    constexpr int NCB = CB / IB, LT = IB * 17;  // column blocks; one LDS tile
-    const __amdgpu_buffer_rsrc_t rX = block_rsrc(S + (k0 + IB * wave) * ld + f0, ((int64_t)(IB - 1) * ld + CB) * 8);
-    const __amdgpu_buffer_rsrc_t rL = block_rsrc(S + f0 * ld + f0, ((int64_t)(CB - 1) * ld + CB) * 8);
-    const __amdgpu_buffer_rsrc_t rD = block_rsrc(dinv_f, NCB * IB * IB * 8);
-    double* Tw = Tws + wave * LT;
-    // this wave's 16 rows of A = S(j, f) (final: the workgroup waited for its writers), MFMA output layout:
-    // acc[t][r] = A[lk + 4 r][16 t + lr]; sc1 loads (written by other workgroups in this launch)
-    dbl4 acc[NCB];
-#pragma unroll
-    for (int t = 0; t < NCB; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            acc[t][r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
-                                                       rX, (int)(((int64_t)(lk + 4 * r) * ld + IB * t + lr) * 8), 0, SC1));
-    constexpr int NS = fset_count(SET), NT = (NS + POTRF_NW - 1) / POTRF_NW;
-    int ta[NT], tb[NT];
-    dbl4 c[NT];
-#pragma unroll
-    for (int i = 0; i < NT; ++i) {
-        fset_tile(SET, wave + POTRF_NW * i, ta[i], tb[i]);
-        if (wave + POTRF_NW * i < NS)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) c[i][r] = smem[(ta[i] * (ta[i] + 1) / 2 + tb[i]) * LT + (lk + 4 * r) * 17 + lr];
-    }
-#pragma unroll
-    for (int t = 0; t < NCB; ++t) {
-        double* L = Lb + (t & 1) * NCB * LT;
-        if (tid == 0) {  // column block t of L_ff and D_t published
-            unsigned spins = 0;
-            while (__hip_atomic_load(colflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(t + 1)) {
-                __builtin_amdgcn_s_sleep(1);
-                if (spin_expired(spins, scal)) break;
-            }
-        }
-        // every wave drained its X_{t-1} stores before this barrier (end of the previous step): blocks
-        // [0, t) are published; the previous step's readers of Xb are done
-        __syncthreads();
-        if (t > 0 && tid == 0) __hip_atomic_store(prog, (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        {   // tiles (t+1+u, t), u < 7 - t, into slots u; D_t into slot 7: (8 - t) x 128 double2 items
-            double2 v[2];
-            int dst[2];
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const int i = tid + POTRF_THREADS * q, u = i >> 7, n = (i >> 3) & 15, m = (i & 7) * 2;
-                dst[q] = -1;
-                if (u < NCB - 1 - t) {
-                    v[q] = ld_sc1(rL, ((int64_t)((t + 1 + u) * IB + n) * ld + t * IB + m) * 8);
-                    dst[q] = u * LT + n * 17 + m;
-                } else if (u == NCB - 1 - t) {
-                    v[q] = ld_sc1(rD, (int64_t)(t * IB * IB + n * IB + m) * 8);
-                    dst[q] = (NCB - 1) * LT + n * 17 + m;
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-                if (dst[q] >= 0) {
-                    L[dst[q]] = v[q].x;
-                    L[dst[q] + 1] = v[q].y;
-                }
-        }
-        __syncthreads();  // column block t in LDS
-        if (tr && tid == 0) tr[8 + t] = wall_clock64();  // FBA_PANEL_TRACE: block t in LDS
-        // X_t = A_t D_t'
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Tw[(lk + 4 * r) * 17 + lr] = acc[t][r];
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_wave_barrier();
-        double av[4];
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) av[kk] = Tw[lr * 17 + 4 * kk + lk];
-        dbl4 x = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) x = mfma(av[kk], L[(NCB - 1) * LT + lr * 17 + 4 * kk + lk], x);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Tw[(lk + 4 * r) * 17 + lr] = x[r];
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_wave_barrier();
-        double xa[4];
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) xa[kk] = -Tw[lr * 17 + 4 * kk + lk];
-        {   // X_t's rows: write-through to S(j, f), and into Xb for the update
-            const int n = lane >> 2, m = 4 * (lane & 3);
-            double2 v0, v1;
-            v0.x = Tw[n * 17 + m];
-            v0.y = Tw[n * 17 + m + 1];
-            v1.x = Tw[n * 17 + m + 2];
-            v1.y = Tw[n * 17 + m + 3];
-            st_sc1(rX, ((int64_t)n * ld + IB * t + m) * 8, v0);
-            st_sc1(rX, ((int64_t)n * ld + IB * t + m + 2) * 8, v1);
-            double* xr = Xb + (IB * wave + n) * 17 + m;
-            xr[0] = v0.x;
-            xr[1] = v0.y;
-            xr[2] = v1.x;
-            xr[3] = v1.y;
-        }
-        // right-looking: A_s -= X_t L_st' for s > t
-#pragma unroll
-        for (int s2 = t + 1; s2 < NCB; ++s2)
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-                acc[s2] = mfma(xa[kk], L[(s2 - t - 1) * LT + lr * 17 + 4 * kk + lk], acc[s2]);
-        if (t == NCB - 1) {  // the last block: published before the update (the split helper waits for it)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0) __hip_atomic_store(prog, (unsigned)NCB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __syncthreads();  // X_t complete in Xb
-        }
-        // C(a, b) -= X_t(a) X_t(b)' on this wave's tiles of SET
-        double xu[NT][4], yu[NT][4];
-#pragma unroll
-        for (int i = 0; i < NT; ++i)
-            if (wave + POTRF_NW * i < NS) {
-#pragma unroll
-                for (int kk = 0; kk < 4; ++kk) {
-                    xu[i][kk] = -Xb[(IB * ta[i] + lr) * 17 + 4 * kk + lk];
-                    yu[i][kk] = Xb[(IB * tb[i] + lr) * 17 + 4 * kk + lk];
-                }
-            }
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-            for (int i = 0; i < NT; ++i)
-                if (wave + POTRF_NW * i < NS) c[i] = mfma(xu[i][kk], yu[i][kk], c[i]);
-        if (tr && tid == 0) tr[16 + t] = wall_clock64();  // FBA_PANEL_TRACE: block t applied
-        if (t < NCB - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // X_t drained: published at the next barrier
-    }
-#pragma unroll
-    for (int i = 0; i < NT; ++i)
-        if (wave + POTRF_NW * i < NS)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) smem[(ta[i] * (ta[i] + 1) / 2 + tb[i]) * LT + (lk + 4 * r) * 17 + lr] = c[i][r];
-}
-
 // diag_body (role 0): diagonal block j.  C_jj (its final in-place writers done) is loaded into LDS; with
 // a fused source f (rec[2] >= 0) C_jj -= X X', X = L(j, f), as the panel halves of (f, j) publish X
 // (fused_apply: all tiles, or with a split helper, rec[9] >= 0, those of tile columns < FLOW_CSPLIT);
 // then the late partials (the other sources of f's level, scratch quarters, slot order); then the potrf
 // on the LDS block, whose bulk waves add the helper's partial (scratch slot rec[10], flag rec[9]).
-// (at_potrf: called by every thread right before the potrf starts -- the dynamic dispatch's trigger of
-// the records that consume the block's published columns, FlowDyn)
-template <class AtPotrf>
 __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, const int32_t* __restrict__ rec,
                                           const int32_t* __restrict__ lists, double* __restrict__ dinv,
                                           double* __restrict__ scal, unsigned* __restrict__ colflags,
                                           unsigned* __restrict__ fl, const double* __restrict__ P,
-                                          double* __restrict__ smem, uint64_t* __restrict__ tr, AtPotrf&& at_potrf) {
+                                          double* __restrict__ smem, uint64_t* __restrict__ tr) {
     const int j = rec[1], f = rec[2];
     wait_list_sc1(lists + rec[3], rec[4], fl, scal);  // the final in-place writers of C_jj's quarters
     if (tr && threadIdx.x == 0) tr[1] = wall_clock64();
     if (f < 0 && rec[6] == 0) {
-        at_potrf();
         potrf_body<false>(S, ld, j, dinv, scal, nullptr, colflags + j, smem, tr ? tr + 16 : nullptr);
         return;
     }
@@ -2251,25 +2087,15 @@ __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, co
             smem[p * IB * 17 + n * 17 + m + 1] = v[q].y;
         }
     }
-    if (f >= 0 && rec[12]) {  // self panel: this workgroup solves its rows of f's panel itself
-        const int64_t f0 = (int64_t)f * CB;
-        wait_list_sc1(lists + rec[13], rec[14], fl, scal);  // the final writers of S(j, f)'s quarters
-        double* Lb = reinterpret_cast<double*>(sy + 32);
-        double* Tws = Lb + 2 * (CB / IB) * IB * 17;
-        const double* dinv_f = dinv + (int64_t)f * (CB / IB) * IB * IB;
-        if (rec[9] >= 0)
-            selfpanel_apply<1>(S, ld, k0, f0, dinv_f, colflags + f, fl + rec[7], smem, Dall, Lb, Tws, scal, tr);
-        else
-            selfpanel_apply<0>(S, ld, k0, f0, dinv_f, colflags + f, fl + rec[7], smem, Dall, Lb, Tws, scal, tr);
-    } else if (f >= 0) {
+    if (f >= 0) {
         const int64_t f0 = (int64_t)f * CB;
         const __amdgpu_buffer_rsrc_t rX = block_rsrc(S + k0 * ld + f0, ((int64_t)(CB - 1) * ld + CB) * 8);
         const unsigned* p0 = fl + rec[7];
         const unsigned* p1 = rec[8] >= 0 ? fl + rec[8] : nullptr;
         if (rec[9] >= 0)  // split: the tiles of tile columns >= FLOW_CSPLIT come from the helper record
-            fused_apply<1>(rX, ld, p0, p1, rec[11], Xb[0], Xb[1], sy, smem, nullptr, scal, tr);
+            fused_apply<1>(rX, ld, p0, p1, Xb[0], Xb[1], sy, smem, nullptr, scal, tr);
         else
-            fused_apply<0>(rX, ld, p0, p1, rec[11], Xb[0], Xb[1], sy, smem, nullptr, scal, tr);
+            fused_apply<0>(rX, ld, p0, p1, Xb[0], Xb[1], sy, smem, nullptr, scal, tr);
     }
     if (tr && threadIdx.x == 0) tr[4] = wall_clock64();
     // late partials: the other sources of f's level, 64x64 row-major scratch quarters, added in slot
@@ -2306,7 +2132,6 @@ __device__ __forceinline__ void diag_body(double* __restrict__ S, int64_t ld, co
     }
     __syncthreads();  // the block final in LDS; the counters and buffers free
     if (tr && threadIdx.x == 0) tr[5] = wall_clock64();
-    at_potrf();
     potrf_body<false, true>(S, ld, j, dinv, scal, nullptr, colflags + j, smem, tr ? tr + 16 : nullptr,
                             rec[9] >= 0 ? P + (int64_t)rec[10] * 4096 : nullptr, rec[9] >= 0 ? fl + rec[9] : nullptr);
 #undef AT
@@ -2324,7 +2149,7 @@ __device__ __forceinline__ void split_helper_body(double* __restrict__ S, int64_
     const __amdgpu_buffer_rsrc_t rX = block_rsrc(S + k0 * ld + f0, ((int64_t)(CB - 1) * ld + CB) * 8);
     double* Dall = smem + POTRF_NT * IB * 17;
     int* sy = reinterpret_cast<int*>(Dall + (CB / IB) * IB * 17);
-    fused_apply<2>(rX, ld, fl + rec[7], rec[8] >= 0 ? fl + rec[8] : nullptr, 0, Dall, reinterpret_cast<double*>(sy + 32), sy, smem,
+    fused_apply<2>(rX, ld, fl + rec[7], rec[8] >= 0 ? fl + rec[8] : nullptr, Dall, reinterpret_cast<double*>(sy + 32), sy, smem,
                    P + (int64_t)rec[10] * 4096, scal, tr);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -2731,79 +2556,19 @@ constexpr size_t FLOW_LDS = FLOW_LDS_A > FLOW_LDS_B ? FLOW_LDS_A : FLOW_LDS_B;
 static_assert(FLOW_LDS + 16 <= 160 * 1024, "k_chol_flow LDS (+ the static ticket word)");
 static_assert(SYRKW_LDS >= sizeof(double) * 128 * LDW + 3 * sizeof(int), "syrk_flow_body broadcast words");
 
-// Dynamic dispatch of k_chol_flow's records (FlowDyn, fba_order.cpp build_flow): one workgroup per record;
-// when it starts, a workgroup takes the next slot of a FIFO of READY records (one atomic add, then a poll of
-// that slot, written once -- the flag hand-off of every other wait in this file).  A record becomes ready
-// when every producer has triggered it: a "start" producer at its own claim (a diagonal block: when its
-// potrf starts), a "done" producer at its end; the trigger that completes the count appends the record to
-// the FIFO.  Records consume their producers' output progressively (flags), so a start trigger only means
-// the producer is running -- resident and progressing -- and every wait of a claimed record points to a
-// running or finished record: the earliest unfinished record in any topological order has only finished
-// producers, so the launch always progresses whatever the number of resident workgroups (as many
-// workgroups as records, and every record is appended exactly once, so each slot is filled).  The
-// records ready at launch come first, in priority order (the longest remaining path, host estimate).
-// (FBA_FLOW_DYN=0: the static order -- one record per workgroup in ticket order, each holding its CU from
-// dispatch to end; update tasks of later levels dispatched early then hold most CUs while the middle
-// levels' diagonal blocks wait for one.)  A bitmap of ready records scanned by the starting workgroups
-// was measured unusable: polled words that many workgroups keep changing by atomics read stale for up to
-// ~0.5 s, and the workgroups racing for the same bit serialise.
-struct FlowDyn {
-    const int32_t* info;    // [n][8]: need, -, consumer offset, start consumers, done consumers
-    const int32_t* cons;    // consumer record ids (start consumers first)
-    const int32_t* init;    // [n_init] the records ready at launch (no producer), priority order
-    unsigned* cnt;          // [n] triggers received        } zeroed by k_border_rhs
-    unsigned* ring;         // [n] FIFO slots: record + 1   } ahead of every
-    unsigned* head;         // [1] slots taken              } factorisation
-    unsigned* tail;         // [1] records appended         }
-    int n, n_init;
-};
-
-// the consumers [first, first + count) of record r's list: one thread each, any thread count
-__device__ __forceinline__ void dyn_trigger(const FlowDyn& d, int r, int first, int count, uint64_t* __restrict__ trace) {
-    const int off = d.info[8 * r + 2] + first;
-    for (int i = threadIdx.x; i < count; i += blockDim.x) {
-        const int c = d.cons[off + i];
-        const unsigned old = __hip_atomic_fetch_add(d.cnt + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old + 1 == (unsigned)d.info[8 * c]) {
-            const unsigned slot = d.n_init + __hip_atomic_fetch_add(d.tail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(d.ring + slot, (unsigned)c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (trace) trace[FTRACE * (int64_t)c + 49] = wall_clock64();  // FBA_PANEL_TRACE: ready
-        }
-    }
-}
-
-// thread 0: the record of this workgroup's FIFO slot (-1: the slot stayed empty within the bounded wait)
-__device__ __forceinline__ int dyn_claim(const FlowDyn& d, double* __restrict__ scal) {
-    const unsigned s = __hip_atomic_fetch_add(d.head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (s < (unsigned)d.n_init) return d.init[s];
-    if (s >= (unsigned)d.n) return -1;
-    unsigned spins = 0, v;
-    while ((v = __hip_atomic_load(d.ring + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
-        __builtin_amdgcn_s_sleep(1);
-        if (spin_expired(spins, scal)) return -1;
-    }
-    return (int)v - 1;
-}
-
 __device__ __forceinline__ void flow_record(int rid, double* __restrict__ S, int64_t ld, const int32_t* __restrict__ lists,
                                             const int32_t* __restrict__ recs, double* __restrict__ dinv,
                                             double* __restrict__ linv, double* __restrict__ scal,
                                             unsigned* __restrict__ colflags, unsigned* __restrict__ fl,
                                             unsigned* __restrict__ cnt, double* __restrict__ P,
                                             uint64_t* __restrict__ trace, double* __restrict__ gblk,
-                                            const FlowDyn* __restrict__ dyp, double* __restrict__ smem) {
+                                            double* __restrict__ smem) {
     const int32_t* rec = recs + Sched::FLOW_REC * (int64_t)rid;
     uint64_t* tr = trace ? trace + FTRACE * (int64_t)rid : nullptr;
     if (tr && threadIdx.x == 0) tr[0] = wall_clock64();
     const int role = rec[0];
-    // (dyp: the dynamic dispatch's state, read from memory where needed so it holds no registers across
-    // the record bodies)
-    // start triggers: at the claim, except a diagonal block's (when its potrf starts)
-    if (dyp && role != 0) dyn_trigger(*dyp, rid, 0, dyp->info[8 * rid + 3], trace);
     if (role == 0) {
-        diag_body(S, ld, rec, lists, dinv, scal, colflags, fl, P, smem, tr, [&]() {
-            if (dyp) dyn_trigger(*dyp, rid, 0, dyp->info[8 * rid + 3], trace);
-        });
+        diag_body(S, ld, rec, lists, dinv, scal, colflags, fl, P, smem, tr);
     } else if (role == 1) {
         wait_list_sc1(lists + rec[3], rec[4], fl, scal);  // the final writers of the panel block's quarters
         if (tr && threadIdx.x == 0) tr[1] = wall_clock64();
@@ -2821,10 +2586,6 @@ __device__ __forceinline__ void flow_record(int rid, double* __restrict__ S, int
         __syncthreads();
         trtri_body(S, ld, rec[1], dinv, linv, smem);
     }
-    if (dyp) {  // done triggers (after every wave's part of the record)
-        __syncthreads();
-        dyn_trigger(*dyp, rid, dyp->info[8 * rid + 3], dyp->info[8 * rid + 4], trace);
-    }
     if (tr) {
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -2834,6 +2595,17 @@ __device__ __forceinline__ void flow_record(int rid, double* __restrict__ S, int
     }
 }
 
+// POOLED = false: one workgroup per record (grid = records).  POOLED = true (FBA_FLOW_MAIN = K): a
+// persistent grid of one workgroup per CU in two pools -- the first K workgroups to start run the
+// critical records (diagonal blocks, panel halves, split helpers: pools[0, n_main)), the others the update
+// tasks and inverses (pools[n_main, n)), each pool taking its records in the static order from its own
+// ticket -- so update tasks waiting on progressively published columns never hold every CU while a
+// diagonal block waits for one.  Deadlock-free: the earliest unfinished record (static order) has all
+// its producers done; its pool hands out its records in order, so it is taken as soon as the records
+// before it in that pool -- all finished -- released their workgroups, and every pool keeps >= 1
+// workgroup (pool by arrival order: only running workgroups are counted).  ticket: [0] static ticket,
+// [3] arrivals, [4], [5] the pools' tickets (zeroed with the other sync words by k_border_rhs).
+template <bool POOLED>
 __global__ __launch_bounds__(POTRF_THREADS) void k_chol_flow(double* __restrict__ S, int64_t ld,
                                                              const int32_t* __restrict__ lists,
                                                              const int32_t* __restrict__ recs,
@@ -2842,32 +2614,48 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_chol_flow(double* __restrict_
                                                              unsigned* __restrict__ fl, unsigned* __restrict__ cnt,
                                                              double* __restrict__ P, uint64_t* __restrict__ trace,
                                                              double* __restrict__ gblk, unsigned* __restrict__ ticket,
-                                                             const FlowDyn* __restrict__ dyp) {
+                                                             const int32_t* __restrict__ pools, int n_main, int n_all,
+                                                             int k_main) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     __shared__ int s_ticket;
-    const uint64_t t_wg = trace ? wall_clock64() : 0;
-    if (dyp) {  // dynamic dispatch: this workgroup runs the record of its FIFO slot
-        if (threadIdx.x == 0) s_ticket = dyn_claim(*dyp, scal);
-    } else if (threadIdx.x == 0) {
-        // static order: the record comes from an atomic ticket, not from blockIdx: tickets follow the
-        // order in which the workgroups really start, and every record waits only for records of smaller
-        // index (build_flow's order check), so each wait points to a workgroup that has already started
-        // and is resident (or done) -- progress does not depend on the hardware dispatching blockIdx in
-        // order, nor on every record being co-resident
-        s_ticket = (int)__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (!POOLED) {
+        const uint64_t t_wg = trace ? wall_clock64() : 0;
+        if (threadIdx.x == 0) {
+            // static order: the record comes from an atomic ticket, not from blockIdx: tickets follow the
+            // order in which the workgroups really start, and every record waits only for records of smaller
+            // index (build_flow's order check), so each wait points to a workgroup that has already started
+            // and is resident (or done) -- progress does not depend on the hardware dispatching blockIdx in
+            // order, nor on every record being co-resident
+            s_ticket = (int)__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // a record that starts after a hand-off timeout is skipped (its inputs may never be published)
+        if (threadIdx.x == 0 && s_ticket >= 0 && hand_off_aborted(scal)) s_ticket = -1;
+        __syncthreads();
+        const int rid = s_ticket;
+        if (rid < 0) return;
+        if (trace && threadIdx.x == 0) trace[FTRACE * (int64_t)rid + 48] = t_wg;
+        flow_record(rid, S, ld, lists, recs, dinv, linv, scal, colflags, fl, cnt, P, trace, gblk, smem);
+    } else {
+        __shared__ int s_pool;
+        if (threadIdx.x == 0)
+            s_pool = __hip_atomic_fetch_add(ticket + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)k_main ? 0 : 1;
+        __syncthreads();
+        const int pool = s_pool;
+        const int first = pool ? n_main : 0, count = pool ? n_all - n_main : n_main;
+        for (;;) {
+            const uint64_t t_wg = trace ? wall_clock64() : 0;
+            if (threadIdx.x == 0) {
+                const unsigned t = __hip_atomic_fetch_add(ticket + 4 + pool, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_ticket = (t < (unsigned)count && !hand_off_aborted(scal)) ? pools[first + t] : -1;
+            }
+            __syncthreads();
+            const int rid = s_ticket;
+            if (rid < 0) return;
+            if (trace && threadIdx.x == 0) trace[FTRACE * (int64_t)rid + 48] = t_wg;
+            flow_record(rid, S, ld, lists, recs, dinv, linv, scal, colflags, fl, cnt, P, trace, gblk, smem);
+            __syncthreads();  // (s_ticket and the LDS are the next record's)
+        }
     }
-    // a record that starts after a hand-off timeout is skipped (its inputs may never be published); with
-    // the dynamic dispatch it still triggers its consumers, which then skip too
-    if (threadIdx.x == 0 && s_ticket >= 0 && hand_off_aborted(scal)) s_ticket = dyp ? -2 - s_ticket : -1;
-    __syncthreads();
-    const int rid = s_ticket;
-    if (rid < -1 && dyp) {
-        dyn_trigger(*dyp, -2 - rid, 0, dyp->info[8 * (-2 - rid) + 3] + dyp->info[8 * (-2 - rid) + 4], nullptr);
-        return;
-    }
-    if (rid < 0) return;
-    if (trace && threadIdx.x == 0) trace[FTRACE * (int64_t)rid + 48] = t_wg;
-    flow_record(rid, S, ld, lists, recs, dinv, linv, scal, colflags, fl, cnt, P, trace, gblk, dyp, smem);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3147,10 +2935,10 @@ int launch_cholesky(Ctx& c, int part) {
         const int64_t fo = b ? s.flow_nprog + s.flow_nuflag : 0, co = b ? s.flow_ncounter : 0, so = b ? s.flow_nscratch : 0;
         const bool pp = c.probe == 2 && c.probe_n < (int)c.probe_ev.size() / 2;
         if (pp) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
-        k_chol_flow<<<(unsigned)n, POTRF_THREADS, FLOW_LDS, c.stream>>>(
+        k_chol_flow<false><<<(unsigned)n, POTRF_THREADS, FLOW_LDS, c.stream>>>(
             c.d_S, ld, c.d_sched, c.d_sched + (b ? T.rec : s.flow_rec), c.d_dinv, c.d_linv, c.d_scal, c.d_flags,
             c.d_tflags + fo, c.d_counters + co, c.d_P + so * 4096, nullptr, c.set.inner_constraints ? c.d_gblk : nullptr,
-            c.d_tickets + (b ? 2 : 0), nullptr);
+            c.d_tickets + (b ? 2 : 0), nullptr, 0, 0, 0);
         if (pp) {
             FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], c.stream));
             c.probe_flops += b ? T.flops : s.flow_flops;
@@ -3163,10 +2951,16 @@ int launch_cholesky(Ctx& c, int part) {
         // the whole factorisation + forward solve in one persistent launch (flags zeroed by k_border_rhs)
         const bool pp = c.probe == 2 && c.probe_n < (int)c.probe_ev.size() / 2;
         if (pp) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
-        k_chol_flow<<<(unsigned)s.flow_n, POTRF_THREADS, FLOW_LDS, c.stream>>>(
-            c.d_S, ld, c.d_sched, c.d_sched + s.flow_rec, c.d_dinv, c.d_linv, c.d_scal, c.d_flags, c.d_tflags,
-            c.d_counters, c.d_P, c.d_ptrace, c.set.inner_constraints ? c.d_gblk : nullptr, c.d_tickets,
-            c.flow_dyn ? reinterpret_cast<const FlowDyn*>(c.d_dynargs) : nullptr);
+        const int grid = (int)std::min<int64_t>(c.n_cu, s.flow_n);  // (both pools need a workgroup)
+        if (c.flow_main > 0 && c.flow_main < grid)
+            k_chol_flow<true><<<(unsigned)grid, POTRF_THREADS, FLOW_LDS, c.stream>>>(
+                c.d_S, ld, c.d_sched, c.d_sched + s.flow_rec, c.d_dinv, c.d_linv, c.d_scal, c.d_flags, c.d_tflags,
+                c.d_counters, c.d_P, c.d_ptrace, c.set.inner_constraints ? c.d_gblk : nullptr, c.d_tickets,
+                c.d_sched + s.flow_pool, s.flow_pool_main, s.flow_n, c.flow_main);
+        else
+            k_chol_flow<false><<<(unsigned)s.flow_n, POTRF_THREADS, FLOW_LDS, c.stream>>>(
+                c.d_S, ld, c.d_sched, c.d_sched + s.flow_rec, c.d_dinv, c.d_linv, c.d_scal, c.d_flags, c.d_tflags,
+                c.d_counters, c.d_P, c.d_ptrace, c.set.inner_constraints ? c.d_gblk : nullptr, c.d_tickets, nullptr, 0, 0, 0);
         if (pp) {
             FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], c.stream));
             c.probe_flops += s.flow_flops;
@@ -3334,7 +3128,8 @@ int chol_setup(Ctx& c) {
     FBA_HIP(hipFuncSetAttribute((const void*)k_potrf128<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)POTRF_LDS));
     FBA_HIP(hipFuncSetAttribute((const void*)k_trsm128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRSM_LDS));
     FBA_HIP(hipFuncSetAttribute((const void*)k_panel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)PANEL_LDS));
-    FBA_HIP(hipFuncSetAttribute((const void*)k_chol_flow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)FLOW_LDS));
+    FBA_HIP(hipFuncSetAttribute((const void*)k_chol_flow<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)FLOW_LDS));
+    FBA_HIP(hipFuncSetAttribute((const void*)k_chol_flow<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)FLOW_LDS));
     // FBA_CHOL_FLOW=0: the level-by-level k_panel launches instead of the persistent dataflow launch
     c.chol_flow = !(getenv("FBA_CHOL_FLOW") && atoi(getenv("FBA_CHOL_FLOW")) == 0);
     static_assert(TRSM_LDS >= POTRF_LDS, "k_panel LDS");
@@ -3344,44 +3139,27 @@ int chol_setup(Ctx& c) {
     // (one more than the blocks: k_bwd_flow's border-combine flag; a multiple of 16 bytes)
     c.flags_bytes = (size_t)((c.L.n_pad / CB + 1 + 3) / 4 * 4) * sizeof(unsigned);
     const size_t nf = c.flags_bytes / sizeof(unsigned);
-    // [flags][bflags][split-target counters][update flags][2 tickets: k_chol_flow, k_bwd_flow]
-    // [flags][bflags][split-target counters][update flags][2 tickets: k_chol_flow, k_bwd_flow]
-    // [dynamic dispatch: triggers per record, FIFO slots, head, tail]
-    // FBA_FLOW_DYN=1: k_chol_flow's records by dynamic dispatch (FlowDyn) instead of the static ticket
-    // order; measured at config 4 (k_chol_flow per launch, FBA_DYN_EAGER = 0 / 1 / 2 / 4 / all): 661 / 545 /
-    // 519 / 515 / 559 us vs 466 us static -- the static order's level priorities beat FIFO-of-ready dispatch
-    c.flow_dyn = getenv("FBA_FLOW_DYN") && atoi(getenv("FBA_FLOW_DYN")) != 0 && c.sched.flow_dyn_n > 0;
-    const int64_t ndyn = c.flow_dyn ? 2 * (int64_t)c.sched.flow_dyn_n + 2 : 0;
-    c.n_sync = (int64_t)(2 * nf + std::max(c.sched.n_counters, 1) + std::max(c.sched.n_tflags, 1) + 3) + ndyn;
+    // [flags][bflags][split-target counters][update flags][tickets: k_chol_flow, k_bwd_flow, flow B, and
+    // k_chol_flow<true>'s arrivals and two pool tickets]
+    c.n_sync = (int64_t)(2 * nf + std::max(c.sched.n_counters, 1) + std::max(c.sched.n_tflags, 1) + 6);
     FBA_HIP(hipMalloc((void**)&c.d_flags, sizeof(unsigned) * c.n_sync));
     FBA_HIP(hipMemset(c.d_flags, 0, sizeof(unsigned) * c.n_sync));
     c.d_bflags = c.d_flags + nf;
     c.d_counters = c.d_bflags + nf;
     c.d_tflags = c.d_counters + std::max(c.sched.n_counters, 1);
     c.d_tickets = c.d_tflags + std::max(c.sched.n_tflags, 1);
-    c.d_dyn = c.flow_dyn ? c.d_tickets + 3 : nullptr;
-    if (c.sched.split && (!c.chol_flow || c.flow_dyn || !c.sched.flow_ok || !c.sched.top.ok)) {
-        set_error("subtree split needs the static-order k_chol_flow schedule (FBA_CHOL_FLOW / FBA_FLOW_DYN unset)");
+    // FBA_FLOW_MAIN = K (0 < K < #CU): k_chol_flow as a persistent grid of one workgroup per CU, K of them
+    // for the critical records (k_chol_flow<true>); unset / 0: one workgroup per record
+    c.flow_main = getenv("FBA_FLOW_MAIN") ? atoi(getenv("FBA_FLOW_MAIN")) : 0;
+    // FBA_BWD_LEVELS=1: the level-by-level backward solve (k_bwd_wave) instead of k_bwd_flow
+    c.bwd_flow = !(getenv("FBA_BWD_LEVELS") && atoi(getenv("FBA_BWD_LEVELS")) != 0);
+    // the subtree split runs flow A / flow B of k_chol_flow and k_bwd_flow's ownership masks and border
+    // scales: the per-level paths (k_panel, k_bwd_wave + k_border_combine + k_neg_copy) know neither
+    if (c.sched.split && (!c.chol_flow || !c.bwd_flow || !c.sched.flow_ok || !c.sched.top.ok)) {
+        set_error("subtree split needs the k_chol_flow / k_bwd_flow schedules (FBA_CHOL_FLOW and FBA_BWD_LEVELS unset)");
         return FBA_ERR_UNSUPPORTED;
     }
-    if (c.flow_dyn) {  // the dispatch state's addresses, uploaded once
-        FlowDyn dy{};
-        dy.info = c.d_sched + c.sched.flow_dyn_info;
-        dy.cons = c.d_sched + c.sched.flow_dyn_cons;
-        dy.init = c.d_sched + c.sched.flow_dyn_init;
-        dy.cnt = c.d_dyn;
-        dy.ring = dy.cnt + c.sched.flow_dyn_n;
-        dy.head = dy.ring + c.sched.flow_dyn_n;
-        dy.tail = dy.head + 1;
-        dy.n = c.sched.flow_dyn_n;
-        dy.n_init = c.sched.flow_dyn_ninit;
-        FBA_HIP(hipMalloc(&c.d_dynargs, sizeof(FlowDyn)));
-        FBA_HIP(hipMemcpy(c.d_dynargs, &dy, sizeof(FlowDyn), hipMemcpyHostToDevice));
-    }
     FBA_HIP(hipFuncSetAttribute((const void*)k_bwd_flow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)BWD_LDS));
-    c.bwd_flow = !(getenv("FBA_BWD_LEVELS") && atoi(getenv("FBA_BWD_LEVELS")) != 0);
-    c.panel_progressive = !(getenv("FBA_PANEL_PROGRESSIVE") && atoi(getenv("FBA_PANEL_PROGRESSIVE")) == 0);
-    c.merge_updates = !(getenv("FBA_MERGE_UPDATES") && atoi(getenv("FBA_MERGE_UPDATES")) == 0);
     // every level's trailing updates run inside the next level's k_panel (config 4: 968 iter/s merged
     // at any size vs 931 with the levels of > 450 tasks in their own k_syrk_multi launch, now that the
     // in-launch update runs on eight waves with coalesced whole-row loads; it measured the other way
@@ -3389,12 +3167,12 @@ int chol_setup(Ctx& c) {
     c.merge_max = getenv("FBA_MERGE_MAX") ? atoi(getenv("FBA_MERGE_MAX")) : (1 << 30);
     FBA_HIP(hipFuncSetAttribute((const void*)k_trtri128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRTRI_LDS));
 
-    // FBA_FLAG_SPINS (tests): the bound of every hand-off poll, process-wide (the device global is one per
-    // loaded code object), set by every context creation; unset: the default 1 << 22
+    // FBA_FLAG_SPINS (tests): the bound of every hand-off poll of THIS context (scal[SCAL_SPINS], read
+    // by spin_expired), taken when the context is created; unset: the default 1 << 22
     {
         const char* fs = getenv("FBA_FLAG_SPINS");
-        const unsigned v = fs ? (unsigned)std::max(1L, atol(fs)) : 1u << 22;
-        FBA_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_flag_spins), &v, sizeof v));
+        const double v = fs ? (double)std::max(1L, atol(fs)) : (double)(1u << 22);
+        FBA_HIP(hipMemcpy(c.d_scal + SCAL_SPINS, &v, sizeof v, hipMemcpyHostToDevice));
     }
     c.probe_ev.assign(2 * std::max(c.sched.n_waves, 1), nullptr);
     for (auto& e : c.probe_ev) FBA_HIP(hipEventCreate(&e));

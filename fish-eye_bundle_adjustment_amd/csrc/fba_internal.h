@@ -25,6 +25,7 @@ constexpr int FLOW_CSPLIT = 3;
 // k_bwd_flow's "not yet published" value of the solution blocks X (a signalling NaN with a payload no
 // arithmetic produces): the consumers poll the data itself, k_border_rhs resets it every solve
 constexpr uint64_t X_SENTINEL = 0x7FF4DEADBEEF5A5Aull;
+constexpr int SCAL_SPINS = 6;  // d_scal slot: this context's hand-off poll bound (fba_chol.hip spin_expired)
 constexpr int CHUNK_OBS = 256;  // observations per k_lin_reduce / k_lin_point workgroup (chunk)
 // tie points per chunk and co-visibility terms per chunk staged in LDS (a single larger point's are
 // read from HBM instead): smaller for nK >= 6, whose wider Jacobian rows leave less of the 160 KiB LDS
@@ -101,13 +102,14 @@ struct Sched {
     int64_t flow_rec = 0;
     int flow_n = 0, flow_nprog = 0, flow_nuflag = 0, flow_ncounter = 0, flow_nscratch = 0;
     int flow_cnt[5] = {0, 0, 0, 0, 0};  // records per role
+    // the records of the two dispatch pools of k_chol_flow's persistent variant, record ids in the static
+    // order: [flow_pool_main critical records: diagonal blocks, panel halves, split helpers][the others:
+    // update tasks, inverses]
+    int64_t flow_pool = 0;
+    int flow_pool_main = 0;
     bool flow_ok = false;
     double flow_flops = 0.0;
     double flow_bytes = 0.0;      // operand bytes the records load and store (build_flow)
-    // dynamic dispatch of the records (k_chol_flow FlowDyn): per record [need, 0, consumer offset,
-    // start consumers, done consumers, 0, 0, 0], the consumer lists, the records ready at launch
-    int flow_dyn_n = 0, flow_dyn_ninit = 0;
-    int64_t flow_dyn_info = 0, flow_dyn_cons = 0, flow_dyn_init = 0;
 
     // subtree split (fba_options.split, world > 1): the elimination tree is cut into a TOP part (the
     // columns above the cut: separators, camera rows) and subtrees dealt to the ranks.  A rank's points
@@ -288,9 +290,6 @@ struct Ctx {
     unsigned* d_counters = nullptr; // [Sched::n_counters] split-target arrival counters
     unsigned* d_tflags = nullptr;   // [Sched::n_tflags] update-target completion flags (merged k_panel)
     unsigned* d_tickets = nullptr;  // [2] start-order tickets of k_chol_flow / k_bwd_flow records
-    unsigned* d_dyn = nullptr;      // k_chol_flow dynamic dispatch state (FlowDyn; zeroed with the flags)
-    void* d_dynargs = nullptr;      // the FlowDyn struct itself (device copy: its addresses)
-    bool flow_dyn = true;           // k_chol_flow records dispatched dynamically (FBA_FLOW_DYN=0: static order)
     int64_t n_sync = 0;           // unsigned words of flags + bflags + counters (one allocation at d_flags,
                                   // zeroed by k_border_rhs ahead of every factorisation)
     bool bwd_flow = true;
@@ -323,6 +322,9 @@ struct Ctx {
 
     // state
     bool have_lin = false;       // d_J holds a linearisation
+    bool solved = false;         // this accumulation's solve enqueued (S holds its factor now)
+    bool force_sync = false;
+    int flow_main = 0;           // FBA_FLOW_MAIN: k_chol_flow's critical-record pool size (0: per-record grid)     // FBA_SYNC=1 at creation: wait for a solve by hipStreamSynchronize
     bool have_delta = false;
     bool have_factor = false;
     bool pending = false;        // fba_solve_update_async enqueued, fba_solve_finish not yet called    // d_S holds the factor of the last solve (fba_covariance consumes it)
@@ -382,8 +384,6 @@ int launch_gen_keys(Ctx& c);
 int launch_gen_reduce(Ctx& c);
 int launch_gen_backsub(Ctx& c);
 int launch_gen_cov(Ctx& c, const double* Z, const double* Wz, int nz, double* pdiag);
-int launch_params_zero(Ctx& c, double* copy_to);  // k_params (+ copy of the linearisation point) and the
-                                                   // zeroing of the factor's pattern blocks, one launch
 int launch_accumulate(Ctx& c, bool zeroed = false);  // zero S (unless zeroed), image, pair, camera blocks
 int launch_border(Ctx& c);       // alpha, G G^T border, RHS rows
 int chol_setup(Ctx& c);

@@ -132,30 +132,6 @@ __global__ __launch_bounds__(PARAMS_WG) void k_params(const double* __restrict__
     for (int64_t i = t + 4 * st; i < n_copy; i += st) xcopy[i] = xfull[i];
 }
 
-// the per-iteration head of the accumulation in one launch: workgroups < npb build the parameter
-// tables and copy the linearisation point (k_params), the rest zero the factor's pattern blocks
-// (8 workgroups of 16 rows per 128x128 block, Sched::zero)
-__global__ __launch_bounds__(256) void k_params_zero(const double* __restrict__ xfull, const double* __restrict__ caminfo,
-                                                     double* __restrict__ img_tab, double* __restrict__ cam_tab,
-                                                     double* __restrict__ G, const uint8_t* __restrict__ active, int n_img,
-                                                     int n_cam, int nk, int cw, int cam_stride, int ic,
-                                                     double* __restrict__ xcopy, int64_t n_copy, int npb,
-                                                     double* __restrict__ S, int64_t ld, const int32_t* __restrict__ blk) {
-    if ((int)blockIdx.x < npb) {
-        params_body(blockIdx.x * 256 + threadIdx.x, npb * 256, xfull, caminfo, img_tab, cam_tab, G, active, n_img, n_cam,
-                    nk, cw, cam_stride, ic, xcopy, n_copy);
-        return;
-    }
-    const int zb = blockIdx.x - npb, b = zb >> 3;
-    const int64_t r0 = (int64_t)blk[2 * b] * NB + (zb & 7) * 16, c0 = (int64_t)blk[2 * b + 1] * NB;
-    const double2 z = {0.0, 0.0};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int i = threadIdx.x + 256 * q, r = i >> 6, c = (i & 63) * 2;
-        *reinterpret_cast<double2*>(S + (r0 + r) * ld + c0 + c) = z;
-    }
-}
-
 
 // ------------------------------------------------------------------------------------------------
 // Device layouts (observation-major so a thread / wave touches contiguous bytes):
@@ -1419,17 +1395,6 @@ static inline unsigned cam_mask(const fba_settings& s, int nk) {
 static inline double px_of(const Ctx& c) { return 1.0 / (c.set.meas_std_x * c.set.meas_std_x); }
 static inline double py_of(const Ctx& c) { return 1.0 / (c.set.meas_std_y * c.set.meas_std_y); }
 
-// k_params (with the linearisation-point copy) and k_zero_blocks in one launch (fba_step's accumulation)
-int launch_params_zero(Ctx& c, double* copy_to) {
-    const int n = c.L.n_img + c.L.n_cam;
-    const int npb = (int)std::max<int64_t>((n + 255) / 256, std::min<int64_t>(256, (c.L.u_full + 255) / 256));
-    k_params_zero<<<(unsigned)(npb + 8 * c.sched.nzero), 256, 0, c.stream>>>(
-        c.d_xfull, c.d_caminfo, c.d_img_tab, c.d_cam_tab, c.d_G, c.d_active, c.L.n_img, c.L.n_cam, c.L.nk, c.L.cw,
-        c.cam_tab_stride, c.set.inner_constraints, copy_to, c.L.u_full, npb, c.d_S, c.L.ld, c.d_sched + c.sched.zero);
-    FBA_HIP(hipGetLastError());
-    return FBA_OK;
-}
-
 int launch_params(Ctx& c, const double* x, double* copy_to) {
     const int n = c.L.n_img + c.L.n_cam;
     const int64_t nb = (n + PARAMS_WG - 1) / PARAMS_WG;
@@ -1606,12 +1571,15 @@ __global__ void k_pack(double* __restrict__ S, int64_t ld, double* __restrict__ 
 //   [the accumulated diagonal of the top rows carrying image unknowns, packed before the subtree flow]
 //   [Gram partials (16 x 16) of every non-top block column: this rank's own, zeros for the others']
 //   [this rank's 7 inner-constraint weight sums over its subtree rows (k_border_weights' segments)]
+//   [1: this rank's flow A aborted (a hand-off timed out, scal[1] < 0): its top-block contributions are
+//    incomplete; after the sum every rank sees it, raises the abort ahead of flow B and fails the step]
 // dir 0: S (+ gblk, weight segments) -> buffer; dir 1: buffer -> S top blocks, gblk.  (The diagonal part
 // is written by k_pack_topdiag ahead of the subtree flow.)
 __global__ __launch_bounds__(256) void k_pack_split(double* __restrict__ S, int64_t ld, double* __restrict__ red,
                                                     const int32_t* __restrict__ tb, int ntb, int64_t n_pad, int nrhs,
                                                     double* __restrict__ gblk, const int8_t* __restrict__ bown, int nb,
-                                                    int64_t red_gblk, int64_t red_w, const double* __restrict__ wseg, int dir) {
+                                                    int64_t red_gblk, int64_t red_w, const double* __restrict__ wseg,
+                                                    double* __restrict__ scal, int dir) {
     const int q = blockIdx.x;
     if (q < ntb) {  // one top block per workgroup
         const int64_t a = tb[2 * q], b = tb[2 * q + 1];
@@ -1641,6 +1609,11 @@ __global__ __launch_bounds__(256) void k_pack_split(double* __restrict__ S, int6
             double v = 0.0;
             for (int sg = 0; sg < 32; ++sg) v += wseg[sg * 14 + 7 + threadIdx.x];  // (BW_SEG segments)
             red[red_w + threadIdx.x] = v;
+        }
+        if (threadIdx.x == 7) {
+            // (flow A has finished: k_pack_split follows it on the stream, so scal[1] is final here)
+            if (dir == 0) red[red_w + 7] = scal[1] < 0.0 ? 1.0 : 0.0;
+            else if (red[red_w + 7] != 0.0) scal[1] = -1.0;  // some rank's flow A aborted: skip flow B, k_update
         }
     }
 }
@@ -1692,7 +1665,7 @@ int launch_pack_split(Ctx& c, int dir) {
     }
     k_pack_split<<<(unsigned)(s.n_top_blocks + 1), 256, 0, c.stream>>>(
         c.d_S, c.L.ld, c.d_red, c.d_sched + s.top_blocks, s.n_top_blocks, c.L.n_pad, c.L.nrhs, c.d_gblk, c.d_bown,
-        (int)(c.L.n_pad / 128), c.red_gblk, c.red_w, c.d_bscr, dir);
+        (int)(c.L.n_pad / 128), c.red_gblk, c.red_w, c.d_bscr, c.d_scal, dir);
     FBA_HIP(hipGetLastError());
     if (dir == 1 && c.set.inner_constraints) {
         k_split_weights<<<1, 256, 0, c.stream>>>(c.d_red, c.red_diag, c.red_w, c.d_topdiag, c.n_topdiag, c.d_G,

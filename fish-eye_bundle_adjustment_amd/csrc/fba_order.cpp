@@ -424,7 +424,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
                        const std::vector<int32_t>& level, int64_t nb, const std::function<int64_t(int64_t)>& real_rows,
                        bool verbose, const std::vector<char>* inc = nullptr) {
     auto in = [&](int64_t k) { return !inc || (*inc)[k] != 0; };
-    constexpr int REC = Sched::FLOW_REC, CB_BLOCKS = NB / 16, IB_BLOCK = 16;
+    constexpr int REC = Sched::FLOW_REC, CB_BLOCKS = NB / 16;
     // sources per update task (FBA_FLOW_SPLIT; a target quarter's sources of one level are split into
     // groups of at most SPLIT, summed through scratch partials when there are several groups); config 4
     // (iter/s, two runs each): 1: 1050, 2: 1120 / 1137, 3: 1153 / 1143, 4: 1152 / 1147, all in one: 1087
@@ -435,51 +435,24 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     for (int64_t k = 0; k < nb; ++k)
         for (int32_t i : R[k])
             if (i < nb && in(k)) srcs[i].push_back((int32_t)k);
-    // dispatch keys by "as late as possible" levels (FBA_FLOW_ALAP=1): a column's key level is its
-    // elimination-tree parent's minus one (the root keeps its own), so the records of a shallow subtree,
-    // which has slack before its parent needs it, sort behind the same-level records of the longest chain
-    // (levels count up from the leaves, so a shallow subtree's records otherwise come first).  Measured
-    // and not kept (iter/s | k_chol_flow us, same box): config 4 1197-1202 | 474-482 vs 1238-1244 |
-    // 456-458, config 5 265 | 2568 vs 279 | 2388, convergent unchanged (one chain) -- a shallow subtree's
-    // records dispatched late then hold the CUs when the chain's own records arrive
-    const bool alapm = getenv("FBA_FLOW_ALAP") && atoi(getenv("FBA_FLOW_ALAP")) != 0;
-    std::vector<int> klev(level.begin(), level.end());
-    if (alapm)
-        for (int64_t j = nb - 1; j >= 0; --j) {
-            int32_t par = -1;
-            for (int32_t r : R[j])
-                if (r > j && r < nb && (par < 0 || r < par)) par = r;
-            if (par >= 0) klev[j] = std::max(level[j], klev[par] - 1);
-        }
-    auto kl = [&](int64_t x) { return klev[x]; };
+    // (dispatch keys by as-late-as-possible levels measured slower: config 4 1197-1202 vs 1238-1244
+    // iter/s -- a shallow subtree's records dispatched late then hold the CUs when the chain's arrive)
+    auto kl = [&](int64_t x) { return level[x]; };
     std::vector<int32_t> fsrc(nb, -1);
-    // FBA_FLOW_FUSE=0: no fused sources (every diagonal update by update tasks; the potrf loads its block)
-    static const bool fuse = !(getenv("FBA_FLOW_FUSE") && atoi(getenv("FBA_FLOW_FUSE")) == 0);
-    for (int64_t j = 0; j < nb && fuse; ++j)
+    for (int64_t j = 0; j < nb; ++j)
         for (int32_t k : srcs[j])
             if (in(j))
             if (fsrc[j] < 0 || level[k] > level[fsrc[j]] || (level[k] == level[fsrc[j]] && k > fsrc[j])) fsrc[j] = k;
     auto halves = [&](int64_t r) { return real_rows(r) > NB / 2 ? 2 : 1; };
     // the fused source's panel rows of block j are solved by two panel-half records and handed to j's
-    // diagonal workgroup.  FBA_FLOW_SELF=1: that workgroup solves them itself (selfpanel_apply: one
-    // hand-off between two levels' potrfs instead of two) -- measured and not kept (config 4, two runs
-    // each: 1133 / 1139 iter/s, k_chol_flow 521.5 us, vs 1228 / 1222 and 454.4 us): one CU's f64 MFMA rate
-    // paces the panel solve plus the fused update at ~3 us per column block, behind the potrf's ~2.4 us,
-    // so the diagonal block lands 14 us after the source's last column instead of 12
-    static const bool selfp = getenv("FBA_FLOW_SELF") && atoi(getenv("FBA_FLOW_SELF")) == 1;
-    auto self_panel = [&](int64_t k, int64_t r) { return selfp && r < nb && fsrc[r] == (int32_t)k; };
-    // progress flags of every panel half (k, r, h), r in R[k] (the RHS block row included); a self panel
-    // has one flag for both halves (raised by the diagonal workgroup of r)
+    // diagonal workgroup (that workgroup solving them itself measured slower: config 4 1133-1139 vs
+    // 1222-1228 iter/s -- one CU's f64 MFMA rate then paces the panel solve plus the fused update)
+    // progress flags of every panel half (k, r, h), r in R[k] (the RHS block row included)
     std::map<std::tuple<int32_t, int32_t, int32_t>, int32_t> prog;
     int np = 0;
     for (int64_t k = 0; k < nb; ++k)
         for (int32_t r : R[k]) {
             if (!in(k)) break;
-            if (self_panel(k, r)) {
-                for (int h = 0; h < halves(r); ++h) prog[std::make_tuple((int32_t)k, r, h)] = np;
-                ++np;
-                continue;
-            }
             for (int h = 0; h < halves(r); ++h) prog[std::make_tuple((int32_t)k, r, h)] = np++;
         }
     struct Task {
@@ -489,72 +462,45 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     };
     std::vector<Task> T;
     std::vector<int> col_task(nb, -1), prog_task(np, -1);
-    std::map<int, int> follow;  // record -> the record dispatched right after it (a self panel's split helper)
     std::vector<std::vector<int>> uflag_tasks;  // update flag -> the records that may raise it
     std::vector<std::vector<int32_t>> flag_deps;  // per record: flags it waits for (resolved to records)
     auto new_uflag = [&]() { uflag_tasks.emplace_back(); return (int32_t)(np + uflag_tasks.size() - 1); };
-    // FBA_FLOW_TIE=1: within a (level, role) the records of higher block columns first (the nested
-    // dissection numbers the separators, the longest chain, last); measured and not kept: config 4
-    // 1228-1230 | 458-466 us vs 1240-1245 | 449-454 us, config 5 unchanged
-    const bool tie_desc = getenv("FBA_FLOW_TIE") && atoi(getenv("FBA_FLOW_TIE")) == 1;
     auto add = [&](std::initializer_list<int32_t> r, std::array<int, 3> key) {
         Task t;
         t.rec.fill(0);
         int q = 0;
         for (int32_t v : r) t.rec[q++] = v;
-        if (tie_desc) key[2] = -key[2];
         t.key = key;
         T.push_back(std::move(t));
         flag_deps.emplace_back();
         return (int)T.size() - 1;
     };
-    // FBA_FLOW_KSPLIT = K (1..8): the fused update's first K column blocks go to three helper update
-    // tasks (late partials) and the diagonal workgroup applies the rest; measured at config 4 (iter/s):
-    // K = 0 (default, the workgroup applies all eight) 1129, 2: 1078, 4: 1076, 5: 1096, 6: 1091 -- the
-    // helpers' extra hand-off costs more than the diagonal workgroup's arithmetic they take over
-    static const int ksplit = getenv("FBA_FLOW_KSPLIT") ? std::max(0, std::min(8, atoi(getenv("FBA_FLOW_KSPLIT")))) : 0;
-    // FBA_FLOW_CSPLIT=0 disables the tile-column split of the fused updates (helper records, role 4): the
+    // the tile-column split of the fused updates (helper records, role 4): the
     // diagonal workgroup applies the tiles of tile columns < FLOW_CSPLIT, a helper workgroup the others
     // (consuming the same published rows) into a scratch partial that the potrf's bulk waves add at
     // their step FLOW_CSPLIT - 2, well after the potrf has started -- so the update's arithmetic no
     // longer trails the panel solves (the diagonal workgroup alone is MFMA-bound at ~1.5 us per
-    // column block, behind panel halves that publish one every ~1-2 us)
-    static const bool csplit = !(getenv("FBA_FLOW_CSPLIT") && atoi(getenv("FBA_FLOW_CSPLIT")) == 0);
-    // FBA_FLOW_PROMOTE (panel halves) and FBA_FLOW_LOOKAHEAD = D (an update task dispatched among the
-    // records of level max(source level, level of need - D); default: at its source level) reorder the
-    // dispatch; measured at config 4 (iter/s): default 1125-1130, PROMOTE=1 1126, PROMOTE=2 1102, D = 0 /
-    // 1 / 2 / 3 / 5: 724 / 760 / 828 / 916 / 1035 -- an update deferred towards its need lands on the
-    // critical path.  (FBA_PANEL_TRACE=3: the mid levels' panel halves start late because the CUs are
-    // held by update tasks that wait for progressively published source columns, ~20 us each.)
-    // FBA_FLOW_DEFER = N (updates among the records of level min(source level + N, need - 1)): config 4
-    // 1172-1180 iter/s at N = 0, 1135-1140 at 1, 1058-1063 at 2
-    static const int defer = getenv("FBA_FLOW_DEFER") ? atoi(getenv("FBA_FLOW_DEFER")) : 0;
+    // column block, behind panel halves that publish one every ~1-2 us).  (Measured and not kept: the
+    // fused update's first column blocks on helper update tasks, 1076-1096 vs 1129 iter/s; panel halves
+    // promoted a level, 1102-1126 vs 1125-1130; update tasks deferred towards their need, 724-1035 --
+    // an update deferred lands on the critical path.)
     // FBA_FLOW_MERGE = G: writer groups over consecutive source levels when the target is read >= G levels later
     // (config 4, k_chol_flow per launch: G = 0 / 1 / 2 / 3: 465 / 458 / 453 / 454 us; convergent config 4:
     // 3.80 / 3.18 / 3.22 ms); FBA_FLOW_MSPLIT: the sources a merged group may hold (default SPLIT)
     const int merge_gap = getenv("FBA_FLOW_MERGE") ? atoi(getenv("FBA_FLOW_MERGE")) : 2;
     const int msplit = getenv("FBA_FLOW_MSPLIT") ? std::max(1, atoi(getenv("FBA_FLOW_MSPLIT"))) : SPLIT;
-    static const int promote_mode = getenv("FBA_FLOW_PROMOTE") ? atoi(getenv("FBA_FLOW_PROMOTE")) : 0;
-    static const int lookahead = getenv("FBA_FLOW_LOOKAHEAD") ? atoi(getenv("FBA_FLOW_LOOKAHEAD")) : 1000;
     int nslot = 0, ncnt = 0, n_whole_t = 0;
     // diagonal blocks
     for (int64_t j = 0; j < nb; ++j) {
         if (!in(j)) continue;
         const int32_t f = fsrc[j];
         int need = kl(j) - 1;
-        const bool sp = f >= 0 && self_panel(f, j);
         const int32_t p0 = f >= 0 ? prog[std::make_tuple(f, (int32_t)j, 0)] : -1;
-        const int32_t p1 = (f >= 0 && halves(j) > 1 && !sp) ? prog[std::make_tuple(f, (int32_t)j, 1)] : -1;
-        const bool split = csplit && f >= 0 && halves(j) > 1 && ksplit == 0;
+        const int32_t p1 = (f >= 0 && halves(j) > 1) ? prog[std::make_tuple(f, (int32_t)j, 1)] : -1;
+        const bool split = f >= 0 && halves(j) > 1;
         const int32_t hflag = split ? new_uflag() : -1, hslot = split ? nslot++ : -1;
-        // (rec[12] = 1: self panel, rec[7] its progress flag; rec[13..14]: the panel block's writer list)
-        col_task[j] = add({0, (int32_t)j, f, 0, 0, 0, 0, p0, p1, hflag, hslot, f >= 0 ? (sp ? 0 : ksplit) : 0, sp ? 1 : 0},
-                          {need, 0, (int)j});
-        if (sp) {
-            prog_task[p0] = col_task[j];
-            T[col_task[j]].deps.push_back(col_task[f]);  // consumes f's potrf progressively
-            s.flow_flops += 2.0 * 64.0 * NB * NB;       // the panel rows (two halves' worth)
-        } else if (f >= 0) {
+        col_task[j] = add({0, (int32_t)j, f, 0, 0, 0, 0, p0, p1, hflag, hslot}, {need, 0, (int)j});
+        if (f >= 0) {
             flag_deps[col_task[j]].push_back(p0);
             if (p1 >= 0) flag_deps[col_task[j]].push_back(p1);
         }
@@ -563,28 +509,19 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
             flag_deps[hid] = {p0};
             if (p1 >= 0) flag_deps[hid].push_back(p1);
             uflag_tasks[hflag - np].push_back(hid);
-            // a self panel's helper consumes the diagonal workgroup's own published rows, and that
-            // workgroup adds the helper's partial only inside its potrf, after its panel is published: the
-            // helper is dispatched right after it (follow[]), and that wait is the one exception to "every
-            // wait points to an earlier record" -- every record dispatched before the helper is running or
-            // done and none of them waits for this block, so the helper gets a CU
-            if (sp) follow[col_task[j]] = hid;
-            else flag_deps[col_task[j]].push_back(hflag);
+            flag_deps[col_task[j]].push_back(hflag);
         }
-        s.flow_flops += (double)NB * NB * NB / 3.0 + (f >= 0 ? (double)NB * NB * NB * (8 - ksplit) / 8.0 : 0.0);
+        s.flow_flops += (double)NB * NB * NB / 3.0 + (f >= 0 ? (double)NB * NB * NB : 0.0);
     }
     // panel-half solves
     for (int64_t k = 0; k < nb; ++k)
         for (int32_t r : R[k])
             if (in(k))
-            for (int h = 0; h < halves(r) && !self_panel(k, r); ++h) {
+            for (int h = 0; h < halves(r); ++h) {
                 const int32_t p = prog[std::make_tuple((int32_t)k, r, h)];
                 // rec[7]: the RHS block row's half 0 accumulates its rows' Gram into partial k
-                // FBA_FLOW_PROMOTE: 1 = the panel halves feeding a fused diagonal update (the critical
-                // chain) are dispatched among the previous level's records, 2 = every panel half
-                const bool promote = promote_mode == 2 || (promote_mode == 1 && r < nb && fsrc[r] == (int32_t)k);
                 const int id = add({1, (int32_t)k, 2 * r + h, 0, 0, p, 0, (r == nb && h == 0) ? (int32_t)k : -1},
-                                   {kl(k) - (promote ? 1 : 0), 1, (int)(k * (nb + 1) + r) * 2 + h});
+                                   {kl(k), 1, (int)(k * (nb + 1) + r) * 2 + h});
                 T[id].deps.push_back(col_task[k]);
                 prog_task[p] = id;
                 s.flow_flops += 64.0 * NB * NB;
@@ -695,10 +632,8 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
                         slot = nslot;
                         nslot += 4;
                     }
-                    int wk = w;
-                    for (int32_t k : S) wk = std::max(wk, kl(k));
-                    const int need = kl(b);
-                    const int lev = defer > 0 ? std::max(wk, std::min(wk + defer, need - 1)) : std::max(wk, need - lookahead);
+                    int lev = w;  // dispatched among the records of its sources' level
+                    for (int32_t k : S) lev = std::max(lev, kl(k));
                     const int id = add({2, a, b, 4, soff, g1 - g0, slot, mode, wflag, prev, cidx, first, ng, 0, CB_BLOCKS},
                                        {lev, rank, (int)(b * (nb + 1) + a) * 4});
                     flag_deps[id] = fd;
@@ -754,16 +689,8 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
                         mode = 0;
                         flag = wflag;
                     }
-                    // dispatch level: the source level, deferred to `lookahead` levels before the
-                    // target is read (its diagonal workgroup at level[b] - 1, its panel halves at
-                    // level[b]), so updates of far-away targets do not hold CUs ahead of the next
-                    // levels' panel halves
-                    int wk = w;
-                    for (int32_t k : S) wk = std::max(wk, kl(k));
-                    const int need = a == b ? kl(b) - 1 : kl(b);
-                    // FBA_FLOW_DEFER = N: among the records of level min(source level + N, need - 1)
-                    const int lev = defer > 0 && !is_late ? std::max(wk, std::min(wk + defer, need - 1))
-                                                          : std::max(wk, need - lookahead);
+                    int lev = w;  // dispatched among the records of its sources' level
+                    for (int32_t k : S) lev = std::max(lev, kl(k));
                     const int id = add({2, a, b, q, soff, g1 - g0, slot, mode, flag, is_late ? -1 : prev, cidx, first, ng, 0,
                                         CB_BLOCKS},
                                        {lev, is_late ? 2 : rank, (int)(b * (nb + 1) + a) * 4 + q});
@@ -774,26 +701,6 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
                 if (!is_late) prev = wflag;
             }
             writer[std::make_tuple(a, b, q)] = prev;
-        }
-    }
-    // the helpers of the fused updates: column blocks [0, ksplit) of f_j's panel rows j, per quarter
-    for (int64_t j = 0; j < nb && ksplit > 0; ++j) {
-        const int32_t f = fsrc[j];
-        if (!in(j)) continue;
-        if (f < 0 || self_panel(f, j)) continue;
-        for (int q : {0, 2, 3}) {
-            const int qr = q >> 1, qc = q & 1;
-            if (q > 0 && halves(j) < 2) continue;
-            const int32_t pa = prog.at(std::make_tuple(f, (int32_t)j, qr)), pb = prog.at(std::make_tuple(f, (int32_t)j, qc));
-            const int32_t soff = (int32_t)buf.size();
-            buf.insert(buf.end(), {f, pa, pb});
-            const int32_t slot = nslot++, flag = new_uflag();
-            late[j].push_back({q, slot, flag});
-            const int id = add({2, (int32_t)j, (int32_t)j, q, soff, 1, slot, 2, flag, -1, -1, slot, 1, 0, ksplit},
-                               {level[f], 2, (int)(j * (nb + 1) + j) * 4 + q});
-            flag_deps[id] = {pa, pb};
-            uflag_tasks[flag - np].push_back(id);
-            s.flow_flops += 2.0 * 64 * 64 * IB_BLOCK * ksplit;
         }
     }
     // panel halves wait for the final writers of their quarters; diagonal blocks for those of their
@@ -821,17 +728,6 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
             X.rec[3] = woff;
             X.rec[4] = (int32_t)buf.size() - woff;
             for (int32_t x = woff; x < (int32_t)buf.size(); ++x) flag_deps[id].push_back(buf[x]);
-            if (X.rec[12]) {  // self panel: the final writers of S(j, f)'s quarters, as a panel half waits
-                const int32_t f = X.rec[2], poff = (int32_t)buf.size();
-                for (int h = 0; h < halves(j); ++h)
-                    for (int qc = 0; qc < halves(f); ++qc) {
-                        auto it = writer.find(std::make_tuple(j, f, 2 * h + qc));
-                        if (it != writer.end() && it->second >= 0) buf.push_back(it->second);
-                    }
-                X.rec[13] = poff;
-                X.rec[14] = (int32_t)buf.size() - poff;
-                for (int32_t x = poff; x < (int32_t)buf.size(); ++x) flag_deps[id].push_back(buf[x]);
-            }
             const int32_t loff = (int32_t)buf.size();
             for (auto& l : late[j]) {
                 buf.insert(buf.end(), l.begin(), l.end());
@@ -841,12 +737,10 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
             X.rec[6] = (int32_t)late[j].size();
         }
     }
-    // inverses of the diagonal blocks below the top level (FBA_FLOW_INV_LAST=1: all after the last level's
-    // records, so they hold no CU while the middle levels run; config 4: 1160-1167 vs 1162-1170 iter/s)
-    static const bool inv_last = getenv("FBA_FLOW_INV_LAST") && atoi(getenv("FBA_FLOW_INV_LAST")) != 0;
+    // inverses of the diagonal blocks below the top level
     for (int64_t j = 0; j < nb; ++j)
         if (level[j] < nw - 1 && in(j)) {
-            const int id = add({3, (int32_t)j}, {inv_last ? nw : kl(j) + 1, 5, (int)j});
+            const int id = add({3, (int32_t)j}, {kl(j) + 1, 5, (int)j});
             T[id].deps.push_back(col_task[j]);
             s.flow_flops += (double)NB * NB * NB / 3.0;
         }
@@ -880,15 +774,10 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
             const int i = ready.top();
             ready.pop();
             if (placed[i]) continue;
-            std::vector<int> emit{i};
-            auto fw = follow.find(i);
-            if (fw != follow.end()) emit.push_back(fw->second);  // (its only producer is i)
-            for (int e : emit) {
-                placed[e] = 1;
-                ord.push_back(e);
-                for (int x : succ[e])
-                    if (--indeg[x] == 0 && !placed[x]) ready.push(x);
-            }
+            placed[i] = 1;
+            ord.push_back(i);
+            for (int x : succ[i])
+                if (--indeg[x] == 0 && !placed[x]) ready.push(x);
         }
     }
     if ((int)ord.size() != n) ok = false;  // a dependency cycle
@@ -910,82 +799,18 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
             buf.insert(buf.end(), T[i].rec.begin(), T[i].rec.end());
             s.flow_cnt[T[i].rec[0]]++;
         }
-    // dynamic dispatch tables (k_chol_flow FlowDyn, record ids = positions in the static order).  Eager
-    // records (diagonal blocks, split helpers, panel halves feeding the next level or the RHS rows, update
-    // tasks whose target is read at the next level, late partials) become ready while their producers
-    // run: a panel half when its diagonal block's potrf starts, a diagonal block / update / helper when
-    // the panel halves it consumes are claimed, a diagonal block when its late partials are claimed.
-    // Everything else -- the in-place writer a record waits for at its start, and every producer of a
-    // lazy record (updates of later levels' targets, inverses) -- triggers at its end, so a lazy record
-    // holds no CU while it could only wait.  Priority: the longest path to the end (estimated us).
-    s.flow_dyn_n = 0;
-    if (ok && n > 0) {
-        auto B0 = [&](int i) { return buf[T[i].rec[4]]; };  // an update's first source column
-        // FBA_DYN_EAGER = D: a panel half (k, r) / an update of sources at level w is eager when its block
-        // row / target is read within D levels of its source's (the RHS rows: always)
-        static const int D = getenv("FBA_DYN_EAGER") ? atoi(getenv("FBA_DYN_EAGER")) : 1;
-        auto eager = [&](int i) {
-            const auto& r = T[i].rec;
-            switch (r[0]) {
-                case 0: case 4: return true;
-                case 1: { const int k = r[1], rr = r[2] >> 1; return rr == nb || level[rr] <= level[k] + D; }
-                case 2: {
-                    if (r[7] == 2) return true;  // a late partial
-                    const int a = r[1], b = r[2], w = level[B0(i)];
-                    return (a == b ? level[b] - 1 : (b == nb ? w : level[b])) - w <= D;
-                }
-                default: return false;
+    // the two pools of the persistent dispatch (k_chol_flow<true>): each a subsequence of the static order,
+    // so every wait of a record still points to an earlier record of its own pool or of the other
+    s.flow_pool = (int64_t)buf.size();
+    s.flow_pool_main = 0;
+    if (ok) {
+        for (int q = 0; q < n; ++q)
+            if (T[ord[q]].rec[0] == 0 || T[ord[q]].rec[0] == 1 || T[ord[q]].rec[0] == 4) {
+                buf.push_back(q);
+                ++s.flow_pool_main;
             }
-        };
-        auto start_edge = [&](int d, int i) {
-            if (!eager(i)) return false;
-            // a panel half of the block, or a self-panel diagonal workgroup consuming it: at its potrf's start
-            if (T[d].rec[0] == 0)
-                return T[i].rec[0] == 1 || T[i].rec[0] == 4 || (T[i].rec[0] == 0 && T[i].rec[12] != 0);
-            return true;  // consumed progressively, or waited for by a running record
-        };
-        auto dur = [&](int i) {
-            const auto& r = T[i].rec;
-            switch (r[0]) {
-                case 0: return r[2] >= 0 ? 28.0 : 18.0;
-                case 1: return 8.0;
-                case 2: return 2.0 + 4.0 * r[5];
-                case 4: return 10.0;
-                default: return 10.0;
-            }
-        };
-        std::vector<double> up(n, 0.0);
-        for (int q = n - 1; q >= 0; --q) {  // reverse topological order
-            const int i = ord[q];
-            double m = 0.0;
-            for (int x : succ[i]) m = std::max(m, up[x]);
-            up[i] = dur(i) + m;
-        }
-        std::vector<int> byprio(ord);  // descending priority, ties in the static order
-        std::stable_sort(byprio.begin(), byprio.end(), [&](int a, int b) { return up[a] > up[b]; });
-        const int64_t info = (int64_t)buf.size();
-        buf.resize(buf.size() + 8 * (size_t)n, 0);
-        std::vector<int32_t> cons;
-        for (int q = 0; q < n; ++q) {  // record q = ord[q]
-            const int i = ord[q];
-            std::vector<int32_t> st, dn;
-            for (int x : succ[i]) (start_edge(i, x) ? st : dn).push_back(pos[x]);
-            int32_t* e = &buf[info + 8 * (int64_t)q];
-            e[0] = (int32_t)T[i].deps.size();
-            e[2] = (int32_t)cons.size();
-            e[3] = (int32_t)st.size();
-            e[4] = (int32_t)dn.size();
-            cons.insert(cons.end(), st.begin(), st.end());
-            cons.insert(cons.end(), dn.begin(), dn.end());
-        }
-        s.flow_dyn_info = info;
-        s.flow_dyn_cons = (int64_t)buf.size();
-        buf.insert(buf.end(), cons.begin(), cons.end());
-        s.flow_dyn_init = (int64_t)buf.size();
-        s.flow_dyn_ninit = 0;
-        for (int i : byprio)
-            if (T[i].deps.empty()) { buf.push_back(pos[i]); s.flow_dyn_ninit++; }
-        s.flow_dyn_n = n;
+        for (int q = 0; q < n; ++q)
+            if (T[ord[q]].rec[0] == 2 || T[ord[q]].rec[0] == 3) buf.push_back(q);
     }
     // operand bytes the records move (each record's global loads and stores as the kernels issue them:
     // a diagonal block its 128x128 block, the fused source's 128 panel rows, late / helper partials, the
@@ -1339,7 +1164,6 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
         T.flops = s.flow_flops;
         s.flow_flops = 0.0;
         build_flow(s, buf, R, level, nb, real_rows, c.opt.verbose, &inc_own);
-        s.flow_dyn_n = 0;  // (static ticket order only)
         s.n_tflags = std::max(s.n_tflags, s.flow_nprog + s.flow_nuflag + T.nprog + T.nuflag);
         s.n_counters = std::max(s.n_counters, s.flow_ncounter + T.ncounter);
         s.n_scratch = std::max(s.n_scratch, s.flow_nscratch + T.nscratch);

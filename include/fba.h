@@ -135,6 +135,12 @@ int fba_image_order(const fba_problem* p, int32_t* order /*[n_slots]*/, int32_t*
 int fba_create(const fba_problem* p, const fba_settings* s, const fba_options* o, fba_ctx** out);
 void fba_destroy(fba_ctx* ctx);
 
+/* The solve the context actually runs: *split = 1 when fba_options.split was honoured (subtree split:
+ * reduce-buffer layout, ownership and the one-solve-per-accumulation rule of the split), 0 for the
+ * replicated / single-GPU solve -- a split request falls back to the replicated solve when the block
+ * pattern cannot be cut (no reference counterpart). */
+int fba_solve_mode(fba_ctx* ctx, int32_t* split);
+
 /* Buildxhat.m: initial xhat in the reference's layout.  xhat may be NULL to query u only. */
 int fba_buildxhat(fba_ctx* ctx, double* xhat /*[u]*/, int64_t* u_out);
 
@@ -227,6 +233,10 @@ int fba_probe_stats(fba_ctx* ctx, double* out /*[4]*/);
  * (k_border_combine, one workgroup on `device`) for a given symmetric 15x15 Gram matrix of the
  * forward-solved rows [y | A (7) | B (7)] (row-major): coef = [z; k] solving
  * [[A'A - I, A'B], [B'A, B'B]] [z; k] = -[A'y; B'y]. */
+/* (tests) The bound of every device hand-off poll of this context, in sleeps (0: the default 1 << 22,
+ * ~0.3 s; FBA_FLAG_SPINS in the environment sets it at fba_create): a low bound forces the timeout
+ * path -- the abort reaches every wait, the step returns FBA_ERR_HIP and xhat stays as before it. */
+int fba_set_spin_bound(fba_ctx* ctx, int64_t spins);
 int fba_test_border_solve(int32_t device, const double* gram /*[225]*/, double* coef /*[14]*/);
 
 #ifdef __cplusplus

@@ -364,7 +364,7 @@ int main(int argc, char** argv) {
     };
     // one flow: its records (at rec_off, n_rec), flag / counter / scratch spaces of its own; cols_ok(k):
     // the columns the flow may factor, tgt_ok(a, b): the blocks it may write (subtree split checks)
-    struct FlowView { const int32_t* B; int64_t rec; int n, nfl, ncnt, nscr, dyn_n; int64_t dyn_info, dyn_cons, dyn_init; int dyn_ninit; int64_t nbuf; };
+    struct FlowView { const int32_t* B; int64_t rec; int n, nfl, ncnt, nscr; int64_t nbuf; };
     auto emulate = [&](const FlowView& v, const std::function<bool(int64_t)>& cols_ok,
                        const std::function<bool(int64_t, int64_t)>& tgt_ok) -> int {
     const int32_t* B = v.B;
@@ -373,69 +373,9 @@ int main(int argc, char** argv) {
     std::vector<int> slot_set(std::max(v.nscr, 1), 0);
     auto flag_ok = [&](int32_t x, unsigned q) { return x >= 0 && x < (int32_t)fl.size() && fl[x] >= q; };
     if (v.rec + (int64_t)Sched::FLOW_REC * v.n > v.nbuf) return fail("flow record bounds");
-    // -- the dynamic dispatch (k_chol_flow FlowDyn): W workers take FIFO slots of ready records (the
-    // records ready at launch first); a claimed record completes once every producer has completed (a
-    // diagonal block's start triggers fire then: its potrf start); no state may be stuck.  The completion
-    // order is a valid execution of the records and is emulated below like the static order --
+    // records in the static ticket order (k_chol_flow: every wait points to an earlier record)
     std::vector<int> order;
-    if (v.dyn_n > 0) {
-        const int nd = v.dyn_n, W = 3 + seed % 29;
-        const int32_t* info = B + v.dyn_info;
-        const int32_t* cons = B + v.dyn_cons;
-        const int32_t* init = B + v.dyn_init;
-        if (nd != v.n) return fail("dyn: record count");
-        std::vector<int> cnt(nd, 0), pdone(nd, 0), started(nd, 0), fifo;
-        for (int q = 0; q < v.dyn_ninit; ++q) {
-            if (init[q] < 0 || init[q] >= nd || info[8 * init[q]] != 0) return fail("dyn: initial ready list");
-            fifo.push_back(init[q]);
-        }
-        int nzero = 0;
-        for (int r = 0; r < nd; ++r) nzero += info[8 * r] == 0;
-        if (nzero != v.dyn_ninit) return fail("dyn: initial ready count");
-        auto trig = [&](int r, int first, int count, bool completion) {
-            for (int i = 0; i < count; ++i) {
-                const int c = cons[info[8 * r + 2] + first + i];
-                if (++cnt[c] == info[8 * c]) fifo.push_back(c);
-                if (cnt[c] > info[8 * c]) return false;
-            }
-            if (completion)
-                for (int i = 0; i < info[8 * r + 3] + info[8 * r + 4]; ++i) pdone[cons[info[8 * r + 2] + i]]++;
-            return true;
-        };
-        std::vector<int> running;
-        size_t head = 0;
-        std::mt19937 pick(seed);
-        while ((int)order.size() < nd) {
-            bool prog = false;
-            while (head < fifo.size() && (int)running.size() < W) {
-                const int r = fifo[head++];
-                running.push_back(r);
-                if (B[v.rec + (int64_t)Sched::FLOW_REC * r] != 0 && !trig(r, 0, info[8 * r + 3], false))
-                    return fail("dyn: trigger count");
-                prog = true;
-            }
-            for (int r : running)  // diagonal blocks whose producers are all complete start their potrf
-                if (!started[r] && B[v.rec + (int64_t)Sched::FLOW_REC * r] == 0 && pdone[r] == info[8 * r]) {
-                    started[r] = 1;
-                    if (!trig(r, 0, info[8 * r + 3], false)) return fail("dyn: trigger count");
-                    prog = true;
-                }
-            std::vector<int> can;
-            for (size_t q = 0; q < running.size(); ++q)
-                if (pdone[running[q]] == info[8 * running[q]]) can.push_back((int)q);
-            if (!can.empty()) {
-                const int q = can[pick() % can.size()], r = running[q];
-                running.erase(running.begin() + q);
-                if (!trig(r, info[8 * r + 3], info[8 * r + 4], true)) return fail("dyn: trigger count");
-                order.push_back(r);
-                prog = true;
-            }
-            if (!prog) return fail("dyn: dispatch stuck (no ready record, no completable running record)");
-        }
-        if (fifo.size() != (size_t)nd) return fail("dyn: a record appended twice or never");
-    } else {
-        for (int b = 0; b < v.n; ++b) order.push_back(b);
-    }
+    for (int b = 0; b < v.n; ++b) order.push_back(b);
     std::vector<char> ran(v.n, 0);
     // a split helper (role 4): tiles (ta, tb), tb >= FLOW_CSPLIT, of C_jj -= X X', X = L(j, f)
     auto run_helper = [&](const int32_t* rec) -> int {
@@ -466,32 +406,16 @@ int main(int argc, char** argv) {
             for (int x = 0; x < rec[4]; ++x)
                 if (!flag_ok(B[rec[3] + x], 1)) return fail("flow: diagonal block waits for an unset flag");
             double* C = Fk(j, j);
-            if (f >= 0 && rec[12]) {  // self panel: this record solves its rows of f's panel itself
-                if (colf[f] != 8 || f >= j) return fail("flow: self panel before its source");
-                for (int x = 0; x < rec[14]; ++x)
-                    if (!flag_ok(B[rec[13] + x], 1)) return fail("flow: self panel waits for an unset flag");
-                if (rec[8] >= 0 || rec[11] != 0) return fail("flow: self panel record fields");
-                solve_rows(f, j, 0, NB);
-                fl[rec[7]] = 8;
-                if (rec[9] >= 0) {  // its split helper, dispatched right after it, runs beside its potrf
-                    const int hb = b + 1;
-                    const int32_t* hr = B + v.rec + (int64_t)Sched::FLOW_REC * hb;
-                    if (hb >= v.n || hr[0] != 4 || hr[1] != j || ran[hb]) return fail("flow: self panel's helper not next");
-                    ran[hb] = 1;
-                    if (run_helper(hr)) return 1;
-                }
-            }
             if (f >= 0) {
                 if (colf[f] != 8 || f >= j) return fail("flow: fused source not factored");
                 if (!flag_ok(rec[7], 8) || (rec[8] >= 0 && !flag_ok(rec[8], 8))) return fail("flow: fused rows not solved");
                 const double* X = Fk(j, f);
-                // the column blocks [rec[11], 8) (the helpers' partials the rest); with a split helper
-                // (rec[9] >= 0) only the tile columns < FLOW_CSPLIT
+                // every column block; with a split helper (rec[9] >= 0) only the tile columns < FLOW_CSPLIT
                 const int cmax = rec[9] >= 0 ? 16 * FLOW_CSPLIT : NB;
                 for (int a = 0; a < NB; ++a)
                     for (int c2 = 0; c2 <= a && c2 < cmax; ++c2) {
                         double v = 0.0;
-                        for (int t = 16 * rec[11]; t < NB; ++t) v += X[(size_t)a * n + t] * X[(size_t)c2 * n + t];
+                        for (int t = 0; t < NB; ++t) v += X[(size_t)a * n + t] * X[(size_t)c2 * n + t];
                         C[(size_t)a * n + c2] -= v;
                     }
             }
@@ -653,7 +577,7 @@ int main(int argc, char** argv) {
         for (int r = 0; r < split_world; ++r) {
             const Sched& q = per[r];
             FlowView v{q.buf.data(), q.flow_rec, q.flow_n, q.flow_nprog + q.flow_nuflag, q.flow_ncounter, q.flow_nscratch,
-                       0, 0, 0, 0, 0, (int64_t)q.buf.size()};
+                       (int64_t)q.buf.size()};
             auto own = [&](int64_t k) { return k < nb && br[k] == r; };
             auto topb = [&](int64_t k) { return k == nb || br[k] < 0; };
             if (emulate(v, own, [&](int64_t a, int64_t bb) { return (own(a) || topb(a)) && (own(bb) || topb(bb)); })) return 1;
@@ -661,7 +585,7 @@ int main(int argc, char** argv) {
                 if (own(k) && colf[k] != 8) return fail("split: a subtree column left unfactored");
         }
         const Sched& q = per[0];
-        FlowView vt{q.buf.data(), q.top.rec, q.top.n, q.top.nprog + q.top.nuflag, q.top.ncounter, q.top.nscratch, 0, 0, 0, 0, 0,
+        FlowView vt{q.buf.data(), q.top.rec, q.top.n, q.top.nprog + q.top.nuflag, q.top.ncounter, q.top.nscratch,
                     (int64_t)q.buf.size()};
         auto topc = [&](int64_t k) { return k < nb && br[k] < 0; };
         if (emulate(vt, topc, [&](int64_t a, int64_t bb) { return (a == nb || br[a] < 0) && br[bb] < 0; })) return 1;
@@ -672,8 +596,7 @@ int main(int argc, char** argv) {
         }
         printf("split world=%d top_columns=%d top_blocks=%d ", split_world, ntop, per[0].n_top_blocks);
     } else {
-        FlowView v{s.buf.data(), s.flow_rec, s.flow_n, s.flow_nprog + s.flow_nuflag, s.flow_ncounter, s.flow_nscratch,
-                   s.flow_dyn_n, s.flow_dyn_info, s.flow_dyn_cons, s.flow_dyn_init, s.flow_dyn_ninit, nbuf};
+        FlowView v{s.buf.data(), s.flow_rec, s.flow_n, s.flow_nprog + s.flow_nuflag, s.flow_ncounter, s.flow_nscratch, nbuf};
         if (emulate(v, [](int64_t) { return true; }, [](int64_t, int64_t) { return true; })) return 1;
     }
     double ferr = 0.0;

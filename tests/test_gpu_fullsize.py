@@ -359,27 +359,132 @@ def test_subtree_split_two_ranks_match_single_context(fba, scenes, config):
 
 def test_handoff_timeout_fails_safe(fba, scenes, monkeypatch):
     """A device hand-off timeout in the factorisation (every poll bounded, fba_chol.hip) must not leave a
-    wrong iterate behind: with the poll bound forced down to one sleep (FBA_FLAG_SPINS, read when a context
-    is created) some wait of k_chol_flow / k_bwd_flow expires, the abort reaches every other wait, the
-    step returns FBA_ERR_HIP and xhat is exactly as before it.  The same context then steps normally
-    once the bound is back (the sync words are re-zeroed ahead of every factorisation) and matches a
-    fresh context bit for bit."""
+    wrong iterate behind: with the poll bound forced down to one sleep (FBA_FLAG_SPINS at context
+    creation: this context's bound, scal[SCAL_SPINS]) some wait of k_chol_flow / k_bwd_flow expires, the
+    abort reaches every other wait, the step returns FBA_ERR_HIP and xhat is exactly as before it.  A
+    context created beside it with the default bound is unaffected (the bound is per context), and the
+    failed context, its bound restored (fba_set_spin_bound), then steps normally (the sync words are
+    re-zeroed ahead of every factorisation) and matches the fresh context bit for bit."""
     folder = _scene(3, scenes)
     ds = fba.load_folder(folder)
     monkeypatch.setenv("FBA_FLAG_SPINS", "1")
     ctx = _ctx(fba, ds)
+    monkeypatch.delenv("FBA_FLAG_SPINS")
+    fresh = _ctx(fba, ds)
     try:
         x0 = ctx.get_xhat()
         with pytest.raises(fba.capi.FBAError) as ei:
             ctx.step()
         assert ei.value.code == 3 and "timeout" in str(ei.value), ei.value  # FBA_ERR_HIP
         assert np.array_equal(ctx.get_xhat(), x0)
-        monkeypatch.delenv("FBA_FLAG_SPINS")
-        fresh = _ctx(fba, ds)  # (resets the process-wide bound to its default)
-        try:
-            d, d_fresh = ctx.step(), fresh.step()
-            assert d == d_fresh and np.array_equal(ctx.get_xhat(), fresh.get_xhat())
-        finally:
-            fresh.close()
+        ctx.set_spin_bound(0)
+        d, d_fresh = ctx.step(), fresh.step()
+        assert d == d_fresh and np.array_equal(ctx.get_xhat(), fresh.get_xhat())
     finally:
         ctx.close()
+        fresh.close()
+
+
+def _sum_buffers(hip, ranks):
+    """the all-reduce of the ranks' reduce buffers, on the host"""
+    bufs = [c.reduce_buffer() for c in ranks]
+    assert bufs[0][1] == bufs[1][1]
+    total = np.zeros(bufs[0][1])
+    for p, n in bufs:
+        a = np.empty(n)
+        assert hip.hipMemcpy(a.ctypes.data, p, n * 8, 2) == 0
+        total += a
+    for p, n in bufs:
+        assert hip.hipMemcpy(p, total.ctypes.data, n * 8, 1) == 0
+
+
+def test_subtree_split_abort_reaches_every_rank(fba, scenes):
+    """Subtree split (config 3, two rank contexts on one GPU): a hand-off timeout inside rank 0's flow A
+    (run in fba_accumulate) leaves its top-block contributions incomplete.  The abort travels in the
+    reduce buffer (its last slot), so after the sum EVERY rank skips flow B and the update and returns
+    FBA_ERR_HIP with xhat as before -- not only the rank that timed out.  With the bound restored, the
+    next accumulation / solve of both ranks reassembles the single context's first iterate (1e-9 per
+    group and per element)."""
+    import ctypes
+    folder = _scene(3, scenes)
+    ds = fba.load_folder(folder)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    mk = lambda **kw: fba.capi.Context(ds.pack(), fba.capi.make_settings(ds.settings), **kw)  # noqa: E731
+    single = mk()
+    ranks = [mk(rank=r, world=2, split=True) for r in range(2)]
+    try:
+        assert all(c.split for c in ranks)
+        x0 = [c.get_xhat() for c in ranks]
+        ranks[0].set_spin_bound(1)
+        for c in ranks:
+            c.accumulate()
+            c.synchronize()
+        _sum_buffers(hip, ranks)
+        for c, x in zip(ranks, x0):
+            with pytest.raises(fba.capi.FBAError) as ei:
+                c.solve_update()
+            assert ei.value.code == 3, ei.value
+            assert np.array_equal(c.get_xhat(), x)
+        ranks[0].set_spin_bound(0)
+        d1 = single.step()
+        for c in ranks:
+            c.accumulate()
+            c.synchronize()
+        _sum_buffers(hip, ranks)
+        parts = [c.solve_update() for c in ranks]
+        assert abs(sum(parts) - d1) <= 1e-9 * d1
+        xr = sum(c.get_xhat(owned_only=True) for c in ranks)
+        dsc = dist_scaling_of(__import__("fba_oracle").load_folder(folder))
+        names = fba.xhat_names(ds)
+        # (one pass from the start: reduction-order rounding moves k1, the ill-conditioned radial direction,
+        # by 8.5e-10 of its group -- measured; the later passes of the two-pass test contract it to 3e-11)
+        err = group_rel_err(xr, single.get_xhat(), names, dsc)
+        assert max(err.values()) <= 1e-9, err
+        err = elem_rel_err(xr, single.get_xhat(), names, dsc)
+        assert max(err.values()) <= 1e-9, err
+    finally:
+        single.close()
+        for c in ranks:
+            c.close()
+
+
+def test_subtree_split_guards(fba, scenes, tmp_path, monkeypatch):
+    """The split's contract at its edges: one solve per accumulation (a second fba_solve_update of the same
+    accumulation is refused with FBA_ERR_ARG instead of running flow B on spent tickets); the per-level
+    backward solve (FBA_BWD_LEVELS=1), which knows neither the ranks' column ownership nor the split's
+    border scales, is refused at creation (FBA_ERR_UNSUPPORTED) like the per-level factorisation; and a
+    split request on a block pattern that cannot be cut (12 images: one block of image rows) falls back
+    to the replicated solve, which fba_solve_mode / Context.split report."""
+    import ctypes
+    folder = _scene(3, scenes)
+    ds = fba.load_folder(folder)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    mk = lambda d, **kw: fba.capi.Context(d.pack(), fba.capi.make_settings(d.settings), **kw)  # noqa: E731
+    ranks = [mk(ds, rank=r, world=2, split=True) for r in range(2)]
+    try:
+        for c in ranks:
+            c.accumulate()
+            c.synchronize()
+        _sum_buffers(hip, ranks)
+        for c in ranks:
+            c.solve_update()
+        with pytest.raises(fba.capi.FBAError) as ei:
+            ranks[0].solve_update()
+        assert ei.value.code == 1 and "one fba_solve_update per fba_accumulate" in str(ei.value)
+    finally:
+        for c in ranks:
+            c.close()
+    monkeypatch.setenv("FBA_BWD_LEVELS", "1")
+    with pytest.raises(fba.capi.FBAError) as ei:
+        mk(ds, rank=0, world=2, split=True)
+    assert ei.value.code == 5, ei.value
+    monkeypatch.delenv("FBA_BWD_LEVELS")
+    from fba_amd import synth
+    small = fba.load_folder(synth.write_folder(synth.generate(12, 240, seed=17), str(tmp_path / "s12")))
+    c = mk(small, rank=0, world=2, split=True)
+    try:
+        assert not c.split
+    finally:
+        c.close()

@@ -24,22 +24,19 @@ def checker(tmp_path_factory):
     return exe
 
 
-@pytest.mark.parametrize("n_img,seed,leaf,merge,self_panel,block", [
-    (40, 1, None, None, 0, None), (300, 2, None, None, 0, None), (300, 1, 60, None, 0, None),
-    (420, 3, 100, None, 0, None), (200, 4, 0, None, 0, None), (300, 2, None, 1, 0, None), (300, 1, 60, 2, 0, None),
-    # FBA_FLOW_SELF=1 (diagonal workgroups solving their fused source's panel rows; measured, off by default)
-    (300, 2, None, None, 1, None), (420, 3, 100, None, 1, None),
+@pytest.mark.parametrize("n_img,seed,leaf,merge,block", [
+    (40, 1, None, None, None), (300, 2, None, None, None), (300, 1, 60, None, None),
+    (420, 3, 100, None, None), (200, 4, 0, None, None), (300, 2, None, 1, None), (300, 1, 60, 2, None),
     # FBA_FLOW_BLOCK: whole-block update tasks -- every group (1, the default of a throughput-bound
     # factorisation), all but the urgent last group (2), the groups with slack (3): whole-block and
     # quarter writers of one target chained
-    (300, 2, None, None, 0, 1), (420, 3, 100, None, 0, 2), (300, 1, 60, 2, 0, 3), (40, 1, None, None, 0, 1),
-    (300, 2, None, None, 0, "1s1"), (420, 3, 100, None, 0, "1m8")])
-def test_level_schedule_matches_dense_cholesky(checker, n_img, seed, leaf, merge, self_panel, block):
+    (300, 2, None, None, 1), (420, 3, 100, None, 2), (300, 1, 60, 2, 3), (40, 1, None, None, 1),
+    (300, 2, None, None, "1s1"), (420, 3, 100, None, "1m8")])
+def test_level_schedule_matches_dense_cholesky(checker, n_img, seed, leaf, merge, block):
     env = dict(os.environ)
     env.pop("FBA_ND_LEAF", None)
     env.pop("FBA_FLOW_MERGE", None)
     env.pop("FBA_FLOW_BLOCK", None)
-    env["FBA_FLOW_SELF"] = str(self_panel)
     env.pop("FBA_FLOW_SPLIT", None)
     env.pop("FBA_FLOW_MSPLIT", None)
     if block is not None:  # "1s1": one source per record, "1m8": merged groups of up to 8 sources
@@ -72,7 +69,6 @@ def test_subtree_split_schedule(checker, n_img, seed, leaf, world):
     env = dict(os.environ)
     env.pop("FBA_ND_LEAF", None)
     env.pop("FBA_FLOW_MERGE", None)
-    env["FBA_FLOW_SELF"] = "0"
     if leaf is not None:
         env["FBA_ND_LEAF"] = str(leaf)
     env["SCHED_SPLIT_WORLD"] = str(world)
