@@ -352,13 +352,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     }
     // default: lexicographic order of the points' (sorted) image sets -- consecutive points share most
     // of their co-visible pairs, so the rows k_pairs gathers for one pair sit close together
-    // (FBA_POINT_ORDER=morton: the Z-curve order alone)
-    const char* po = getenv("FBA_POINT_ORDER");
-    if (po && std::string(po) == "morton") {
-        std::stable_sort(lps.begin(), lps.end(), [&](int32_t a, int32_t b) {
-            return tie_cam[a] != tie_cam[b] ? tie_cam[a] < tie_cam[b] : zkey[a] < zkey[b];
-        });
-    } else {
+    {
         std::vector<std::vector<int32_t>> iset(L.n_tie);
         for (int32_t t : lps) {
             for (int64_t i : tie_obs[t]) iset[t].push_back(c->img_new[p->img[i]]);
@@ -836,8 +830,7 @@ static inline void mark(Ctx* c, int i) {
 }
 
 static bool graph_eligible(const Ctx* c) {
-    static const bool off = getenv("FBA_NO_GRAPH") && atoi(getenv("FBA_NO_GRAPH")) != 0;
-    return !off && c->graphs_ok && c->stream && !c->timing && !c->probe && !c->d_lrprof && !c->d_ptrace;
+    return c->graphs_ok && c->stream && !c->timing && !c->probe && !c->d_lrprof && !c->d_ptrace;
 }
 
 // run body() on the context's stream, through a graph captured from its first run when eligible

@@ -2595,17 +2595,6 @@ __device__ __forceinline__ void flow_record(int rid, double* __restrict__ S, int
     }
 }
 
-// POOLED = false: one workgroup per record (grid = records).  POOLED = true (FBA_FLOW_MAIN = K): a
-// persistent grid of one workgroup per CU in two pools -- the first K workgroups to start run the
-// critical records (diagonal blocks, panel halves, split helpers: pools[0, n_main)), the others the update
-// tasks and inverses (pools[n_main, n)), each pool taking its records in the static order from its own
-// ticket -- so update tasks waiting on progressively published columns never hold every CU while a
-// diagonal block waits for one.  Deadlock-free: the earliest unfinished record (static order) has all
-// its producers done; its pool hands out its records in order, so it is taken as soon as the records
-// before it in that pool -- all finished -- released their workgroups, and every pool keeps >= 1
-// workgroup (pool by arrival order: only running workgroups are counted).  ticket: [0] static ticket,
-// [3] arrivals, [4], [5] the pools' tickets (zeroed with the other sync words by k_border_rhs).
-template <bool POOLED>
 __global__ __launch_bounds__(POTRF_THREADS) void k_chol_flow(double* __restrict__ S, int64_t ld,
                                                              const int32_t* __restrict__ lists,
                                                              const int32_t* __restrict__ recs,
@@ -2613,49 +2602,32 @@ __global__ __launch_bounds__(POTRF_THREADS) void k_chol_flow(double* __restrict_
                                                              double* __restrict__ scal, unsigned* __restrict__ colflags,
                                                              unsigned* __restrict__ fl, unsigned* __restrict__ cnt,
                                                              double* __restrict__ P, uint64_t* __restrict__ trace,
-                                                             double* __restrict__ gblk, unsigned* __restrict__ ticket,
-                                                             const int32_t* __restrict__ pools, int n_main, int n_all,
-                                                             int k_main) {
+                                                             double* __restrict__ gblk, unsigned* __restrict__ ticket) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     __shared__ int s_ticket;
-    if constexpr (!POOLED) {
-        const uint64_t t_wg = trace ? wall_clock64() : 0;
-        if (threadIdx.x == 0) {
-            // static order: the record comes from an atomic ticket, not from blockIdx: tickets follow the
-            // order in which the workgroups really start, and every record waits only for records of smaller
-            // index (build_flow's order check), so each wait points to a workgroup that has already started
-            // and is resident (or done) -- progress does not depend on the hardware dispatching blockIdx in
-            // order, nor on every record being co-resident
-            s_ticket = (int)__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        // a record that starts after a hand-off timeout is skipped (its inputs may never be published)
-        if (threadIdx.x == 0 && s_ticket >= 0 && hand_off_aborted(scal)) s_ticket = -1;
-        __syncthreads();
-        const int rid = s_ticket;
-        if (rid < 0) return;
-        if (trace && threadIdx.x == 0) trace[FTRACE * (int64_t)rid + 48] = t_wg;
-        flow_record(rid, S, ld, lists, recs, dinv, linv, scal, colflags, fl, cnt, P, trace, gblk, smem);
-    } else {
-        __shared__ int s_pool;
-        if (threadIdx.x == 0)
-            s_pool = __hip_atomic_fetch_add(ticket + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)k_main ? 0 : 1;
-        __syncthreads();
-        const int pool = s_pool;
-        const int first = pool ? n_main : 0, count = pool ? n_all - n_main : n_main;
-        for (;;) {
-            const uint64_t t_wg = trace ? wall_clock64() : 0;
-            if (threadIdx.x == 0) {
-                const unsigned t = __hip_atomic_fetch_add(ticket + 4 + pool, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s_ticket = (t < (unsigned)count && !hand_off_aborted(scal)) ? pools[first + t] : -1;
-            }
-            __syncthreads();
-            const int rid = s_ticket;
-            if (rid < 0) return;
-            if (trace && threadIdx.x == 0) trace[FTRACE * (int64_t)rid + 48] = t_wg;
-            flow_record(rid, S, ld, lists, recs, dinv, linv, scal, colflags, fl, cnt, P, trace, gblk, smem);
-            __syncthreads();  // (s_ticket and the LDS are the next record's)
-        }
+    const uint64_t t_wg = trace ? wall_clock64() : 0;
+    if (threadIdx.x == 0) {
+        // static order: the record comes from an atomic ticket, not from blockIdx: tickets follow the
+        // order in which the workgroups really start, and every record waits only for records of smaller
+        // index (build_flow's order check), so each wait points to a workgroup that has already started
+        // and is resident (or done) -- progress does not depend on the hardware dispatching blockIdx in
+        // order, nor on every record being co-resident.  (Measured and not kept, round 5: the critical
+        // records -- diagonal blocks, panel halves, split helpers -- and the others in two queues, each a
+        // subsequence of this order, (a) on a persistent grid of one workgroup per CU, K of them for the
+        // critical queue: 1,122-1,297 us per launch at config 4 for K = 48..176 vs 451 us, the record
+        // bodies inside the workgroup's loop spilling 2,320 B per lane; (b) one workgroup per record with
+        // a budget of K resident critical records and #CU - K others: 580-868 us for K = 32..128, and a
+        // hand-off timeout at K = 176 -- the update queue runs ahead of the critical one, whose budget
+        // then throttles the wide lower levels.)
+        s_ticket = (int)__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    // a record that starts after a hand-off timeout is skipped (its inputs may never be published)
+    if (threadIdx.x == 0 && s_ticket >= 0 && hand_off_aborted(scal)) s_ticket = -1;
+    __syncthreads();
+    const int rid = s_ticket;
+    if (rid < 0) return;
+    if (trace && threadIdx.x == 0) trace[FTRACE * (int64_t)rid + 48] = t_wg;
+    flow_record(rid, S, ld, lists, recs, dinv, linv, scal, colflags, fl, cnt, P, trace, gblk, smem);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2935,10 +2907,10 @@ int launch_cholesky(Ctx& c, int part) {
         const int64_t fo = b ? s.flow_nprog + s.flow_nuflag : 0, co = b ? s.flow_ncounter : 0, so = b ? s.flow_nscratch : 0;
         const bool pp = c.probe == 2 && c.probe_n < (int)c.probe_ev.size() / 2;
         if (pp) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
-        k_chol_flow<false><<<(unsigned)n, POTRF_THREADS, FLOW_LDS, c.stream>>>(
+        k_chol_flow<<<(unsigned)n, POTRF_THREADS, FLOW_LDS, c.stream>>>(
             c.d_S, ld, c.d_sched, c.d_sched + (b ? T.rec : s.flow_rec), c.d_dinv, c.d_linv, c.d_scal, c.d_flags,
             c.d_tflags + fo, c.d_counters + co, c.d_P + so * 4096, nullptr, c.set.inner_constraints ? c.d_gblk : nullptr,
-            c.d_tickets + (b ? 2 : 0), nullptr, 0, 0, 0);
+            c.d_tickets + (b ? 2 : 0));
         if (pp) {
             FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], c.stream));
             c.probe_flops += b ? T.flops : s.flow_flops;
@@ -2951,16 +2923,9 @@ int launch_cholesky(Ctx& c, int part) {
         // the whole factorisation + forward solve in one persistent launch (flags zeroed by k_border_rhs)
         const bool pp = c.probe == 2 && c.probe_n < (int)c.probe_ev.size() / 2;
         if (pp) FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n], c.stream));
-        const int grid = (int)std::min<int64_t>(c.n_cu, s.flow_n);  // (both pools need a workgroup)
-        if (c.flow_main > 0 && c.flow_main < grid)
-            k_chol_flow<true><<<(unsigned)grid, POTRF_THREADS, FLOW_LDS, c.stream>>>(
-                c.d_S, ld, c.d_sched, c.d_sched + s.flow_rec, c.d_dinv, c.d_linv, c.d_scal, c.d_flags, c.d_tflags,
-                c.d_counters, c.d_P, c.d_ptrace, c.set.inner_constraints ? c.d_gblk : nullptr, c.d_tickets,
-                c.d_sched + s.flow_pool, s.flow_pool_main, s.flow_n, c.flow_main);
-        else
-            k_chol_flow<false><<<(unsigned)s.flow_n, POTRF_THREADS, FLOW_LDS, c.stream>>>(
-                c.d_S, ld, c.d_sched, c.d_sched + s.flow_rec, c.d_dinv, c.d_linv, c.d_scal, c.d_flags, c.d_tflags,
-                c.d_counters, c.d_P, c.d_ptrace, c.set.inner_constraints ? c.d_gblk : nullptr, c.d_tickets, nullptr, 0, 0, 0);
+        k_chol_flow<<<(unsigned)s.flow_n, POTRF_THREADS, FLOW_LDS, c.stream>>>(
+            c.d_S, ld, c.d_sched, c.d_sched + s.flow_rec, c.d_dinv, c.d_linv, c.d_scal, c.d_flags, c.d_tflags,
+            c.d_counters, c.d_P, c.d_ptrace, c.set.inner_constraints ? c.d_gblk : nullptr, c.d_tickets);
         if (pp) {
             FBA_HIP(hipEventRecord(c.probe_ev[2 * c.probe_n + 1], c.stream));
             c.probe_flops += s.flow_flops;
@@ -3018,7 +2983,7 @@ int launch_cholesky(Ctx& c, int part) {
         }
         pend = -1;
         if (W.ntask == 0) continue;
-        if (c.merge_updates && W.ntask <= c.merge_max) pend = w;  // into the next level's k_panel
+        if (c.merge_updates) pend = w;  // into the next level's k_panel
         else updates(w);
     }
     if (pend >= 0) updates(pend);
@@ -3128,8 +3093,7 @@ int chol_setup(Ctx& c) {
     FBA_HIP(hipFuncSetAttribute((const void*)k_potrf128<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)POTRF_LDS));
     FBA_HIP(hipFuncSetAttribute((const void*)k_trsm128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRSM_LDS));
     FBA_HIP(hipFuncSetAttribute((const void*)k_panel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)PANEL_LDS));
-    FBA_HIP(hipFuncSetAttribute((const void*)k_chol_flow<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)FLOW_LDS));
-    FBA_HIP(hipFuncSetAttribute((const void*)k_chol_flow<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)FLOW_LDS));
+    FBA_HIP(hipFuncSetAttribute((const void*)k_chol_flow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)FLOW_LDS));
     // FBA_CHOL_FLOW=0: the level-by-level k_panel launches instead of the persistent dataflow launch
     c.chol_flow = !(getenv("FBA_CHOL_FLOW") && atoi(getenv("FBA_CHOL_FLOW")) == 0);
     static_assert(TRSM_LDS >= POTRF_LDS, "k_panel LDS");
@@ -3139,18 +3103,14 @@ int chol_setup(Ctx& c) {
     // (one more than the blocks: k_bwd_flow's border-combine flag; a multiple of 16 bytes)
     c.flags_bytes = (size_t)((c.L.n_pad / CB + 1 + 3) / 4 * 4) * sizeof(unsigned);
     const size_t nf = c.flags_bytes / sizeof(unsigned);
-    // [flags][bflags][split-target counters][update flags][tickets: k_chol_flow, k_bwd_flow, flow B, and
-    // k_chol_flow<true>'s arrivals and two pool tickets]
-    c.n_sync = (int64_t)(2 * nf + std::max(c.sched.n_counters, 1) + std::max(c.sched.n_tflags, 1) + 6);
+    // [flags][bflags][split-target counters][update flags][3 tickets: k_chol_flow, k_bwd_flow, flow B]
+    c.n_sync = (int64_t)(2 * nf + std::max(c.sched.n_counters, 1) + std::max(c.sched.n_tflags, 1) + 3);
     FBA_HIP(hipMalloc((void**)&c.d_flags, sizeof(unsigned) * c.n_sync));
     FBA_HIP(hipMemset(c.d_flags, 0, sizeof(unsigned) * c.n_sync));
     c.d_bflags = c.d_flags + nf;
     c.d_counters = c.d_bflags + nf;
     c.d_tflags = c.d_counters + std::max(c.sched.n_counters, 1);
     c.d_tickets = c.d_tflags + std::max(c.sched.n_tflags, 1);
-    // FBA_FLOW_MAIN = K (0 < K < #CU): k_chol_flow as a persistent grid of one workgroup per CU, K of them
-    // for the critical records (k_chol_flow<true>); unset / 0: one workgroup per record
-    c.flow_main = getenv("FBA_FLOW_MAIN") ? atoi(getenv("FBA_FLOW_MAIN")) : 0;
     // FBA_BWD_LEVELS=1: the level-by-level backward solve (k_bwd_wave) instead of k_bwd_flow
     c.bwd_flow = !(getenv("FBA_BWD_LEVELS") && atoi(getenv("FBA_BWD_LEVELS")) != 0);
     // the subtree split runs flow A / flow B of k_chol_flow and k_bwd_flow's ownership masks and border
@@ -3163,8 +3123,7 @@ int chol_setup(Ctx& c) {
     // every level's trailing updates run inside the next level's k_panel (config 4: 968 iter/s merged
     // at any size vs 931 with the levels of > 450 tasks in their own k_syrk_multi launch, now that the
     // in-launch update runs on eight waves with coalesced whole-row loads; it measured the other way
-    // round with the earlier four-wave sliced update); FBA_MERGE_MAX caps the merged size
-    c.merge_max = getenv("FBA_MERGE_MAX") ? atoi(getenv("FBA_MERGE_MAX")) : (1 << 30);
+    // round with the earlier four-wave sliced update)
     FBA_HIP(hipFuncSetAttribute((const void*)k_trtri128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRTRI_LDS));
 
     // FBA_FLAG_SPINS (tests): the bound of every hand-off poll of THIS context (scal[SCAL_SPINS], read

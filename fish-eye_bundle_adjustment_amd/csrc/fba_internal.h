@@ -102,11 +102,6 @@ struct Sched {
     int64_t flow_rec = 0;
     int flow_n = 0, flow_nprog = 0, flow_nuflag = 0, flow_ncounter = 0, flow_nscratch = 0;
     int flow_cnt[5] = {0, 0, 0, 0, 0};  // records per role
-    // the records of the two dispatch pools of k_chol_flow's persistent variant, record ids in the static
-    // order: [flow_pool_main critical records: diagonal blocks, panel halves, split helpers][the others:
-    // update tasks, inverses]
-    int64_t flow_pool = 0;
-    int flow_pool_main = 0;
     bool flow_ok = false;
     double flow_flops = 0.0;
     double flow_bytes = 0.0;      // operand bytes the records load and store (build_flow)
@@ -293,7 +288,6 @@ struct Ctx {
     int64_t n_sync = 0;           // unsigned words of flags + bflags + counters (one allocation at d_flags,
                                   // zeroed by k_border_rhs ahead of every factorisation)
     bool bwd_flow = true;
-    int merge_max = 1 << 30;        // ... for levels of at most this many update tasks (FBA_MERGE_MAX)
     bool merge_updates = true;      // a level's trailing updates inside the next level's k_panel
                                     // (FBA_MERGE_UPDATES=0: their own k_syrk_multi launch)
     bool chol_flow = true;          // the factorisation as one persistent k_chol_flow launch (FBA_CHOL_FLOW=0:
@@ -323,11 +317,10 @@ struct Ctx {
     // state
     bool have_lin = false;       // d_J holds a linearisation
     bool solved = false;         // this accumulation's solve enqueued (S holds its factor now)
-    bool force_sync = false;
-    int flow_main = 0;           // FBA_FLOW_MAIN: k_chol_flow's critical-record pool size (0: per-record grid)     // FBA_SYNC=1 at creation: wait for a solve by hipStreamSynchronize
+    bool force_sync = false;     // FBA_SYNC=1 at creation: wait for a solve by hipStreamSynchronize
     bool have_delta = false;
-    bool have_factor = false;
-    bool pending = false;        // fba_solve_update_async enqueued, fba_solve_finish not yet called    // d_S holds the factor of the last solve (fba_covariance consumes it)
+    bool have_factor = false;    // d_S holds the factor of the last solve (fba_covariance consumes it)
+    bool pending = false;        // fba_solve_update_async enqueued, fba_solve_finish not yet called
     std::vector<int32_t> ref_img_cam;  // [n_img_ref] camera of each EXT image (-1: no observation)
     int iterations = 0;
     bool timing = false;

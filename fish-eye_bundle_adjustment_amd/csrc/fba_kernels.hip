@@ -432,7 +432,7 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     const int32_t* __restrict__ chunk_obs, const int32_t* __restrict__ chunk_pt, const int32_t* __restrict__ lp_start,
     const int32_t* __restrict__ A, const AccPlan plan, double* __restrict__ WT, double* __restrict__ PT,
     double* __restrict__ ppart, double* __restrict__ ipart, double* __restrict__ cpart, int64_t u_c, int type,
-    int cam_stride, unsigned eop_mask, unsigned cam_mask, double px, double py, uint64_t* __restrict__ tprof, int dbg,
+    int cam_stride, unsigned eop_mask, unsigned cam_mask, double px, double py, uint64_t* __restrict__ tprof,
     int n_chunks, double* __restrict__ S, int64_t ld, const int32_t* __restrict__ zblk,
     const int32_t* __restrict__ xoff) {
     using LY = Lay<NK>;
@@ -729,7 +729,7 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     constexpr int NV = (IV + GL - 1) / GL * GL, M = NV / GL;  // padded to the GL-lane reduce-scatter
     {
         const int nk = ki1 - ki0, nu = 3 * nk, g8 = t & (GL - 1);
-        for (int ub = t / GL; ub < nu && !(dbg & 1); ub += LR_THREADS / GL) {
+        for (int ub = t / GL; ub < nu; ub += LR_THREADS / GL) {
             const int part = ub / nk, K = ki0 + ub % nk;
             const int x0 = s_iko[K - ki0], x1 = s_iko[K - ki0 + 1];
             double v[NV];
@@ -850,10 +850,8 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
             for (int q = 0; q < 6; ++q) out[q] = double2{-acc[2 * q], -acc[2 * q + 1]};
         }
     };
-    if (!(dbg & 2)) {  // FBA_LR_SKIP (profiling only): bit 2 leaves out the pair items
-        if (stage_terms) pair_items(s_pkt, s_term, 0);
-        else pair_items(A + plan.pk_t + kp0, A + plan.pk_term + tb0, tb0);
-    }
+    if (stage_terms) pair_items(s_pkt, s_term, 0);
+    else pair_items(A + plan.pk_t + kp0, A + plan.pk_term + tb0, tb0);
     __syncthreads();
     stamp(5);
 }
@@ -1450,8 +1448,7 @@ int launch_accumulate(Ctx& c, bool zeroed) {
     k_lin_reduce<NKV><<<(unsigned)(nlr + ztail), LR_THREADS, LR<NKV>::LDS, c.stream>>>(                           \
         c.d_xy, c.d_img, c.d_cam, c.d_pt, c.d_lp_tie, c.d_ctl, c.d_xfull, c.d_img_tab, c.d_cam_tab,                \
         c.d_chunk_obs, c.d_chunk_pt, c.d_lp_start, c.d_acc, c.acc, c.d_WT, c.d_pt_tab, c.d_ppart, c.d_ipart,       \
-        c.d_cpart, c.L.u_c, c.set.type, c.cam_tab_stride, em, cm, px, py, c.d_lrprof,                              \
-        c.d_lrprof && getenv("FBA_LR_SKIP") ? atoi(getenv("FBA_LR_SKIP")) : 0, (int)nlr, c.d_S, L.ld,              \
+        c.d_cpart, c.L.u_c, c.set.type, c.cam_tab_stride, em, cm, px, py, c.d_lrprof, (int)nlr, c.d_S, L.ld,      \
         c.d_sched + c.sched.zero, c.d_xoff);                                                                      \
     {                                                                                                             \
         const int npb = (int)((c.n_pairs + 3) / 4), nib = (L.n_img + 1) / 2, ncb = (L.n_cam * CAM_SEG + 1) / 2;   \

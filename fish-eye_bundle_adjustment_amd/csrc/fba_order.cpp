@@ -65,17 +65,7 @@ class Dissection {
   public:
     // pos: image centres (3 per image) for coordinate bisection, or empty (level-structure bisection)
     Dissection(const Graph& g, int leaf, std::vector<double> pos)
-        : g_(g), leaf_(leaf), pos_(std::move(pos)), tag_(g.n, -1), lev_(g.n, -1), deg_(g.n, 0) {
-        // the split fractions tried by a bisection, in percent (FBA_ND_FRAC="lo,hi,step")
-        if (const char* fr = getenv("FBA_ND_FRAC")) {
-            int a = 0, b = 0, c = 0;
-            if (sscanf(fr, "%d,%d,%d", &a, &b, &c) == 3 && a > 0 && b < 100 && a <= b && c > 0) {
-                frac_lo_ = a;
-                frac_hi_ = b;
-                frac_step_ = c;
-            }
-        }
-    }
+        : g_(g), leaf_(leaf), pos_(std::move(pos)), tag_(g.n, -1), lev_(g.n, -1), deg_(g.n, 0) {}
 
     // order the vertices (all of one tag), appending to out; -1 entries are padding slots
     void nd(std::vector<int32_t> verts, std::vector<int32_t>& out) {
@@ -378,11 +368,10 @@ std::vector<int32_t> camera_order(const fba_problem* p) {
     std::vector<int32_t> all(p->n_img), out;
     for (int v = 0; v < p->n_img; ++v) all[v] = v;
     out.reserve(p->n_img + p->n_img / 8);
-    // coordinate bisection on the approximate image centres when they span the block (FBA_ND_MODE=bfs:
+    // coordinate bisection on the approximate image centres when they span the block (otherwise a
     // level-structure bisection of the graph alone)
     std::vector<double> pos;
-    const char* me = getenv("FBA_ND_MODE");
-    if (p->eop0 && !(me && std::string(me) == "bfs")) {
+    if (p->eop0) {
         pos.resize(3 * (size_t)p->n_img);
         double lo = 1e300, hi = -1e300;
         for (int v = 0; v < p->n_img; ++v)
@@ -799,19 +788,6 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
             buf.insert(buf.end(), T[i].rec.begin(), T[i].rec.end());
             s.flow_cnt[T[i].rec[0]]++;
         }
-    // the two pools of the persistent dispatch (k_chol_flow<true>): each a subsequence of the static order,
-    // so every wait of a record still points to an earlier record of its own pool or of the other
-    s.flow_pool = (int64_t)buf.size();
-    s.flow_pool_main = 0;
-    if (ok) {
-        for (int q = 0; q < n; ++q)
-            if (T[ord[q]].rec[0] == 0 || T[ord[q]].rec[0] == 1 || T[ord[q]].rec[0] == 4) {
-                buf.push_back(q);
-                ++s.flow_pool_main;
-            }
-        for (int q = 0; q < n; ++q)
-            if (T[ord[q]].rec[0] == 2 || T[ord[q]].rec[0] == 3) buf.push_back(q);
-    }
     // operand bytes the records move (each record's global loads and stores as the kernels issue them:
     // a diagonal block its 128x128 block, the fused source's 128 panel rows, late / helper partials, the
     // published factor and leaf inverses; a panel half its 64 rows in and out, the column's factor and

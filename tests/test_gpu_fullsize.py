@@ -74,9 +74,11 @@ def test_config3_adjust_matches_oracle(fba, fbo, oracle, scenes):
                                  {"FBA_CHOL_FLOW": "0", "FBA_BWD_LEVELS": "1"},
                                  {"FBA_FLOW_BLOCK": "1"}, {"FBA_FLOW_BLOCK": "3"},
                                  {"FBA_FLOW_BLOCK": "1", "FBA_FLOW_SPLIT": "1"},
-                                 {"FBA_FLOW_BLOCK": "1", "FBA_FLOW_MSPLIT": "8"}],
+                                 {"FBA_FLOW_BLOCK": "1", "FBA_FLOW_MSPLIT": "8"},
+                                 {"FBA_FLOW_MERGE": "0"}, {"FBA_ND_LEAF": "60"}],
                          ids=["per-level-factor", "per-level-backward", "both", "whole-block-updates",
-                              "whole-block-then-quarters", "whole-block-partials", "whole-block-merged-partials"])
+                              "whole-block-then-quarters", "whole-block-partials", "whole-block-merged-partials",
+                              "no-level-merging", "nd-leaf-60"])
 def test_config3_fallback_paths_match_oracle(fba, fbo, oracle, scenes, env, monkeypatch):
     """The non-default solve paths (read per context in chol_setup): the per-level k_panel launches
     instead of the persistent k_chol_flow (with k_border_gram -> k_border_combine), and the per-level
@@ -85,7 +87,9 @@ def test_config3_fallback_paths_match_oracle(fba, fbo, oracle, scenes, env, monk
     (syrk_block_body; config 3 is latency-bound, so its default is quarter records) for every writer
     group, or for the leading groups with the quarter records chained after them; with one source per
     record (FBA_FLOW_SPLIT=1) or merged writer groups of up to 8 sources (FBA_FLOW_MSPLIT=8), so targets
-    are summed through the 128 x 128 scratch partials the last arriving record combines."""
+    are summed through the 128 x 128 scratch partials the last arriving record combines.  FBA_FLOW_MERGE=0:
+    one writer group per source level (no merging of consecutive levels); FBA_ND_LEAF=60: smaller
+    nested-dissection leaves (another block pattern)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     _check_adjust(fba, fbo, oracle, _scene(3, scenes))
