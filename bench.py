@@ -218,10 +218,10 @@ def main():
         probe(2, "k_panel", "one elimination-tree level: the 128x128 f64 diagonal-block potrf, the panel "
                             "solves and the previous level's trailing updates as in-launch dataflow; a latency-"
                             "bound chain, one launch per level")
-    # k_syrk_multi runs only for levels whose updates are not merged into the next level's k_panel
-    # (FBA_MERGE_MAX; by default every level's are)
-    roof_bulk = probe(1, "k_syrk_multi", "Cholesky trailing update of a level not merged into the next k_panel "
-                                         "(FBA_MERGE_MAX), 64x64 f64 MFMA tiles, K = 128 per source column")
+    # k_syrk_multi runs only on the per-level path (FBA_CHOL_FLOW=0), for the levels whose updates do not
+    # fit into the next level's k_panel launch (and the last level's)
+    roof_bulk = probe(1, "k_syrk_multi", "Cholesky trailing update of a level not merged into the next k_panel, "
+                                         "64x64 f64 MFMA tiles, K = 128 per source column")
     if not roof_bulk["launches"]:
         roof_bulk = None
     # (no dense-equivalent Cholesky rate: u_c^3/3 over the block-sparse factor's time measures the

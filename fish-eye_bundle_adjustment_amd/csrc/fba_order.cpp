@@ -541,21 +541,27 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     //                mode 3 272.0-272.3 | 2445-2446 (vs 276.0 | 2394-2399 and 276.4-276.7 | 2362-2383, same box)
     //   convergent:  quarters 234-236 | 3076-3134, all whole 252-254 | 2781-2828, mode 3 258-258.5 | 2717-2739
     // so the default (FBA_FLOW_BLOCK unset) makes every group whole (mode 1, the one setting that gains on
-    // both) for a throughput-bound factorisation -- update work per elimination-tree level >= 1 GFLOP
-    // (config 4: 0.39, config 5: 1.9, convergent: 1.6) -- and keeps quarters otherwise.  0: quarters,
+    // both) for a throughput-bound factorisation -- update work per elimination-tree level >= 1.5 GFLOP
+    // (config 4: 0.39, config 5: 1.92, convergent: 1.6) -- and keeps quarters otherwise.  0: quarters,
     // 1: every group whole, 2: all but the urgent last group, 3: the leading groups whose sources fit the
-    // levels left
-    // (counted over every column whatever inc holds, so the two flows of the subtree split take the
-    // decision of the single-context schedule and sum every target in the same order)
+    // levels left.  Counted over the columns this flow holds and the levels they span: the subtree split's
+    // flows each hold a fraction of the work per level (config 5, 4 ranks: flow A 1.05, flow B 0.32
+    // GFLOP per level; per iteration flow A + flow B 1.036 + 0.788 ms with quarters vs 1.251 + 0.927 ms
+    // with whole blocks, profiles/r05_v3_split_scaling_config5*.log)
     double upd_flops = 0.0;
-    for (int64_t k = 0; k < nb; ++k)
+    std::vector<char> lev_used(nb + 1, 0);
+    int nw_in = 0;
+    for (int64_t k = 0; k < nb; ++k) {
+        if (!in(k)) continue;
+        if (!lev_used[level[k]]) { lev_used[level[k]] = 1; ++nw_in; }
         for (size_t bi = 0; bi < R[k].size(); ++bi)
             if (R[k][bi] < nb)
                 for (size_t ai = bi; ai < R[k].size(); ++ai) upd_flops += (R[k][ai] == R[k][bi] ? 3 : 4) * 2.0 * 64 * 64 * NB;
-    const int blockm = getenv("FBA_FLOW_BLOCK") ? atoi(getenv("FBA_FLOW_BLOCK")) : (nw > 0 && upd_flops / nw >= 1e9 ? 1 : 0);
+    }
+    const int blockm = getenv("FBA_FLOW_BLOCK") ? atoi(getenv("FBA_FLOW_BLOCK")) : (nw_in > 0 && upd_flops / nw_in >= 1.5e9 ? 1 : 0);
     if (verbose)
         fprintf(stderr, "[fba] flow schedule: update work %.2f GFLOP over %d levels, update records mode %d\n", upd_flops * 1e-9,
-                nw, blockm);
+                nw_in, blockm);
     for (auto& t : tg) {
         const int32_t a = t.first.first, b = t.first.second;
         std::map<int, std::vector<int32_t>> bylev;
@@ -586,12 +592,11 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
         if (whole) {
             gq = groups.size();
             if (blockm == 2 && level[b] == groups.back().first + 1) gq = groups.size() - 1;
-            // 3: a group is whole while its sources fit the levels left before the target is read
-            // (FBA_FLOW_BLOCK_R levels per source, default 1)
-            const double blk_r = getenv("FBA_FLOW_BLOCK_R") ? atof(getenv("FBA_FLOW_BLOCK_R")) : 1.0;
+            // 3: a group is whole while its sources fit the levels left before the target is read (one
+            // level per source)
             if (blockm == 3)
                 for (gq = 0; gq < groups.size(); ++gq)
-                    if (std::min<double>((double)groups[gq].second.size(), SPLIT) * blk_r > level[b] - groups[gq].first - 1)
+                    if (std::min<double>((double)groups[gq].second.size(), SPLIT) > level[b] - groups[gq].first - 1)
                         break;
             int32_t prev = -1;
             if (gq > 0) ++n_whole_t;
@@ -1042,10 +1047,16 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
     // subtree split (Sched::split): cut the elimination tree.  parent(k) = the first block row below
     // column k; a subtree's columns touch only their own rows and their ancestors', so two subtrees never
     // share a block.  Starting from the roots, the subtree of the largest work (1 + r + r^2 block
-    // products for a column of r panel blocks) moves its root column to the top until there are at
-    // least `world` subtrees and none holds more than 1.25x the average; the subtrees are then dealt to
-    // the ranks largest first, each to the least loaded (LPT).  The local inner-constraint border's block
-    // rows must stay in a subtree (their weights come from one rank's diagonal); otherwise no split.
+    // products for a column of r panel blocks) moves its root column to the top until there are at least
+    // w subtrees and none holds more than 1.25x the average (the balance cut for w).  The balance cuts for
+    // w = 2 .. world are priced on the world ranks by a cost model of one iteration (split_cost below):
+    // the ranks' linearisation and subtree flows side by side, then the top blocks' exchange, then the top
+    // flow on every rank; per elimination-tree level max(LAT, work x TAU) -- a latency-bound chain where
+    // the level is narrow, throughput where it is wide.  The cheapest is kept, so more ranks never take a
+    // deeper cut than pays (a rank may then get no subtree: it only linearises its share of the top's
+    // points).  Subtrees are dealt to the
+    // ranks largest first, each to the least loaded (LPT).  The local inner-constraint border's block rows
+    // must stay in a subtree (their weights come from one rank's diagonal); otherwise no split.
     s.split = false;
     std::vector<char> inc_own, inc_top;
     if (c.opt.split && c.opt.world > 1 && nb > 1) {
@@ -1055,38 +1066,104 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
         for (int64_t k = 0; k < nb; ++k)
             for (int32_t r : R[k])
                 if (r < nb) { parent[k] = r; kids[r].push_back((int32_t)k); break; }
-        std::vector<double> sw(nb, 0.0);  // children have smaller indices than their parents
+        std::vector<double> sw(nb, 0.0), wk(nb, 0.0);  // children have smaller indices than their parents
         for (int64_t k = 0; k < nb; ++k) {
             const double r = (double)R[k].size();
-            sw[k] += 1.0 + r + r * r;
+            wk[k] = 1.0 + r + r * r;
+            sw[k] += wk[k];
             if (parent[k] >= 0) sw[parent[k]] += sw[k];
         }
-        std::vector<int32_t> frontier;
-        for (int64_t k = 0; k < nb; ++k)
-            if (parent[k] < 0) frontier.push_back((int32_t)k);
-        std::vector<char> top(nb, 0);
-        for (;;) {
-            double tot = 0.0, mx = -1.0;
-            int imx = -1;
-            for (size_t q = 0; q < frontier.size(); ++q) {
-                tot += sw[frontier[q]];
-                if (sw[frontier[q]] > mx) { mx = sw[frontier[q]]; imx = (int)q; }
+        // cost model constants (config 4 / 5 records): LAT = the critical chain of one
+        // elimination-tree level (potrf + hand-offs), TAU = one 128^3 block product at the throughput the
+        // wide levels reach (config 5: 22.5 TFLOP/s), BW = the all-reduce's algorithm bandwidth over xGMI,
+        // LIN = linearising and reducing one block column's points (k_lin_reduce + k_red_blocks, config 4:
+        // 47 columns in 235 us)
+        constexpr double LAT = 30.0, TAU = 0.19, BW = 100e3, LIN = 5.0;  // us, us, bytes per us, us
+        const int nlev = nb > 0 ? 1 + *std::max_element(level.begin(), level.end()) : 0;
+        std::vector<int32_t> owner(nb);
+        auto deal = [&](const std::vector<int32_t>& front, std::vector<double>& load, std::vector<int32_t>& root_rank) {
+            std::vector<int32_t> f(front);
+            std::stable_sort(f.begin(), f.end(), [&](int32_t a, int32_t b) { return sw[a] > sw[b]; });
+            load.assign(W, 0.0);
+            root_rank.assign(nb, -1);
+            for (int32_t k : f) {
+                const int r = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+                root_rank[k] = r;
+                load[r] += sw[k];
             }
-            if (imx < 0 || ((int)frontier.size() >= W && mx <= 1.25 * tot / W)) break;
-            const int32_t k = frontier[imx];
-            if (kids[k].empty()) break;  // one column: no further cut
-            top[k] = 1;
-            frontier.erase(frontier.begin() + imx);
-            frontier.insert(frontier.end(), kids[k].begin(), kids[k].end());
+        };
+        auto split_cost = [&](const std::vector<char>& top, const std::vector<int32_t>& front) {
+            std::vector<double> load;
+            std::vector<int32_t> rr;
+            deal(front, load, rr);
+            for (int64_t k = nb - 1; k >= 0; --k)
+                owner[k] = top[k] ? -1 : (rr[k] >= 0 ? rr[k] : (parent[k] >= 0 ? owner[parent[k]] : -1));
+            std::vector<double> lw((size_t)(W + 1) * nlev, 0.0);  // per rank (W: the top) and level: work
+            std::vector<double> cols(W + 1, 0.0);
+            double top_blocks = 0.0;
+            for (int64_t k = 0; k < nb; ++k) {
+                lw[(size_t)(owner[k] < 0 ? W : owner[k]) * nlev + level[k]] += wk[k];
+                cols[owner[k] < 0 ? W : owner[k]] += 1.0;
+                if (owner[k] < 0) top_blocks += 1.0 + (double)R[k].size();
+            }
+            auto flow = [&](int who) {
+                double t = 0.0;
+                for (int l = 0; l < nlev; ++l)
+                    if (lw[(size_t)who * nlev + l] > 0.0) t += std::max(LAT, lw[(size_t)who * nlev + l] * TAU);
+                return t;
+            };
+            double a = 0.0;
+            for (int r = 0; r < W; ++r) a = std::max(a, LIN * (cols[r] + cols[W] / W) + flow(r));
+            return a + 2.0 * (W - 1) / W * top_blocks * NB * NB * 8.0 / BW + flow(W);
+        };
+        std::vector<int32_t> roots;
+        for (int64_t k = 0; k < nb; ++k)
+            if (parent[k] < 0) roots.push_back((int32_t)k);
+        // the balance cut for w subtrees: the largest subtree's root to the top until there are at least
+        // w subtrees and none holds more than 1.25x the average
+        auto balance_cut = [&](int w, std::vector<char>& tp, std::vector<int32_t>& fr) {
+            fr = roots;
+            tp.assign(nb, 0);
+            for (;;) {
+                double tot = 0.0, mx = -1.0;
+                int imx = -1;
+                for (size_t q = 0; q < fr.size(); ++q) {
+                    tot += sw[fr[q]];
+                    if (sw[fr[q]] > mx) { mx = sw[fr[q]]; imx = (int)q; }
+                }
+                if (imx < 0 || ((int)fr.size() >= w && mx <= 1.25 * tot / w)) break;
+                const int32_t k = fr[imx];
+                if (kids[k].empty()) break;  // one column: no further cut
+                tp[k] = 1;
+                fr.erase(fr.begin() + imx);
+                fr.insert(fr.end(), kids[k].begin(), kids[k].end());
+            }
+        };
+        // candidates: the balance cuts for w = 2 .. W subtrees, each priced on the W ranks; the cheapest
+        // is kept (ties: the larger w)
+        std::vector<int32_t> frontier;
+        std::vector<char> top(nb, 0);
+        double best = 1e300;
+        int best_w = -1;
+        for (int w = 2; w <= W; ++w) {
+            std::vector<char> tp;
+            std::vector<int32_t> fr;
+            balance_cut(w, tp, fr);
+            if (fr.size() < 2) continue;
+            const double cst = split_cost(tp, fr);
+            if (c.opt.verbose) {
+                int nt = 0;
+                for (char t : tp) nt += t;
+                fprintf(stderr, "[fba] subtree split candidate w=%d: %d top columns, %zu subtrees, modelled %.0f us\n", w, nt,
+                        fr.size(), cst);
+            }
+            if (cst <= best) { best = cst; best_w = w; frontier = fr; top = tp; }
         }
-        std::stable_sort(frontier.begin(), frontier.end(), [&](int32_t a, int32_t b) { return sw[a] > sw[b]; });
-        std::vector<double> load(W, 0.0);
-        std::vector<int32_t> root_rank(nb, -1);
-        for (int32_t k : frontier) {
-            const int r = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-            root_rank[k] = r;
-            load[r] += sw[k];
-        }
+        const int best_step = best_w;
+        if (best_step < 0) frontier.clear();
+        std::vector<double> load;
+        std::vector<int32_t> root_rank;
+        deal(frontier, load, root_rank);
         std::vector<int32_t> br(nb, -1);
         for (int64_t k = nb - 1; k >= 0; --k)  // parents first
             br[k] = top[k] ? -1 : (root_rank[k] >= 0 ? root_rank[k] : (parent[k] >= 0 ? br[parent[k]] : -1));
@@ -1114,8 +1191,8 @@ void build_schedule(Ctx& c, const std::vector<std::pair<int32_t, int32_t>>& pair
             if (c.opt.verbose) {
                 int ntop = 0;
                 for (int64_t k = 0; k < nb; ++k) ntop += br[k] < 0;
-                fprintf(stderr, "[fba] subtree split: %d top columns (%d top blocks), %zu subtrees; work per rank:", ntop,
-                        s.n_top_blocks, frontier.size());
+                fprintf(stderr, "[fba] subtree split: %d top columns (%d top blocks), %zu subtrees, modelled %.0f us per "
+                        "factorisation; work per rank:", ntop, s.n_top_blocks, frontier.size(), best);
                 for (double v : load) fprintf(stderr, " %.0f", v);
                 fprintf(stderr, "; top columns:");
                 for (int64_t k = 0; k < nb; ++k)
