@@ -250,6 +250,18 @@ def main():
         out["cpu_baseline"], dense = cpu_baseline(folder, args.cpu_seconds)
         if dense:
             out["cpu_baseline_dense"] = dense
+        cb = out["cpu_baseline"]
+        if cb.get("value"):
+            # how to read the GPU/CPU ratio: per phase, like for like (the CPU's linearise + per-point
+            # Schur costs ~cores x its ms per point; the factorisations run on the same block pattern)
+            lin_gpu = t["linearize"] + t["point"] + t["accumulate"]
+            lin_cpu = cb["phase_ms"]["linearize_reduce"]
+            out["gpu_vs_cpu"] = {
+                "iteration": value / cb["value"],
+                "linearise_reduce": lin_cpu / lin_gpu if lin_gpu > 0 else None,
+                "factor": cb["solve_ms"]["factor"] / t["cholesky"] if t["cholesky"] > 0 else None,
+                "cpu_linearise_reduce_us_per_point_per_core": 1e3 * lin_cpu * cb["cores"] / ds.n_pts,
+                "gpu_linearise_reduce_ns_per_point": 1e6 * lin_gpu / ds.n_pts}
     if rank == 0:
         print(json.dumps(out))
     if world > 1:

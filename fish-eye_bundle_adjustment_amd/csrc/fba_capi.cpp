@@ -5,6 +5,7 @@
 // pairs), allocates device memory once, and drives the kernels of fba_kernels.hip / fba_chol.hip.
 // The loop semantics are the reference's main.m:407-494; the unknown layout is Buildxhat.m:6-134.
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -164,7 +165,7 @@ static void partition(const fba_problem* p, int world, std::vector<int32_t>& tie
 static void destroy(Ctx* c) {
     if (!c) return;
     void* ptrs[] = {c->d_chunk_obs, c->d_chunk_pt, c->d_xy, c->d_img, c->d_cam, c->d_pt, c->d_ctl, c->d_lp_tie, c->d_xoff, c->d_lrt, c->d_lp_start, c->d_lp_cam,
-                    c->d_acc, c->d_ppart, c->d_ipart, c->d_cpart, c->d_cseg, c->d_bscr, c->d_gblk, c->d_lrprof, c->d_ptrace, c->d_gpairs, c->d_red, c->d_xfull, c->d_xlin, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
+                    c->d_acc, c->d_ppart, c->d_U, c->d_ipart, c->d_cpart, c->d_cseg, c->d_bscr, c->d_gblk, c->d_lrprof, c->d_ptrace, c->d_gpairs, c->d_red, c->d_xfull, c->d_xlin, c->d_delta, c->d_img_tab, c->d_cam_tab, c->d_G, c->d_J, c->d_WT,
                     c->d_pt_tab, c->d_P, c->d_flags, c->d_S, c->d_X, c->d_dinv, c->d_linv, c->d_scal, c->d_part, c->d_res, c->d_caminfo,
                     c->d_active, c->d_counted, c->d_obs_pho, c->d_sched, c->d_gpt, c->d_gcu, c->d_gug, c->d_xpart,
                     c->d_kpart, c->d_bown, c->d_rown, c->d_topdiag};
@@ -465,9 +466,15 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     // observation terms and its image keys with their observations; per pair / image / camera the
     // partial slots the reduce kernels add up, in chunk order
     AccPlan& A = c->acc;
-    std::vector<int32_t> ck_cam, ck_pk{0}, pk_t{0}, pk_term, ck_ik{0}, ik_o{0}, ik_obs;
+    std::vector<int32_t> ck_cam, ck_pk{0}, pk_t{0}, pk_term, ck_ik{0}, ik_o{0}, ik_obs, ck_tm;
     std::vector<std::pair<int32_t, int32_t>> pk_key;
     std::vector<int32_t> ik_img;
+    // a chunk's pair terms take the U-row path (AccPlan::ck_tm) when its pair keys hold at most tm_ratio
+    // terms each on average: a partial row costs 288 B written and read back per key, the U-row path
+    // one 144-B U row per observation plus two cached U-row reads per term (FBA_PAIR_TERMS: the ratio;
+    // 0 = never, tested both ways in tests/test_gpu_parity.py)
+    const double tm_ratio = getenv("FBA_PAIR_TERMS") ? atof(getenv("FBA_PAIR_TERMS")) : 2.0;
+    std::vector<std::array<int32_t, 4>> tterm;  // (e1, e2, a, b) of the U-row chunks' terms, chunk order
     for (int64_t ch = 0; ch < c->n_chunks_lr; ++ch) {
         const int o0 = chunk_obs[ch], o1 = chunk_obs[ch + 1];
         ck_cam.push_back(cam[o0]);
@@ -496,10 +503,19 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
             else
                 kr.back().second = q + 1;
         std::stable_sort(kr.begin(), kr.end(), [](const auto& x, const auto& y) { return x.second - x.first > y.second - y.first; });
-        for (auto& r : kr) {
-            pk_key.emplace_back(std::get<0>(tk[r.first]), std::get<1>(tk[r.first]));
-            for (size_t q = r.first; q < r.second; ++q) pk_term.push_back(std::get<2>(tk[q]));
-            pk_t.push_back((int32_t)pk_term.size());
+        const bool tmode = !kr.empty() && (double)tk.size() <= tm_ratio * (double)kr.size();
+        ck_tm.push_back(tmode ? 1 : 0);
+        if (tmode) {
+            for (size_t q = 0; q < tk.size(); ++q) {  // (e1, e2) ascending, point order within a key
+                const int32_t tm = std::get<2>(tk[q]);
+                tterm.push_back({std::get<0>(tk[q]), std::get<1>(tk[q]), o0 + (tm & 0xffff), o0 + (tm >> 16)});
+            }
+        } else {
+            for (auto& r : kr) {
+                pk_key.emplace_back(std::get<0>(tk[r.first]), std::get<1>(tk[r.first]));
+                for (size_t q = r.first; q < r.second; ++q) pk_term.push_back(std::get<2>(tk[q]));
+                pk_t.push_back((int32_t)pk_term.size());
+            }
         }
         ck_pk.push_back((int32_t)pk_key.size());
         std::vector<std::pair<int32_t, int32_t>> io;  // (image, local obs)
@@ -596,10 +612,28 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     G.n_kt = (int64_t)kt.size();
     // the local co-visible pairs and, per pair, its partial slots
     std::vector<std::pair<int32_t, int32_t>> lpairs(pk_key);
+    for (auto& t : tterm) lpairs.emplace_back(t[0], t[1]);
     std::sort(lpairs.begin(), lpairs.end());
     lpairs.erase(std::unique(lpairs.begin(), lpairs.end()), lpairs.end());
     c->n_pairs = (int64_t)lpairs.size();
-    c->n_pair_terms = (int64_t)pk_term.size();
+    c->n_pair_terms = (int64_t)(pk_term.size() + tterm.size());
+    // the U-row terms per pair (counting sort by pair: chunk order kept)
+    std::vector<int32_t> tp_start(c->n_pairs + 1, 0), tp_ab(2 * tterm.size());
+    {
+        std::vector<int32_t> pid(tterm.size());
+        for (size_t q = 0; q < tterm.size(); ++q) {
+            pid[q] = (int32_t)(std::lower_bound(lpairs.begin(), lpairs.end(), std::make_pair(tterm[q][0], tterm[q][1])) -
+                               lpairs.begin());
+            tp_start[pid[q] + 1]++;
+        }
+        for (int64_t q = 0; q < c->n_pairs; ++q) tp_start[q + 1] += tp_start[q];
+        std::vector<int32_t> fill(tp_start.begin(), tp_start.end() - 1);
+        for (size_t q = 0; q < tterm.size(); ++q) {
+            const int32_t x = fill[pid[q]]++;
+            tp_ab[2 * x] = tterm[q][2];
+            tp_ab[2 * x + 1] = tterm[q][3];
+        }
+    }
     std::vector<int32_t> rp_start(c->n_pairs + 1, 0), rp_list(pk_key.size()), rp_e;
     {
         std::vector<int32_t> pid(pk_key.size());
@@ -630,6 +664,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     }
     A.n_pk = (int64_t)pk_key.size();
     A.n_ik = (int64_t)ik_img.size();
+    A.n_tt = (int64_t)tterm.size();
     std::vector<int32_t> abuf;
     auto put = [&](const std::vector<int32_t>& v) {
         const int64_t off = (int64_t)abuf.size();
@@ -660,6 +695,9 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     A.img_cam = put(img_cam);
     A.rc_start = put(rc_start);
     A.rc_list = put(rc_list);
+    A.ck_tm = put(ck_tm);
+    A.tp_start = put(tp_start);
+    A.tp_ab = put(tp_ab);
     G.g_obs = put(g_obs);
     G.g_gi = put(g_gi);
     G.g_gc = put(g_gc);
@@ -771,6 +809,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         (rc = dalloc(&c->d_J, (size_t)c->ncomp * c->n_obs_pad)) || (rc = dalloc(&c->d_WT, (size_t)18 * c->n_obs_pad)) ||
         (rc = dalloc(&c->d_pt_tab, (size_t)c->pt_comp * c->n_lp_pad)) ||
         (rc = dalloc(&c->d_ppart, (size_t)A.n_pk * 36)) ||
+        (rc = dalloc(&c->d_U, A.n_tt > 0 ? (size_t)18 * c->n_obs_pad : 1)) ||
         (rc = dalloc(&c->d_ipart, (size_t)A.n_ik * (27 + 6 * L.cw))) ||
         (rc = dalloc(&c->d_cpart, (size_t)(c->n_chunks_lr + G.n_gc) * npk)) ||
         (rc = dalloc(&c->d_gpt, (size_t)G.n_gp * 18)) || (rc = dalloc(&c->d_gcu, (size_t)G.n_gc * 6 * L.cw)) ||
@@ -807,9 +846,9 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     for (auto& e : c->ev) FBA_HIP(hipEventCreate(&e));
     if (opt.verbose)
         fprintf(stderr, "[fba] rank %d/%d: n_obs %ld (tie %ld), points %ld, pairs %ld (%ld terms), u_c %ld, n_pad %ld; "
-                "chunks %ld, pair keys %ld, image keys %ld; general points %ld\n",
+                "chunks %ld, pair keys %ld, U-row pair terms %ld, image keys %ld; general points %ld\n",
                 opt.rank, opt.world, (long)c->n_obs, (long)c->n_obs_tie, (long)c->n_lp, (long)c->n_pairs,
-                (long)c->n_pair_terms, (long)L.u_c, (long)L.n_pad, (long)c->n_chunks_lr, (long)c->acc.n_pk, (long)c->acc.n_ik, (long)G.n_gp);
+                (long)c->n_pair_terms, (long)L.u_c, (long)L.n_pad, (long)c->n_chunks_lr, (long)c->acc.n_pk, (long)c->acc.n_tt, (long)c->acc.n_ik, (long)G.n_gp);
     *out = c;
     return FBA_OK;
 }
@@ -1119,12 +1158,6 @@ static int solve_finish(Ctx* c, double* dsum, bool recopy) {
     }
     c->solve_seq = c->h_pinned[4];
     if (c->d_ptrace && !c->sched.split) print_panel_trace(c);
-    if (getenv("FBA_DEBUG_WEIGHTS")) {  // (diagnostic) the inner-constraint weights W_l, W_d of this solve
-        double w[24];
-        if (hipMemcpy(w, c->d_scal, sizeof w, hipMemcpyDeviceToHost) == hipSuccess)
-            fprintf(stderr, "[fba] rank %d weights W_l %.17g %.17g %.17g W_d %.17g %.17g %.17g %.17g\n", c->opt.rank, w[8], w[9],
-                    w[14], w[16], w[17], w[18], w[22]);
-    }
     if (c->timing) {
         float ms;
         for (int i = 0; i < 7; ++i) {

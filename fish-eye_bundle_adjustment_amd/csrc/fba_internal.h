@@ -149,7 +149,13 @@ struct AccPlan {
     int64_t img_cam = 0;   // [n_img] camera of each image (-1: no local observation)
     int64_t rc_start = 0;  // [n_cam+1] chunks of each camera
     int64_t rc_list = 0;
-    int64_t n_pk = 0, n_ik = 0;
+    // pair terms reduced from U rows (a chunk whose pair keys hold few terms each -- a dense network's
+    // -- registers no pair keys: its pair-block contributions -U_a U_b' are summed by k_red_blocks from
+    // the observations' U rows, Ctx::d_U, instead of 288-B partial rows written and read back)
+    int64_t ck_tm = 0;     // [n_chunks] 1: the chunk's pair terms go to the U-row path
+    int64_t tp_start = 0;  // [n_pairs+1] U-row terms of each local pair, chunk order
+    int64_t tp_ab = 0;     // [2 n_tt] (a, b): global observations in image e1 / e2
+    int64_t n_pk = 0, n_ik = 0, n_tt = 0;
 };
 
 // General tie points (fba_general.hip): the points the chunked fast path does not take -- seen by
@@ -233,6 +239,7 @@ struct Ctx {
     AccPlan acc;                     // accumulation plan (offsets into d_acc)
     int32_t* d_acc = nullptr;
     double* d_ppart = nullptr;       // [acc.n_pk][36] pair-block partials
+    double* d_U = nullptr;           // [n_obs_pad][18] U = W R of the observations of U-row chunks (acc.ck_tm)
     double* d_ipart = nullptr;       // [acc.n_ik][27 + 6 cw] image partials: diagonal block, RHS, image-camera
     uint64_t* d_lrprof = nullptr;    // FBA_LR_PROFILE: k_lin_reduce phase timestamps [n_chunks][8]
     uint64_t* d_ptrace = nullptr;    // FBA_PANEL_TRACE: k_panel workgroup timestamps [level][PTRACE_WG][8]

@@ -392,7 +392,9 @@ __global__ __launch_bounds__(256) void k_lin_point(
 //         image e    Je'PJe - U U' (lower), Je'Pw - U rb, Jc'PJe - Uc U'     (its observations)
 //         pair e1>e2 -sum U_i U_j'  over the chunk's points seen by both     (= -T_i W_j')
 //       each summed in a fixed order and stored as one partial; k_red_* add the partials of a
-//       block in chunk order, so the result is deterministic.
+//       block in chunk order, so the result is deterministic.  A U-row chunk (AccPlan::ck_tm: its
+//       pair keys hold few terms each, a dense network's) registers no pair keys and writes its
+//       observations' U rows instead (Ug, 144 B each); k_red_blocks sums those terms per pair.
 // The Schur complement identities: W V^-1 W' = U U', W V^-1 b = U rb, Wc V^-1 W' = Uc U'.
 // ------------------------------------------------------------------------------------------------
 __constant__ int c_tri_a[21] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 4, 5, 5, 5, 5, 5, 5};
@@ -434,7 +436,7 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     double* __restrict__ ppart, double* __restrict__ ipart, double* __restrict__ cpart, int64_t u_c, int type,
     int cam_stride, unsigned eop_mask, unsigned cam_mask, double px, double py, uint64_t* __restrict__ tprof,
     int n_chunks, double* __restrict__ S, int64_t ld, const int32_t* __restrict__ zblk,
-    const int32_t* __restrict__ xoff) {
+    const int32_t* __restrict__ xoff, double* __restrict__ Ug) {
     using LY = Lay<NK>;
     using R_ = LR<NK>;
     if ((int)blockIdx.x >= n_chunks) {  // tail workgroups: zero one 128x128 block of the factor's pattern
@@ -635,6 +637,7 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     __syncthreads();
     stamp(2);
     // (C)
+    const bool urow = A[plan.ck_tm + c] != 0;  // U-row chunk: its pair terms are reduced by k_red_blocks
     if (active) {
         double* u = Us + t * US;
         if (p >= 0) {
@@ -654,6 +657,11 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
                 u[3 * a] = v0 * r00;
                 u[3 * a + 1] = v0 * r01 + v1 * r11;
                 u[3 * a + 2] = v0 * r02 + v1 * r12 + v2 * r22;
+            }
+            if (urow) {
+                double2* ug = reinterpret_cast<double2*>(Ug + (int64_t)o * 18);
+#pragma unroll
+                for (int m = 0; m < 9; ++m) ug[m] = double2{u[2 * m], u[2 * m + 1]};
             }
         } else {
 #pragma unroll
@@ -856,33 +864,75 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     stamp(5);
 }
 
-// k_red_pairs: S(e1, e2) = the sum of the pair's partials in chunk order (one wave per pair)
-__device__ __forceinline__ void red_pairs_body(int blk, const double* __restrict__ ppart, const int32_t* __restrict__ A,
-                                               const AccPlan& plan, double* __restrict__ S, int64_t ld, int64_t n_pairs) {
-    const int64_t pr = (int64_t)blk * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (pr >= n_pairs || lane >= 36) return;
+// k_red_pairs: S(e1, e2) = the sum of the pair's partials in chunk order; three pairs per wave, 18 lanes
+// each holding two adjacent entries (16-B loads and stores) of the pair's 36
+constexpr int RP_PER_WAVE = 3, RP_PER_WG = 4 * RP_PER_WAVE;
+__device__ __forceinline__ void red_pairs_body(int blk, const double* __restrict__ ppart, const double* __restrict__ Ug,
+                                               const int32_t* __restrict__ A, const AccPlan& plan, double* __restrict__ S,
+                                               int64_t ld, int64_t n_pairs) {
+    const int lane = threadIdx.x & 63, sub = lane / 18, l = lane - 18 * sub;
+    const int64_t pr = ((int64_t)blk * 4 + (threadIdx.x >> 6)) * RP_PER_WAVE + sub;
+    if (sub >= RP_PER_WAVE || pr >= n_pairs) return;
     // the partials in chunk order, one contiguous range (pair-major slots), 8 (then 4) loads in flight
-    // (fixed association: ((s + p0) + p1) + ...)
+    // (fixed association per entry: ((s + p0) + p1) + ...)
     const int q0 = A[plan.rp_start + pr], q1 = A[plan.rp_start + pr + 1];
-    const double* pp = ppart + lane;
-    double s = 0.0;
+    const int t0 = A[plan.tp_start + pr], t1 = A[plan.tp_start + pr + 1];
+    const int64_t e1 = A[plan.rp_e + 2 * pr], e2 = A[plan.rp_e + 2 * pr + 1];
+    const double2* pp = reinterpret_cast<const double2*>(ppart) + l;
+    double sx = 0.0, sy = 0.0;
     int q = q0;
     for (; q + 8 <= q1; q += 8) {
-        double p[8];
+        double2 p[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) p[j] = pp[(int64_t)(q + j) * 36];
+        for (int j = 0; j < 8; ++j) p[j] = pp[(int64_t)(q + j) * 18];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s += p[j];
+        for (int j = 0; j < 8; ++j) { sx += p[j].x; sy += p[j].y; }
     }
-    for (; q + 4 <= q1; q += 4) {
-        const double p0 = pp[(int64_t)q * 36], p1 = pp[(int64_t)(q + 1) * 36], p2 = pp[(int64_t)(q + 2) * 36],
-                     p3 = pp[(int64_t)(q + 3) * 36];
-        s = (((s + p0) + p1) + p2) + p3;
+    if (q + 4 <= q1) {
+        double2 p[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) p[j] = pp[(int64_t)(q + j) * 18];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { sx += p[j].x; sy += p[j].y; }
+        q += 4;
     }
-    for (; q < q1; ++q) s += pp[(int64_t)q * 36];
-    const int64_t e1 = A[plan.rp_e + 2 * pr], e2 = A[plan.rp_e + 2 * pr + 1];
-    S[(6 * e1 + lane / 6) * ld + 6 * e2 + lane % 6] = s;
+    for (; q < q1; ++q) {
+        const double2 p = pp[(int64_t)q * 18];
+        sx += p.x;
+        sy += p.y;
+    }
+    const int e = 2 * l;  // entries e, e + 1 of the row-major 6 x 6 block: row e / 6, columns e % 6 (even)
+    const int er = e / 6, ec = e % 6;
+    // then the U-row terms (AccPlan::ck_tm chunks), in chunk order, TB in flight:
+    // S(e1, e2)[r][c] -= U_a[r] . U_b[c], U rows of 6 x 3 (row r at 3 r; rows ec, ec + 1 of U_b as three
+    // 16-B loads)
+    constexpr int TB = 2;
+    for (int t = t0; t < t1; t += TB) {
+        const int nt = min(TB, t1 - t);
+        int oa[TB], ob[TB];
+#pragma unroll
+        for (int u = 0; u < TB; ++u) {
+            oa[u] = u < nt ? A[plan.tp_ab + 2 * (t + u)] : 0;
+            ob[u] = u < nt ? A[plan.tp_ab + 2 * (t + u) + 1] : 0;
+        }
+        double ua[TB][3];
+        double2 ub[TB][3];
+#pragma unroll
+        for (int u = 0; u < TB; ++u)
+            if (u < nt) {
+                const double* a = Ug + (int64_t)oa[u] * 18 + 3 * er;
+                const double2* b = reinterpret_cast<const double2*>(Ug + (int64_t)ob[u] * 18 + 3 * ec);
+#pragma unroll
+                for (int m = 0; m < 3; ++m) { ua[u][m] = a[m]; ub[u][m] = b[m]; }
+            }
+#pragma unroll
+        for (int u = 0; u < TB; ++u)
+            if (u < nt) {
+                sx -= ua[u][0] * ub[u][0].x + ua[u][1] * ub[u][0].y + ua[u][2] * ub[u][1].x;
+                sy -= ua[u][0] * ub[u][1].y + ua[u][1] * ub[u][2].x + ua[u][2] * ub[u][2].y;
+            }
+    }
+    *reinterpret_cast<double2*>(S + (6 * e1 + er) * ld + 6 * e2 + ec) = double2{sx, sy};
 }
 
 // k_red_images: the diagonal block, RHS and image-camera block of image e from its partials
@@ -896,7 +946,7 @@ __device__ __forceinline__ void red_images_body(int e, int q, const double* __re
     if (r0 == r1 || q >= NIMG) return;
     // the partials in chunk order (image-major slots: one contiguous range) with 8 loads in flight; same
     // association as the plain running sum (((s + p0) + p1) + ...), so the result does not depend on the
-    // batching
+    // batching (32 in flight: convergent k_red_blocks 329 -> 323 us, at 64 more VGPRs for the whole launch)
     const double* ip = ipart + q;
     double s = 0.0;
     int x = r0;
@@ -945,17 +995,17 @@ __device__ __forceinline__ void red_cam_seg_body(int sg, int q, int n_cam, const
     cseg[((int64_t)k * CAM_SEG + g) * NCAM + q] = (s0 + s1) + (s2 + s3);
 }
 
-// the three independent reductions in one launch: workgroups [0, npb) the image pairs (4 per
+// the three independent reductions in one launch: workgroups [0, npb) the image pairs (RP_PER_WG per
 // workgroup), then two images per workgroup (128 threads each), then two camera segments per workgroup
 template <int NK>
 __global__ __launch_bounds__(256) void k_red_blocks(const double* __restrict__ ppart, const double* __restrict__ ipart,
                                                     const double* __restrict__ cpart, const int32_t* __restrict__ A,
                                                     const AccPlan plan, double* __restrict__ S, int64_t ld,
                                                     int64_t n_pairs, int64_t n_pad, int n_img, int n_cam, int npb,
-                                                    int nib, double* __restrict__ cseg) {
+                                                    int nib, double* __restrict__ cseg, const double* __restrict__ Ug) {
     const int b = blockIdx.x;
     if (b < npb) {
-        red_pairs_body(b, ppart, A, plan, S, ld, n_pairs);
+        red_pairs_body(b, ppart, Ug, A, plan, S, ld, n_pairs);
     } else if (b < npb + nib) {
         red_images_body<NK>(2 * (b - npb) + (threadIdx.x >> 7), threadIdx.x & 127, ipart, A, plan, S, ld, n_pad, n_img);
     } else {
@@ -1449,12 +1499,12 @@ int launch_accumulate(Ctx& c, bool zeroed) {
         c.d_xy, c.d_img, c.d_cam, c.d_pt, c.d_lp_tie, c.d_ctl, c.d_xfull, c.d_img_tab, c.d_cam_tab,                \
         c.d_chunk_obs, c.d_chunk_pt, c.d_lp_start, c.d_acc, c.acc, c.d_WT, c.d_pt_tab, c.d_ppart, c.d_ipart,       \
         c.d_cpart, c.L.u_c, c.set.type, c.cam_tab_stride, em, cm, px, py, c.d_lrprof, (int)nlr, c.d_S, L.ld,      \
-        c.d_sched + c.sched.zero, c.d_xoff);                                                                      \
+        c.d_sched + c.sched.zero, c.d_xoff, c.d_U);                                                               \
     {                                                                                                             \
-        const int npb = (int)((c.n_pairs + 3) / 4), nib = (L.n_img + 1) / 2, ncb = (L.n_cam * CAM_SEG + 1) / 2;   \
+        const int npb = (int)((c.n_pairs + RP_PER_WG - 1) / RP_PER_WG), nib = (L.n_img + 1) / 2, ncb = (L.n_cam * CAM_SEG + 1) / 2;   \
         k_red_blocks<NKV><<<(unsigned)(npb + nib + ncb), 256, 0, c.stream>>>(                                     \
             c.d_ppart, c.d_ipart, c.d_cpart, c.d_acc, c.acc, c.d_S, L.ld, c.n_pairs, L.n_pad, L.n_img, L.n_cam, npb, \
-            nib, c.d_cseg);                                                                                       \
+            nib, c.d_cseg, c.d_U);                                                                                \
     }                                                                                                             \
     k_red_cam<NKV><<<(unsigned)L.n_cam, 128, 0, c.stream>>>(c.d_cseg, c.d_S, L.ld, L.n_pad, L.n_img)
     FBA_NK_DISPATCH(L.nk, ACC);

@@ -72,7 +72,6 @@ class Dissection {
         if ((int)verts.size() <= leaf_) return rcm(verts, out);
         std::vector<int32_t> A, B, S;
         if (!(pos_.empty() ? bisect(verts, A, B, S) : bisect_geo(verts, A, B, S))) return rcm(verts, out);
-        if (getenv("FBA_ND_DEBUG")) fprintf(stderr, "nd %zu -> A %zu B %zu S %zu\n", verts.size(), A.size(), B.size(), S.size());
         verts.clear();
         verts.shrink_to_fit();
         nd(std::move(A), out);

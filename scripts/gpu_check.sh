@@ -31,6 +31,9 @@ for step in "$@"; do
     pmc5) cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
           run pmc5_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$PWD/gpurun_out/pmc5_fetch" -o run -- python bench.py --config 5 --steps 2 --warmup 1 --no-cpu
           run pmc5_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$PWD/gpurun_out/pmc5_write" -o run -- python bench.py --config 5 --steps 2 --warmup 1 --no-cpu ;;
+    pmcconv) cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+          run pmcc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$PWD/gpurun_out/pmcc_fetch" -o run -- python bench.py --network convergent --steps 2 --warmup 1 --no-cpu
+          run pmcc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$PWD/gpurun_out/pmcc_write" -o run -- python bench.py --network convergent --steps 2 --warmup 1 --no-cpu ;;
     leaf) run leaf 60 ./scripts/ubench/leaf_lat ;;
     conv) run conv 600 python bench.py --network convergent --steps 5 --warmup 1 --no-cpu --verbose ;;
     convprof) cd /tmp && export TMPDIR=/tmp && cd - > /dev/null

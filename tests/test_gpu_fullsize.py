@@ -72,34 +72,42 @@ def test_config3_adjust_matches_oracle(fba, fbo, oracle, scenes):
 
 @pytest.mark.parametrize("env", [{"FBA_CHOL_FLOW": "0"}, {"FBA_BWD_LEVELS": "1"},
                                  {"FBA_CHOL_FLOW": "0", "FBA_BWD_LEVELS": "1"},
-                                 {"FBA_FLOW_BLOCK": "1"}, {"FBA_FLOW_BLOCK": "3"},
+                                 {"FBA_FLOW_BLOCK": "1"}, {"FBA_FLOW_BLOCK": "2"}, {"FBA_FLOW_BLOCK": "3"},
                                  {"FBA_FLOW_BLOCK": "1", "FBA_FLOW_SPLIT": "1"},
                                  {"FBA_FLOW_BLOCK": "1", "FBA_FLOW_MSPLIT": "8"},
-                                 {"FBA_FLOW_MERGE": "0"}, {"FBA_ND_LEAF": "60"}],
+                                 {"FBA_FLOW_MERGE": "0"}, {"FBA_ND_LEAF": "60"}, {"FBA_PAIR_TERMS": "1000"}],
                          ids=["per-level-factor", "per-level-backward", "both", "whole-block-updates",
-                              "whole-block-then-quarters", "whole-block-partials", "whole-block-merged-partials",
-                              "no-level-merging", "nd-leaf-60"])
+                              "whole-block-but-last-group", "whole-block-then-quarters", "whole-block-partials", "whole-block-merged-partials",
+                              "no-level-merging", "nd-leaf-60", "pair-terms-from-u-rows"])
 def test_config3_fallback_paths_match_oracle(fba, fbo, oracle, scenes, env, monkeypatch):
     """The non-default solve paths (read per context in chol_setup): the per-level k_panel launches
     instead of the persistent k_chol_flow (with k_border_gram -> k_border_combine), and the per-level
     k_bwd_wave backward solve instead of k_bwd_flow -- the paths build_flow's order check falls back
     to, and the one the 2-rank rehearsal used.  FBA_FLOW_BLOCK: k_chol_flow's whole-block update records
     (syrk_block_body; config 3 is latency-bound, so its default is quarter records) for every writer
-    group, or for the leading groups with the quarter records chained after them; with one source per
+    group, for all but each target's last group, or for the leading groups with the quarter records
+    chained after them; with one source per
     record (FBA_FLOW_SPLIT=1) or merged writer groups of up to 8 sources (FBA_FLOW_MSPLIT=8), so targets
     are summed through the 128 x 128 scratch partials the last arriving record combines.  FBA_FLOW_MERGE=0:
     one writer group per source level (no merging of consecutive levels); FBA_ND_LEAF=60: smaller
-    nested-dissection leaves (another block pattern)."""
+    nested-dissection leaves (another block pattern); FBA_PAIR_TERMS=1000: every chunk's pair terms
+    reduced by k_red_blocks from the observations' U rows (AccPlan::ck_tm; the grid's keys hold ~12 terms
+    each, so by default they take the partial rows)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     _check_adjust(fba, fbo, oracle, _scene(3, scenes))
 
 
-def test_convergent_config3_adjust_matches_oracle(fba, fbo, oracle, scenes):
+@pytest.mark.parametrize("env", [{}, {"FBA_PAIR_TERMS": "0"}], ids=["default", "pair-partials"])
+def test_convergent_config3_adjust_matches_oracle(fba, fbo, oracle, scenes, env, monkeypatch):
     """config 3's counts (200 images x 5,000 tie points) as a convergent network (synth.
     generate_convergent: every tie point seen by 10 images drawn from the whole block, the reference's
     close-range setting): a dense reduced camera system, so the factorisation takes its dense-chain,
-    MFMA-throughput form.  Whole adjustment against the C oracle's direct bordered solve."""
+    MFMA-throughput form.  Whole adjustment against the C oracle's direct bordered solve.  Its chunks'
+    pair keys hold ~1 term each, so by default their terms are reduced from U rows (AccPlan::ck_tm);
+    FBA_PAIR_TERMS=0 forces the partial rows."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     from fba_amd import synth
     folder = os.path.join(scenes, "c3_convergent")
     if not os.path.exists(os.path.join(folder, ".done")):
