@@ -806,7 +806,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     if ((rc = dalloc(&c->d_delta, L.u_full)) || (rc = dalloc(&c->d_xlin, L.u_full)) || (rc = dalloc(&c->d_img_tab, (size_t)L.n_img * IMG_TAB)) ||
         (rc = dalloc(&c->d_cam_tab, (size_t)L.n_cam * c->cam_tab_stride)) ||
         (rc = dalloc(&c->d_G, (size_t)std::max(L.n_img, 1) * 42)) ||
-        (rc = dalloc(&c->d_J, (size_t)c->ncomp * c->n_obs_pad)) || (rc = dalloc(&c->d_WT, (size_t)18 * c->n_obs_pad)) ||
+        (rc = dalloc(&c->d_J, (size_t)c->ncomp * c->n_obs_pad)) || (rc = dalloc(&c->d_WT, (size_t)12 * c->n_obs_pad)) ||
         (rc = dalloc(&c->d_pt_tab, (size_t)c->pt_comp * c->n_lp_pad)) ||
         (rc = dalloc(&c->d_ppart, (size_t)A.n_pk * 36)) ||
         (rc = dalloc(&c->d_U, A.n_tt > 0 ? (size_t)18 * c->n_obs_pad : 1)) ||

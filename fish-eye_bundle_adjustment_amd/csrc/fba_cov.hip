@@ -358,6 +358,7 @@ __global__ __launch_bounds__(256) void k_cov_pts(const double* __restrict__ S, i
 
 // backward solve of one right-hand-side row (fba_chol.hip)
 int launch_backward_rows(Ctx& c, int row0, int nrows, double* X);
+int launch_obs_T(Ctx& c, double* T);
 int launch_trtri_last(Ctx& c);
 int launch_border_gram(Ctx& c, double* gpart, int* nseg);
 
@@ -522,8 +523,14 @@ int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, 
     if (d_iblk && n_iblk > 0)
         k_cov_img<<<(unsigned)n_iblk, 256, 0, c.stream>>>(c.d_S, ld, d_Z, d_Wz, nz, n_pad, d_islot, d_icam, L.n_img, L.cw,
                                                           d_iblk);
+    double* d_T = nullptr;  // T = W Vinv per tie observation, rebuilt from the records (OBS_REC)
+    if (d_pdiag && c.n_lp > 0 &&
+        ((rc = alloc(&d_T, (size_t)18 * std::max<int64_t>(c.n_obs_tie, 1))) || (rc = launch_obs_T(c, d_T)))) {
+        cleanup();
+        return rc;
+    }
     if (d_pdiag && c.n_lp > 0)
-        k_cov_pts<<<(unsigned)((c.n_lp + 3) / 4), 256, 0, c.stream>>>(c.d_S, ld, d_Z, d_Wz, nz, n_pad, c.d_WT, c.d_pt_tab,
+        k_cov_pts<<<(unsigned)((c.n_lp + 3) / 4), 256, 0, c.stream>>>(c.d_S, ld, d_Z, d_Wz, nz, n_pad, d_T, c.d_pt_tab,
                                                                       c.pt_comp, c.d_lp_start, c.d_lp_tie, c.d_lp_cam,
                                                                       c.d_img, c.n_lp, L.n_img, L.cw, L.u_c, d_pdiag);
     FBA_HIP(hipGetLastError());

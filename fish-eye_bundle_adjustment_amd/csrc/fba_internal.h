@@ -282,7 +282,7 @@ struct Ctx {
     double* d_bscr = nullptr;    // border scratch: [32][14] weight segment sums | [16][120] Gram segments
     double* d_gblk = nullptr;    // [n_pad / NB][16][16] per-column-block Gram partials of the forward-solved
                                  // RHS rows (k_chol_flow; inner constraints)
-    double* d_WT = nullptr;      // [n_obs_pad][18] per-obs T = W V^-1 (back-substitution)
+    double* d_WT = nullptr;      // [n_obs_pad][12] per-obs record: Jp and the EOP rotation columns (OBS_REC)
     double* d_pt_tab = nullptr;  // [n_lp_pad][pt_comp] Vinv(6) vb(3) b(3) Wc(3cw) Tc(3cw)
     int pt_comp = 0;
     int64_t n_lp_pad = 0;

@@ -147,6 +147,40 @@ struct Lay {
     static constexpr int PS = 12 + 6 * CW;
 };
 
+// The per-observation record of the back-substitution, WT[o] (OBS_REC = 12 doubles, 96 B): the raw
+// tie-point Jacobian rows Jp (x: 0..2, y: 3..5) and the rotation columns of the EOP rows (x: 6..8, y:
+// 9..11).  The position columns of the EOP rows are -Jp (obs_model: d(UVW)/dXc = -d(UVW)/dX exactly),
+// masked by the EOP mask; so W = Je'PJp and T = W Vinv follow from the record and the point's Vinv.
+constexpr int OBS_REC = 12;
+__device__ __forceinline__ void obs_rec_rows(const double* __restrict__ r, unsigned eop_mask, double (&j0)[6],
+                                             double (&j1)[6]) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const double en = (eop_mask >> q) & 1u ? 1.0 : 0.0;
+        j0[q] = -r[q] * en;
+        j1[q] = -r[3 + q] * en;
+        j0[3 + q] = r[6 + q];
+        j1[3 + q] = r[9 + q];
+    }
+}
+// T = W Vinv (6 x 3, row a at 3 a) of one observation from its record and the point's Vinv (00 01 02 11 12 22)
+__device__ __forceinline__ void obs_rec_T(const double* __restrict__ r, const double* __restrict__ vi, unsigned eop_mask,
+                                          double px, double py, double* __restrict__ To) {
+    double j0[6], j1[6];
+    obs_rec_rows(r, eop_mask, j0, j1);
+    const double I00 = vi[0], I01 = vi[1], I02 = vi[2], I11 = vi[3], I12 = vi[4], I22 = vi[5];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        const double e0 = px * j0[a], e1 = py * j1[a];
+        const double v0 = e0 * r[0] + e1 * r[3];
+        const double v1 = e0 * r[1] + e1 * r[4];
+        const double v2 = e0 * r[2] + e1 * r[5];
+        To[3 * a] = v0 * I00 + v1 * I01 + v2 * I02;
+        To[3 * a + 1] = v0 * I01 + v1 * I11 + v2 * I12;
+        To[3 * a + 2] = v0 * I02 + v1 * I12 + v2 * I22;
+    }
+}
+
 // Forward model and Jacobian of one image point (BuildAwG.m:163-503 by the chain rule).
 template <int NK>
 __device__ __forceinline__ void obs_model(double x, double y, const double* __restrict__ it,
@@ -257,7 +291,7 @@ __device__ __forceinline__ void obs_model(double x, double y, const double* __re
 // k_lin_point: one workgroup per chunk of whole tie points (<= 256 observations), one thread per
 // image point.  (1) linearise and store J; (2) one thread per point reduces its observations
 // (staged in LDS): V = Jp'PJp, b = Jp'Pw, Wc = Jc'PJp, Vinv, vb, Tc; (3) one thread per observation
-// forms W = Je'PJp and T = W Vinv.  Chunks of control observations run step (1) only.
+// stores its record (OBS_REC).  Chunks of control observations run step (1) only.
 // ------------------------------------------------------------------------------------------------
 template <int NK>
 __global__ __launch_bounds__(256) void k_lin_point(
@@ -360,20 +394,14 @@ __global__ __launch_bounds__(256) void k_lin_point(
         vinv[t][3] = I11; vinv[t][4] = I12; vinv[t][5] = I22;
     }
     __syncthreads();
-    if (active && p >= 0) {
-        const double* vi = vinv[p - p0];
-        const double I00 = vi[0], I01 = vi[1], I02 = vi[2], I11 = vi[3], I12 = vi[4], I22 = vi[5];
-        double* To = WT + (int64_t)o * 18;
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            const double e0 = px * jr[0][a], e1 = py * jr[1][a];
-            const double v0 = e0 * jr[0][6 + CW + 0] + e1 * jr[1][6 + CW + 0];
-            const double v1 = e0 * jr[0][6 + CW + 1] + e1 * jr[1][6 + CW + 1];
-            const double v2 = e0 * jr[0][6 + CW + 2] + e1 * jr[1][6 + CW + 2];
-            To[3 * a] = v0 * I00 + v1 * I01 + v2 * I02;
-            To[3 * a + 1] = v0 * I01 + v1 * I11 + v2 * I12;
-            To[3 * a + 2] = v0 * I02 + v1 * I12 + v2 * I22;
-        }
+    if (active && p >= 0) {  // the observation's record (OBS_REC)
+        double2* r = reinterpret_cast<double2*>(WT + (int64_t)o * OBS_REC);
+        r[0] = double2{jr[0][6 + CW], jr[0][7 + CW]};
+        r[1] = double2{jr[0][8 + CW], jr[1][6 + CW]};
+        r[2] = double2{jr[1][7 + CW], jr[1][8 + CW]};
+        r[3] = double2{jr[0][3], jr[0][4]};
+        r[4] = double2{jr[0][5], jr[1][3]};
+        r[5] = double2{jr[1][4], jr[1][5]};
     }
 }
 
@@ -383,9 +411,10 @@ __global__ __launch_bounds__(256) void k_lin_point(
 // registers and LDS only -- no Jacobian round trip through HBM, no gathers:
 //   (A) one thread per observation: forward model and Jacobian (obs_model, BuildAwG.m:163-503);
 //   (B) one thread per point: V = Jp'PJp, b = Jp'Pw, Wc = Jc'PJp, V^-1, vb = V^-1 b, Tc = Wc V^-1
-//       (vb, Tc to HBM for the back-substitution), and the factor R = L^-T of V = L L' (so
+//       (V^-1, vb, Tc to HBM for the back-substitution), and the factor R = L^-T of V = L L' (so
 //       V^-1 = R R'), rb = R'b, Uc = Wc R;
-//   (C) one thread per observation: W = Je'PJp, T = W V^-1 (to HBM, back-substitution), U = W R;
+//   (C) one thread per observation: W = Je'PJp, U = W R; its record (OBS_REC, 96 B: Jp and the
+//       rotation columns of Je) to HBM for the back-substitution;
 //       the observation's P^1/2-scaled Jacobian rows and misclosures into LDS;
 //   (D) every (key, entry) of the chunk's partial sums (keys from the host plan, AccPlan):
 //         camera     Jc'PJc - Uc Uc',  Jc'Pw - Uc rb                         (summed over the chunk)
@@ -611,6 +640,7 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
         double* P = PT + (int64_t)lp * PS;
         double* pp = PP + tp * PPS;
         if (g == 0) {
+            P[0] = I00; P[1] = I01; P[2] = I02; P[3] = I11; P[4] = I12; P[5] = I22;
             P[6] = I00 * b0 + I01 * b1 + I02 * b2;
             P[7] = I01 * b0 + I11 * b1 + I12 * b2;
             P[8] = I02 * b0 + I12 * b1 + I22 * b2;
@@ -644,16 +674,21 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
             const double* pp = PP + (p - p0) * PPS;
             const double I00 = pp[0], I01 = pp[1], I02 = pp[2], I11 = pp[3], I12 = pp[4], I22 = pp[5];
             const double r00 = pp[6], r01 = pp[7], r02 = pp[8], r11 = pp[9], r12 = pp[10], r22 = pp[11];
-            double* To = WT + (int64_t)o * 18;
+            {  // the observation's record (OBS_REC): the back-substitution forms T from it and Vinv
+                double2* r = reinterpret_cast<double2*>(WT + (int64_t)o * OBS_REC);
+                r[0] = double2{jr[0][6 + CW], jr[0][7 + CW]};
+                r[1] = double2{jr[0][8 + CW], jr[1][6 + CW]};
+                r[2] = double2{jr[1][7 + CW], jr[1][8 + CW]};
+                r[3] = double2{jr[0][3], jr[0][4]};
+                r[4] = double2{jr[0][5], jr[1][3]};
+                r[5] = double2{jr[1][4], jr[1][5]};
+            }
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
                 const double e0 = px * jr[0][a], e1 = py * jr[1][a];
                 const double v0 = e0 * jr[0][6 + CW + 0] + e1 * jr[1][6 + CW + 0];
                 const double v1 = e0 * jr[0][6 + CW + 1] + e1 * jr[1][6 + CW + 1];
                 const double v2 = e0 * jr[0][6 + CW + 2] + e1 * jr[1][6 + CW + 2];
-                To[3 * a] = v0 * I00 + v1 * I01 + v2 * I02;
-                To[3 * a + 1] = v0 * I01 + v1 * I11 + v2 * I12;
-                To[3 * a + 2] = v0 * I02 + v1 * I12 + v2 * I22;
                 u[3 * a] = v0 * r00;
                 u[3 * a + 1] = v0 * r01 + v1 * r11;
                 u[3 * a + 2] = v0 * r02 + v1 * r12 + v2 * r22;
@@ -1005,7 +1040,12 @@ __global__ __launch_bounds__(256) void k_red_blocks(const double* __restrict__ p
                                                     int nib, double* __restrict__ cseg, const double* __restrict__ Ug) {
     const int b = blockIdx.x;
     if (b < npb) {
-        red_pairs_body(b, ppart, Ug, A, plan, S, ld, n_pairs);
+        // XCD-aware: workgroup b runs on XCD b % 8 (round-robin dispatch); give each XCD a contiguous range
+        // of the pairs, sorted by (e1, e2), so the U rows of an image's observations, gathered by all its
+        // pairs (U-row terms), stay in that XCD's L2
+        const int q = npb / 8, r = npb % 8, x = b % 8, i = b / 8;
+        const int bx = x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+        red_pairs_body(bx, ppart, Ug, A, plan, S, ld, n_pairs);
     } else if (b < npb + nib) {
         red_images_body<NK>(2 * (b - npb) + (threadIdx.x >> 7), threadIdx.x & 127, ipart, A, plan, S, ld, n_pad, n_img);
     } else {
@@ -1163,17 +1203,18 @@ __global__ __launch_bounds__(256) void k_border_rhs(double* __restrict__ S, cons
 
 
 // ------------------------------------------------------------------------------------------------
-// back-substitution of tie points: dp = -(vb + sum_o T_o^T d_e(o) + Tc^T d_cam)
+// back-substitution of tie points: dp = -(vb + Vinv sum_o W_o^T d_e(o) + Tc^T d_cam)
 // ------------------------------------------------------------------------------------------------
 // one workgroup per chunk (<= 256 observations of <= 64 whole tie points): thread per observation
-// u_o = T_o' d_e(o) into LDS (contiguous 144-byte T records, coalesced across the wave), then thread
-// per point d_p = -(vb + sum_o u_o + Tc' d_cam), its observations summed in order
+// w_o = W_o' d_e(o) = Jp' P (Je d_e) into LDS (its 96-byte record, OBS_REC, coalesced across the wave),
+// then thread per point d_p = -(vb + Vinv sum_o w_o + Tc' d_cam), its observations summed in order
 template <int NK>
 __global__ __launch_bounds__(256) void k_backsub(const double* __restrict__ WT, const double* __restrict__ PT,
                                                  const int32_t* __restrict__ chunk_obs, const int32_t* __restrict__ chunk_pt,
                                                  const int32_t* __restrict__ lp_start, const int32_t* __restrict__ lp_tie,
                                                  const int32_t* __restrict__ lp_cam, const int32_t* __restrict__ img,
-                                                 double* __restrict__ delta, int64_t u_c, int n_img) {
+                                                 double* __restrict__ delta, int64_t u_c, int n_img, unsigned eop_mask,
+                                                 double px, double py) {
     using LY = Lay<NK>;
     constexpr int CW = LY::CW, PS = LY::PS;
     __shared__ double u[CHUNK_OBS][3];
@@ -1182,26 +1223,36 @@ __global__ __launch_bounds__(256) void k_backsub(const double* __restrict__ WT, 
     if (p1 == p0) return;  // control chunk (uniform)
     const int o0 = chunk_obs[c], o = o0 + t;
     if (o < chunk_obs[c + 1]) {
-        const double2* T = reinterpret_cast<const double2*>(WT + (int64_t)o * 18);
-        double2 tv[9];
+        const double2* R = reinterpret_cast<const double2*>(WT + (int64_t)o * OBS_REC);
+        double2 rv[OBS_REC / 2];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) tv[k] = T[k];
+        for (int k = 0; k < OBS_REC / 2; ++k) rv[k] = R[k];
+        const double* r = reinterpret_cast<const double*>(rv);
         const double* de = delta + 6 * (int64_t)img[o];
-        const double* tf = reinterpret_cast<const double*>(tv);
-        double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+        double j0[6], j1[6];
+        obs_rec_rows(r, eop_mask, j0, j1);
+        double e0 = 0.0, e1 = 0.0;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             const double e = de[a];
-            d0 += tf[3 * a] * e; d1 += tf[3 * a + 1] * e; d2 += tf[3 * a + 2] * e;
+            e0 += j0[a] * e;
+            e1 += j1[a] * e;
         }
-        u[t][0] = d0; u[t][1] = d1; u[t][2] = d2;
+        e0 *= px;
+        e1 *= py;
+        u[t][0] = r[0] * e0 + r[3] * e1;
+        u[t][1] = r[1] * e0 + r[4] * e1;
+        u[t][2] = r[2] * e0 + r[5] * e1;
     }
     __syncthreads();
     const int p = p0 + t;
     if (p < p1) {
         const double* P = PT + (int64_t)p * PS;
-        double d0 = P[6], d1 = P[7], d2 = P[8];
-        for (int q = lp_start[p] - o0; q < lp_start[p + 1] - o0; ++q) { d0 += u[q][0]; d1 += u[q][1]; d2 += u[q][2]; }
+        double w0 = 0.0, w1 = 0.0, w2 = 0.0;
+        for (int q = lp_start[p] - o0; q < lp_start[p + 1] - o0; ++q) { w0 += u[q][0]; w1 += u[q][1]; w2 += u[q][2]; }
+        double d0 = P[6] + (P[0] * w0 + P[1] * w1 + P[2] * w2);
+        double d1 = P[7] + (P[1] * w0 + P[3] * w1 + P[4] * w2);
+        double d2 = P[8] + (P[2] * w0 + P[4] * w1 + P[5] * w2);
         const double* dk = delta + 6 * (int64_t)n_img + (int64_t)lp_cam[p] * CW;
         const double* Tc = P + 12 + 3 * CW;
 #pragma unroll
@@ -1211,6 +1262,17 @@ __global__ __launch_bounds__(256) void k_backsub(const double* __restrict__ WT, 
         double* out = delta + u_c + 3 * (int64_t)lp_tie[p];
         out[0] = -d0; out[1] = -d1; out[2] = -d2;
     }
+}
+
+// T = W Vinv of every observation of the regular chunks (the covariance's k_cov_pts reads T rows)
+__global__ __launch_bounds__(256) void k_obs_T(const double* __restrict__ WT, const double* __restrict__ PT, int ps,
+                                               const int32_t* __restrict__ pt, int64_t n_obs, unsigned eop_mask, double px,
+                                               double py, double* __restrict__ T) {
+    const int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (o >= n_obs) return;
+    const int p = pt[o];
+    if (p < 0) return;
+    obs_rec_T(WT + o * OBS_REC, PT + (int64_t)p * ps, eop_mask, px, py, T + o * 18);
 }
 
 
@@ -1443,6 +1505,16 @@ static inline unsigned cam_mask(const fba_settings& s, int nk) {
 static inline double px_of(const Ctx& c) { return 1.0 / (c.set.meas_std_x * c.set.meas_std_x); }
 static inline double py_of(const Ctx& c) { return 1.0 / (c.set.meas_std_y * c.set.meas_std_y); }
 
+// T = W Vinv of the tie observations (the first n_obs_tie) into T [n_obs_tie][18], for k_cov_pts
+int launch_obs_T(Ctx& c, double* T) {
+    const int64_t n = c.n_obs_tie;
+    if (n <= 0) return FBA_OK;
+    k_obs_T<<<(unsigned)((n + 255) / 256), 256, 0, c.stream>>>(c.d_WT, c.d_pt_tab, c.pt_comp, c.d_pt, n, eop_mask(c.set),
+                                                               px_of(c), py_of(c), T);
+    FBA_HIP(hipGetLastError());
+    return FBA_OK;
+}
+
 int launch_params(Ctx& c, const double* x, double* copy_to) {
     const int n = c.L.n_img + c.L.n_cam;
     const int64_t nb = (n + PARAMS_WG - 1) / PARAMS_WG;
@@ -1543,7 +1615,7 @@ int launch_backsub_update(Ctx& c) {
 #define BS(NKV)                                                                                                    \
     k_backsub<NKV><<<(unsigned)c.n_chunks_lr, 256, 0, c.stream>>>(c.d_WT, c.d_pt_tab, c.d_chunk_obs, c.d_chunk_pt,    \
                                                               c.d_lp_start, c.d_lp_tie, c.d_lp_cam, c.d_img, c.d_delta, \
-                                                              L.u_c, L.n_img)
+                                                              L.u_c, L.n_img, eop_mask(c.set), px_of(c), py_of(c))
         FBA_NK_DISPATCH(L.nk, BS);
 #undef BS
         FBA_HIP(hipGetLastError());
