@@ -313,7 +313,7 @@ def test_config4_two_rank_shards_match_single_context(fba, scenes):
             c.close()
 
 
-@pytest.mark.parametrize("config", [3, 4, 5])
+@pytest.mark.parametrize("config", [3, 4, 5, "3-convergent"])
 def test_subtree_split_two_ranks_match_single_context(fba, scenes, config):
     """The subtree-split factorisation (fba_options.split): two rank contexts on one
     GPU, each factoring its own subtrees of the elimination tree inside fba_accumulate, their reduce
@@ -322,9 +322,19 @@ def test_subtree_split_two_ranks_match_single_context(fba, scenes, config):
     would; each then factors the top columns, back-substitutes and updates.  Over two Gauss-Newton passes
     at configs 3, 4 and 5 the ranks' owned entries reassemble the single context's xhat to 1e-10 per
     parameter group (1e-9 at config 5, below) and 1e-9 per element, and the deltasum shares add up to the single context's
-    deltasum.  (One GPU stands in for two: the collective itself is unmeasured here.)"""
+    deltasum.  (One GPU stands in for two: the collective itself is unmeasured here.)  "3-convergent":
+    config 3's counts as a convergent network -- a dense reduced system whose elimination tree is a chain,
+    so the split falls back to the replicated solve (fba_solve_mode), with its chunks' pair terms reduced
+    from U rows (AccPlan::ck_tm) on each rank."""
     import ctypes
-    folder = _scene(config, scenes)
+    if config == "3-convergent":
+        from fba_amd import synth
+        folder = os.path.join(scenes, "c3_convergent")
+        if not os.path.exists(os.path.join(folder, ".done")):
+            synth.make_config(3, folder, network="convergent")
+            open(os.path.join(folder, ".done"), "w").close()
+    else:
+        folder = _scene(config, scenes)
     ds = fba.load_folder(folder)
     hip = ctypes.CDLL("libamdhip64.so")
     hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
