@@ -475,7 +475,9 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
     // FBA_FLOW_MERGE = G: writer groups over consecutive source levels when the target is read >= G levels later
     // (config 4, k_chol_flow per launch: G = 0 / 1 / 2 / 3: 465 / 458 / 453 / 454 us; convergent config 4:
     // 3.80 / 3.18 / 3.22 ms); FBA_FLOW_MSPLIT: the sources a merged group may hold (default SPLIT)
-    const int merge_gap = getenv("FBA_FLOW_MERGE") ? atoi(getenv("FBA_FLOW_MERGE")) : 2;
+    // (default: 2 for a quarter-record schedule, 1 for a whole-block one, decided below -- same-box A/B, three
+    // runs each, G = 2 / 1: convergent config 4 270.0 / 273.8 iter/s, config 5 280.4 / 282.2, config 4 1,266 / 1,258)
+    int merge_gap = getenv("FBA_FLOW_MERGE") ? atoi(getenv("FBA_FLOW_MERGE")) : -1;
     const int msplit = getenv("FBA_FLOW_MSPLIT") ? std::max(1, atoi(getenv("FBA_FLOW_MSPLIT"))) : SPLIT;
     int nslot = 0, ncnt = 0, n_whole_t = 0;
     // diagonal blocks
@@ -558,6 +560,7 @@ static void build_flow(Sched& s, std::vector<int32_t>& buf, const std::vector<st
                 for (size_t ai = bi; ai < R[k].size(); ++ai) upd_flops += (R[k][ai] == R[k][bi] ? 3 : 4) * 2.0 * 64 * 64 * NB;
     }
     const int blockm = getenv("FBA_FLOW_BLOCK") ? atoi(getenv("FBA_FLOW_BLOCK")) : (nw_in > 0 && upd_flops / nw_in >= 1.5e9 ? 1 : 0);
+    if (merge_gap < 0) merge_gap = blockm > 0 ? 1 : 2;
     if (verbose)
         fprintf(stderr, "[fba] flow schedule: update work %.2f GFLOP over %d levels, update records mode %d\n", upd_flops * 1e-9,
                 nw_in, blockm);
