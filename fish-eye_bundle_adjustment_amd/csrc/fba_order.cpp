@@ -360,8 +360,10 @@ std::vector<int32_t> camera_order(const fba_problem* p) {
     const char* le = getenv("FBA_ND_LEAF");
     // levels at configs 3 / 4 / 5 (cuts along the best of five directions, minimum-vertex-cover
     // separators): leaf 100 -> 7 / 16 / 31, 150 -> 7 / 17 / 31; config 4 measured 808-812 iter/s at 100,
-    // 804 at 120, 776-778 at 150
-    int leaf = le ? atoi(le) : 100;
+    // 804 at 120, 776-778 at 150 (round 1).  Round 5, same box: config 4 1,266-1,272 at 100, 1,270-1,277
+    // at 130, 1,251-1,270 at 120; config 5 282.8 at 100, 288.9 / 289.1 at 160, 284.9 at 200, 281-282 at
+    // 250 / 320; config 3 flat -- larger scenes take larger leaves: 100 (n / 1000)^(1/3), at least 100
+    int leaf = le ? atoi(le) : std::max(100, (int)std::lround(100.0 * std::cbrt(p->n_img / 1000.0)));
     if (leaf <= 0) leaf = p->n_img;  // 0: reverse Cuthill-McKee only
     Graph g = covis_graph(p);
     std::vector<int32_t> all(p->n_img), out;
