@@ -83,42 +83,53 @@ __device__ __forceinline__ void params_body(int t, int nthreads, const double* _
 #pragma unroll
             for (int i = 0; i < 42; ++i) g[i] = slot ? rows[i] : 0.0;
         }
-    } else if (t < n_img + n_cam) {
-        int k = t - n_img;
-        const double* q = xfull + 6 * (int64_t)n_img + (int64_t)k * cw;
-        const double* ci = caminfo + 5 * k;
-        double* o = cam_tab + (int64_t)k * cam_stride;
+    }
+}
+
+// the camera table of camera k, one workgroup: thread 0 the header, thread j in 1..nk the distortion term j
+// (its rmax^(2j) and reciprocal) -- the nk pow calls in parallel instead of one thread's chain
+__device__ __forceinline__ void cam_params_body(int k, int j, const double* __restrict__ xfull,
+                                                const double* __restrict__ caminfo, double* __restrict__ cam_tab, int n_img,
+                                                int nk, int cw, int cam_stride) {
+    const double* q = xfull + 6 * (int64_t)n_img + (int64_t)k * cw;
+    const double* ci = caminfo + 5 * k;
+    double* o = cam_tab + (int64_t)k * cam_stride;
+    const double hx = (ci[3] - ci[1]) * 0.5, hy = (ci[4] - ci[2]) * 0.5;
+    const double rmax = sqrt(hx * hx + hy * hy);  // BuildAwG.m:422
+    if (j == 0) {
         o[0] = q[0];            // xp
         o[1] = q[1];            // yp
         o[2] = q[2];            // c
         o[3] = ci[0];           // y_dir
         o[4] = q[3 + nk];       // P1
         o[5] = q[4 + nk];       // P2
-        double hx = (ci[3] - ci[1]) * 0.5, hy = (ci[4] - ci[2]) * 0.5;
-        double rmax = sqrt(hx * hx + hy * hy);  // BuildAwG.m:422
+        o[6] = pow(rmax, 2.0);  // rmax^2 (= the j = 1 term below)
         o[7] = rmax;
-        for (int j = 1; j <= nk; ++j) {
-            o[CAM_TAB_HDR + j - 1] = q[2 + j];                   // K_j
-            o[CAM_TAB_HDR + nk + j - 1] = pow(rmax, 2.0 * j);    // rmax^(2j), BuildAwG.m:424-426
-            o[CAM_TAB_HDR + 2 * nk + j - 1] = 1.0 / o[CAM_TAB_HDR + nk + j - 1];  // its reciprocal (obs_model)
-        }
-        o[6] = o[CAM_TAB_HDR + nk];                              // rmax^2
+    } else if (j <= nk) {
+        o[CAM_TAB_HDR + j - 1] = q[2 + j];                     // K_j
+        const double r2j = pow(rmax, 2.0 * j);                  // rmax^(2j), BuildAwG.m:424-426
+        o[CAM_TAB_HDR + nk + j - 1] = r2j;
+        o[CAM_TAB_HDR + 2 * nk + j - 1] = 1.0 / r2j;            // its reciprocal (obs_model)
     }
 }
 
-// 64-thread workgroups: [0, nb) the image and camera tables, [nb, grid) the copy of the linearisation
-// point with four independent loads in flight per thread, so the table waves do not first wait out
-// serial copy iterations (kernel time = max of the two instead of their sum)
+// 64-thread workgroups: [0, nbi) the image tables, [nbi, nb) one camera each, [nb, grid) the copy of
+// the linearisation point with four independent loads in flight per thread, so the table waves do not
+// first wait out serial copy iterations (kernel time = max of the three instead of their sum)
 constexpr int PARAMS_WG = 64;
 __global__ __launch_bounds__(PARAMS_WG) void k_params(const double* __restrict__ xfull, const double* __restrict__ caminfo,
                                                       double* __restrict__ img_tab, double* __restrict__ cam_tab,
                                                       double* __restrict__ G, const uint8_t* __restrict__ active, int n_img,
                                                       int n_cam, int nk, int cw, int cam_stride, int ic,
                                                       double* __restrict__ xcopy, int64_t n_copy) {
-    const int nb = (n_img + n_cam + PARAMS_WG - 1) / PARAMS_WG;
-    if ((int)blockIdx.x < nb) {
-        params_body(blockIdx.x * PARAMS_WG + threadIdx.x, nb * PARAMS_WG, xfull, caminfo, img_tab, cam_tab, G, active,
+    const int nbi = (n_img + PARAMS_WG - 1) / PARAMS_WG, nb = nbi + n_cam;
+    if ((int)blockIdx.x < nbi) {
+        params_body(blockIdx.x * PARAMS_WG + threadIdx.x, nbi * PARAMS_WG, xfull, caminfo, img_tab, cam_tab, G, active,
                     n_img, n_cam, nk, cw, cam_stride, ic, nullptr, 0);
+        return;
+    }
+    if ((int)blockIdx.x < nb) {
+        cam_params_body(blockIdx.x - nbi, threadIdx.x, xfull, caminfo, cam_tab, n_img, nk, cw, cam_stride);
         return;
     }
     if (!xcopy) return;
@@ -1516,8 +1527,7 @@ int launch_obs_T(Ctx& c, double* T) {
 }
 
 int launch_params(Ctx& c, const double* x, double* copy_to) {
-    const int n = c.L.n_img + c.L.n_cam;
-    const int64_t nb = (n + PARAMS_WG - 1) / PARAMS_WG;
+    const int64_t nb = (c.L.n_img + PARAMS_WG - 1) / PARAMS_WG + c.L.n_cam;
     const int64_t blocks = copy_to ? nb + std::min<int64_t>(2048, (c.L.u_full + 4 * PARAMS_WG - 1) / (4 * PARAMS_WG)) : nb;
     k_params<<<(unsigned)blocks, PARAMS_WG, 0, c.stream>>>(x ? x : c.d_xfull, c.d_caminfo, c.d_img_tab, c.d_cam_tab, c.d_G,
                                                     c.d_active, c.L.n_img, c.L.n_cam, c.L.nk, c.L.cw, c.cam_tab_stride,
