@@ -953,14 +953,15 @@ __device__ __forceinline__ void red_pairs_body(int blk, const double* __restrict
     // S(e1, e2)[r][c] -= U_a[r] . U_b[c], U rows of 6 x 3 (row r at 3 r; rows ec, ec + 1 of U_b as three
     // 16-B loads)
     constexpr int TB = 2;
+    int oa[TB], ob[TB];  // the batch's observations, loaded one batch ahead (the next batch's indices are
+                         // in flight with this batch's U rows): convergent k_red_blocks 362.6 -> 337.0 us
+#pragma unroll
+    for (int u = 0; u < TB; ++u) {
+        oa[u] = t0 + u < t1 ? A[plan.tp_ab + 2 * (t0 + u)] : 0;
+        ob[u] = t0 + u < t1 ? A[plan.tp_ab + 2 * (t0 + u) + 1] : 0;
+    }
     for (int t = t0; t < t1; t += TB) {
         const int nt = min(TB, t1 - t);
-        int oa[TB], ob[TB];
-#pragma unroll
-        for (int u = 0; u < TB; ++u) {
-            oa[u] = u < nt ? A[plan.tp_ab + 2 * (t + u)] : 0;
-            ob[u] = u < nt ? A[plan.tp_ab + 2 * (t + u) + 1] : 0;
-        }
         double ua[TB][3];
         double2 ub[TB][3];
 #pragma unroll
@@ -971,6 +972,12 @@ __device__ __forceinline__ void red_pairs_body(int blk, const double* __restrict
 #pragma unroll
                 for (int m = 0; m < 3; ++m) { ua[u][m] = a[m]; ub[u][m] = b[m]; }
             }
+        const int tn = t + TB;
+#pragma unroll
+        for (int u = 0; u < TB; ++u) {
+            oa[u] = tn + u < t1 ? A[plan.tp_ab + 2 * (tn + u)] : 0;
+            ob[u] = tn + u < t1 ? A[plan.tp_ab + 2 * (tn + u) + 1] : 0;
+        }
 #pragma unroll
         for (int u = 0; u < TB; ++u)
             if (u < nt) {
