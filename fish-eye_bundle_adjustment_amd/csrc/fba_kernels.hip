@@ -910,49 +910,42 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     stamp(5);
 }
 
-// k_red_pairs: S(e1, e2) = the sum of the pair's partials in chunk order; three pairs per wave, 18 lanes
-// each holding two adjacent entries (16-B loads and stores) of the pair's 36
-constexpr int RP_PER_WAVE = 3, RP_PER_WG = 4 * RP_PER_WAVE;
+// k_red_pairs: S(e1, e2) = the sum of the pair's partials in chunk order; seven pairs per wave, 9 lanes
+// each holding a 2 x 2 sub-block (rows er, er + 1, columns ec, ec + 1; 16-B loads and stores) of the pair's
+// 6 x 6 block
+constexpr int RP_PER_WAVE = 7, RP_PER_WG = 4 * RP_PER_WAVE;
 __device__ __forceinline__ void red_pairs_body(int blk, const double* __restrict__ ppart, const double* __restrict__ Ug,
                                                const int32_t* __restrict__ A, const AccPlan& plan, double* __restrict__ S,
                                                int64_t ld, int64_t n_pairs) {
-    const int lane = threadIdx.x & 63, sub = lane / 18, l = lane - 18 * sub;
+    const int lane = threadIdx.x & 63, sub = lane / 9, l = lane - 9 * sub;
     const int64_t pr = ((int64_t)blk * 4 + (threadIdx.x >> 6)) * RP_PER_WAVE + sub;
     if (sub >= RP_PER_WAVE || pr >= n_pairs) return;
-    // the partials in chunk order, one contiguous range (pair-major slots), 8 (then 4) loads in flight
+    const int er = 2 * (l / 3), ec = 2 * (l % 3);
+    // the partials in chunk order, one contiguous range (pair-major slots), 4 x 2 loads in flight
     // (fixed association per entry: ((s + p0) + p1) + ...)
     const int q0 = A[plan.rp_start + pr], q1 = A[plan.rp_start + pr + 1];
     const int t0 = A[plan.tp_start + pr], t1 = A[plan.tp_start + pr + 1];
     const int64_t e1 = A[plan.rp_e + 2 * pr], e2 = A[plan.rp_e + 2 * pr + 1];
-    const double2* pp = reinterpret_cast<const double2*>(ppart) + l;
-    double sx = 0.0, sy = 0.0;
+    const double2* pp = reinterpret_cast<const double2*>(ppart) + (6 * er + ec) / 2;  // row er; row er + 1 at + 3
+    double2 s0 = {0.0, 0.0}, s1 = {0.0, 0.0};
+    auto add = [&](double2& a, const double2 b) { a.x += b.x; a.y += b.y; };
     int q = q0;
-    for (; q + 8 <= q1; q += 8) {
-        double2 p[8];
+    while (q + 4 <= q1) {
+        double2 p[4][2];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) p[j] = pp[(int64_t)(q + j) * 18];
+        for (int j = 0; j < 4; ++j) { p[j][0] = pp[(int64_t)(q + j) * 18]; p[j][1] = pp[(int64_t)(q + j) * 18 + 3]; }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { sx += p[j].x; sy += p[j].y; }
-    }
-    if (q + 4 <= q1) {
-        double2 p[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) p[j] = pp[(int64_t)(q + j) * 18];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { sx += p[j].x; sy += p[j].y; }
+        for (int j = 0; j < 4; ++j) { add(s0, p[j][0]); add(s1, p[j][1]); }
         q += 4;
     }
     for (; q < q1; ++q) {
-        const double2 p = pp[(int64_t)q * 18];
-        sx += p.x;
-        sy += p.y;
+        add(s0, pp[(int64_t)q * 18]);
+        add(s1, pp[(int64_t)q * 18 + 3]);
     }
-    const int e = 2 * l;  // entries e, e + 1 of the row-major 6 x 6 block: row e / 6, columns e % 6 (even)
-    const int er = e / 6, ec = e % 6;
     // then the U-row terms (AccPlan::ck_tm chunks), in chunk order, TB in flight:
-    // S(e1, e2)[r][c] -= U_a[r] . U_b[c], U rows of 6 x 3 (row r at 3 r; rows ec, ec + 1 of U_b as three
-    // 16-B loads)
-    constexpr int TB = 2;
+    // S(e1, e2)[r][c] -= U_a[r] . U_b[c], U rows of 6 x 3 (row r at 3 r: rows er, er + 1 of U_a and ec,
+    // ec + 1 of U_b as three 16-B loads each)
+    constexpr int TB = 1;
     int oa[TB], ob[TB];  // the batch's observations, loaded one batch ahead (the next batch's indices are
                          // in flight with this batch's U rows): convergent k_red_blocks 362.6 -> 337.0 us
 #pragma unroll
@@ -962,15 +955,18 @@ __device__ __forceinline__ void red_pairs_body(int blk, const double* __restrict
     }
     for (int t = t0; t < t1; t += TB) {
         const int nt = min(TB, t1 - t);
-        double ua[TB][3];
-        double2 ub[TB][3];
+        double ua[TB][6], ub[TB][6];
 #pragma unroll
         for (int u = 0; u < TB; ++u)
             if (u < nt) {
-                const double* a = Ug + (int64_t)oa[u] * 18 + 3 * er;
+                const double2* a = reinterpret_cast<const double2*>(Ug + (int64_t)oa[u] * 18 + 3 * er);
                 const double2* b = reinterpret_cast<const double2*>(Ug + (int64_t)ob[u] * 18 + 3 * ec);
 #pragma unroll
-                for (int m = 0; m < 3; ++m) { ua[u][m] = a[m]; ub[u][m] = b[m]; }
+                for (int m = 0; m < 3; ++m) {
+                    const double2 va = a[m], vb = b[m];
+                    ua[u][2 * m] = va.x; ua[u][2 * m + 1] = va.y;
+                    ub[u][2 * m] = vb.x; ub[u][2 * m + 1] = vb.y;
+                }
             }
         const int tn = t + TB;
 #pragma unroll
@@ -981,11 +977,16 @@ __device__ __forceinline__ void red_pairs_body(int blk, const double* __restrict
 #pragma unroll
         for (int u = 0; u < TB; ++u)
             if (u < nt) {
-                sx -= ua[u][0] * ub[u][0].x + ua[u][1] * ub[u][0].y + ua[u][2] * ub[u][1].x;
-                sy -= ua[u][0] * ub[u][1].y + ua[u][1] * ub[u][2].x + ua[u][2] * ub[u][2].y;
+                const double* x = ua[u];
+                const double* y = ub[u];
+                s0.x -= x[0] * y[0] + x[1] * y[1] + x[2] * y[2];
+                s0.y -= x[0] * y[3] + x[1] * y[4] + x[2] * y[5];
+                s1.x -= x[3] * y[0] + x[4] * y[1] + x[5] * y[2];
+                s1.y -= x[3] * y[3] + x[4] * y[4] + x[5] * y[5];
             }
     }
-    *reinterpret_cast<double2*>(S + (6 * e1 + er) * ld + 6 * e2 + ec) = double2{sx, sy};
+    *reinterpret_cast<double2*>(S + (6 * e1 + er) * ld + 6 * e2 + ec) = s0;
+    *reinterpret_cast<double2*>(S + (6 * e1 + er + 1) * ld + 6 * e2 + ec) = s1;
 }
 
 // k_red_images: the diagonal block, RHS and image-camera block of image e from its partials
