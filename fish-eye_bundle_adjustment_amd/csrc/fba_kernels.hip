@@ -989,29 +989,37 @@ __device__ __forceinline__ void red_pairs_body(int blk, const double* __restrict
     *reinterpret_cast<double2*>(S + (6 * e1 + er + 1) * ld + 6 * e2 + ec) = s1;
 }
 
-// k_red_images: the diagonal block, RHS and image-camera block of image e from its partials
+// k_red_images: the diagonal block, RHS and image-camera block of image e from its partials; one image per
+// workgroup, the two 128-thread halves summing the first and the second half of its partial rows (a dense
+// network's image has ~440 of them: the chain of load round trips is the time), then half 1's sums are
+// added to half 0's in LDS -- ((p0 + p1) + ...) + ((pm + pm+1) + ...), a fixed order
 template <int NK>
-__device__ __forceinline__ void red_images_body(int e, int q, const double* __restrict__ ipart,
-                                                const int32_t* __restrict__ A, const AccPlan& plan,
-                                                double* __restrict__ S, int64_t ld, int64_t n_pad, int n_img) {
+__device__ __forceinline__ void red_images_body(int e, const double* __restrict__ ipart, const int32_t* __restrict__ A,
+                                                const AccPlan& plan, double* __restrict__ S, int64_t ld, int64_t n_pad,
+                                                int n_img) {
     constexpr int CW = 5 + NK, NIMG = LR<NK>::NIMG;
-    if (e >= n_img) return;
-    const int r0 = A[plan.ri_start + e], r1 = A[plan.ri_start + e + 1];
-    if (r0 == r1 || q >= NIMG) return;
-    // the partials in chunk order (image-major slots: one contiguous range) with 8 loads in flight; same
-    // association as the plain running sum (((s + p0) + p1) + ...), so the result does not depend on the
-    // batching (32 in flight: convergent k_red_blocks 329 -> 323 us, at 64 more VGPRs for the whole launch)
-    const double* ip = ipart + q;
+    __shared__ double half1[128];
+    const int q = threadIdx.x & 127, h = threadIdx.x >> 7;
+    const int r0 = A[plan.ri_start + e], r1 = A[plan.ri_start + e + 1];  // (uniform per workgroup)
+    if (r0 == r1) return;
+    const int rm = r0 + (r1 - r0) / 2;
+    const int xa = h ? rm : r0, xb = h ? r1 : rm;
+    // (8 loads in flight; 32 measured: convergent k_red_blocks 329 -> 323 us, at 64 more VGPRs for the launch)
+    const double* ip = ipart + (q < NIMG ? q : 0);
     double s = 0.0;
-    int x = r0;
-    for (; x + 8 <= r1; x += 8) {
+    int x = xa;
+    for (; x + 8 <= xb; x += 8) {
         double p[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) p[j] = ip[(int64_t)(x + j) * NIMG];
 #pragma unroll
         for (int j = 0; j < 8; ++j) s += p[j];
     }
-    for (; x < r1; ++x) s += ip[(int64_t)x * NIMG];
+    for (; x < xb; ++x) s += ip[(int64_t)x * NIMG];
+    if (h) half1[q] = s;
+    __syncthreads();
+    if (h || q >= NIMG) return;
+    s += half1[q];
     if (q < 21) {
         S[(6 * (int64_t)e + c_tri_a[q]) * ld + 6 * e + c_tri_b[q]] = s;
     } else if (q < 27) {
@@ -1050,7 +1058,7 @@ __device__ __forceinline__ void red_cam_seg_body(int sg, int q, int n_cam, const
 }
 
 // the three independent reductions in one launch: workgroups [0, npb) the image pairs (RP_PER_WG per
-// workgroup), then two images per workgroup (128 threads each), then two camera segments per workgroup
+// workgroup), then one image per workgroup, then two camera segments per workgroup
 template <int NK>
 __global__ __launch_bounds__(256) void k_red_blocks(const double* __restrict__ ppart, const double* __restrict__ ipart,
                                                     const double* __restrict__ cpart, const int32_t* __restrict__ A,
@@ -1066,7 +1074,7 @@ __global__ __launch_bounds__(256) void k_red_blocks(const double* __restrict__ p
         const int bx = x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
         red_pairs_body(bx, ppart, Ug, A, plan, S, ld, n_pairs);
     } else if (b < npb + nib) {
-        red_images_body<NK>(2 * (b - npb) + (threadIdx.x >> 7), threadIdx.x & 127, ipart, A, plan, S, ld, n_pad, n_img);
+        red_images_body<NK>(b - npb, ipart, A, plan, S, ld, n_pad, n_img);
     } else {
         red_cam_seg_body<NK>(2 * (b - npb - nib) + (threadIdx.x >> 7), threadIdx.x & 127, n_cam, cpart, A, plan, cseg);
     }
@@ -1591,7 +1599,7 @@ int launch_accumulate(Ctx& c, bool zeroed) {
         c.d_cpart, c.L.u_c, c.set.type, c.cam_tab_stride, em, cm, px, py, c.d_lrprof, (int)nlr, c.d_S, L.ld,      \
         c.d_sched + c.sched.zero, c.d_xoff, c.d_U);                                                               \
     {                                                                                                             \
-        const int npb = (int)((c.n_pairs + RP_PER_WG - 1) / RP_PER_WG), nib = (L.n_img + 1) / 2, ncb = (L.n_cam * CAM_SEG + 1) / 2;   \
+        const int npb = (int)((c.n_pairs + RP_PER_WG - 1) / RP_PER_WG), nib = L.n_img, ncb = (L.n_cam * CAM_SEG + 1) / 2;   \
         k_red_blocks<NKV><<<(unsigned)(npb + nib + ncb), 256, 0, c.stream>>>(                                     \
             c.d_ppart, c.d_ipart, c.d_cpart, c.d_acc, c.acc, c.d_S, L.ld, c.n_pairs, L.n_pad, L.n_img, L.n_cam, npb, \
             nib, c.d_cseg, c.d_U);                                                                                \
