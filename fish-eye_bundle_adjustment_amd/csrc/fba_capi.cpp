@@ -531,6 +531,8 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         if (!io.empty()) ik_o.push_back((int32_t)ik_obs.size());
         ck_ik.push_back((int32_t)ik_img.size());
     }
+    // image-key lanes of k_lin_reduce: 4 when the chunks' image keys hold <= 2 observations on average
+    c->ik_lanes = (ck_ik.back() > 0 && ik_obs.size() <= 2 * (size_t)ck_ik.back()) ? 4 : 8;
     // general points: gimg / gpc groups and their keys, appended after the chunks' keys
     GenPlan& G = c->gen;
     G.n_gp = (int64_t)gps.size();
@@ -846,9 +848,9 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     for (auto& e : c->ev) FBA_HIP(hipEventCreate(&e));
     if (opt.verbose)
         fprintf(stderr, "[fba] rank %d/%d: n_obs %ld (tie %ld), points %ld, pairs %ld (%ld terms), u_c %ld, n_pad %ld; "
-                "chunks %ld, pair keys %ld, U-row pair terms %ld, image keys %ld; general points %ld\n",
+                "chunks %ld, pair keys %ld, U-row pair terms %ld, image keys %ld (%d lanes each); general points %ld\n",
                 opt.rank, opt.world, (long)c->n_obs, (long)c->n_obs_tie, (long)c->n_lp, (long)c->n_pairs,
-                (long)c->n_pair_terms, (long)L.u_c, (long)L.n_pad, (long)c->n_chunks_lr, (long)c->acc.n_pk, (long)c->acc.n_tt, (long)c->acc.n_ik, (long)G.n_gp);
+                (long)c->n_pair_terms, (long)L.u_c, (long)L.n_pad, (long)c->n_chunks_lr, (long)c->acc.n_pk, (long)c->acc.n_tt, (long)c->acc.n_ik, c->ik_lanes, (long)G.n_gp);
     *out = c;
     return FBA_OK;
 }

@@ -240,6 +240,7 @@ struct Ctx {
     int32_t* d_acc = nullptr;
     double* d_ppart = nullptr;       // [acc.n_pk][36] pair-block partials
     double* d_U = nullptr;           // [n_obs_pad][18] U = W R of the observations of U-row chunks (acc.ck_tm)
+    int ik_lanes = 8;                // k_lin_reduce's lanes per image-key unit (4: keys of <= 2 observations)
     double* d_ipart = nullptr;       // [acc.n_ik][27 + 6 cw] image partials: diagonal block, RHS, image-camera
     uint64_t* d_lrprof = nullptr;    // FBA_LR_PROFILE: k_lin_reduce phase timestamps [n_chunks][8]
     uint64_t* d_ptrace = nullptr;    // FBA_PANEL_TRACE: k_panel workgroup timestamps [level][PTRACE_WG][8]

@@ -466,7 +466,7 @@ struct LR {
 
 constexpr int LR_THREADS = 512;  // observation phases use the first CHUNK_OBS threads, (D) all of them
 
-template <int NK>
+template <int NK, int IKL>
 __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     const double* __restrict__ xy, const int32_t* __restrict__ img, const int32_t* __restrict__ cam,
     const int32_t* __restrict__ pt, const int32_t* __restrict__ lp_tie, const double* __restrict__ ctl,
@@ -773,12 +773,12 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
     // xor-butterfly over the 8 lanes; part-major unit order keeps the rows of a wave on one path
     constexpr int HALF = (CW + 1) / 2;
     constexpr int IV = 27 > 6 * HALF ? 27 : 6 * HALF;  // values per unit
-#ifndef FBA_IK_LANES
-#define FBA_IK_LANES 8
-#endif
-    // lanes per unit (8 or 4; -DFBA_IK_LANES=4 measured: image keys 6.54 -> 8.82 us per chunk, 1,229 ->
-    // 1,190 iter/s -- fewer lanes per key serialise more observations per lane)
-    constexpr int GL = FBA_IK_LANES;
+    // lanes per unit, per launch (IKL, Ctx::ik_lanes): 8, or 4 when the scene's image keys hold <= 2
+    // observations on average (a dense network's chunks: ~1.1 -- on eight lanes seven would mostly idle and
+    // the units take twice the rounds: convergent k_lin_reduce 331.9 -> 313.4 us).  A grid's keys (~7
+    // observations) on 4 lanes measured slower (image keys 6.54 -> 8.82 us per chunk); both lane counts in
+    // one kernel slowed the eight-lane path (config 4 206.1 -> 210.2 us), hence two instantiations
+    constexpr int GL = IKL;
     static_assert(GL == 8 || GL == 4, "image-key lanes per unit");
     constexpr int NV = (IV + GL - 1) / GL * GL, M = NV / GL;  // padded to the GL-lane reduce-scatter
     {
@@ -1591,13 +1591,16 @@ int launch_accumulate(Ctx& c, bool zeroed) {
     if (nlr == 0 && c.gen.n_gp == 0) return FBA_OK;
     const unsigned em = eop_mask(c.set), cm = cam_mask(c.set, c.L.nk);
     const double px = px_of(c), py = py_of(c);
+#define LR_ARGS                                                                                                   \
+    c.d_xy, c.d_img, c.d_cam, c.d_pt, c.d_lp_tie, c.d_ctl, c.d_xfull, c.d_img_tab, c.d_cam_tab, c.d_chunk_obs,    \
+        c.d_chunk_pt, c.d_lp_start, c.d_acc, c.acc, c.d_WT, c.d_pt_tab, c.d_ppart, c.d_ipart, c.d_cpart, c.L.u_c, \
+        c.set.type, c.cam_tab_stride, em, cm, px, py, c.d_lrprof, (int)nlr, c.d_S, L.ld, c.d_sched + c.sched.zero, \
+        c.d_xoff, c.d_U
 #define ACC(NKV)                                                                                                  \
-    if (nlr > 0)                                                                                                  \
-    k_lin_reduce<NKV><<<(unsigned)(nlr + ztail), LR_THREADS, LR<NKV>::LDS, c.stream>>>(                           \
-        c.d_xy, c.d_img, c.d_cam, c.d_pt, c.d_lp_tie, c.d_ctl, c.d_xfull, c.d_img_tab, c.d_cam_tab,                \
-        c.d_chunk_obs, c.d_chunk_pt, c.d_lp_start, c.d_acc, c.acc, c.d_WT, c.d_pt_tab, c.d_ppart, c.d_ipart,       \
-        c.d_cpart, c.L.u_c, c.set.type, c.cam_tab_stride, em, cm, px, py, c.d_lrprof, (int)nlr, c.d_S, L.ld,      \
-        c.d_sched + c.sched.zero, c.d_xoff, c.d_U);                                                               \
+    if (nlr > 0 && c.ik_lanes == 4)                                                                               \
+        k_lin_reduce<NKV, 4><<<(unsigned)(nlr + ztail), LR_THREADS, LR<NKV>::LDS, c.stream>>>(LR_ARGS);           \
+    else if (nlr > 0)                                                                                             \
+        k_lin_reduce<NKV, 8><<<(unsigned)(nlr + ztail), LR_THREADS, LR<NKV>::LDS, c.stream>>>(LR_ARGS);           \
     {                                                                                                             \
         const int npb = (int)((c.n_pairs + RP_PER_WG - 1) / RP_PER_WG), nib = L.n_img, ncb = (L.n_cam * CAM_SEG + 1) / 2;   \
         k_red_blocks<NKV><<<(unsigned)(npb + nib + ncb), 256, 0, c.stream>>>(                                     \
@@ -1607,13 +1610,17 @@ int launch_accumulate(Ctx& c, bool zeroed) {
     k_red_cam<NKV><<<(unsigned)L.n_cam, 128, 0, c.stream>>>(c.d_cseg, c.d_S, L.ld, L.n_pad, L.n_img)
     FBA_NK_DISPATCH(L.nk, ACC);
 #undef ACC
+#undef LR_ARGS
     FBA_HIP(hipGetLastError());
     return FBA_OK;
 }
 
 int acc_setup(Ctx& c) {
-#define SET(NKV) \
-    FBA_HIP(hipFuncSetAttribute((const void*)k_lin_reduce<NKV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LR<NKV>::LDS))
+#define SET(NKV)                                                                                                     \
+    FBA_HIP(hipFuncSetAttribute((const void*)k_lin_reduce<NKV, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,     \
+                                (int)LR<NKV>::LDS));                                                                  \
+    FBA_HIP(hipFuncSetAttribute((const void*)k_lin_reduce<NKV, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,     \
+                                (int)LR<NKV>::LDS))
     FBA_NK_DISPATCH(c.L.nk, SET);
 #undef SET
     return FBA_OK;
