@@ -2725,7 +2725,7 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
                                                   const double* __restrict__ bsc) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* Li = smem;              // [128][128] Linv_j, or L_jj for a root column
-    double* Dt = Li + CB * CB;      // [8][16][16] the leaf inverses of a root column
+    double* Dt = Li + CB * CB;      // [8][16][16] the leaf inverses of a root column (else: partial sums)
     double* xs = Dt + (CB / IB) * IB * IB;  // [128] x_i of the current source
     double* ys = xs + CB;           // [128]
     double* red = ys + CB;          // [512]
@@ -2771,40 +2771,20 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
         if (root)
             for (int q = tid; q < (CB / IB) * IB * IB; q += 256) Dt[q] = dinv[(int64_t)j * (CB / IB) * IB * IB + q];
     }
-    double a0 = 0.0, a1 = 0.0;
-    const __amdgpu_buffer_rsrc_t rX = block_rsrc(X, n_pad * 8);
-    for (int q = src_start[j]; q < src_start[j + 1]; ++q) {
-        const int i = src[q];
-        const double* M = S + (int64_t)i * CB * ld + (int64_t)j * CB;  // L(i, j), written by earlier launches
-        double2 m[32];
+    // u_j = y_j + F_j c (the inner-constraint combine, coefficients cs) does not depend on the sources:
+    // formed ahead of them, off the chain of published x blocks (the coefficients come from the combine
+    // workgroup, an earlier ticket, or a previous launch)
+    // (row ur of thread tid: tid for a root, whose substitution reads y from LDS; else row 32 h + (lane & 31),
+    // so that wave h forms the 32 entries of y_j its rows of the final product need without another barrier)
+    const int ur = root ? tid : 32 * h + (c2 & 31);
+    const bool uown = ur < CB;
+    double u = 0.0;
+    if (uown) u = S[n_pad * ld + (int64_t)j * CB + ur];
+    if (coef) {
+        double f[14];
+        if (uown)
 #pragma unroll
-        for (int r = 0; r < 32; ++r) m[r] = *reinterpret_cast<const double2*>(M + (int64_t)(h * 32 + r) * ld + 2 * c2);
-        if (tid < CB / 2) {  // wave 0 polls x_i itself (sc1) until none of its 128 values is the sentinel
-            unsigned spins = 0;
-            double2 v;
-            for (;;) {
-                asm volatile("" ::: "memory");  // the load is re-issued every spin (not hoisted)
-                v = ld_sc1(rX, ((int64_t)i * CB + 2 * tid) * 8);
-                const bool ok = __builtin_bit_cast(uint64_t, v.x) != X_SENTINEL && __builtin_bit_cast(uint64_t, v.y) != X_SENTINEL;
-                if (__all(ok)) break;
-                __builtin_amdgcn_s_sleep(1);
-                if (spin_expired(spins, scal)) break;
-            }
-            xs[2 * tid] = v.x;
-            xs[2 * tid + 1] = v.y;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < 32; ++r) {
-            const double xr = xs[h * 32 + r];
-            a0 += m[r].x * xr;
-            a1 += m[r].y * xr;
-        }
-        __syncthreads();  // xs is rewritten by the next source
-    }
-    red[h * 128 + 2 * c2] = a0;
-    red[h * 128 + 2 * c2 + 1] = a1;
-    if (coef) {  // the border coefficients: from the combine workgroup (its flag), or a previous launch
+            for (int m = 0; m < 14; ++m) f[m] = S[(n_pad + 1 + m) * ld + (int64_t)j * CB + ur];
         if (combine && tid == 0) {
             unsigned spins = 0;
             while (__hip_atomic_load(flags + nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 1u) {
@@ -2818,19 +2798,45 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
             cs[2 * tid] = v.x;
             cs[2 * tid + 1] = v.y;
         }
-    }
-    __syncthreads();
-    if (tid < CB) {
-        const double s = (red[tid] + red[128 + tid]) + (red[256 + tid] + red[384 + tid]);
-        // u_j = y_j + F_j c (the inner-constraint combine, coefficients cs), then - s
-        double u = S[n_pad * ld + (int64_t)j * CB + tid];
-        if (coef)
+        __syncthreads();
+        if (uown)
 #pragma unroll
-            for (int m = 0; m < 14; ++m) u += S[(n_pad + 1 + m) * ld + (int64_t)j * CB + tid] * cs[m];
-        ys[tid] = u - s;
+            for (int m = 0; m < 14; ++m) u += f[m] * cs[m];
     }
+    double a0 = 0.0, a1 = 0.0;
+    const __amdgpu_buffer_rsrc_t rX = block_rsrc(X, n_pad * 8);
+    for (int q = src_start[j]; q < src_start[j + 1]; ++q) {
+        const int i = src[q];
+        const double* M = S + (int64_t)i * CB * ld + (int64_t)j * CB;  // L(i, j), written by earlier launches
+        double2 m[32];
+#pragma unroll
+        for (int r = 0; r < 32; ++r) m[r] = *reinterpret_cast<const double2*>(M + (int64_t)(h * 32 + r) * ld + 2 * c2);
+        // each wave polls the 32 values of x_i its rows need (sc1; lane l holds 2 (l & 15), + 1) until none
+        // is the sentinel, and takes them lane by lane (readlane): no workgroup barrier per source
+        unsigned spins = 0;
+        double2 v;
+        for (;;) {
+            asm volatile("" ::: "memory");  // the load is re-issued every spin (not hoisted)
+            v = ld_sc1(rX, ((int64_t)i * CB + h * 32 + 2 * (c2 & 15)) * 8);
+            const bool ok = __builtin_bit_cast(uint64_t, v.x) != X_SENTINEL && __builtin_bit_cast(uint64_t, v.y) != X_SENTINEL;
+            if (__all(ok)) break;
+            __builtin_amdgcn_s_sleep(1);
+            if (spin_expired(spins, scal)) break;
+        }
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            const double xr = readlane_d((r & 1) ? v.y : v.x, r >> 1);
+            a0 += m[r].x * xr;
+            a1 += m[r].y * xr;
+        }
+    }
+    red[h * 128 + 2 * c2] = a0;
+    red[h * 128 + 2 * c2 + 1] = a1;
     __syncthreads();
+    const double yu = uown ? u - ((red[ur] + red[128 + ur]) + (red[256 + ur] + red[384 + ur])) : 0.0;
     if (root) {
+        if (tid < CB) ys[tid] = yu;
+        __syncthreads();
         // x = L^-T y by substitution in wave 0 alone (no workgroup barriers): tiles s = 7 .. 0,
         // x_s = D_s' (y_s - sum_{t>s} L_ts' x_t); lane (c = lane & 15, quarter g = lane >> 4) sums the
         // rows g, g+4, .. below tile s for column c, the quarters added by a fixed xor butterfly
@@ -2864,20 +2870,22 @@ __global__ __launch_bounds__(256) void k_bwd_flow(const double* __restrict__ S, 
         }
         return;
     }
-    // x_j = Linv_j' y_j from LDS
+    // x_j = Linv_j' y_j from LDS, y_j's row 32 h + r from lane r of wave h; the partial sums go to the
+    // leaf-inverse area (a root's only), as other waves may still read `red`
     double b0 = 0.0, b1 = 0.0;
 #pragma unroll 8
     for (int r = 0; r < 32; ++r) {
-        const double yr = ys[h * 32 + r];
+        const double yr = readlane_d(yu, r);
         const double2 l = *reinterpret_cast<const double2*>(Li + (h * 32 + r) * CB + 2 * c2);
         b0 += l.x * yr;
         b1 += l.y * yr;
     }
-    red[h * 128 + 2 * c2] = b0;
-    red[h * 128 + 2 * c2 + 1] = b1;
+    double* red2 = Dt;
+    red2[h * 128 + 2 * c2] = b0;
+    red2[h * 128 + 2 * c2 + 1] = b1;
     __syncthreads();
     if (tid < CB) {
-        const double x = (red[tid] + red[128 + tid]) + (red[256 + tid] + red[384 + tid]);
+        const double x = (red2[tid] + red2[128 + tid]) + (red2[256 + tid] + red2[384 + tid]);
         st_sc1(rX, ((int64_t)j * CB + tid) * 8, x);
         const int64_t g = (int64_t)j * CB + tid;
         if (g < u_c) delta[g] = -x;
