@@ -683,7 +683,6 @@ __global__ __launch_bounds__(LR_THREADS) void k_lin_reduce(
         double* u = Us + t * US;
         if (p >= 0) {
             const double* pp = PP + (p - p0) * PPS;
-            const double I00 = pp[0], I01 = pp[1], I02 = pp[2], I11 = pp[3], I12 = pp[4], I22 = pp[5];
             const double r00 = pp[6], r01 = pp[7], r02 = pp[8], r11 = pp[9], r12 = pp[10], r22 = pp[11];
             {  // the observation's record (OBS_REC): the back-substitution forms T from it and Vinv
                 double2* r = reinterpret_cast<double2*>(WT + (int64_t)o * OBS_REC);
@@ -1030,6 +1029,11 @@ __device__ __forceinline__ void red_images_body(int e, const double* __restrict_
     }
 }
 
+constexpr int BW_SEG = 32;
+__device__ __forceinline__ void border_weights_body(int seg, const double* __restrict__ S, const double* __restrict__ G,
+                                                    double* __restrict__ scal, double* __restrict__ part, int64_t ld,
+                                                    int n_img, int n_loc, int ic, const int8_t* __restrict__ rown);
+
 // camera block (lower) and camera RHS from the chunk partials of the camera, in two fixed-order
 // stages: k_red_cam_seg sums CAM_SEG contiguous segments of the camera's chunk list in parallel
 // (one workgroup each, 4 loads in flight per thread), k_red_cam adds the segment sums in order
@@ -1080,11 +1084,25 @@ __global__ __launch_bounds__(256) void k_red_blocks(const double* __restrict__ p
     }
 }
 
+// workgroups [0, n_cam): one camera each; [n_cam, n_cam + BW_SEG) when bw: the border weights' segments
+// (k_border_weights' work, which needs only the image rows' diagonal: no launch of its own ahead of the
+// solve when nothing adds to S between the two, border_weights_in_accumulate)
+struct BorderW {
+    const double* G;
+    double* scal;
+    double* part;
+    int n_loc, ic;
+};
+
 template <int NK>
-__global__ __launch_bounds__(128) void k_red_cam(const double* __restrict__ cseg, double* __restrict__ S, int64_t ld,
-                                                 int64_t n_pad, int n_img) {
+__global__ __launch_bounds__(256) void k_red_cam(const double* __restrict__ cseg, double* __restrict__ S, int64_t ld,
+                                                 int64_t n_pad, int n_img, int n_cam, BorderW bw) {
     constexpr int CW = 5 + NK, NCAM = LR<NK>::NCAM, NPK = CW * (CW + 1) / 2;
     const int k = blockIdx.x, q = threadIdx.x;
+    if (k >= n_cam) {
+        border_weights_body(k - n_cam, S, bw.G, bw.scal, bw.part, ld, n_img, bw.n_loc, bw.ic, nullptr);
+        return;
+    }
     if (q >= NCAM) return;
     const double* p = cseg + (int64_t)k * CAM_SEG * NCAM + q;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
@@ -1115,18 +1133,17 @@ __global__ __launch_bounds__(128) void k_red_cam(const double* __restrict__ cseg
 // in k_border_combine.  scal: [1] Cholesky failure flag, [2] sumabs, [8..14] W_l, [16..22] D^2.
 // ------------------------------------------------------------------------------------------------
 // k_border_weights: BW_SEG workgroups, each the 14 weight sums over a contiguous range of the 6 n_img
-// EOP rows -> part[seg][14]; the consumer (k_border_rhs) adds the segments in order
-constexpr int BW_SEG = 32;
+// EOP rows -> part[seg][14]; the consumer (k_border_rhs) adds the segments in order (BW_SEG above)
 
 // rown (subtree split, per row): the weight sums over all images (7..13) take only this rank's images'
 // rows -- a wholly-top image's diagonal is complete only after the ranks' sum (k_split_weights adds them)
-__global__ __launch_bounds__(256) void k_border_weights(const double* __restrict__ S, const double* __restrict__ G,
-                                                        double* __restrict__ scal, double* __restrict__ part, int64_t ld,
-                                                        int n_img, int n_loc, int ic, const int8_t* __restrict__ rown) {
+__device__ __forceinline__ void border_weights_body(int seg, const double* __restrict__ S, const double* __restrict__ G,
+                                                    double* __restrict__ scal, double* __restrict__ part, int64_t ld,
+                                                    int n_img, int n_loc, int ic, const int8_t* __restrict__ rown) {
     __shared__ double red[4][14];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int64_t n = 6 * (int64_t)n_img;
-    const int64_t i0 = n * blockIdx.x / BW_SEG, i1 = n * (blockIdx.x + 1) / BW_SEG;
+    const int64_t i0 = n * seg / BW_SEG, i1 = n * (seg + 1) / BW_SEG;
     double a[14];
 #pragma unroll
     for (int m = 0; m < 14; ++m) a[m] = 0.0;
@@ -1152,8 +1169,14 @@ __global__ __launch_bounds__(256) void k_border_weights(const double* __restrict
         if (lane == 0) red[wave][m] = v;
     }
     __syncthreads();
-    if (tid < 14) part[blockIdx.x * 14 + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
-    if (blockIdx.x == 0 && tid == 0) scal[1] = 0.0;  // Cholesky failure flag
+    if (tid < 14) part[seg * 14 + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+    if (seg == 0 && tid == 0) scal[1] = 0.0;  // Cholesky failure flag
+}
+
+__global__ __launch_bounds__(256) void k_border_weights(const double* __restrict__ S, const double* __restrict__ G,
+                                                        double* __restrict__ scal, double* __restrict__ part, int64_t ld,
+                                                        int n_img, int n_loc, int ic, const int8_t* __restrict__ rown) {
+    border_weights_body(blockIdx.x, S, G, scal, part, ld, n_img, n_loc, ic, rown);
 }
 
 // the 14 weights (W_l: 0..6, D^2: 7..13) from the segment sums, into LDS w[14]; every thread calls it
@@ -1581,6 +1604,12 @@ __global__ __launch_bounds__(256) void k_zero_blocks(double* __restrict__ S, int
     }
 }
 
+// the border weights read the image rows' diagonal of S: final at the end of the accumulation when no
+// general tie points (launch_gen_reduce) and no other rank (launch_pack / the split) add to S after it
+bool border_weights_in_accumulate(const Ctx& c) {
+    return c.n_chunks_lr > 0 && c.gen.n_gp == 0 && c.opt.world <= 1 && !c.sched.split;
+}
+
 int launch_accumulate(Ctx& c, bool zeroed) {
     const Layout& L = c.L;
     // the pattern is zeroed by tail workgroups of k_lin_reduce (it does not touch S), unless done already
@@ -1607,7 +1636,10 @@ int launch_accumulate(Ctx& c, bool zeroed) {
             c.d_ppart, c.d_ipart, c.d_cpart, c.d_acc, c.acc, c.d_S, L.ld, c.n_pairs, L.n_pad, L.n_img, L.n_cam, npb, \
             nib, c.d_cseg, c.d_U);                                                                                \
     }                                                                                                             \
-    k_red_cam<NKV><<<(unsigned)L.n_cam, 128, 0, c.stream>>>(c.d_cseg, c.d_S, L.ld, L.n_pad, L.n_img)
+    k_red_cam<NKV><<<(unsigned)(L.n_cam + (bwa ? BW_SEG : 0)), 256, 0, c.stream>>>(c.d_cseg, c.d_S, L.ld, L.n_pad,   \
+                                                                               L.n_img, L.n_cam, bw)
+    const bool bwa = border_weights_in_accumulate(c);
+    const BorderW bw{c.d_G, c.d_scal, c.d_bscr, c.n_loc, c.set.inner_constraints};
     FBA_NK_DISPATCH(L.nk, ACC);
 #undef ACC
 #undef LR_ARGS
@@ -1630,8 +1662,10 @@ int launch_border(Ctx& c) {
     const Layout& L = c.L;
     const int ic = c.set.inner_constraints;
     const int8_t* rown = c.sched.split ? c.d_rown : nullptr;
-    k_border_weights<<<BW_SEG, 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, c.d_bscr, L.ld, L.n_img, c.n_loc, ic, rown);
-    FBA_HIP(hipGetLastError());
+    if (!border_weights_in_accumulate(c)) {
+        k_border_weights<<<BW_SEG, 256, 0, c.stream>>>(c.d_S, c.d_G, c.d_scal, c.d_bscr, L.ld, L.n_img, c.n_loc, ic, rown);
+        FBA_HIP(hipGetLastError());
+    }
     const int nbr = (ic && c.n_loc > 0) ? 6 * c.n_loc : 0;
     k_border_rhs<<<(unsigned)(nbr + (L.n_pad + 255) / 256), 256, 0, c.stream>>>(
         c.d_S, c.d_G, c.d_scal, c.d_bscr, c.d_active, L.ld, L.n_pad, L.u_c, L.n_img, c.n_loc, ic, nbr, c.d_flags,
