@@ -804,8 +804,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
     c->cam_tab_stride = CAM_TAB_HDR + 3 * L.nk;  // header | K_j | rmax^(2j) | rmax^-(2j)
     c->pt_comp = 12 + 6 * L.cw;
     const int npk = L.cw * (L.cw + 1) / 2 + L.cw;
-    c->n_part = (int)std::max<int64_t>(std::max<int64_t>((L.u_full + 255) / 256, (c->n_obs + 255) / 256 * 3),
-                                       c->n_chunks_lr + (L.u_c + 255) / 256) + 8;  // (+ k_backsub's fused update parts)
+    c->n_part = (int)std::max<int64_t>((L.u_full + 255) / 256, (c->n_obs + 255) / 256 * 3) + 8;
     if ((rc = dalloc(&c->d_delta, L.u_full)) || (rc = dalloc(&c->d_xlin, L.u_full)) || (rc = dalloc(&c->d_img_tab, (size_t)L.n_img * IMG_TAB)) ||
         (rc = dalloc(&c->d_cam_tab, (size_t)L.n_cam * c->cam_tab_stride)) ||
         (rc = dalloc(&c->d_G, (size_t)std::max(L.n_img, 1) * 42)) ||

@@ -1258,90 +1258,19 @@ __global__ __launch_bounds__(256) void k_border_rhs(double* __restrict__ S, cons
 // one workgroup per chunk (<= 256 observations of <= 64 whole tie points): thread per observation
 // w_o = W_o' d_e(o) = Jp' P (Je d_e) into LDS (its 96-byte record, OBS_REC, coalesced across the wave),
 // then thread per point d_p = -(vb + Vinv sum_o w_o + Tc' d_cam), its observations summed in order
-// a workgroup's 256 values summed in a fixed order (xor butterfly per wave, then the four wave sums in
-// order); every thread calls it, thread 0 returns the sum
-__device__ __forceinline__ double block_sum256(double a, double* red) {
-#pragma unroll
-    for (int w = 32; w > 0; w >>= 1) a += __shfl_xor(a, w, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
-    __syncthreads();
-    return (red[0] + red[1]) + (red[2] + red[3]);
-}
-
-// element i of the update (i < u_full): de-scaled delta_i, xhat_i += it (unless a hand-off aborted), and
-// its |delta_i| share of deltasum (NaN for a non-finite delta)
-__device__ __forceinline__ double update_elem(int64_t i, double* __restrict__ xfull, double* __restrict__ delta,
-                                              const double* __restrict__ cam_tab, const uint8_t* __restrict__ counted,
-                                              int n_img, int n_cam, int nk, int cw, int cam_stride, bool apply) {
-    double d = delta[i], a = 0.0;
-    const int64_t cb = 6 * (int64_t)n_img;
-    if (i >= cb && i < cb + (int64_t)n_cam * cw) {
-        const int64_t k = (i - cb) / cw;
-        const int c = (int)((i - cb) % cw);
-        const double* ct = cam_tab + k * cam_stride;
-        if (c >= 3 && c < 3 + nk) d = d / ct[CAM_TAB_HDR + nk + (c - 3)];  // K_j / rmax^(2j)
-        else if (c >= 3 + nk) d = d / ct[6];                               // P / rmax^2
-    }
-    delta[i] = d;
-    if (apply) xfull[i] += d;
-    if (counted[i]) a = fabs(d);
-    if (!isfinite(d)) a = __builtin_nan("");
-    return a;
-}
-
-// Fused update (up.X != nullptr, update_in_backsub): the image / camera corrections are read as -X (the
-// backward solve's x; delta = -x there) and workgroups [n_chunks, ..) apply k_update's element work to
-// the u_c range (de-scaling delta in place), while each chunk workgroup adds its tie points' corrections
-// to xhat; every workgroup's share of deltasum goes to up.part[blockIdx.x] (k_sum_parts adds them)
-struct UpdArgs {
-    const double* X;
-    double* xfull;
-    const double* cam_tab;
-    const uint8_t* counted;
-    double* part;
-    const double* scal;
-    int n_chunks, n_cam, nk, cw, cam_stride;
-};
-
 template <int NK>
 __global__ __launch_bounds__(256) void k_backsub(const double* __restrict__ WT, const double* __restrict__ PT,
                                                  const int32_t* __restrict__ chunk_obs, const int32_t* __restrict__ chunk_pt,
                                                  const int32_t* __restrict__ lp_start, const int32_t* __restrict__ lp_tie,
                                                  const int32_t* __restrict__ lp_cam, const int32_t* __restrict__ img,
                                                  double* __restrict__ delta, int64_t u_c, int n_img, unsigned eop_mask,
-                                                 double px, double py, const UpdArgs up) {
+                                                 double px, double py) {
     using LY = Lay<NK>;
     constexpr int CW = LY::CW, PS = LY::PS;
     __shared__ double u[CHUNK_OBS][3];
-    __shared__ double red[4];
     const int c = blockIdx.x, t = threadIdx.x;
-    const bool fused = up.X != nullptr;
-    if (fused && c >= up.n_chunks) {  // the update of the u_c range (uniform)
-        const int64_t i = (int64_t)(c - up.n_chunks) * 256 + t;
-        const bool apply = !(up.scal[1] < 0.0);
-        const double a = i < u_c ? update_elem(i, up.xfull, delta, up.cam_tab, up.counted, n_img, up.n_cam, up.nk, up.cw,
-                                               up.cam_stride, apply)
-                                 : 0.0;
-        const double s = block_sum256(a, red);
-        if (t == 0) up.part[c] = s;
-        return;
-    }
     const int p0 = chunk_pt[c], p1 = chunk_pt[c + 1];
-    if (p1 == p0) {  // control chunk (uniform)
-        if (fused && t == 0) up.part[c] = 0.0;
-        return;
-    }
-    // the raw image / camera corrections: delta, or -X while the fused update de-scales delta meanwhile
-    const double* dsrc = fused ? up.X : delta;
-    const double dsg = fused ? -1.0 : 1.0;
-    // (fused: the point's xhat entries and counted flags loaded now, their latency behind the observations)
-    const int p = p0 + t;
-    const int64_t ip = p < p1 ? u_c + 3 * (int64_t)lp_tie[p] : 0;
-    double xf[3] = {0.0, 0.0, 0.0};
-    bool cn[3] = {false, false, false};
-    if (fused && p < p1)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) { xf[k] = up.xfull[ip + k]; cn[k] = up.counted[ip + k] != 0; }
+    if (p1 == p0) return;  // control chunk (uniform)
     const int o0 = chunk_obs[c], o = o0 + t;
     if (o < chunk_obs[c + 1]) {
         const double2* R = reinterpret_cast<const double2*>(WT + (int64_t)o * OBS_REC);
@@ -1349,13 +1278,13 @@ __global__ __launch_bounds__(256) void k_backsub(const double* __restrict__ WT, 
 #pragma unroll
         for (int k = 0; k < OBS_REC / 2; ++k) rv[k] = R[k];
         const double* r = reinterpret_cast<const double*>(rv);
-        const double* de = dsrc + 6 * (int64_t)img[o];
+        const double* de = delta + 6 * (int64_t)img[o];
         double j0[6], j1[6];
         obs_rec_rows(r, eop_mask, j0, j1);
         double e0 = 0.0, e1 = 0.0;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
-            const double e = dsg * de[a];
+            const double e = de[a];
             e0 += j0[a] * e;
             e1 += j1[a] * e;
         }
@@ -1366,7 +1295,7 @@ __global__ __launch_bounds__(256) void k_backsub(const double* __restrict__ WT, 
         u[t][2] = r[2] * e0 + r[5] * e1;
     }
     __syncthreads();
-    double a = 0.0;
+    const int p = p0 + t;
     if (p < p1) {
         const double* P = PT + (int64_t)p * PS;
         double w0 = 0.0, w1 = 0.0, w2 = 0.0;
@@ -1374,29 +1303,14 @@ __global__ __launch_bounds__(256) void k_backsub(const double* __restrict__ WT, 
         double d0 = P[6] + (P[0] * w0 + P[1] * w1 + P[2] * w2);
         double d1 = P[7] + (P[1] * w0 + P[3] * w1 + P[4] * w2);
         double d2 = P[8] + (P[2] * w0 + P[4] * w1 + P[5] * w2);
-        const double* dk = dsrc + 6 * (int64_t)n_img + (int64_t)lp_cam[p] * CW;
+        const double* dk = delta + 6 * (int64_t)n_img + (int64_t)lp_cam[p] * CW;
         const double* Tc = P + 12 + 3 * CW;
 #pragma unroll
         for (int k = 0; k < CW; ++k) {
-            const double e = dsg * dk[k];
-            d0 += Tc[3 * k] * e; d1 += Tc[3 * k + 1] * e; d2 += Tc[3 * k + 2] * e;
+            d0 += Tc[3 * k] * dk[k]; d1 += Tc[3 * k + 1] * dk[k]; d2 += Tc[3 * k + 2] * dk[k];
         }
-        double* out = delta + ip;
+        double* out = delta + u_c + 3 * (int64_t)lp_tie[p];
         out[0] = -d0; out[1] = -d1; out[2] = -d2;
-        if (fused) {  // k_update's work on the point's three corrections (no de-scaling for tie points)
-            const bool apply = !(up.scal[1] < 0.0);
-            const double dd[3] = {-d0, -d1, -d2};
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                if (apply) up.xfull[ip + k] = xf[k] + dd[k];
-                if (cn[k]) a += fabs(dd[k]);
-            }
-            if (!(isfinite(d0) && isfinite(d1) && isfinite(d2))) a = __builtin_nan("");
-        }
-    }
-    if (fused) {
-        const double s = block_sum256(a, red);
-        if (t == 0) up.part[c] = s;
     }
 }
 
@@ -1417,6 +1331,16 @@ __global__ __launch_bounds__(256) void k_obs_T(const double* __restrict__ WT, co
 // ------------------------------------------------------------------------------------------------
 // (scal[1] < 0: a hand-off of the factorisation or backward solve timed out, fba_chol.hip -- delta is not
 // a solution, xhat stays as it was and the host reports FBA_ERR_HIP)
+// a workgroup's 256 values summed in a fixed order (xor butterfly per wave, then the four wave sums in
+// order); every thread calls it, thread 0 returns the sum
+__device__ __forceinline__ double block_sum256(double a, double* red) {
+#pragma unroll
+    for (int w = 32; w > 0; w >>= 1) a += __shfl_xor(a, w, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+    __syncthreads();
+    return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 __global__ __launch_bounds__(256) void k_update(double* __restrict__ xfull, double* __restrict__ delta,
                                                 const double* __restrict__ cam_tab, const uint8_t* __restrict__ counted,
                                                 double* __restrict__ part, int64_t u_full, int n_img, int n_cam, int nk,
@@ -1424,7 +1348,22 @@ __global__ __launch_bounds__(256) void k_update(double* __restrict__ xfull, doub
     __shared__ double red[4];
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool apply = !(scal[1] < 0.0);
-    const double a = i < u_full ? update_elem(i, xfull, delta, cam_tab, counted, n_img, n_cam, nk, cw, cam_stride, apply) : 0.0;
+    double a = 0.0;
+    if (i < u_full) {
+        double d = delta[i];
+        const int64_t cb = 6 * (int64_t)n_img;
+        if (i >= cb && i < cb + (int64_t)n_cam * cw) {
+            const int64_t k = (i - cb) / cw;
+            const int c = (int)((i - cb) % cw);
+            const double* ct = cam_tab + k * cam_stride;
+            if (c >= 3 && c < 3 + nk) d = d / ct[CAM_TAB_HDR + nk + (c - 3)];  // K_j / rmax^(2j)
+            else if (c >= 3 + nk) d = d / ct[6];                               // P / rmax^2
+        }
+        delta[i] = d;
+        if (apply) xfull[i] += d;
+        if (counted[i]) a = fabs(d);
+        if (!isfinite(d)) a = __builtin_nan("");
+    }
     const double s = block_sum256(a, red);
     if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
@@ -1433,9 +1372,16 @@ __global__ __launch_bounds__(256) void k_update(double* __restrict__ xfull, doub
 __global__ void k_sum_parts(const double* __restrict__ part, int n, double* __restrict__ scal, double* __restrict__ host) {
     __shared__ double red[4];
     double a = 0.0;
-    // each thread sums a contiguous range (fixed order), then block_sum256's fixed order
-    const int per = (n + 255) / 256;
-    for (int i = threadIdx.x * per; i < min(n, (threadIdx.x + 1) * per); ++i) a += part[i];
+    // thread t sums parts t, t + 256, ... in order (coalesced, 16 loads in flight), then block_sum256's
+    // fixed order
+    for (int i0 = threadIdx.x; i0 < n; i0 += 16 * 256) {
+        double x[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = i0 + 256 * k < n ? part[i0 + 256 * k] : 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (i0 + 256 * k < n) a += x[k];
+    }
     const double sum = block_sum256(a, red);
     if (threadIdx.x == 0) {
         scal[2] = sum;
@@ -1671,11 +1617,6 @@ bool border_weights_in_accumulate(const Ctx& c) {
     return c.n_chunks_lr > 0 && c.gen.n_gp == 0 && c.opt.world <= 1 && !c.sched.split;
 }
 
-// k_update's work inside k_backsub (UpdArgs): every tie point a regular one of this rank's chunks
-bool update_in_backsub(const Ctx& c) {
-    return border_weights_in_accumulate(c) && c.n_lp > 0 && c.n_lp == c.L.n_tie;
-}
-
 int launch_accumulate(Ctx& c, bool zeroed) {
     const Layout& L = c.L;
     // the pattern is zeroed by tail workgroups of k_lin_reduce (it does not touch S), unless done already
@@ -1744,29 +1685,20 @@ int launch_backsub_update(Ctx& c) {
     const Layout& L = c.L;
     int rc;
     if ((rc = launch_gen_backsub(c))) return rc;
-    // the update inside k_backsub's launch when its chunks hold every tie point (no general points, one
-    // rank, no split): one launch fewer per iteration
-    const bool fuse = update_in_backsub(c);
-    const int nbu = (int)((L.u_c + 255) / 256);
     if (c.n_lp > 0) {
-        const UpdArgs up{fuse ? c.d_X : nullptr, c.d_xfull, c.d_cam_tab, c.d_counted, c.d_part, c.d_scal,
-                         (int)c.n_chunks_lr, L.n_cam, L.nk, L.cw, c.cam_tab_stride};
 #define BS(NKV)                                                                                                    \
-    k_backsub<NKV><<<(unsigned)(c.n_chunks_lr + (fuse ? nbu : 0)), 256, 0, c.stream>>>(                            \
-        c.d_WT, c.d_pt_tab, c.d_chunk_obs, c.d_chunk_pt, c.d_lp_start, c.d_lp_tie, c.d_lp_cam, c.d_img, c.d_delta,  \
-        L.u_c, L.n_img, eop_mask(c.set), px_of(c), py_of(c), up)
+    k_backsub<NKV><<<(unsigned)c.n_chunks_lr, 256, 0, c.stream>>>(c.d_WT, c.d_pt_tab, c.d_chunk_obs, c.d_chunk_pt,    \
+                                                              c.d_lp_start, c.d_lp_tie, c.d_lp_cam, c.d_img, c.d_delta, \
+                                                              L.u_c, L.n_img, eop_mask(c.set), px_of(c), py_of(c))
         FBA_NK_DISPATCH(L.nk, BS);
 #undef BS
         FBA_HIP(hipGetLastError());
     }
-    int nblk = (int)(c.n_chunks_lr + nbu);
-    if (!fuse) {
-        nblk = (int)((L.u_full + 255) / 256);
-        // (forming deltasum in k_update's last-arriving workgroup measured slower: 612 agent-scope atomics)
-        k_update<<<nblk, 256, 0, c.stream>>>(c.d_xfull, c.d_delta, c.d_cam_tab, c.d_counted, c.d_part, L.u_full,
-                                             L.n_img, L.n_cam, L.nk, L.cw, c.cam_tab_stride, c.d_scal);
-        FBA_HIP(hipGetLastError());
-    }
+    const int nblk = (int)((L.u_full + 255) / 256);
+    // (forming deltasum in k_update's last-arriving workgroup measured slower: 612 agent-scope atomics)
+    k_update<<<nblk, 256, 0, c.stream>>>(c.d_xfull, c.d_delta, c.d_cam_tab, c.d_counted, c.d_part, L.u_full,
+                                         L.n_img, L.n_cam, L.nk, L.cw, c.cam_tab_stride, c.d_scal);
+    FBA_HIP(hipGetLastError());
     k_sum_parts<<<1, 256, 0, c.stream>>>(c.d_part, nblk, c.d_scal, c.d_hpinned);
     FBA_HIP(hipGetLastError());
     return FBA_OK;
