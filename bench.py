@@ -53,19 +53,41 @@ def phase_roofline(ds, ms_phase, n_steps):
     return t, chol_flops, lin_bytes
 
 
-def pmc_traffic(config, kernel, network="grid"):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this workload
-    (profiles/*pmc_config<N>.json, made by scripts/pmc_summary.py: FETCH_SIZE x2 per the gfx950
-    correction + WRITE_SIZE), or None."""
+def build_id():
+    """The identity of the library build this tree runs: a hash of libfba's sources (the HIP kernels, the
+    host C++, the public header and the Makefile).  scripts/pmc_summary.py stamps it into every PMC
+    summary, so the bench line takes counter data only from a summary of the very build it measured."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "fish-eye_bundle_adjustment_amd", "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.cpp")) +
+                   glob.glob(os.path.join(csrc, "*.h")) + [os.path.join(csrc, "Makefile"),
+                                                           os.path.join(ROOT, "include", "fba.h")])
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_summary(config, kernel, network="grid"):
+    """The committed rocprofv3 PMC summary of this workload AND this build (profiles/*pmc_config<N>.json
+    written by scripts/pmc_summary.py, whose build_id equals build_id()): (file name, the kernel's entry),
+    or (None, None) when no summary of this build exists -- then the line carries no counter data rather
+    than an older build's."""
     import glob
     tag = f"{config}" + ("" if network == "grid" else f"_{network}")
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_config{tag}.json")), reverse=True):
+    bid = build_id()
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_config{tag}.json"))):
         with open(f) as fh:
             d = json.load(fh)
+        if d.get("build_id") != bid or d.get("network", "grid") != network:
+            continue
         k = d.get("kernels", {}).get(kernel)
         if k:
-            return k["hbm_bytes_per_launch"]
-    return None
+            return os.path.relpath(f, ROOT), k
+    return None, None
 
 
 def cpu_baseline(folder, seconds):
@@ -200,13 +222,18 @@ def main():
         ctx.set_probe(0)
         avg_s = pr["ms"] * 1e-3 / max(pr["launches"], 1)
         flops_launch = pr["flops"] / max(pr["launches"], 1)
+        # the committed PMC summaries are single-context launches of one build: a subtree-split launch
+        # (flow A / B, a fraction of the records) or a build without a summary gets none
+        src, pm = (None, None) if ctx.split else pmc_summary(args.config, name, args.network)
         r = {"bound": "mfma", "kernel": f"{name} ({note})",
              "achieved": flops_launch / avg_s / 1e12 if avg_s > 0 else None, "peak": FP64_PEAK_TFLOPS,
              "unit": "TFLOP/s", "launches": pr["launches"], "avg_launch_us": avg_s * 1e6,
              "flops_per_launch": flops_launch,
-             # the committed PMC summaries are single-context launches: a subtree-split launch (flow A / B,
-             # a fraction of the records) has none
-             "traffic": None if ctx.split else pmc_traffic(args.config, name, args.network)}
+             "traffic": pm["hbm_bytes_per_launch"] if pm else None,
+             "mfma_busy": pm.get("mfma_busy_frac") if pm else None,
+             "pmc_summary": src, "build_id": build_id()}
+        if pm and pm.get("avg_launch_us"):
+            r["traffic_GBs"] = pm["hbm_bytes_per_launch"] / (pm["avg_launch_us"] * 1e-6) / 1e9
         r["frac"] = r["achieved"] / r["peak"] if r["achieved"] else None
         return r
     flow = os.environ.get("FBA_CHOL_FLOW", "1") != "0"

@@ -752,7 +752,7 @@ static int create(const fba_problem* p, const fba_settings* s, const fba_options
         c->red_diag = n;
         c->red_gblk = c->red_diag + c->n_topdiag;
         c->red_w = c->red_gblk + 256 * ng;
-        c->n_red = c->red_w + 8;
+        c->n_red = c->red_w + 9;  // 7 weight sums, the abort flag, the pivot-failure row
     }
     // which full-space entries are estimated / owned / counted
     std::vector<uint8_t> active(L.n_pad, 0), counted(L.u_full, 0);
@@ -993,11 +993,11 @@ static int solve_enqueue(Ctx* c) {
         set_error("one fba_solve_update per fba_accumulate (the solve factors the accumulated system in place)");
         return FBA_ERR_ARG;
     }
+    // marked before the launches: a solve that fails part way may already have factored S in place, so a
+    // retry must accumulate again too (accumulate() clears the mark)
+    c->solved = true;
     const int rc = run_graph(c, 1, [&] { return solve_body(c); });
-    if (rc == FBA_OK) {
-        ++c->solves_enqueued;  // k_sum_parts' count once this solve is done
-        c->solved = true;
-    }
+    if (rc == FBA_OK) ++c->solves_enqueued;  // k_sum_parts' count once this solve is done
     return rc;
 }
 
@@ -1211,7 +1211,7 @@ int fba_abi_version(void) { return FBA_ABI_VERSION; }
 int fba_set_spin_bound(fba_ctx* ctx, int64_t spins) {
     if (!ctx || spins < 0) { set_error("fba_set_spin_bound: bad argument"); return FBA_ERR_ARG; }
     Ctx* c = reinterpret_cast<Ctx*>(ctx);
-    const double v = spins > 0 ? (double)spins : (double)(1u << 22);
+    const double v = spin_bound_value(spins);
     FBA_HIP(hipStreamSynchronize(c->stream));
     FBA_HIP(hipMemcpy(c->d_scal + SCAL_SPINS, &v, sizeof v, hipMemcpyHostToDevice));
     return FBA_OK;

@@ -3135,10 +3135,10 @@ int chol_setup(Ctx& c) {
     FBA_HIP(hipFuncSetAttribute((const void*)k_trtri128, hipFuncAttributeMaxDynamicSharedMemorySize, (int)TRTRI_LDS));
 
     // FBA_FLAG_SPINS (tests): the bound of every hand-off poll of THIS context (scal[SCAL_SPINS], read
-    // by spin_expired), taken when the context is created; unset: the default 1 << 22
+    // by spin_expired), taken when the context is created; unset or <= 0: the default 1 << 22
     {
         const char* fs = getenv("FBA_FLAG_SPINS");
-        const double v = fs ? (double)std::max(1L, atol(fs)) : (double)(1u << 22);
+        const double v = spin_bound_value(fs ? atoll(fs) : 0);
         FBA_HIP(hipMemcpy(c.d_scal + SCAL_SPINS, &v, sizeof v, hipMemcpyHostToDevice));
     }
     c.probe_ev.assign(2 * std::max(c.sched.n_waves, 1), nullptr);

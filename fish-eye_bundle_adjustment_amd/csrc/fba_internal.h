@@ -26,6 +26,11 @@ constexpr int FLOW_CSPLIT = 3;
 // arithmetic produces): the consumers poll the data itself, k_border_rhs resets it every solve
 constexpr uint64_t X_SENTINEL = 0x7FF4DEADBEEF5A5Aull;
 constexpr int SCAL_SPINS = 6;  // d_scal slot: this context's hand-off poll bound (fba_chol.hip spin_expired)
+// the value stored there for a requested bound: <= 0 means the default 1 << 22 (~0.3 s), and a bound is
+// clamped to 2^32 - 1 (spin_expired compares it with a 32-bit counter)
+inline double spin_bound_value(long long spins) {
+    return spins <= 0 ? (double)(1u << 22) : (double)(spins < 0xffffffffLL ? spins : 0xffffffffLL);
+}
 constexpr int CHUNK_OBS = 256;  // observations per k_lin_reduce / k_lin_point workgroup (chunk)
 // tie points per chunk and co-visibility terms per chunk staged in LDS (a single larger point's are
 // read from HBM instead): smaller for nK >= 6, whose wider Jacobian rows leave less of the 160 KiB LDS

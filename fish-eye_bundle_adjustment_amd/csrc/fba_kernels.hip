@@ -1766,6 +1766,8 @@ __global__ void k_pack(double* __restrict__ S, int64_t ld, double* __restrict__ 
 //   [this rank's 7 inner-constraint weight sums over its subtree rows (k_border_weights' segments)]
 //   [1: this rank's flow A aborted (a hand-off timed out, scal[1] < 0): its top-block contributions are
 //    incomplete; after the sum every rank sees it, raises the abort ahead of flow B and fails the step]
+//   [1: this rank's flow A met a non-positive pivot (scal[1] = row + 1 > 0): after the sum every rank reports
+//    it, so the ranks agree that the step failed]
 // dir 0: S (+ gblk, weight segments) -> buffer; dir 1: buffer -> S top blocks, gblk.  (The diagonal part
 // is written by k_pack_topdiag ahead of the subtree flow.)
 __global__ __launch_bounds__(256) void k_pack_split(double* __restrict__ S, int64_t ld, double* __restrict__ red,
@@ -1805,8 +1807,18 @@ __global__ __launch_bounds__(256) void k_pack_split(double* __restrict__ S, int6
         }
         if (threadIdx.x == 7) {
             // (flow A has finished: k_pack_split follows it on the stream, so scal[1] is final here)
-            if (dir == 0) red[red_w + 7] = scal[1] < 0.0 ? 1.0 : 0.0;
-            else if (red[red_w + 7] != 0.0) scal[1] = -1.0;  // some rank's flow A aborted: skip flow B, k_update
+            const double f = scal[1];
+            if (dir == 0) {
+                red[red_w + 7] = f < 0.0 ? 1.0 : 0.0;  // a hand-off timed out
+                red[red_w + 8] = f > 0.0 ? f : 0.0;    // a non-positive pivot at row f - 1 of this rank's subtree
+            } else if (red[red_w + 7] != 0.0) {
+                scal[1] = -1.0;  // some rank's flow A aborted: skip flow B, k_update
+            } else if (red[red_w + 8] != 0.0 && f == 0.0) {
+                // some rank's flow A hit a non-positive pivot: every rank reports it (FBA_ERR_NOT_SPD), as the
+                // failing rank does, instead of solving on top blocks that hold its bad Schur updates
+                // (the row is the failing rank's, or the sum of the rows when several ranks failed)
+                scal[1] = red[red_w + 8];
+            }
         }
     }
 }

@@ -101,10 +101,13 @@ def parse_settings(cfg_rows, folder):
         s["Meas_std_y"] = float(vy) if oky else float(v)  # main.m:397-402
         s["no_std_y"] = 0 if oky else 1                     # main.m:129 (the .out settings list)
     else:
-        # main.m:125-127 sets sigma = 1 (the reference then trips over rmfield at main.m:399)
+        # main.m:125-127 sets sigma = 1 and no_std_y = 1 without a Meas_std_y field, so the reference then
+        # fails in rmfield at main.m:399 (the reference text run on such a .cfg: tests/golden/
+        # ref_cam0_nostd.json); load_folder raises that failure once the joins before it are done
         s["Meas_std"] = 1.0
         s["Meas_std_y"] = 1.0
         s["no_std_y"] = 1
+        s["_no_meas_std"] = True
     v, ok = find_setting(cfg_rows, "Type")
     s["type"] = v if ok else "fisheye"
     v, ok = find_setting(cfg_rows, "Check_Points", True)
@@ -250,6 +253,10 @@ def load_folder(folder, project_dir=None):
         raise IngestError("EXT must list exactly the images measured in .pho, in unknown order (Buildxhat.m:22)")
     if n and (cam.max() >= numCam):
         raise IngestError("INT must list exactly the cameras used, in order (Buildxhat.m:65)")
+    if s.pop("_no_meas_std", False):
+        # main.m:397-399: no_std_y is set but the Meas_std_y field was never created -> rmfield fails
+        raise IngestError("no Meas_std in the .cfg: the reference fails at main.m:399 "
+                          "(rmfield of the absent Meas_std_y field)")
     return Dataset(folder=folder, settings=s, pho_target=[r[0] for r in pho], pho_image=[r[1] for r in pho],
                    xy=xy, img=img, cam=cam, tie=tie, xyz_fixed=xyz, EXT=EXT, INT=INT, TIE=TIE, CNT=CNT,
                    numImg=numImg, numCam=numCam, numGCP=len(cnt_used), CZE=CZE)

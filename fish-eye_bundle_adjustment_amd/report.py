@@ -19,6 +19,7 @@ LINE = "*" * 109  # main.m:635
 DECIMALS = 5      # main.m:686
 PADDING = 4       # main.m:634
 VERSION = "fba_amd 1 (MI355X HIP path)"
+PRODUCER = "fba_amd, the MI355X-native HIP implementation (not the MATLAB reference)"
 
 
 def num2str(x, prec=None):
@@ -106,7 +107,10 @@ def write_out(path, data, res, seconds, version=VERSION, date=None):
     n = data.n
     with open(path, "w") as fh:
         fh.write("Version: " + version)
-        fh.write("Fish-eye model Bundle Adjustment\nWynand Tredoux -- University of Calgary -- 2020\n\n")
+        # main.m:637's title and author line, with this build named as the producer of the numbers below
+        # (the model and the report layout are the reference's; the line count is unchanged)
+        fh.write("Fish-eye model Bundle Adjustment\nResults produced by " + PRODUCER + "; model and report format: "
+                 "Wynand Tredoux -- University of Calgary -- 2020\n\n")
         fh.write(LINE)
         fh.write(f"\n\nExecution date:\t{date}\nTime Taken:\t\t{num2str(seconds)} seconds\nIterations:\t\t"
                  f"{res.iterations}\nModel Used:\t\t{s['type']}")

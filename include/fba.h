@@ -163,7 +163,10 @@ int fba_build_awg(fba_ctx* ctx, const double* xhat, double* A, double* w, double
  *   fba_accumulate      linearise this rank's observations at the device xhat and accumulate the
  *                       (point-reduced) normal equations into the reduce buffer;
  *   fba_reduce_buffer   device pointer + length (doubles) of that buffer: ranks sum it elementwise
- *                       (e.g. an RCCL all-reduce) between the two calls;
+ *                       (e.g. an RCCL all-reduce) between the two calls.  With world == 1 there is
+ *                       nothing to sum and the buffer IS the context's reduced system; the solve
+ *                       reads weights fba_accumulate already derived from it, so the caller must not
+ *                       modify it between fba_accumulate and fba_solve_update (reading is fine);
  *   fba_solve_update    bordered solve, point back-substitution, de-scaling, xhat update.
  *                       *deltasum_part receives this rank's share of sumabs(delta) (sum over ranks
  *                       = the reference's deltasum).
@@ -229,14 +232,16 @@ int fba_set_timing(fba_ctx* ctx, int32_t enabled);
 int fba_set_probe(fba_ctx* ctx, int32_t enabled);
 int fba_probe_stats(fba_ctx* ctx, double* out /*[4]*/);
 
+/* (tests) The bound of every device hand-off poll of this context, in sleeps (0: the default
+ * 1 << 22, ~0.3 s; negative: FBA_ERR_ARG; values above 2^32 - 1 are clamped to it; FBA_FLAG_SPINS in
+ * the environment sets it at fba_create, where <= 0 is the default): a low bound forces the timeout path -- the abort
+ * reaches every wait, the step returns FBA_ERR_HIP and xhat stays as before it. */
+int fba_set_spin_bound(fba_ctx* ctx, int64_t spins);
+
 /* Test hook (no reference counterpart): the 14x14 bordered solve of the inner-constraint combine
  * (k_border_combine, one workgroup on `device`) for a given symmetric 15x15 Gram matrix of the
  * forward-solved rows [y | A (7) | B (7)] (row-major): coef = [z; k] solving
  * [[A'A - I, A'B], [B'A, B'B]] [z; k] = -[A'y; B'y]. */
-/* (tests) The bound of every device hand-off poll of this context, in sleeps (0: the default 1 << 22,
- * ~0.3 s; FBA_FLAG_SPINS in the environment sets it at fba_create): a low bound forces the timeout
- * path -- the abort reaches every wait, the step returns FBA_ERR_HIP and xhat stays as before it. */
-int fba_set_spin_bound(fba_ctx* ctx, int64_t spins);
 int fba_test_border_solve(int32_t device, const double* gram /*[225]*/, double* coef /*[14]*/);
 
 #ifdef __cplusplus

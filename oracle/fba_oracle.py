@@ -129,9 +129,10 @@ def load_folder(folder):
         s["Meas_std"] = v
         vy, oky = find_setting(cfg, "Meas_std_y")
         s["Meas_std_y"] = vy if oky else v
-    else:  # the reference then fails in rmfield (main.m:399); sigma = 1 is the documented intent
+    else:  # main.m:125-127; the reference then fails in rmfield (main.m:399), raised after the joins
         s["Meas_std"] = 1.0
         s["Meas_std_y"] = 1.0
+        s["_no_meas_std"] = True
     v, ok = find_setting(cfg, "Type")  # main.m:133-137
     s["type"] = v if ok else "fisheye"
     v, ok = find_setting(cfg, "Check_Points", True)
@@ -237,6 +238,9 @@ def load_folder(folder):
         cnt_used.add(k)
         xyz[i] = CNT[k][1:4]
         tie_index[i] = tie_pos.get(r[0], -1)
+    if s.pop("_no_meas_std", False):
+        raise ValueError("no Meas_std in the .cfg: the reference fails at main.m:399 (rmfield of the absent "
+                         "Meas_std_y field)")
     data = Data(
         settings=s, x=x, y=y, target=[r[0] for r in pho], image=[r[1] for r in pho],
         ext_index=ext_index, cam_num=cam_num, tie_index=tie_index, eop_fixed=eop,

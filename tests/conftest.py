@@ -29,7 +29,7 @@ def oracle():
 
 
 def variant_folder(tmp_root, name, cfg_edits, src=CAM0):
-    """Copy cam0 with edited .cfg keys (value strings as in the .cfg)."""
+    """Copy cam0 with edited .cfg keys (value strings as in the .cfg; None removes the key's line)."""
     dst = os.path.join(tmp_root, name)
     os.makedirs(dst, exist_ok=True)
     for f in os.listdir(src):
@@ -40,12 +40,13 @@ def variant_folder(tmp_root, name, cfg_edits, src=CAM0):
     for ln in lines:
         toks = ln.split("#", 1)[0].split()
         if toks and toks[0] in cfg_edits:
-            out.append(f"{toks[0]}\t{cfg_edits[toks[0]]}")
+            if cfg_edits[toks[0]] is not None:
+                out.append(f"{toks[0]}\t{cfg_edits[toks[0]]}")
             seen.add(toks[0])
         else:
             out.append(ln)
     for k, v in cfg_edits.items():
-        if k not in seen:
+        if k not in seen and v is not None:
             out.append(f"{k}\t{v}")
     with open(os.path.join(dst, "config.cfg"), "w") as fh:
         fh.write("\n".join(out) + "\n")

@@ -92,9 +92,29 @@ def extract(env, awg):
         dof=float(data.elems[0]["n"] - len(names)))
 
 
+def run_nostd(ref_root, root):
+    """cam0 with no Meas_std line in its .cfg: what the reference text does (main.m:123-127 sets
+    Meas_std = 1 and no_std_y = 1, then main.m:397-399 calls rmfield on the absent Meas_std_y).  Writes
+    ref_cam0_nostd.json: the interpreter's error and the main.m line it was raised at."""
+    import json
+    folder = variant_folder(root, "nostd", {"Meas_std": None, "Meas_std_y": None})
+    try:
+        run_reference(ref_root, folder)
+        out = {"error": None}
+    except mlang.MatlabError as e:
+        out = {"error": str(e)}
+    out["cfg_edit"] = "cam0 config.cfg without its Meas_std (and Meas_std_y) line"
+    with open(os.path.join(HERE, "ref_cam0_nostd.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    print("nostd:", out["error"], flush=True)
+
+
 def main(ref_root):
     root = tempfile.mkdtemp()
-    only = sys.argv[2:] or sorted(CAM0_VARIANTS)
+    only = sys.argv[2:] or sorted(CAM0_VARIANTS) + ["nostd"]
+    if "nostd" in only:
+        run_nostd(ref_root, root)
+        only = [n for n in only if n != "nostd"]
     for name in only:
         folder = variant_folder(root, name, CAM0_VARIANTS[name])
         t0 = time.time()

@@ -476,6 +476,55 @@ def test_subtree_split_abort_reaches_every_rank(fba, scenes):
             c.close()
 
 
+def test_subtree_split_pivot_failure_reaches_every_rank(fba, scenes):
+    """Subtree split (config 3, two rank contexts on one GPU): a non-positive pivot inside rank 0's flow A
+    (rank 0's image EOPs set to NaN, so its subtree blocks are NaN: the potrf's `d > 0` test fails) is
+    reported through the reduce buffer (the pivot-failure slot after the abort flag), so EVERY rank
+    returns FBA_ERR_NOT_SPD for that step -- the ranks agree that it failed.  With xhat restored, the next
+    passes of both ranks reassemble the single context's iterates."""
+    import ctypes
+    folder = _scene(3, scenes)
+    ds = fba.load_folder(folder)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    mk = lambda **kw: fba.capi.Context(ds.pack(), fba.capi.make_settings(ds.settings), **kw)  # noqa: E731
+    single = mk()
+    ranks = [mk(rank=r, world=2, split=True) for r in range(2)]
+    try:
+        assert all(c.split for c in ranks)
+        x0 = [c.get_xhat() for c in ranks]
+        bad = x0[0].copy()
+        bad[:6 * ds.numImg] = np.nan
+        ranks[0].set_xhat(bad)
+        for c in ranks:
+            c.accumulate()
+            c.synchronize()
+        _sum_buffers(hip, ranks)
+        for c in ranks:
+            with pytest.raises(fba.capi.FBAError) as ei:
+                c.solve_update()
+            assert ei.value.code == 4 and "not positive definite" in str(ei.value), ei.value
+        for c, x in zip(ranks, x0):
+            c.set_xhat(x)
+        for _ in range(2):
+            d1 = single.step()
+            for c in ranks:
+                c.accumulate()
+                c.synchronize()
+            _sum_buffers(hip, ranks)
+            parts = [c.solve_update() for c in ranks]
+            assert abs(sum(parts) - d1) <= 1e-9 * d1
+        xr = sum(c.get_xhat(owned_only=True) for c in ranks)
+        dsc = dist_scaling_of(__import__("fba_oracle").load_folder(folder))
+        names = fba.xhat_names(ds)
+        err = elem_rel_err(xr, single.get_xhat(), names, dsc)
+        assert max(err.values()) <= 1e-9, err
+    finally:
+        single.close()
+        for c in ranks:
+            c.close()
+
+
 def test_subtree_split_guards(fba, scenes, tmp_path, monkeypatch):
     """The split's contract at its edges: one solve per accumulation (a second fba_solve_update of the same
     accumulation is refused with FBA_ERR_ARG instead of running flow B on spent tickets); the per-level

@@ -111,6 +111,24 @@ def test_missing_setting_is_an_error(fba, tmp_path):
     assert fba.main(folder) == 1
 
 
+def test_missing_meas_std_fails_as_the_reference_text(fba, oracle, tmp_path):
+    """A .cfg without Meas_std: main.m:123-127 sets Meas_std = 1 and no_std_y = 1 but never creates a
+    Meas_std_y field, so main.m:399's rmfield fails and the reference stops.  The reference's own text run
+    on cam0 without that line (tests/golden/make_ref_golden.py -> ref_cam0_nostd.json) fails exactly
+    there; ingest (and the oracle's restatement) raise at the same point, and main() returns the error."""
+    import json
+    from conftest import variant_folder
+    ref = json.load(open(os.path.join(ROOT, "tests", "golden", "ref_cam0_nostd.json")))
+    assert ref["error"] and "rmfield" in ref["error"] and "Meas_std_y" in ref["error"] and "line 399" in ref["error"]
+    folder = variant_folder(str(tmp_path), "nostd", {"Meas_std": None, "Meas_std_y": None})
+    assert all(not ln.startswith("Meas_std") for ln in open(os.path.join(folder, "config.cfg")))
+    with pytest.raises(fba.IngestError, match="main.m:399"):
+        fba.load_folder(folder)
+    with pytest.raises(ValueError, match="main.m:399"):
+        oracle.load_folder(folder)
+    assert fba.main(folder) == 1
+
+
 def test_synthetic_scene_files_roundtrip(fba, oracle, tmp_path):
     from fba_amd import synth
     sc = synth.generate(9, 100, seed=3)

@@ -61,6 +61,10 @@ def test_out_report_layout(cam0_outputs):
     pos = [txt.index(h) for h in heads]
     assert pos == sorted(pos)
     lines = txt.splitlines()
+    # main.m:636-637's header lines, with this build named as the producer (the reference's author line
+    # otherwise attributes these numbers to the MATLAB program)
+    assert lines[0].startswith("Version: fba_amd") and lines[0].endswith("Fish-eye model Bundle Adjustment")
+    assert lines[1].startswith("Results produced by fba_amd") and "Wynand Tredoux" in lines[1] and lines[2] == ""
 
     def row(name):
         ln = next(x for x in lines if x.startswith(name + " ."))
