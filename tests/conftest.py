@@ -68,6 +68,35 @@ CAM0_VARIANTS = {
 }
 
 
+# SURVEY section 8(c) golden 3: a small synthetic fish-eye free network -- the north-star model
+# (equidistant, BuildAwG.m:186-187) with inner constraints and no control (BuildAwG.m:514-527), all EOP +
+# IOP + 5 radial + 2 decentering unknowns, at a well-conditioned point (two exact restatements of the
+# reference agree to <= 2.3e-12 of every parameter group's scale, solver_spread).  The reference's own
+# text run on it: tests/golden/ref_synth_fisheye_free.npz (tests/golden/make_ref_golden.py synth_fe).
+SYNTH_FE = {"n_img": 12, "n_tie": 300, "seed": 34, "obs_per_point": 8}
+
+
+def synth_fe_folder(root):
+    """the scene's folder (deterministic: synth.generate with SYNTH_FE, .17g text) and a hash of its files"""
+    import hashlib
+    import fba_import
+    fba_import.load()
+    from fba_amd import synth
+    p = dict(SYNTH_FE)
+    sc = synth.generate(p.pop("n_img"), p.pop("n_tie"), **p)
+    folder = synth.write_folder(sc, os.path.join(root, "synth_fe"))
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(folder)):
+        with open(os.path.join(folder, f), "rb") as fh:
+            h.update(f.encode() + fh.read())
+    return folder, h.hexdigest()
+
+
+@pytest.fixture(scope="session")
+def synth_fe(tmp_path_factory):
+    return synth_fe_folder(str(tmp_path_factory.mktemp("synth_fe")))
+
+
 @pytest.fixture(scope="session")
 def cam0_folders(tmp_path_factory):
     root = str(tmp_path_factory.mktemp("cam0v"))

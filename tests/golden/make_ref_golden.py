@@ -13,6 +13,11 @@ enable_plots = false; the version/date strings only feed the .out header).  The 
 interpreted from their text too: functions/ReadFiles.m, findSetting.m, Buildxhat.m, BuildAwG.m,
 BuildRSD.m, sumabs.m.  MATLAB built-ins (readmatrix, inv, mtimes, ...) are restated in mlang.py.
 
+Also (`make_ref_golden.py /root/reference synth_fe`): the same run on conftest.SYNTH_FE, a synthetic
+equidistant fish-eye free network (12 images x 300 tie points, inner constraints, no control, all EOP +
+IOP + 5 radial + 2 decentering) -> ref_synth_fisheye_free.npz; and (`nostd`) cam0 without its Meas_std
+line -> ref_cam0_nostd.json (the reference stops in rmfield at main.m:399).
+
 Only numbers are stored: per-iteration xhat and deltasum, the iteration count, sigma0^2, RMSx / RMSy
 / RMS, v, the numeric RSD columns, dist_scaling, A / w / G of the first BuildAwG call, diag(Cx) after
 the de-scaling and the sigma0^2 scaling (main.m:460-482, :602) and the Correlation sub-blocks the
@@ -28,9 +33,10 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.join(HERE, ".."))
+sys.path.insert(0, os.path.join(HERE, "..", ".."))
 
 import mlang  # noqa: E402
-from conftest import CAM0_VARIANTS, variant_folder  # noqa: E402
+from conftest import CAM0_VARIANTS, synth_fe_folder, variant_folder  # noqa: E402
 
 MAIN_FIRST, MAIN_LAST = 61, 628
 FUNCS = ["ReadFiles", "findSetting", "Buildxhat", "BuildAwG", "BuildRSD", "sumabs"]
@@ -66,7 +72,11 @@ def extract(env, awg):
     pts = data.elems[0]["points"].elems
     n_img = int(data.elems[0]["numImg"])
     xhat_arr = num(env["xhat_arr"])
-    names = [mlang.text_of(x) for x in env["xhatnames"].a.reshape(-1, order="F")]
+    def name_of(x):  # a tie name is a cell inside the cell when TIE is a cell array (Buildxhat.m:111, :132)
+        while isinstance(x, mlang.MCell) and x.a.size == 1:
+            x = x.a.flat[0]
+        return mlang.text_of(x)
+    names = [name_of(x) for x in env["xhatnames"].a.reshape(-1, order="F")]
     _, A0, w0, G0, ds0 = awg
     A0 = num(A0)
     rows, cols = np.nonzero(A0)
@@ -109,12 +119,29 @@ def run_nostd(ref_root, root):
     print("nostd:", out["error"], flush=True)
 
 
+def run_synth(ref_root, root):
+    """conftest.SYNTH_FE (12 images x 300 tie points, equidistant fish-eye, inner constraints, no control)
+    -> ref_synth_fisheye_free.npz, with the sha256 of the scene's files (the tests regenerate the scene
+    and check that hash before comparing)"""
+    folder, digest = synth_fe_folder(root)
+    t0 = time.time()
+    env, awg = run_reference(ref_root, folder)
+    out = extract(env, awg)
+    out["files_sha256"] = np.array(digest)
+    np.savez_compressed(os.path.join(HERE, "ref_synth_fisheye_free.npz"), **out)
+    print(f"synth_fe: {out['iterations']} iterations, sigma0^2 {out['sigma02']!r}, "
+          f"deltasum {out['deltasum'][-1]:.3e}, {time.time() - t0:.1f} s", flush=True)
+
+
 def main(ref_root):
     root = tempfile.mkdtemp()
-    only = sys.argv[2:] or sorted(CAM0_VARIANTS) + ["nostd"]
+    only = sys.argv[2:] or sorted(CAM0_VARIANTS) + ["nostd", "synth_fe"]
     if "nostd" in only:
         run_nostd(ref_root, root)
         only = [n for n in only if n != "nostd"]
+    if "synth_fe" in only:
+        run_synth(ref_root, root)
+        only = [n for n in only if n != "synth_fe"]
     for name in only:
         folder = variant_folder(root, name, CAM0_VARIANTS[name])
         t0 = time.time()

@@ -132,6 +132,44 @@ def test_adjust_cam0_matches_reference_text(fba, oracle, cam0_folders, variant):
         np.testing.assert_allclose(res.corr, g["corr_blocks"], rtol=0, atol=1e-9)
 
 
+def test_adjust_synthetic_fisheye_matches_reference_text(fba, synth_fe):
+    """SURVEY section 8(c) golden 3 on the device: the HIP path on the synthetic equidistant fish-eye free
+    network (conftest.SYNTH_FE: 12 images x 300 tie points, inner constraints, no control, all EOP + IOP +
+    5 radial + 2 decentering) against the reference's own main.m / BuildAwG.m text run on the same files
+    (tests/golden/ref_synth_fisheye_free.npz).  The scene is well conditioned, so the tight bars hold on
+    EVERY iteration: Buildxhat exact, BuildAwG <= 1e-12, the same iteration count, xhat after every
+    iteration <= 1e-9 per element (entries below 10% of their group's scale at 1e-10 of that scale,
+    conftest.SMALL_SCENE_FLOOR), the deltasum history (1e-6 relative or 1e-9 absolute), sigma0^2 and RMS
+    <= 1e-9, v and RSD <= 1e-9 of their scale, diag(Cx) <= 1e-9 (the distortion terms' variances 1e-8, as
+    on cam0) and the EOP/IOP correlation blocks <= 1e-9 absolute."""
+    from test_reference_text import assert_within, check_awg, load_synth_fe, loop_errors
+    g = load_synth_fe(synth_fe)
+    ds = fba.load_folder(synth_fe[0])
+    ctx = _ctx(fba, ds)
+    try:
+        x0 = ctx.buildxhat()
+        np.testing.assert_array_equal(x0, g["xhat_hist"][0])
+        A, w, G, dsc = ctx.build_awg(x0)
+        check_awg(A, w, G, dsc, g, np.abs(ds.xy).max())
+        hist, dsum = [x0], []
+        for _ in range(int(g["iterations"])):
+            dsum.append(ctx.step())
+            hist.append(ctx.get_xhat())
+        v, rsd, st = ctx.residuals()
+    finally:
+        ctx.close()
+    res = fba.adjust(ds)
+    assert res.iterations == int(g["iterations"])
+    np.testing.assert_array_equal(res.xhat, hist[-1])
+    err = loop_errors(g, hist, dsum, st[3], st[:3], v, rsd, g["dist_scaling"], floor=SMALL_SCENE_FLOOR)
+    print("HIP vs reference text (synthetic fish-eye):", {k: f"{e:.1e}" for k, e in err.items()})
+    assert_within(err, "stage3_pinhole", {})
+    dist = np.array([nm[0] in "kp" and nm[1:2].isdigit() for nm in g["names"]])
+    np.testing.assert_allclose(res.cx_diag[~dist], g["cx_diag"][~dist], rtol=1e-9, atol=0)
+    np.testing.assert_allclose(res.cx_diag[dist], g["cx_diag"][dist], rtol=1e-8, atol=0)
+    np.testing.assert_allclose(res.corr, g["corr_blocks"], rtol=0, atol=1e-9)
+
+
 @pytest.mark.parametrize("typ", ["fisheye", "pinhole", "equisolid", "orthographic", "stereographic"])
 def test_adjust_synthetic_types(fba, oracle, tmp_path, typ):
     from fba_amd import synth

@@ -35,7 +35,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import CAM0_VARIANTS, GOLDEN, elem_rel_err, solver_spread
+from conftest import CAM0_VARIANTS, ELEM_FLOOR, GOLDEN, SMALL_SCENE_FLOOR, elem_rel_err, solver_spread
 
 PINHOLE = ["stage1_pinhole", "stage3_pinhole", "stage3_noic_pinhole", "stage3_sigy_pinhole"]
 FISHEYE = ["stage3_fisheye", "stage3_equisolid", "stage3_orthographic", "stage3_stereographic"]
@@ -67,13 +67,13 @@ def check_awg(A, w, G, ds, g, xy_scale):
     np.testing.assert_allclose(ds, g["dist_scaling"], rtol=1e-14)
 
 
-def loop_errors(g, xhat_hist, deltasum, sigma02, rms, v, rsd, dist_scaling, every_iteration=True):
+def loop_errors(g, xhat_hist, deltasum, sigma02, rms, v, rsd, dist_scaling, every_iteration=True, floor=ELEM_FLOOR):
     """per-group errors of a whole run against the reference's, keyed like conftest.solver_spread
-    (every_iteration=False: the converged xhat only)"""
+    (every_iteration=False: the converged xhat only; floor: conftest.elem_rel_err's)"""
     names = g["names"]
     err = {}
     for k in range(1 if every_iteration else g["iterations"], g["iterations"] + 1):
-        for grp, e in elem_rel_err(xhat_hist[k], g["xhat_hist"][k], names, dist_scaling).items():
+        for grp, e in elem_rel_err(xhat_hist[k], g["xhat_hist"][k], names, dist_scaling, floor).items():
             err["e_" + grp] = max(err.get("e_" + grp, 0.0), e)
     # Sum|delta| of converged iterations adds rounding-level corrections: 1e-6 relative, or 1e-9 absolute
     # = 1e-3 of Threshold_Value (config.cfg:8): each of cam0's 580 corrections is reproducible to ~1e-13
@@ -125,6 +125,49 @@ def test_oracle_matches_reference_text(oracle, cam0_folders, variant):
             k = int(od.cam_num[np.nonzero(od.ext_index == e)[0][0]])
             idx += list(range(u_img * od.numImg + k * u_cam, u_img * od.numImg + (k + 1) * u_cam))
             np.testing.assert_allclose(corr[np.ix_(idx, idx)], g["corr_blocks"][e], rtol=0, atol=1e-9)
+
+
+SYNTH_FE_NPZ = os.path.join(GOLDEN, "ref_synth_fisheye_free.npz")
+
+
+def load_synth_fe(synth_fe):
+    """the reference-text fixture of conftest.SYNTH_FE, after checking that the regenerated scene's files
+    are byte for byte the ones the reference text read"""
+    g = np.load(SYNTH_FE_NPZ, allow_pickle=False)
+    out = {k: g[k] for k in g.files}
+    out["names"] = [str(s) for s in out["names"]]
+    assert str(out["files_sha256"]) == synth_fe[1], "synth.generate / write_folder changed: regenerate the fixture"
+    return out
+
+
+def test_oracle_matches_reference_text_synthetic_fisheye(oracle, synth_fe):
+    """SURVEY section 8(c) golden 3: the north-star model -- equidistant fish-eye (BuildAwG.m:186-187),
+    inner constraints with no control (BuildAwG.m:514-527), all EOP + IOP + 5 radial + 2 decentering --
+    on a synthetic free network (conftest.SYNTH_FE), against main.m:61-628 run from its text.  The scene is
+    well conditioned (two exact restatements agree to <= 2.3e-12 of each parameter group's scale), so the
+    pinhole variants' bars hold on EVERY iteration: xhat per element 1e-9 (entries below 10% of their
+    group's scale -- omega/phi near 0, tie coordinates near the datum's origin -- at 1e-10 of that scale,
+    conftest.SMALL_SCENE_FLOOR), deltasum history, sigma0^2, RMS, v, RSD, diag(Cx) and the correlation
+    blocks."""
+    g = load_synth_fe(synth_fe)
+    od = oracle.load_folder(synth_fe[0])
+    x0, names = oracle.buildxhat(od)
+    assert names == g["names"]
+    np.testing.assert_array_equal(x0, g["xhat_hist"][0])
+    A, w, G, ds = oracle.build_awg(od, x0)
+    check_awg(A, w, G, ds, g, max(np.abs(od.x).max(), np.abs(od.y).max()))
+    ro = oracle.adjust(od)
+    assert ro.iterations == g["iterations"]
+    err = loop_errors(g, ro.xhat_hist, ro.deltasum, ro.sigma02, ro.rms, ro.v, ro.rsd, g["dist_scaling"],
+                      floor=SMALL_SCENE_FLOOR)
+    print("oracle vs reference text (synthetic fish-eye):", {k: f"{v:.1e}" for k, v in err.items()})
+    assert_within(err, "stage3_pinhole", {})
+    cxd, corr = oracle.covariance(od, ro)
+    np.testing.assert_allclose(cxd, g["cx_diag"], rtol=1e-9, atol=0)
+    u_img, u_cam = oracle.counts(od.settings)
+    for e in range(od.numImg):
+        idx = list(range(e * u_img, (e + 1) * u_img)) + list(range(u_img * od.numImg, u_img * od.numImg + u_cam))
+        np.testing.assert_allclose(corr[np.ix_(idx, idx)], g["corr_blocks"][e], rtol=0, atol=1e-9)
 
 
 def test_reference_text_fixtures_are_what_main_prints():
