@@ -124,10 +124,10 @@ def test_control_points_adjust_matches_oracle(fba, fbo, oracle, tmp_path):
 
 
 def test_config3_covariance_matches_oracle(fba, fbo, oracle, scenes):
-    """fba_covariance at config 3 (u = 16,210): the camera-side diagonal of Cx and the EOP/IOP
-    correlation blocks against the dense inverse of the C oracle's last bordered reduced system
-    [S G; G' 0] (the camera block of the bordered inverse of the full normal matrix, main.m:432);
-    every tie-point variance positive and finite."""
+    """fba_covariance at config 3 (u = 16,210): the camera-side diagonal of Cx (1e-8 relative) and the
+    EOP/IOP correlation blocks (1e-8 absolute) against the dense inverse of the C oracle's last bordered
+    reduced system [S G; G' 0] (the camera block of the bordered inverse of the full normal matrix,
+    main.m:432); every tie-point variance positive and finite."""
     import scipy.linalg as sla
     folder = _scene(3, scenes)
     ds = fba.load_folder(folder)
@@ -144,8 +144,11 @@ def test_config3_covariance_matches_oracle(fba, fbo, oracle, scenes):
     sc = distortion_scale(ref.names[:uc], dist_scaling_of(od))
     res = fba.adjust(ds)
     want = s02 * np.diag(C) / sc ** 2
+    # bars: measured 4.4e-10 relative on the diagonal and 1.1e-9 absolute on the correlations (round 6,
+    # profiles/r06_v7_measured_errors.log: the selected inverse of the Cholesky factor against the dense
+    # inverse of the C oracle's own last normal matrix), held to ~20x / ~10x that
     print(f"config 3 diag(Cx): max relative error {np.max(np.abs(res.cx_diag[:uc] - want) / np.abs(want)):.2e}")
-    np.testing.assert_allclose(res.cx_diag[:uc], want, rtol=1e-7)
+    np.testing.assert_allclose(res.cx_diag[:uc], want, rtol=1e-8)
     d = np.sqrt(np.diag(C))
     corr = C / np.outer(d, d)
     cam = 6 * od.numImg
@@ -153,7 +156,7 @@ def test_config3_covariance_matches_oracle(fba, fbo, oracle, scenes):
     for e in range(0, od.numImg, 17):
         idx = list(range(6 * e, 6 * e + 6)) + list(range(cam, cam + 10))
         worst = max(worst, float(np.max(np.abs(res.corr[e] - corr[np.ix_(idx, idx)]))))
-        np.testing.assert_allclose(res.corr[e], corr[np.ix_(idx, idx)], rtol=0, atol=1e-7)
+        np.testing.assert_allclose(res.corr[e], corr[np.ix_(idx, idx)], rtol=0, atol=1e-8)
     print(f"config 3 correlation blocks: max absolute error {worst:.2e}")
     tie = res.cx_diag[uc:]
     assert np.isfinite(tie).all() and (tie > 0).all()
@@ -182,8 +185,9 @@ def test_config4_adjust_matches_oracle(fba, fbo, oracle, scenes):
     rms_ref = (np.sqrt(np.mean(v_ref[0::2] ** 2)), np.sqrt(np.mean(v_ref[1::2] ** 2)))
     assert abs(res.rms[0] - rms_ref[0]) <= 1e-9 * rms_ref[0] and abs(res.rms[1] - rms_ref[1]) <= 1e-9 * rms_ref[1]
     # per observation: v = A delta + w of the last linearisation (main.m:569)
+    # (measured 4.0e-13 of the scale, round 6: profiles/r06_v7_measured_errors.log; held to 1e-10)
     print(f"config 4 v: max |dv| / max |v| = {np.max(np.abs(res.v - v_ref)) / np.max(np.abs(v_ref)):.2e}")
-    assert np.max(np.abs(res.v - v_ref)) <= 1e-7 * np.max(np.abs(v_ref))
+    assert np.max(np.abs(res.v - v_ref)) <= 1e-10 * np.max(np.abs(v_ref))
 
 
 DISTORTION = ("k1", "k2", "k3", "k4", "k5", "p1", "p2")

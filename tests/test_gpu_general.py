@@ -75,9 +75,11 @@ def test_adjust_general(fba, oracle, tmp_path, name):
     assert max(err.values()) <= 1e-9, err
     assert res.sigma02 == pytest.approx(ro.sigma02, rel=1e-9)
     np.testing.assert_allclose(res.deltasum, ro.deltasum, rtol=0, atol=1e-9 * ro.deltasum[0])
+    print(f"general points: v max error {np.abs(res.v - ro.v).max() / np.abs(ro.v).max():.2e} of its scale")
     assert np.abs(res.v - ro.v).max() <= 1e-8 * np.abs(ro.v).max()
     # covariance: camera-side diagonal and EOP/IOP correlation blocks, and every tie variance
     cdo, corro = oracle.covariance(od, ro)
+    print(f"general points covariance: diag(Cx) max relative error {np.max(np.abs(res.cx_diag - cdo) / np.abs(cdo)):.2e}")
     np.testing.assert_allclose(res.cx_diag, cdo, rtol=1e-7, atol=0)
     u_img, u_cam = oracle.counts(od.settings)
     for e in range(od.numImg):
@@ -85,6 +87,8 @@ def test_adjust_general(fba, oracle, tmp_path, name):
         k = int(od.cam_num[np.nonzero(od.ext_index == e)[0][0]])
         idx += list(range(u_img * od.numImg + k * u_cam, u_img * od.numImg + (k + 1) * u_cam))
         np.testing.assert_allclose(res.corr[e], corro[np.ix_(idx, idx)], rtol=0, atol=1e-7)
+        print(f"general points: image {e} correlation block max absolute error "
+              f"{np.max(np.abs(res.corr[e] - corro[np.ix_(idx, idx)])):.2e}") if e == 0 else None
 
 
 def test_point_seen_by_300_images(fba, tmp_path):

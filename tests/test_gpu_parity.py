@@ -386,13 +386,17 @@ def _check_cov(res, od, ro, oracle, rtol=1e-7, atol_corr=1e-7):
     """diag(Cx) and the EOP/IOP correlation sub-blocks of fba_covariance against the oracle's dense
     bordered inverse of the last normal matrix (main.m:428-482, :602)."""
     cdo, corro = oracle.covariance(od, ro)
+    print(f"covariance: diag(Cx) max relative error {np.max(np.abs(res.cx_diag - cdo) / np.abs(cdo)):.2e}")
     np.testing.assert_allclose(res.cx_diag, cdo, rtol=rtol, atol=0)
     u_img, u_cam = oracle.counts(od.settings)
+    worst = 0.0
     for e in range(od.numImg):
         idx = list(range(e * u_img, (e + 1) * u_img))
         k = int(od.cam_num[np.nonzero(od.ext_index == e)[0][0]])
         idx += list(range(u_img * od.numImg + k * u_cam, u_img * od.numImg + (k + 1) * u_cam))
+        worst = max(worst, float(np.max(np.abs(res.corr[e] - corro[np.ix_(idx, idx)]))))
         np.testing.assert_allclose(res.corr[e], corro[np.ix_(idx, idx)], rtol=0, atol=atol_corr)
+    print(f"covariance: correlation blocks max absolute error {worst:.2e}")
 
 
 @pytest.mark.parametrize("variant", ["stage3_pinhole", "stage1_pinhole", "stage3_noic_pinhole", "stage3_sigy_pinhole"])
