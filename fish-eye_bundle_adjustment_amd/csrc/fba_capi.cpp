@@ -1507,11 +1507,8 @@ int fba_covariance(fba_ctx* ctx, double sigma02, double* cx_diag, double* corr) 
         set_error("fba_covariance needs the factor of the last solve (call it once, right after the iterations)");
         return FBA_ERR_ARG;
     }
-    if (c->sched.split) {
-        set_error("fba_covariance: a subtree-split context holds only its own subtrees' factor");
-        return FBA_ERR_UNSUPPORTED;
-    }
     const Layout& L = c->L;
+    const bool split = c->sched.split;
     const int m = 6 + L.cw;
     double *d_cdiag = nullptr, *d_pdiag = nullptr, *d_iblk = nullptr;
     int32_t *d_islot = nullptr, *d_icam = nullptr;
@@ -1556,7 +1553,9 @@ int fba_covariance(fba_ctx* ctx, double sigma02, double* cx_diag, double* corr) 
         std::fill(cx_diag, cx_diag + L.u_ref, 0.0);
         for (int64_t i = 0; i < L.u_full; ++i) {
             const int64_t r = c->full_to_ref[i];
-            if (r < 0 || (i >= L.u_c && !c->full_owned[i])) continue;
+            // (tie entries: this rank's points; camera-side entries: every rank, or with the subtree split
+            // this rank's rows -- its subtrees', and the top's on rank 0 -- so that the ranks' outputs sum)
+            if (r < 0 || ((i >= L.u_c || split) && !c->full_owned[i])) continue;
             cx_diag[r] = sigma02 * (i < L.u_c ? cd[i] : pd[i - L.u_c]);  // main.m:602: Cx = sigma02 .* Cx
         }
     }
@@ -1574,6 +1573,12 @@ int fba_covariance(fba_ctx* ctx, double sigma02, double* cx_diag, double* corr) 
         for (int e = 0; e < L.n_img_ref; ++e) {
             const double* b = ib.data() + (size_t)e * m * m;
             double* out = corr + (size_t)e * mu * mu;
+            // (subtree split: an image's block on the rank that owns its first row -- its subtree's rank, even
+            // when the image straddles into a top block; a wholly-top image on rank 0 -- zeros elsewhere)
+            if (split && !c->full_owned[6 * (int64_t)c->img_new[e]]) {
+                std::fill(out, out + (size_t)mu * mu, 0.0);
+                continue;
+            }
             for (int a = 0; a < (int)sel.size(); ++a)
                 for (int q = 0; q < (int)sel.size(); ++q) {
                     const int ra = sel[a], rq = sel[q];

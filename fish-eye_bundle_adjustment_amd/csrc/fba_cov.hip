@@ -161,8 +161,15 @@ __global__ __launch_bounds__(256) void k_blk_combine(const int64_t* __restrict__
 }
 
 // H^-1 of the 14x14 border system (k_border_combine's H = [[A'A - I, A'B], [B'A, B'B]] from the Gram of
-// the forward-solved rows 1..14), Gauss-Jordan with partial pivoting, one wave; gpart as k_border_gram
-__global__ __launch_bounds__(64) void k_border_hinv(const double* __restrict__ gpart, int nseg, double* __restrict__ hinv) {
+// the forward-solved rows 1..14), Gauss-Jordan with partial pivoting, one wave; gpart as k_border_gram,
+// or (gblk != nullptr) the per-column-block 16 x 16 Gram partials k_chol_flow's RHS panel halves leave,
+// summed in block order -- the subtree split's, all-reduced over the ranks (a rank's S holds the
+// forward-solved rows of its own and the top columns only).  The split forward-solves the B rows
+// unscaled; H and Z (k_border_wz) then both miss the same diagonal scaling D, and Z' H^-1 Z is
+// unchanged by it: Z' D (D H D)^-1 D Z = Z' H^-1 Z.
+__global__ __launch_bounds__(64) void k_border_hinv(const double* __restrict__ gpart, int nseg,
+                                                    const double* __restrict__ gblk, int nblk,
+                                                    double* __restrict__ hinv) {
     __shared__ double g[15][15];
     __shared__ double H[14][28];
     const int tid = threadIdx.x;
@@ -171,7 +178,10 @@ __global__ __launch_bounds__(64) void k_border_hinv(const double* __restrict__ g
         while (rem >= 15 - a) { rem -= 15 - a; ++a; }
         const int b = a + rem;
         double v = 0.0;
-        for (int q = 0; q < nseg; ++q) v += gpart[q * 120 + e];
+        if (gblk)
+            for (int q = 0; q < nblk; ++q) v += gblk[(int64_t)q * 256 + a * 16 + b];
+        else
+            for (int q = 0; q < nseg; ++q) v += gpart[q * 120 + e];
         g[a][b] = g[b][a] = v;
     }
     __syncthreads();
@@ -368,6 +378,13 @@ int launch_border_gram(Ctx& c, double* gpart, int* nseg);
 // Outputs (device, internal order): cdiag [u_c] (de-scaled camera-side diag C), pdiag [3 n_tie]
 // (tie points of this rank), iblk [n_img_ref][(6+cw)^2] (raw C blocks per reference image).
 // ------------------------------------------------------------------------------------------------
+static bool s_split(const Ctx& c) { return c.sched.split; }
+
+// (subtree split) every quantity below for a column of this rank's subtrees or of the top reads only
+// such columns -- the Takahashi recurrence of column k reads Q over k's ancestors, the backward solve of
+// column j the solutions of j's ancestors -- so the selected inverse runs on the whole block pattern as
+// it stands: the other ranks' columns, never factored here, come out as garbage no output reads
+// (fba_covariance keeps the entries of this rank's rows only)
 int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, const int32_t* d_islot,
                       const int32_t* d_icam, int n_iblk) {
     const Layout& L = c.L;
@@ -390,8 +407,13 @@ int launch_covariance(Ctx& c, double* d_cdiag, double* d_pdiag, double* d_iblk, 
         if ((rc = alloc(&d_Z, 14 * (size_t)n_pad)) || (rc = alloc(&d_Wz, 14 * (size_t)n_pad)) ||
             (rc = alloc(&d_h, 196)) || (rc = alloc(&d_g, 64 * 120))) { cleanup(); return rc; }
         int nseg = 0;
-        if ((rc = launch_border_gram(c, d_g, &nseg)) || (rc = launch_backward_rows(c, 1, 14, d_Z))) { cleanup(); return rc; }
-        k_border_hinv<<<1, 64, 0, c.stream>>>(d_g, nseg, d_h);
+        // (subtree split: the Gram from the all-reduced per-block partials; another rank's columns of this
+        // rank's RHS rows were never forward-solved here)
+        if ((!s_split(c) && (rc = launch_border_gram(c, d_g, &nseg))) || (rc = launch_backward_rows(c, 1, 14, d_Z))) {
+            cleanup();
+            return rc;
+        }
+        k_border_hinv<<<1, 64, 0, c.stream>>>(d_g, nseg, s_split(c) ? c.d_gblk : nullptr, (int)nb, d_h);
         k_border_wz<<<(unsigned)((n_pad + 255) / 256), 256, 0, c.stream>>>(d_Z, d_h, d_Wz, n_pad);
     }
 

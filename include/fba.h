@@ -211,10 +211,14 @@ int fba_finish_stats(const fba_problem* p, const fba_settings* s, const double* 
  *   cx_diag [u] (may be NULL): diag(Cx) of the reference's final Cx = sigma02 * (bordered) inverse of
  *           the last normal matrix, distortion entries de-scaled by dist_scaling^2 (main.m:460-482,
  *           diagonal only, as the reference); xhat order.  With world > 1 the tie entries of other
- *           ranks are 0 (camera entries are replicated).
+ *           ranks are 0 (camera entries are replicated); with the subtree split (fba_options.split)
+ *           the camera-side entries too are this rank's rows only (its subtrees' images, and the top's
+ *           images and the camera unknowns on rank 0), so the ranks' outputs sum to the whole vector.
  *   corr [n_img][(u_img+u_cam)^2] (may be NULL): per EXT image, the reference's Correlation matrix
  *           (main.m:446-456) restricted to [the image's estimated EOPs, its camera's estimated
- *           IOP/distortion unknowns] in xhat order, full symmetric, row-major (main.m:831-840). */
+ *           IOP/distortion unknowns] in xhat order, full symmetric, row-major (main.m:831-840); with
+ *           the subtree split only this rank's images (the rank owning the image's first row; wholly
+ *           top images on rank 0), zeros for the others. */
 int fba_covariance(fba_ctx* ctx, double sigma02, double* cx_diag, double* corr);
 
 /* Per-phase device timings of the last fba_step / fba_accumulate+fba_solve_update, in ms:

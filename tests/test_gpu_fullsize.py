@@ -389,6 +389,50 @@ def test_subtree_split_two_ranks_match_single_context(fba, scenes, config):
             c.close()
 
 
+def test_subtree_split_covariance_matches_single_context(fba, scenes):
+    """fba_covariance with the subtree split (config 3, two rank contexts on one GPU, host-summed reduce
+    buffers): each rank's selected inverse runs over its own subtrees and the top -- the Takahashi
+    recurrence of a column reads only its ancestors -- with the border's H from the all-reduced per-block
+    Gram partials; a rank writes the camera-side variances of its own rows (the top's on rank 0), its
+    points' variances and the correlation blocks of its images, so the ranks' outputs sum to the single
+    context's diag(Cx) and correlation blocks.  Bars: 1e-8 relative on diag(Cx), 1e-9 absolute on the
+    correlations (the two contexts factor the same system in another reduction order)."""
+    import ctypes
+    folder = _scene(3, scenes)
+    ds = fba.load_folder(folder)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    mk = lambda **kw: fba.capi.Context(ds.pack(), fba.capi.make_settings(ds.settings), **kw)  # noqa: E731
+    single = mk()
+    ranks = [mk(rank=r, world=2, split=True) for r in range(2)]
+    try:
+        assert all(c.split for c in ranks)
+        for _ in range(2):
+            single.step()
+            for c in ranks:
+                c.accumulate()
+                c.synchronize()
+            _sum_buffers(hip, ranks)
+            for c in ranks:
+                c.solve_update()
+        s02 = 1.0
+        cd1, cr1 = single.covariance(s02)
+        parts = [c.covariance(s02) for c in ranks]
+        cd2 = parts[0][0] + parts[1][0]
+        cr2 = parts[0][1] + parts[1][1]
+        rel = np.max(np.abs(cd2 - cd1) / np.abs(cd1))
+        print(f"split covariance vs single: diag(Cx) {rel:.2e} relative, correlations {np.max(np.abs(cr2 - cr1)):.2e}")
+        assert np.all(cd1 > 0) and rel <= 1e-8, rel
+        np.testing.assert_allclose(cr2, cr1, rtol=0, atol=1e-9)
+        # every entry written by exactly one rank: no image block or variance on both
+        assert not np.any((parts[0][0] != 0) & (parts[1][0] != 0))
+        assert not np.any(np.any(parts[0][1] != 0, axis=(1, 2)) & np.any(parts[1][1] != 0, axis=(1, 2)))
+    finally:
+        single.close()
+        for c in ranks:
+            c.close()
+
+
 def test_handoff_timeout_fails_safe(fba, scenes, monkeypatch):
     """A device hand-off timeout in the factorisation (every poll bounded, fba_chol.hip) must not leave a
     wrong iterate behind: with the poll bound forced down to one sleep (FBA_FLAG_SPINS at context
