@@ -18,23 +18,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(config, prio):
-    """prio: "none" (context-owned streams) or "hi-lo" (A on a high-priority stream, B on a low-priority
-    one: the dispatcher then prefers A's workgroups whenever a CU frees up)"""
+def run(config):
     import fba_import
     fba = fba_import.load()
     import bench
-    import torch
     folder = bench.scene_folder(config, 0, 1)
     ds = fba.load_folder(folder)
-    streams = [None, None]
-    if prio == "hi-lo":
-        lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
-        sa, sb = torch.cuda.Stream(priority=hi), torch.cuda.Stream(priority=lo)
-        print(f"stream priorities: A {hi}, B {lo}", flush=True)
-        streams = [sa.cuda_stream, sb.cuda_stream]
-    mk = lambda s: fba.capi.Context(ds.pack(), fba.capi.make_settings(ds.settings), stream=s)  # noqa: E731
-    a, b = mk(streams[0]), mk(streams[1])
+    mk = lambda: fba.capi.Context(ds.pack(), fba.capi.make_settings(ds.settings))  # noqa: E731
+    a, b = mk(), mk()
     try:
         for _ in range(3):
             a.step()
@@ -81,4 +72,4 @@ if __name__ == "__main__":
     if sys.argv[1] == "--analyse":
         analyse(sys.argv[2])
     else:
-        run(int(sys.argv[1]), sys.argv[2] if len(sys.argv) > 2 else "none")
+        run(int(sys.argv[1]))
