@@ -9,7 +9,7 @@ chunked fast path -- the "blocks" layouts mix both.
 
 Tolerances as tests/test_gpu_parity.py: BuildAwG A per column <= 1e-12; full adjustment: same
 iteration count, xhat <= 1e-9 relative per parameter group (distortion terms in scaled units),
-sigma0^2 <= 1e-9; covariance diag and correlation blocks <= 1e-7.
+sigma0^2 <= 1e-9; covariance diag <= 1e-8 relative and correlation blocks <= 5e-9 absolute.
 """
 import numpy as np
 import pytest
@@ -76,17 +76,19 @@ def test_adjust_general(fba, oracle, tmp_path, name):
     assert res.sigma02 == pytest.approx(ro.sigma02, rel=1e-9)
     np.testing.assert_allclose(res.deltasum, ro.deltasum, rtol=0, atol=1e-9 * ro.deltasum[0])
     print(f"general points: v max error {np.abs(res.v - ro.v).max() / np.abs(ro.v).max():.2e} of its scale")
-    assert np.abs(res.v - ro.v).max() <= 1e-8 * np.abs(ro.v).max()
+    # (round 6, profiles/r06_v8_covariance_errors.log: v <= 6.5e-13 of its scale, diag(Cx) <= 5.7e-10
+    # relative, correlations <= 4.8e-11 on image 0 -- held to 1e-10, 1e-8 and 5e-9)
+    assert np.abs(res.v - ro.v).max() <= 1e-10 * np.abs(ro.v).max()
     # covariance: camera-side diagonal and EOP/IOP correlation blocks, and every tie variance
     cdo, corro = oracle.covariance(od, ro)
     print(f"general points covariance: diag(Cx) max relative error {np.max(np.abs(res.cx_diag - cdo) / np.abs(cdo)):.2e}")
-    np.testing.assert_allclose(res.cx_diag, cdo, rtol=1e-7, atol=0)
+    np.testing.assert_allclose(res.cx_diag, cdo, rtol=1e-8, atol=0)
     u_img, u_cam = oracle.counts(od.settings)
     for e in range(od.numImg):
         idx = list(range(e * u_img, (e + 1) * u_img))
         k = int(od.cam_num[np.nonzero(od.ext_index == e)[0][0]])
         idx += list(range(u_img * od.numImg + k * u_cam, u_img * od.numImg + (k + 1) * u_cam))
-        np.testing.assert_allclose(res.corr[e], corro[np.ix_(idx, idx)], rtol=0, atol=1e-7)
+        np.testing.assert_allclose(res.corr[e], corro[np.ix_(idx, idx)], rtol=0, atol=5e-9)
         print(f"general points: image {e} correlation block max absolute error "
               f"{np.max(np.abs(res.corr[e] - corro[np.ix_(idx, idx)])):.2e}") if e == 0 else None
 

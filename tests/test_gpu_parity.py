@@ -382,9 +382,11 @@ def test_sharded_step_over_rccl_and_device_views(fba, cam0_folders):
     ref.close()
 
 
-def _check_cov(res, od, ro, oracle, rtol=1e-7, atol_corr=1e-7):
+def _check_cov(res, od, ro, oracle, rtol=1e-8, atol_corr=5e-9):
     """diag(Cx) and the EOP/IOP correlation sub-blocks of fba_covariance against the oracle's dense
-    bordered inverse of the last normal matrix (main.m:428-482, :602)."""
+    bordered inverse of the last normal matrix (main.m:428-482, :602).  Bars from the round-6 measurements
+    (profiles/r06_v8_covariance_errors.log): diag(Cx) <= 1.4e-9 relative, correlations <= 3.9e-10 absolute
+    over the cam0 variants and the synthetic scenes -- held to 1e-8 and 5e-9."""
     cdo, corro = oracle.covariance(od, ro)
     print(f"covariance: diag(Cx) max relative error {np.max(np.abs(res.cx_diag - cdo) / np.abs(cdo)):.2e}")
     np.testing.assert_allclose(res.cx_diag, cdo, rtol=rtol, atol=0)
