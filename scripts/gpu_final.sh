@@ -8,4 +8,4 @@ for cfg in 3 5; do
   rc=$?; echo "== config $cfg rc=$rc"; tail -1 gpurun_out/bench_c$cfg.log | cut -c1-300
   [ $rc -ne 0 ] && exit $rc
 done
-bash scripts/gpu_gloo2.sh  # per-level launches: two ranks' persistent kernels cannot share the one GPU
+bash scripts/gpu_gloo2.sh  # both ranks on the one GPU: the flow kernels take their records from start-order tickets
